@@ -1,0 +1,235 @@
+/*
+ * mq.h — C-ABI of the MI355X quick-sat evaluator (libmq.so).
+ *
+ * The reference has no native boundary: quick-sat is the Python loop
+ *   ModelCache.check_quick_sat   mythril/support/support_utils.py:60-67
+ * which, for each cached z3 model in MRU-first order (`reversed(lru_cache.keys())`,
+ * support_utils.py:62), evaluates `is_true(deepcopy(model).eval(expr, model_completion=True))`
+ * (support_utils.py:63-64) and returns the first satisfying model.  It is reached from
+ *   get_model                    mythril/support/model.py:100-103
+ * This header is the native replacement of that loop, batched: N constraint tapes x M
+ * candidate models -> first satisfying candidate index per tape.  Every entry point below
+ * names the reference interface it replaces.  See INTEGRATION.md for the ctypes binding a
+ * Mythril maintainer adds at model.py:101 / support_utils.py:60.
+ *
+ * Conventions:
+ *   - every function returns 0 (MQ_OK) or a negative mq_status; nothing throws across the ABI;
+ *   - input buffers are copied; the caller keeps ownership of host memory;
+ *   - a context is confined to one host thread; calls are synchronous unless named *_async;
+ *   - candidate index 0 is the MRU model (reversed(LRU.keys())[0]).
+ */
+#ifndef MQ_H
+#define MQ_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ status codes */
+typedef enum mq_status {
+  MQ_OK = 0,
+  MQ_ERR_ARG = -1,         /* malformed argument (null pointer, bad size, bad node reference) */
+  MQ_ERR_HIP = -2,         /* HIP runtime error */
+  MQ_ERR_NOMEM = -3,       /* device allocation failed */
+  MQ_ERR_NO_MODELS = -4,   /* mq_eval_* before mq_models_upload */
+  MQ_ERR_NODEV = -5,       /* no usable gfx950 device */
+  MQ_ERR_TAPE = -6,        /* tape is not well sorted (type error) */
+  MQ_ERR_STATE = -7        /* context used after destroy / wrong thread */
+} mq_status;
+
+/* first_hit sentinels: */
+#define MQ_NO_HIT (-1)       /* no candidate satisfies the tape -> caller falls through to z3 */
+#define MQ_UNSUPPORTED (-2)  /* tape uses something the evaluator does not implement -> z3 eval */
+
+/* ------------------------------------------------------------------ tape IR
+ * A tape is a topologically ordered DAG of nodes (postfix order: operands precede users);
+ * the LAST node of a tape is its root and must be Bool-sorted.  Operands a/b/c are indices of
+ * earlier nodes of the same tape unless the opcode says they are immediates.
+ * width: result width in bits; 0 means Bool sort.  Array-sorted nodes (STORE, CONST_ARRAY,
+ * ARRAY_VAR) carry the range width.
+ * Semantics: SMT-LIB 2.6 FixedSizeBitVectors + z3 model completion.
+ * Vocabulary: mythril/laser/smt/{bitvec,bitvec_helper,bool,array,function}.py.
+ */
+typedef enum mq_op {
+  /* leaves */
+  MQ_OP_CONST = 1,        /* a = word offset of the value in const_words (ceil(width/32) LE limbs);
+                             Bool consts use MQ_OP_TRUE/FALSE */
+  MQ_OP_VAR = 2,          /* a = model variable index (BV or Bool); absent => 0 / false */
+  MQ_OP_TRUE = 3,
+  MQ_OP_FALSE = 4,
+  /* Bool connectives (args Bool) */
+  MQ_OP_NOT = 10,         /* a */
+  MQ_OP_AND = 11,         /* a, b   (n-ary z3 and is folded into a chain) */
+  MQ_OP_OR = 12,          /* a, b */
+  MQ_OP_XOR = 13,         /* a, b */
+  MQ_OP_IMPLIES = 14,     /* a => b */
+  MQ_OP_IFF = 15,         /* a == b on Bool */
+  MQ_OP_BITE = 16,        /* a ? b : c on Bool */
+  /* BV predicates (-> Bool) */
+  MQ_OP_EQ = 20,          /* a == b (same width) */
+  MQ_OP_ULT = 21,
+  MQ_OP_ULE = 22,
+  MQ_OP_SLT = 23,
+  MQ_OP_SLE = 24,
+  MQ_OP_UMUL_NOOVFL = 25, /* a*b < 2^W (unsigned) */
+  MQ_OP_SMUL_NOOVFL = 26, /* signed a*b <= 2^(W-1)-1 */
+  MQ_OP_SMUL_NOUDFL = 27, /* signed a*b >= -2^(W-1) */
+  /* BV arithmetic (mod 2^W) */
+  MQ_OP_ADD = 30,
+  MQ_OP_SUB = 31,
+  MQ_OP_MUL = 32,
+  MQ_OP_NEG = 33,         /* a */
+  MQ_OP_UDIV = 34,        /* udiv(a,0) = 2^W-1 */
+  MQ_OP_UREM = 35,        /* urem(a,0) = a */
+  MQ_OP_SDIV = 36,        /* sdiv(a,0) = a<0 ? 1 : -1 */
+  MQ_OP_SREM = 37,        /* srem(a,0) = a (sign of dividend) */
+  MQ_OP_SMOD = 38,        /* smod(a,0) = a (sign of divisor) */
+  /* bitwise / shifts */
+  MQ_OP_BAND = 40,
+  MQ_OP_BOR = 41,
+  MQ_OP_BXOR = 42,
+  MQ_OP_BNOT = 43,        /* a */
+  MQ_OP_SHL = 44,         /* amount = full W-bit value of b; >= W -> 0 */
+  MQ_OP_LSHR = 45,
+  MQ_OP_ASHR = 46,        /* >= W -> sign fill */
+  /* width changes */
+  MQ_OP_EXTRACT = 50,     /* a = arg, b = hi, c = lo (immediates) */
+  MQ_OP_CONCAT = 51,      /* a = high part, b = low part */
+  MQ_OP_ZEXT = 52,        /* a = arg, b = k (immediate) */
+  MQ_OP_SEXT = 53,        /* a = arg, b = k (immediate) */
+  MQ_OP_ITE = 54,         /* a = Bool cond, b = then, c = else (BV) */
+  /* arrays and uninterpreted functions (per-model interpretations) */
+  MQ_OP_SELECT = 60,      /* a = array node, b = index */
+  MQ_OP_STORE = 61,       /* a = array node, b = index, c = value   (array sort) */
+  MQ_OP_CONST_ARRAY = 62, /* a = value node (K(sort, v))            (array sort) */
+  MQ_OP_ARRAY_VAR = 63,   /* a = function id of the model table     (array sort) */
+  MQ_OP_UF = 64,          /* a = function id, b = arg0, c = arg1 (MQ_NONE if arity 1) */
+  /* interpreted keccak256 (Ethereum padding) of the big-endian bytes of a; width 256.
+     NOT z3 semantics: only for keccak-consistent synthetic models and constant folding
+     (keccak_function_manager.py:56-69). */
+  MQ_OP_KECCAK = 70
+} mq_op;
+
+#define MQ_NONE 0xFFFFFFFFu
+
+typedef struct mq_node {
+  uint16_t op;     /* mq_op */
+  uint16_t width;  /* result width in bits, 0 = Bool */
+  uint32_t a, b, c;
+} mq_node;
+
+typedef struct mq_tape_batch {
+  int32_t n_tapes;
+  const int64_t* tape_offsets;   /* [n_tapes+1]: tape t = nodes[tape_offsets[t] .. tape_offsets[t+1]) */
+  const mq_node* nodes;
+  const uint32_t* const_words;   /* pool shared by all tapes (MQ_OP_CONST.a indexes it) */
+  int64_t n_const_words;
+} mq_tape_batch;
+
+/* ------------------------------------------------------------------ candidate models
+ * One batch = M candidate models in global candidate order (0 = MRU), the z3 ModelRef
+ * contents serialized WITHOUT completion (support_utils.py:63 deep-copies because eval with
+ * completion mutates the model; absence is encoded as 0 / empty table here).
+ *   scalar variables: SoA, u32 limbs: var_words[(var_word_off[v] + limb) * n_models + m],
+ *                     var_word_off[v] = sum_{u<v} limbs(var_width[u]), limbs(0) = 1.
+ *   functions (UFs keccak256_<n>, keccak256_<n>-1, Power; array interpretations as-array):
+ *     function f, model m has entries [entry_ptr[f*(M+1)+m], entry_ptr[f*(M+1)+m+1]) of its
+ *     own list; entry e of f occupies words entry_words[entry_base[f] + e*stride_f ..] with
+ *     stride_f = sum_i limbs(arg_width[i]) + limbs(result_width): args first, then value.
+ *     else value of (f, m): else_words[else_base[f] + m*limbs(result_width) ..].
+ *     A function absent from a model has no entries and else value 0 (z3 completion).
+ */
+typedef struct mq_func_desc {
+  uint16_t arity;          /* 1 or 2 */
+  uint16_t result_width;   /* 0 = Bool */
+  uint16_t arg_width[2];
+} mq_func_desc;
+
+typedef struct mq_model_batch {
+  int64_t n_models;
+  int64_t index_base;              /* global candidate index of local model 0 (model-axis shard) */
+  int32_t n_vars;
+  const uint16_t* var_width;       /* [n_vars] */
+  const uint32_t* var_words;
+  int32_t n_funcs;
+  const mq_func_desc* funcs;       /* [n_funcs] */
+  const int64_t* entry_ptr;        /* [n_funcs * (n_models + 1)] */
+  const int64_t* entry_base;       /* [n_funcs] */
+  const uint32_t* entry_words;
+  int64_t n_entry_words;
+  const int64_t* else_base;        /* [n_funcs] */
+  const uint32_t* else_words;
+  int64_t n_else_words;
+} mq_model_batch;
+
+/* ------------------------------------------------------------------ statistics */
+typedef struct mq_stats {
+  double kernel_ms;        /* device time of the evaluation kernels (HIP events) */
+  double node_evals;       /* sum over evaluated (tape, model) pairs of |tape| nodes */
+  double alg_ops;          /* algorithmic 32-bit VALU ops (SURVEY §8(d) cost table) */
+  int64_t pairs_evaluated; /* (tape, model) pairs actually evaluated (early exit skips the rest) */
+  int32_t n_hits;
+  int32_t n_unsupported;
+} mq_stats;
+
+typedef struct mq_ctx mq_ctx;
+typedef struct mq_tapes mq_tapes;
+
+/* Create a context on device dev_ids[0] (one context per GPU; multi-GPU runs one process per
+   GPU and min-reduces first_hit over RCCL in the host layer).  n_dev must be 1. */
+int mq_ctx_create(int n_dev, const int* dev_ids, mq_ctx** out);
+void mq_ctx_destroy(mq_ctx* ctx);
+const char* mq_strerror(int code);
+
+/* Replace the candidate set (ModelCache contents, support_utils.py:56-58 / model.py:125). */
+int mq_models_upload(mq_ctx* ctx, const mq_model_batch* models);
+
+/* Compile + upload a tape batch once (the lowering of simplify(And(*constraints)).raw,
+   model.py:101); reusable across evaluations.  n_unsupported_out may be NULL. */
+int mq_tapes_upload(mq_ctx* ctx, const mq_tape_batch* batch, mq_tapes** out, int32_t* n_unsupported_out);
+void mq_tapes_free(mq_tapes* tapes);
+
+/* check_quick_sat over the batch (support_utils.py:60-67): first_hit_out[t] = smallest
+   global candidate index whose model satisfies tape t, MQ_NO_HIT, or MQ_UNSUPPORTED. */
+int mq_eval_first_hit(mq_ctx* ctx, const mq_tape_batch* batch, int32_t* first_hit_out, mq_stats* stats);
+int mq_eval_tapes_first_hit(mq_ctx* ctx, mq_tapes* tapes, int32_t* first_hit_out, mq_stats* stats);
+
+/* Asynchronous form for the multi-GPU path: writes int32 first_hit[n_tapes] to DEVICE memory
+   d_first_hit on HIP stream `stream` (NULL = context stream); INT32_MAX encodes "no hit" so a
+   min-allreduce over ranks combines shards; mq_finalize_first_hit maps it back to MQ_NO_HIT. */
+int mq_launch_first_hit(mq_ctx* ctx, mq_tapes* tapes, int32_t* d_first_hit, void* stream);
+int mq_finalize_first_hit(mq_ctx* ctx, mq_tapes* tapes, int32_t* d_first_hit, void* stream);
+
+/* Device work counters accumulated by every evaluation launch on this context since the last
+   reset: out[0] (tape, model) pairs evaluated, out[1] node-evals, out[2] algorithmic ops
+   (SURVEY §8(d)).  Synchronizes the context stream. */
+int mq_counters(mq_ctx* ctx, double* out3, int reset);
+
+/* Full verdict matrix for parity dumps: bit (t*M + m) of bits_out = tape t true on model m.
+   bits_out has ceil(n_tapes*M/8) bytes.  Unsupported tapes yield all-zero rows and are
+   reported through first_hit_out (may be NULL). */
+int mq_eval_verdicts(mq_ctx* ctx, const mq_tape_batch* batch, uint8_t* bits_out, int32_t* first_hit_out);
+
+/* Concrete keccak256 (Ethereum padding 0x01) of n messages on the GPU (keccak-f[1600] kernel);
+   message i = data[offsets[i] .. offsets[i+1]), digests_out = 32*n bytes.
+   Replaces eth_hash in sha3 (support_utils.py:92-100) / find_concrete_keccak (kfm.py:56-69). */
+int mq_keccak256(mq_ctx* ctx, const uint8_t* data, const int64_t* offsets, int32_t n, uint8_t* digests_out);
+
+/* Static algorithmic cost of a tape; -1 if malformed. */
+double mq_tape_alg_ops(const mq_tape_batch* batch, int32_t t);
+
+/* Host-only compile report for tape t (no device needed): *supported (0/1), limbs per value L
+   (8 or 16), register-stack depth, LDS temp slots, program words; reason (if unsupported) is
+   copied into why[why_len].  Returns 0 or MQ_ERR_ARG. */
+int mq_tape_compile_info(const mq_tape_batch* batch, int32_t t, int32_t* supported, int32_t* limbs,
+                         int32_t* depth, int32_t* n_temps, int32_t* prog_words, char* why, int32_t why_len);
+
+/* Library version string. */
+const char* mq_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MQ_H */

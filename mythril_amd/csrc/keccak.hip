@@ -1,0 +1,87 @@
+// keccak.hip — keccak256 (Ethereum padding 0x01..0x80, rate 136 B) on gfx950, one message
+// per lane, the 25-lane keccak-f[1600] state in 50 VGPRs (64-bit lanes as u32 pairs are
+// handled by the compiler's 64-bit shifts -> v_alignbit pairs).
+// Replaces eth_hash's keccak in mythril/support/support_utils.py:92-100 and
+// keccak_function_manager.py:56-69 (find_concrete_keccak) for batched concrete hashing.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "qs_launch.h"
+
+namespace mq {
+
+__constant__ uint64_t kRC[24] = {
+    0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808Aull, 0x8000000080008000ull,
+    0x000000000000808Bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
+    0x000000000000008Aull, 0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000Aull,
+    0x000000008000808Bull, 0x800000000000008Bull, 0x8000000000008089ull, 0x8000000000008003ull,
+    0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800Aull, 0x800000008000000Aull,
+    0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
+
+__device__ __forceinline__ uint64_t rol(uint64_t v, int n) { return n ? (v << n) | (v >> (64 - n)) : v; }
+
+__device__ __forceinline__ void keccak_f(uint64_t (&A)[25]) {
+  constexpr int R[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
+  for (int r = 0; r < 24; r++) {
+    uint64_t C[5], Dd[5], B[25];
+#pragma unroll
+    for (int x = 0; x < 5; x++) C[x] = A[x] ^ A[x + 5] ^ A[x + 10] ^ A[x + 15] ^ A[x + 20];
+#pragma unroll
+    for (int x = 0; x < 5; x++) Dd[x] = C[(x + 4) % 5] ^ rol(C[(x + 1) % 5], 1);
+#pragma unroll
+    for (int i = 0; i < 25; i++) A[i] ^= Dd[i % 5];
+#pragma unroll
+    for (int x = 0; x < 5; x++)
+#pragma unroll
+      for (int y = 0; y < 5; y++) B[y + 5 * ((2 * x + 3 * y) % 5)] = rol(A[x + 5 * y], R[x + 5 * y]);
+#pragma unroll
+    for (int y = 0; y < 5; y++)
+#pragma unroll
+      for (int x = 0; x < 5; x++) A[x + 5 * y] = B[x + 5 * y] ^ ((~B[(x + 1) % 5 + 5 * y]) & B[(x + 2) % 5 + 5 * y]);
+    A[0] ^= kRC[r];
+  }
+}
+
+__global__ __launch_bounds__(64) void keccak256_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ off,
+                                                       int n, uint8_t* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t beg = off[i], len = off[i + 1] - off[i];
+  const uint8_t* msg = data + beg;
+  uint64_t A[25];
+#pragma unroll
+  for (int k = 0; k < 25; k++) A[k] = 0;
+  int64_t pos = 0;
+  bool done = false;
+  while (!done) {
+    // absorb one 136-byte block (17 lanes), padding in the final block
+#pragma unroll
+    for (int w = 0; w < 17; w++) {
+      uint64_t lane = 0;
+#pragma unroll
+      for (int b = 0; b < 8; b++) {
+        const int64_t p = pos + 8 * w + b;
+        uint64_t byte = 0;
+        if (p < len) byte = msg[p];
+        else if (p == len) byte = 0x01;
+        if (8 * w + b == 135 && pos + 136 > len) byte |= 0x80;
+        lane |= byte << (8 * b);
+      }
+      A[w] ^= lane;
+    }
+    keccak_f(A);
+    if (pos + 136 > len) done = true;
+    pos += 136;
+  }
+#pragma unroll
+  for (int w = 0; w < 4; w++)
+#pragma unroll
+    for (int b = 0; b < 8; b++) out[(int64_t)i * 32 + 8 * w + b] = (uint8_t)(A[w] >> (8 * b));
+}
+
+hipError_t launch_keccak(const uint8_t* data, const int64_t* offsets, int n, uint8_t* out, hipStream_t st) {
+  hipLaunchKernelGGL(keccak256_kernel, dim3((n + 63) / 64), dim3(64), 0, st, data, offsets, n, out);
+  return hipGetLastError();
+}
+
+}  // namespace mq

@@ -1,0 +1,39 @@
+// tape_compiler.h — boundary tape (mq.h DAG) -> GPU stack program (gprog.h).
+#ifndef MQ_TAPE_COMPILER_H
+#define MQ_TAPE_COMPILER_H
+#include <stdint.h>
+#include <string>
+#include <vector>
+#include "../../include/mq.h"
+#include "gprog.h"
+
+namespace mq {
+
+struct CompiledTape {
+  bool supported = false;
+  std::string why;               // reason when unsupported
+  int L = 0;                     // limbs per value (8 or 16)
+  int depth = 0;                 // max stack slots used
+  int n_temps = 0;               // LDS temp slots
+  std::vector<uint32_t> prog;    // instruction words, terminated by G_END
+  std::vector<uint32_t> consts;  // L-limb padded constants (PUSH_CONST imm indexes this)
+  uint32_t n_nodes = 0;          // DAG size of the boundary tape (metric)
+  double alg_ops = 0;            // SURVEY §8(d) algorithmic cost per model
+};
+
+struct CompileLimits {
+  int max_depth_l8 = 8;
+  int max_depth_l16 = 6;
+  int max_temps_l8 = 16;
+  int max_temps_l16 = 8;
+};
+
+// Compile tape t of the batch. n_funcs/funcs describe the model function table (result
+// widths); pass n_funcs = -1 when unknown (UF widths are then taken from the nodes).
+CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLimits& lim);
+
+// SURVEY §8(d) algorithmic 32-bit op cost of one evaluation of tape t; -1 if malformed.
+double tape_alg_ops(const mq_tape_batch* batch, int32_t t);
+
+}  // namespace mq
+#endif

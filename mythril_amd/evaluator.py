@@ -1,0 +1,231 @@
+"""ctypes binding of libmq.so — the MI355X quick-sat evaluator (include/mq.h).
+
+This is the product path: there is no CPU fallback.  If ``libmq.so`` is missing or no
+gfx950 device is present, constructing :class:`Evaluator` raises :class:`EvaluatorError`
+(the ``get_model`` adapter then keeps the reference behaviour of going to z3 — it never
+evaluates tapes on the CPU).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from ._abi import MqModelBatch, MqStats, MqTapeBatch, as_model_batch, as_tape_batch
+from .models import ModelBatch
+from .tape import TapeBatch
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmq.so")
+NO_HIT = -1
+UNSUPPORTED = -2
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+class EvaluatorError(RuntimeError):
+    pass
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libmq.so (built in-tree by ``python -m mythril_amd.build``); raises if absent."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise EvaluatorError(f"{path} not built: run `python -m mythril_amd.build` (hipcc, gfx950)")
+        L = C.CDLL(path)
+        P = C.c_void_p
+        L.mq_version.restype = C.c_char_p
+        L.mq_strerror.argtypes = [C.c_int]
+        L.mq_strerror.restype = C.c_char_p
+        L.mq_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_int), C.POINTER(P)]
+        L.mq_ctx_destroy.argtypes = [P]
+        L.mq_ctx_destroy.restype = None
+        L.mq_models_upload.argtypes = [P, C.POINTER(MqModelBatch)]
+        L.mq_tapes_upload.argtypes = [P, C.POINTER(MqTapeBatch), C.POINTER(P), C.POINTER(C.c_int32)]
+        L.mq_tapes_free.argtypes = [P]
+        L.mq_tapes_free.restype = None
+        L.mq_eval_first_hit.argtypes = [P, C.POINTER(MqTapeBatch), C.POINTER(C.c_int32), C.POINTER(MqStats)]
+        L.mq_eval_tapes_first_hit.argtypes = [P, P, C.POINTER(C.c_int32), C.POINTER(MqStats)]
+        L.mq_launch_first_hit.argtypes = [P, P, P, P]
+        L.mq_finalize_first_hit.argtypes = [P, P, P, P]
+        L.mq_counters.argtypes = [P, C.POINTER(C.c_double), C.c_int]
+        L.mq_eval_verdicts.argtypes = [P, C.POINTER(MqTapeBatch), C.POINTER(C.c_uint8), C.POINTER(C.c_int32)]
+        L.mq_keccak256.argtypes = [P, C.POINTER(C.c_uint8), C.POINTER(C.c_int64), C.c_int32, C.POINTER(C.c_uint8)]
+        L.mq_tape_alg_ops.argtypes = [C.POINTER(MqTapeBatch), C.c_int32]
+        L.mq_tape_alg_ops.restype = C.c_double
+        L.mq_tape_compile_info.argtypes = [C.POINTER(MqTapeBatch), C.c_int32] + [C.POINTER(C.c_int32)] * 5 + [C.c_char_p, C.c_int32]
+        _lib = L
+        return L
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load_library().mq_strerror(rc).decode()
+        raise EvaluatorError(f"{what}: {msg} ({rc})")
+
+
+@dataclass
+class EvalStats:
+    kernel_ms: float
+    node_evals: float
+    alg_ops: float
+    pairs_evaluated: int
+    n_hits: int
+    n_unsupported: int
+
+
+@dataclass
+class CompileInfo:
+    supported: bool
+    limbs: int
+    depth: int
+    n_temps: int
+    prog_words: int
+    why: str
+
+
+def compile_info(tb: TapeBatch, t: int) -> CompileInfo:
+    """Host-only report of how tape t compiles (no GPU needed)."""
+    L = load_library()
+    s, keep = as_tape_batch(tb)
+    vals = [C.c_int32() for _ in range(5)]
+    why = C.create_string_buffer(256)
+    _check(L.mq_tape_compile_info(C.byref(s), t, *[C.byref(v) for v in vals], why, 256), "compile_info")
+    return CompileInfo(bool(vals[0].value), vals[1].value, vals[2].value, vals[3].value, vals[4].value, why.value.decode())
+
+
+def tape_alg_ops(tb: TapeBatch, t: int) -> float:
+    s, keep = as_tape_batch(tb)
+    return float(load_library().mq_tape_alg_ops(C.byref(s), t))
+
+
+class CompiledTapes:
+    """A tape batch compiled and resident on the device (``mq_tapes``)."""
+
+    def __init__(self, ev: "Evaluator", tb: TapeBatch):
+        self.ev = ev
+        self.n_tapes = tb.n_tapes
+        self.node_counts = tb.sizes()
+        s, keep = as_tape_batch(tb)
+        h = C.c_void_p()
+        nu = C.c_int32()
+        _check(ev.lib.mq_tapes_upload(ev.ctx, C.byref(s), C.byref(h), C.byref(nu)), "mq_tapes_upload")
+        self.handle = h
+        self.n_unsupported = nu.value
+
+    def free(self) -> None:
+        if self.handle:
+            self.ev.lib.mq_tapes_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Evaluator:
+    """One evaluator context per GPU (one process per GPU for multi-GPU runs)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        ctx = C.c_void_p()
+        dev = C.c_int(device)
+        _check(self.lib.mq_ctx_create(1, C.byref(dev), C.byref(ctx)), "mq_ctx_create")
+        self.ctx = ctx
+        self.device = device
+        self.n_models = 0
+        self.index_base = 0
+
+    def close(self) -> None:
+        if getattr(self, "ctx", None):
+            self.lib.mq_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------ models
+    def upload_models(self, mb: ModelBatch) -> None:
+        s, keep = as_model_batch(mb)
+        _check(self.lib.mq_models_upload(self.ctx, C.byref(s)), "mq_models_upload")
+        self.n_models = mb.n_models
+        self.index_base = mb.index_base
+
+    # ------------------------------------------------------------ tapes
+    def compile(self, tb: TapeBatch) -> CompiledTapes:
+        return CompiledTapes(self, tb)
+
+    def first_hit(self, tapes, with_stats: bool = False):
+        """check_quick_sat over a batch: int32[N] of global candidate indices / -1 / -2."""
+        own = not isinstance(tapes, CompiledTapes)
+        ct = self.compile(tapes) if own else tapes
+        out = np.zeros(ct.n_tapes, np.int32)
+        st = MqStats()
+        try:
+            _check(self.lib.mq_eval_tapes_first_hit(self.ctx, ct.handle, out.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(st)),
+                   "mq_eval_tapes_first_hit")
+        finally:
+            if own:
+                ct.free()
+        if with_stats:
+            return out, EvalStats(st.kernel_ms, st.node_evals, st.alg_ops, st.pairs_evaluated, st.n_hits, st.n_unsupported)
+        return out
+
+    def launch_first_hit(self, ct: CompiledTapes, device_ptr: int, stream: int = 0) -> None:
+        """Async: int32 first-hit (INT32_MAX = none) into device memory on a HIP stream."""
+        _check(self.lib.mq_launch_first_hit(self.ctx, ct.handle, C.c_void_p(device_ptr), C.c_void_p(stream or None)),
+               "mq_launch_first_hit")
+
+    def finalize_first_hit(self, ct: CompiledTapes, device_ptr: int, stream: int = 0) -> None:
+        _check(self.lib.mq_finalize_first_hit(self.ctx, ct.handle, C.c_void_p(device_ptr), C.c_void_p(stream or None)),
+               "mq_finalize_first_hit")
+
+    def counters(self, reset: bool = False):
+        """(pairs evaluated, node-evals, algorithmic ops) accumulated on the device."""
+        out = (C.c_double * 3)()
+        _check(self.lib.mq_counters(self.ctx, out, 1 if reset else 0), "mq_counters")
+        return float(out[0]), float(out[1]), float(out[2])
+
+    def verdicts(self, tb: TapeBatch):
+        """Full N x M verdict matrix (bool) and first-hit (parity dumps)."""
+        n = tb.n_tapes * self.n_models
+        bits = np.zeros((n + 7) // 8, np.uint8)
+        fh = np.zeros(tb.n_tapes, np.int32)
+        s, keep = as_tape_batch(tb)
+        _check(self.lib.mq_eval_verdicts(self.ctx, C.byref(s), bits.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                         fh.ctypes.data_as(C.POINTER(C.c_int32))), "mq_eval_verdicts")
+        v = np.unpackbits(bits, bitorder="little")[:n].reshape(tb.n_tapes, self.n_models).astype(bool)
+        return v, fh
+
+    # ------------------------------------------------------------ keccak
+    def keccak256(self, messages: Sequence[bytes]) -> List[bytes]:
+        msgs = [bytes(m) for m in messages]
+        offs = np.zeros(len(msgs) + 1, np.int64)
+        offs[1:] = np.cumsum([len(m) for m in msgs])
+        data = np.frombuffer(b"".join(msgs) or b"\0", dtype=np.uint8).copy()
+        out = np.zeros(32 * len(msgs), np.uint8)
+        _check(self.lib.mq_keccak256(self.ctx, data.ctypes.data_as(C.POINTER(C.c_uint8)), offs.ctypes.data_as(C.POINTER(C.c_int64)),
+                                     len(msgs), out.ctypes.data_as(C.POINTER(C.c_uint8))), "mq_keccak256")
+        return [bytes(out[32 * i:32 * i + 32]) for i in range(len(msgs))]
+
+
+_default: Optional[Evaluator] = None
+
+
+def default_evaluator() -> Evaluator:
+    global _default
+    if _default is None:
+        _default = Evaluator(int(os.environ.get("LOCAL_RANK", "0")))
+    return _default

@@ -1,0 +1,267 @@
+"""Seeded synthetic workloads, all RNG = numpy PCG64 with committed seeds.
+
+* ``c2_workload``  — config C2: N tapes of ~64 DAG nodes over {ADD, MUL, AND, EQ, ULT}
+  with a Bool-AND root over 4 comparisons, V = 8 free 256-bit vars, M i.i.d. uniform
+  256-bit models; 10 % of the tapes have ONE planted satisfying model at a uniformly random
+  index (they contain an EQ so no other model satisfies them w.p. 1-2^-256·M), the other
+  90 % are unsatisfiable against every model (no early exit: the worst case).
+* ``fuzz_tape``    — random well-sorted tapes over the whole op vocabulary and mixed widths
+  (parity tests).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .models import FuncSpec, ModelBatch
+from .tape import BOOL, Op, Tape, TapeBatch, limbs
+
+M256 = (1 << 256) - 1
+
+
+def random_words(rng: np.random.Generator, n_rows: int, n_models: int) -> np.ndarray:
+    return rng.integers(0, 1 << 32, size=(n_rows, n_models), dtype=np.uint64).astype(np.uint32)
+
+
+def _model_value(words: np.ndarray, v: int, m: int, nl: int = 8) -> int:
+    col = words[v * nl:(v + 1) * nl, m]
+    return sum(int(x) << (32 * i) for i, x in enumerate(col))
+
+
+# ---------------------------------------------------------------- C2
+class _C2Expr:
+    """Random expression tree over {ADD, MUL, AND} returned as (tape node, python value fn)."""
+
+    def __init__(self, rng: np.random.Generator, tape: Tape, n_vars: int, vals: Sequence[int]):
+        self.rng, self.t, self.n_vars, self.vals = rng, tape, n_vars, vals
+
+    def leaf(self) -> Tuple[int, int]:
+        if self.rng.random() < 0.7:
+            v = int(self.rng.integers(self.n_vars))
+            return self.t.var(v, 256), self.vals[v]
+        c = int.from_bytes(self.rng.bytes(32), "little")
+        return self.t.const(c, 256), c
+
+    def tree(self, n_ops: int) -> Tuple[int, int]:
+        if n_ops == 0:
+            return self.leaf()
+        left = int(self.rng.integers(0, n_ops))
+        a, va = self.tree(left)
+        b, vb = self.tree(n_ops - 1 - left)
+        op = self.rng.choice(3, p=[0.4, 0.25, 0.35])
+        if op == 0:
+            return self.t.add(a, b), (va + vb) & M256
+        if op == 1:
+            return self.t.mul(a, b), (va * vb) & M256
+        return self.t.band(a, b), va & vb
+
+
+def c2_tape(rng: np.random.Generator, planted_vals: Optional[Sequence[int]], n_vars: int = 8,
+            n_cmp: int = 4, ops_per_side: int = 6) -> Tape:
+    t = Tape()
+    vals = planted_vals if planted_vals is not None else [0] * n_vars
+    gen = _C2Expr(rng, t, n_vars, vals)
+    cmps = []
+    for i in range(n_cmp):
+        a, va = gen.tree(ops_per_side)
+        b, vb = gen.tree(ops_per_side - 1)
+        kind = "eq" if i == 0 else ("eq" if rng.random() < 0.3 else "ult")
+        if kind == "eq":
+            # EQ(a, b + c): planted -> c = a(p) - b(p); else c uniform (unsat w.p. ~1)
+            if planted_vals is not None:
+                c = (va - vb) & M256
+            else:
+                c = int.from_bytes(rng.bytes(32), "little")
+            cmps.append(t.eq(a, t.add(b, t.const(c, 256))))
+        else:
+            if planted_vals is not None and not va < vb:
+                a, b = b, a
+            cmps.append(t.ult(a, b))
+    return t.finish(t.and_(*cmps))
+
+
+def c2_workload(n_tapes: int = 10_000, n_models: int = 100_000, seed: int = 2,
+                planted_frac: float = 0.1, n_vars: int = 8) -> Tuple[TapeBatch, ModelBatch, np.ndarray]:
+    """Returns (tapes, models, expected_first_hit) — expected is exact for planted tapes and -1
+    for the rest (holds w.p. 1 - O(M·2^-256)); tests confirm it with the oracle at small M."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    words = random_words(rng, 8 * n_vars, n_models)
+    tapes: List[Tape] = []
+    expected = np.full(n_tapes, -1, np.int32)
+    planted = rng.random(n_tapes) < planted_frac
+    for i in range(n_tapes):
+        if planted[i]:
+            p = int(rng.integers(n_models))
+            vals = [_model_value(words, v, p) for v in range(n_vars)]
+            tapes.append(c2_tape(rng, vals, n_vars))
+            expected[i] = p
+        else:
+            tapes.append(c2_tape(rng, None, n_vars))
+    models = ModelBatch([256] * n_vars, words)
+    return TapeBatch(tapes), models, expected
+
+
+# ---------------------------------------------------------------- fuzz (parity)
+_BV_BIN = [Op.ADD, Op.SUB, Op.MUL, Op.UDIV, Op.UREM, Op.SDIV, Op.SREM, Op.SMOD,
+           Op.BAND, Op.BOR, Op.BXOR, Op.SHL, Op.LSHR, Op.ASHR]
+_PRED = [Op.EQ, Op.ULT, Op.ULE, Op.SLT, Op.SLE, Op.UMUL_NOOVFL, Op.SMUL_NOOVFL, Op.SMUL_NOUDFL]
+
+
+def interesting_value(rng: np.random.Generator, w: int) -> int:
+    m = (1 << w) - 1
+    r = rng.random()
+    if r < 0.15:
+        return int(rng.choice([0, 1, 2, m, m - 1, 1 << (w - 1), (1 << (w - 1)) - 1, w, w - 1, w + 1])) & m if w > 1 else int(rng.integers(2))
+    if r < 0.3:
+        return int(rng.integers(0, 64)) & m
+    nbytes = (w + 7) // 8
+    return int.from_bytes(rng.bytes(nbytes), "little") & m
+
+
+def fuzz_models(rng: np.random.Generator, var_widths: Sequence[int], n_models: int,
+                funcs: Sequence[FuncSpec] = (), entries_per_model: int = 3,
+                key_pool: Optional[dict] = None) -> ModelBatch:
+    models = []
+    for m in range(n_models):
+        d = {"vars": {}, "funcs": {}}
+        for v, w in enumerate(var_widths):
+            if rng.random() < 0.9:
+                d["vars"][v] = interesting_value(rng, w) if w else int(rng.integers(2))
+        for f, spec in enumerate(funcs):
+            if rng.random() < 0.1:
+                continue  # function absent from this model -> completion default
+            table = {}
+            for _ in range(int(rng.integers(0, entries_per_model + 1))):
+                pool = (key_pool or {}).get(f)
+                if pool and rng.random() < 0.6:
+                    args = pool[int(rng.integers(len(pool)))]
+                else:
+                    args = tuple(interesting_value(rng, aw) for aw in spec.arg_widths)
+                table[args] = interesting_value(rng, spec.result_width) if spec.result_width else int(rng.integers(2))
+            els = interesting_value(rng, spec.result_width) if spec.result_width else int(rng.integers(2))
+            d["funcs"][f] = (table, els)
+        models.append(d)
+    return ModelBatch.from_python(var_widths, models, funcs)
+
+
+class _Fuzz:
+    def __init__(self, rng, tape: Tape, var_widths, funcs, max_width: int, ops=None):
+        self.rng, self.t, self.vw, self.funcs, self.maxw = rng, tape, var_widths, funcs, max_width
+        self.ops = set(ops) if ops is not None else None
+        self.pool = {}  # width -> list of bv nodes
+
+    def allowed(self, op):
+        return self.ops is None or op in self.ops
+
+    def bv_leaf(self, w: int) -> int:
+        cands = [v for v, vw in enumerate(self.vw) if vw == w]
+        if cands and self.rng.random() < 0.6:
+            return self.t.var(int(self.rng.choice(cands)), w)
+        return self.t.const(interesting_value(self.rng, w), w)
+
+    def bv(self, w: int, depth: int) -> int:
+        rng, t = self.rng, self.t
+        if depth <= 0 or rng.random() < 0.2:
+            return self.bv_leaf(w)
+        r = rng.random()
+        if r < 0.45:
+            op = _BV_BIN[int(rng.integers(len(_BV_BIN)))]
+            if not self.allowed(op):
+                return self.bv_leaf(w)
+            a = self.bv(w, depth - 1)
+            if op in (Op.SHL, Op.LSHR, Op.ASHR) and rng.random() < 0.6:
+                b = t.const(int(rng.integers(0, w + 3)) & ((1 << w) - 1), w)
+            else:
+                b = self.bv(w, depth - 1)
+            return t._bin(op, a, b)
+        if r < 0.55 and self.allowed(Op.NEG):
+            x = self.bv(w, depth - 1)
+            return t.neg(x) if rng.random() < 0.5 else (t.bnot(x) if self.allowed(Op.BNOT) else x)
+        if r < 0.65 and self.allowed(Op.ITE):
+            return t.ite(self.boolean(depth - 1), self.bv(w, depth - 1), self.bv(w, depth - 1))
+        if r < 0.75 and self.allowed(Op.EXTRACT):
+            src_w = min(self.maxw, w + int(rng.integers(0, 64)))
+            lo = int(rng.integers(0, src_w - w + 1))
+            return t.extract(lo + w - 1, lo, self.bv(src_w, depth - 1))
+        if r < 0.83 and w >= 2 and self.allowed(Op.CONCAT):
+            hw = int(rng.integers(1, w))
+            return t.concat(self.bv(hw, depth - 1), self.bv(w - hw, depth - 1))
+        if r < 0.90 and w >= 2 and self.allowed(Op.ZEXT):
+            k = int(rng.integers(1, w))
+            x = self.bv(w - k, depth - 1)
+            return t.zext(k, x) if rng.random() < 0.5 else t.sext(k, x)
+        if r < 0.96 and self.funcs and self.allowed(Op.UF):
+            cands = [f for f, s in enumerate(self.funcs) if s.result_width == w]
+            if cands:
+                f = int(rng.choice(cands))
+                spec = self.funcs[f]
+                if spec.arity == 1 and rng.random() < 0.5 and self.allowed(Op.SELECT):
+                    arr = t.array_var(f, w)
+                    for _ in range(int(rng.integers(0, 3))):
+                        arr = t.store(arr, self.bv(spec.arg_widths[0], depth - 2), self.bv(w, depth - 2))
+                    return t.select(arr, self.bv(spec.arg_widths[0], depth - 1))
+                args = [self.bv(aw, depth - 1) for aw in spec.arg_widths]
+                return t.uf(f, w, *args)
+        if self.allowed(Op.SELECT) and self.allowed(Op.CONST_ARRAY) and rng.random() < 0.5:
+            kw = int(rng.choice([8, 32, 256])) if self.maxw >= 256 else 8
+            arr = t.const_array(self.bv(w, depth - 2))
+            for _ in range(int(rng.integers(1, 3))):
+                arr = t.store(arr, self.bv(kw, depth - 2), self.bv(w, depth - 2))
+            return t.select(arr, self.bv(kw, depth - 1))
+        return self.bv_leaf(w)
+
+    def boolean(self, depth: int) -> int:
+        rng, t = self.rng, self.t
+        if depth <= 0:
+            return t.true() if rng.random() < 0.5 else t.false()
+        r = rng.random()
+        if r < 0.55:
+            op = _PRED[int(rng.integers(len(_PRED)))]
+            if not self.allowed(op):
+                op = Op.EQ
+            w = int(rng.choice([w for w in (1, 8, 32, 64, 160, 256, 512) if w <= self.maxw]))
+            a = self.bv(w, depth - 1)
+            b = self.bv(w, depth - 1) if rng.random() < 0.7 else a
+            if op == Op.EQ and rng.random() < 0.3:
+                b = a  # force some true EQs
+            return t._pred(op, a, b)
+        if r < 0.75:
+            return t.and_(self.boolean(depth - 1), self.boolean(depth - 1))
+        if r < 0.85:
+            return t.or_(self.boolean(depth - 1), self.boolean(depth - 1))
+        if r < 0.90:
+            return t.not_(self.boolean(depth - 1))
+        if r < 0.93:
+            return t.xor(self.boolean(depth - 1), self.boolean(depth - 1))
+        if r < 0.95:
+            return t.implies(self.boolean(depth - 1), self.boolean(depth - 1))
+        if r < 0.97:
+            return t.iff(self.boolean(depth - 1), self.boolean(depth - 1))
+        bvars = [v for v, w in enumerate(self.vw) if w == BOOL]
+        if bvars and rng.random() < 0.5:
+            return t.var(int(rng.choice(bvars)), BOOL)
+        return t.bite(self.boolean(depth - 1), self.boolean(depth - 1), self.boolean(depth - 1))
+
+
+def fuzz_tape(rng: np.random.Generator, var_widths: Sequence[int], funcs: Sequence[FuncSpec] = (),
+              depth: int = 4, max_width: int = 256, ops=None) -> Tape:
+    t = Tape()
+    fz = _Fuzz(rng, t, var_widths, funcs, max_width, ops)
+    root = fz.boolean(depth)
+    return t.finish(root)
+
+
+def fuzz_workload(seed: int, n_tapes: int, n_models: int, max_width: int = 256, depth: int = 4,
+                  with_funcs: bool = True, ops=None):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    widths = [w for w in (1, 8, 32, 64, 160, 256, 512) if w <= max_width]
+    var_widths = [int(rng.choice(widths)) for _ in range(10)] + [256, 256, BOOL, 8]
+    funcs: List[FuncSpec] = []
+    if with_funcs:
+        funcs = [FuncSpec(1, 256, (256,)), FuncSpec(1, 8, (256,)), FuncSpec(2, 256, (256, 256))]
+        if max_width >= 512:
+            funcs.append(FuncSpec(1, 256, (512,)))
+    tapes = [fuzz_tape(rng, var_widths, funcs, depth, max_width, ops) for _ in range(n_tapes)]
+    models = fuzz_models(rng, var_widths, n_models, funcs)
+    return TapeBatch(tapes), models

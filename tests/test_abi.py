@@ -1,0 +1,99 @@
+"""CPU tests of the C-ABI boundary: libmq.so loads, exports every symbol include/mq.h declares,
+the Python opcode/struct mirrors match the header, and the host-side tape compiler (no GPU)
+produces the expected programs."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from mythril_amd import evaluator
+from mythril_amd._abi import MqFuncDesc, MqModelBatch, MqNode, MqStats, MqTapeBatch
+from mythril_amd.synth import c2_workload, fuzz_workload
+from mythril_amd.tape import Op, Tape, TapeBatch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = open(os.path.join(ROOT, "include", "mq.h")).read()
+
+
+def test_library_exports_every_declared_symbol():
+    lib = evaluator.load_library()
+    declared = re.findall(r"^\s*(?:int|void|double|const char\*)\s+(mq_\w+)\s*\(", HEADER, re.M)
+    assert len(declared) >= 14
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.mq_version().startswith(b"mq ")
+    assert lib.mq_strerror(-1) == b"invalid argument"
+
+
+def test_opcodes_match_header():
+    hdr = dict((m[0], int(m[1])) for m in re.findall(r"MQ_OP_(\w+)\s*=\s*(\d+)", HEADER))
+    assert hdr == {op.name: int(op) for op in Op}
+
+
+def test_struct_layouts():
+    assert ctypes.sizeof(MqNode) == 16
+    assert ctypes.sizeof(MqFuncDesc) == 8
+    assert ctypes.sizeof(MqTapeBatch) == 40
+    assert ctypes.sizeof(MqModelBatch) == 112
+    assert ctypes.sizeof(MqStats) == 40
+
+
+def test_ctx_create_without_gpu_fails_loudly():
+    """No CPU fallback: with no gfx950 device the evaluator refuses to exist."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(evaluator.EvaluatorError):
+        evaluator.Evaluator(0)
+
+
+def test_compile_c2_tapes():
+    tb, mb, exp = c2_workload(50, 100, seed=2)
+    for t in range(tb.n_tapes):
+        ci = evaluator.compile_info(tb, t)
+        assert ci.supported, ci.why
+        assert ci.limbs == 8
+        assert 2 <= ci.depth <= 8
+        assert ci.n_temps <= 4  # hash-consing shares repeated subterms
+        assert evaluator.tape_alg_ops(tb, t) > 0
+
+
+def test_compile_fuzz_tapes_mostly_supported():
+    for seed, mw in ((0, 256), (1, 512)):
+        tb, mb = fuzz_workload(seed, 60, 4, max_width=mw)
+        infos = [evaluator.compile_info(tb, t) for t in range(tb.n_tapes)]
+        sup = [i for i in infos if i.supported]
+        assert len(sup) >= 0.9 * len(infos), [i.why for i in infos if not i.supported]
+        assert all(i.limbs == (8 if mw == 256 else i.limbs) for i in sup)
+
+
+def test_compile_rejects_what_it_cannot_do():
+    t = Tape()
+    x = t.var(0, 1024)
+    tb = TapeBatch([t.finish(t.eq(x, t.const(3, 1024)))])
+    ci = evaluator.compile_info(tb, 0)
+    assert not ci.supported and "512" in ci.why
+    t = Tape()
+    k = t.keccak(t.var(0, 512))
+    tb = TapeBatch([t.finish(t.eq(k, t.const(3, 256)))])
+    assert not evaluator.compile_info(tb, 0).supported
+
+
+def test_shared_subterms_use_temps():
+    t = Tape()
+    a = t.mul(t.var(0, 256), t.var(1, 256))
+    root = t.and_(t.ult(a, t.const(5, 256)), t.eq(t.add(a, a), t.const(6, 256)))
+    tb = TapeBatch([t.finish(root)])
+    ci = evaluator.compile_info(tb, 0)
+    assert ci.supported and ci.n_temps == 1
+
+
+def test_alg_ops_cost_table():
+    """add = L, mul = L(L+1), eq = L, bool and = 1 (L = 8 at 256 bits)."""
+    t = Tape()
+    x, y = t.var(0, 256), t.var(1, 256)
+    root = t.and_(t.eq(t.add(x, y), t.mul(x, y)), t.ult(x, y))
+    tb = TapeBatch([t.finish(root)])
+    assert evaluator.tape_alg_ops(tb, 0) == 8 + 72 + 8 + 8 + 1

@@ -1,0 +1,165 @@
+"""CPU tests: the oracle (oracle/pyoracle.py + oracle/cref.c) pinned against the reference's
+own vectors (tests/golden) and against hand-derived SMT-LIB 2.6 edge cases, plus the
+Python-spec <-> C restatement agreement on fuzzed tapes."""
+import numpy as np
+import pytest
+
+import cref
+import keccak_ref
+import pyoracle
+from golden_util import check_tape, fixture_tape, load
+from mythril_amd.models import ModelBatch
+from mythril_amd.synth import c2_workload, fuzz_workload
+from mythril_amd.tape import NODE_DTYPE, Tape, TapeBatch
+
+EMPTY_MODELS = ModelBatch([], np.zeros((0, 1), np.uint32))
+
+
+def _value(entry):
+    nodes = np.array([tuple(r) for r in entry["nodes"]], dtype=NODE_DTYPE)
+    vals = pyoracle.eval_nodes(nodes, np.asarray(entry["consts"], np.uint32), EMPTY_MODELS, 0)
+    return vals[entry["value_node"]]
+
+
+@pytest.mark.parametrize("entry", load("shift_vectors.json"), ids=lambda e: e["name"])
+def test_shift_vectors_pyoracle(entry):
+    assert _value(entry) == int(entry["expected"], 16)
+
+
+def test_shift_vectors_count():
+    sv = load("shift_vectors.json")
+    assert sum(e["op"] == "shl" for e in sv) == 11
+    assert sum(e["op"] == "shr" for e in sv) == 11
+    assert sum(e["op"] == "sar" for e in sv) == 16
+
+
+@pytest.mark.parametrize("entry", load("vmtests_kats.json"), ids=lambda e: e["name"])
+def test_vmtests_pyoracle(entry):
+    assert _value(entry) == int(entry["expected"], 16)
+
+
+def test_golden_through_cref():
+    """Same fixtures through the C restatement, as Bool tapes EQ(value, expected) (+ negative)."""
+    entries = load("shift_vectors.json") + load("vmtests_kats.json")
+    tapes = []
+    for e in entries:
+        exp = int(e["expected"], 16)
+        tapes.append(check_tape(e, exp))
+        tapes.append(check_tape(e, exp, negate=True))
+    tb = TapeBatch(tapes)
+    mb = ModelBatch([8], np.zeros((1, 1), np.uint32))
+    v = cref.verdicts(tb, mb)[:, 0]
+    assert v[0::2].all(), [entries[i]["name"] for i in np.flatnonzero(~v[0::2])]
+    assert not v[1::2].any()
+
+
+@pytest.mark.parametrize("entry", load("keccak_kats.json"), ids=lambda e: e["name"])
+def test_keccak_kats(entry):
+    data = bytes.fromhex(entry["data"])
+    assert keccak_ref.keccak256(data).hex() == entry["digest"]
+    assert cref.keccak256(data).hex() == entry["digest"]
+
+
+def test_keccak_permutation_vs_hashlib():
+    import hashlib
+    for n in (0, 1, 135, 136, 137, 272, 1000):
+        d = bytes((i * 7 + 3) & 0xFF for i in range(n))
+        assert keccak_ref.sha3_256(d) == hashlib.sha3_256(d).digest()
+        assert cref.keccak256(d) == keccak_ref.keccak256(d)
+
+
+# ---------------------------------------------------------------- SMT-LIB 2.6 edge vectors
+# (op, width, a, b, expected) — values derived from the SMT-LIB FixedSizeBitVectors definitions
+# (bvudiv/bvurem by zero, signed division rounding, smod sign of divisor, shifts >= width).
+W4 = [
+    ("udiv", 4, 5, 0, 0xF), ("urem", 4, 5, 0, 5), ("udiv", 4, 13, 4, 3), ("urem", 4, 13, 4, 1),
+    ("sdiv", 4, 0x9, 2, 0xD),      # -7 / 2 = -3
+    ("srem", 4, 0x9, 2, 0xF),      # -7 rem 2 = -1
+    ("smod", 4, 0x9, 2, 0x1),      # -7 mod 2 = 1
+    ("smod", 4, 7, 0xE, 0xF),      # 7 mod -2 = -1
+    ("smod", 4, 0x9, 0xE, 0xF),    # -7 mod -2 = -1
+    ("sdiv", 4, 0x8, 0xF, 0x8),    # -8 / -1 overflows to -8
+    ("sdiv", 4, 0x9, 0, 0x1),      # negative / 0 = 1
+    ("sdiv", 4, 0x7, 0, 0xF),      # positive / 0 = -1
+    ("srem", 4, 0x9, 0, 0x9), ("smod", 4, 0x9, 0, 0x9),
+    ("shl", 4, 0x3, 4, 0), ("shl", 4, 0x3, 3, 0x8), ("lshr", 4, 0xF, 5, 0), ("ashr", 4, 0x8, 1, 0xC),
+    ("ashr", 4, 0x8, 9, 0xF), ("ashr", 4, 0x7, 9, 0x0),
+    ("add", 4, 0xF, 1, 0), ("sub", 4, 0, 1, 0xF), ("mul", 4, 7, 3, 5),
+]
+
+
+@pytest.mark.parametrize("op,w,a,b,exp", W4)
+def test_smtlib_edges(op, w, a, b, exp):
+    t = Tape()
+    r = getattr(t, op)(t.const(a, w), t.const(b, w))
+    root = t.eq(r, t.const(exp, w))
+    tb = TapeBatch([t.finish(root)])
+    assert pyoracle.eval_tape(tb, 0, EMPTY_MODELS, 0)
+    assert cref.verdicts(tb, ModelBatch([8], np.zeros((1, 1), np.uint32)))[0, 0]
+
+
+def test_width_changes_and_predicates():
+    t = Tape()
+    x = t.const(0xA5, 8)
+    checks = [
+        t.eq(t.sext(8, x), t.const(0xFFA5, 16)),
+        t.eq(t.zext(8, x), t.const(0x00A5, 16)),
+        t.eq(t.concat(x, t.const(0x3C, 8)), t.const(0xA53C, 16)),
+        t.eq(t.extract(6, 3, x), t.const(0x4, 4)),
+        t.slt(x, t.const(0, 8)),
+        t.ult(t.const(0, 8), x),
+        t.umul_noovfl(t.const(15, 8), t.const(17, 8)),          # 255
+        t.not_(t.umul_noovfl(t.const(16, 8), t.const(16, 8))),  # 256
+        t.not_(t.smul_noovfl(t.const(0xF8, 8), t.const(0xF0, 8))),  # (-8)*(-16) = 128 > 127
+        t.not_(t.smul_noovfl(t.const(8, 8), t.const(16, 8))),   # 128 > 127
+        t.smul_noudfl(t.const(0xF8, 8), t.const(16, 8)),        # -128 ok
+        t.not_(t.smul_noudfl(t.const(0xF8, 8), t.const(17, 8))),  # -136 underflows
+    ]
+    tb = TapeBatch([t.finish(t.and_(*checks))])
+    assert pyoracle.eval_tape(tb, 0, EMPTY_MODELS, 0)
+    assert cref.verdicts(tb, ModelBatch([8], np.zeros((1, 1), np.uint32)))[0, 0]
+
+
+def test_model_completion_defaults():
+    """Absent var -> 0, absent Bool -> false, absent function -> else 0."""
+    from mythril_amd.models import FuncSpec
+    t = Tape()
+    f = FuncSpec(1, 256, (256,))
+    root = t.and_(t.eq(t.var(0, 256), t.const(0, 256)), t.not_(t.var(1, 0)),
+                  t.eq(t.uf(0, 256, t.const(5, 256)), t.const(0, 256)),
+                  t.eq(t.select(t.array_var(0, 256), t.const(9, 256)), t.const(0, 256)))
+    tb = TapeBatch([t.finish(root)])
+    mb = ModelBatch.from_python([256, 0], [{}], [f])
+    assert pyoracle.eval_tape(tb, 0, mb, 0)
+    assert cref.verdicts(tb, mb)[0, 0]
+
+
+def test_store_chain_select_semantics():
+    t = Tape()
+    arr = t.const_array(t.const(7, 256))
+    arr = t.store(arr, t.const(1, 256), t.const(10, 256))
+    arr = t.store(arr, t.const(1, 256), t.const(11, 256))  # outer store wins
+    root = t.and_(t.eq(t.select(arr, t.const(1, 256)), t.const(11, 256)),
+                  t.eq(t.select(arr, t.const(2, 256)), t.const(7, 256)))
+    tb = TapeBatch([t.finish(root)])
+    assert pyoracle.eval_tape(tb, 0, EMPTY_MODELS, 0)
+    assert cref.verdicts(tb, ModelBatch([8], np.zeros((1, 1), np.uint32)))[0, 0]
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_fuzz_python_vs_c(seed):
+    tb, mb = fuzz_workload(seed, 30, 24, max_width=512 if seed % 2 else 256, depth=4)
+    v_py = np.array(pyoracle.verdicts(tb, mb))
+    v_c = cref.verdicts(tb, mb)
+    assert (v_py == v_c).all()
+    fh_c, _ = cref.first_hit(tb, mb)
+    assert list(fh_c) == pyoracle.first_hit(tb, mb)
+
+
+def test_c2_planting():
+    tb, mb, exp = c2_workload(300, 3000, seed=2)
+    fh, _ = cref.first_hit(tb, mb)
+    assert (fh == exp).all()
+    assert (exp >= 0).sum() > 10 and (exp < 0).sum() > 200
+    sizes = tb.sizes()
+    assert 50 <= sizes.mean() <= 80
