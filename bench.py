@@ -28,9 +28,11 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# MI355X INT32 VALU peak: 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz (MI355X_MICROARCH.md:
-# SIMD-32, wave64 VALU over 2 cycles; FP32 vector peak 157.3 TF = the same lane rate x 2 for FMA).
-VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+# MI355X INT32 VALU peak: 256 CU x 64 lane-ops/clk x 2.4 GHz = 39.3 TOPS.
+# Confirmed by mythril_amd/csrc/valu_peak.hip on MI355X: v_add_u32 37.9, v_add_co/addc 36.9,
+# v_mad_u64_u32 35.2 T lane-ops/s (profiles/r01_valu_peak.json).  The FP32 figure of
+# MI355X_MICROARCH.md (SIMD-32, 157 TF with FMA) would imply 78.6 T; integer ops do not reach it.
+VALU_PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12
 HBM_PEAK_GBS = 8000.0
 
 
@@ -101,8 +103,11 @@ def main():
         raise SystemExit(f"{ct.n_unsupported} C2 tapes unsupported by the evaluator")
     dev = torch.device("cuda", local)
     best = torch.empty(tb.n_tapes, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated (non-null) stream: the kernels, the HIP events and RCCL all order on it
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
+    assert sptr != 0
 
     def step():
         ev.launch_first_hit(ct, best.data_ptr(), sptr)

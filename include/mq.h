@@ -217,6 +217,17 @@ int mq_eval_verdicts(mq_ctx* ctx, const mq_tape_batch* batch, uint8_t* bits_out,
    Replaces eth_hash in sha3 (support_utils.py:92-100) / find_concrete_keccak (kfm.py:56-69). */
 int mq_keccak256(mq_ctx* ctx, const uint8_t* data, const int64_t* offsets, int32_t n, uint8_t* digests_out);
 
+/* Context options.  MQ_OPT_USE_ASM (default 1): run eligible 256-bit tapes on the gfx950
+   assembly interpreter, the rest on the HIP C++ interpreter (0: HIP C++ for all — the A/B and
+   parity cross-check).  MQ_OPT_EARLY_EXIT (default 1): waves skip a tape once a lower first
+   hit is published.  MQ_OPT_ASM_READY (query): returns 1 if the assembly interpreter loaded. */
+enum mq_option { MQ_OPT_USE_ASM = 1, MQ_OPT_EARLY_EXIT = 2, MQ_OPT_ASM_READY = 3 };
+int mq_ctx_set_option(mq_ctx* ctx, int option, int value);
+
+/* How a compiled batch is split: tapes on the assembly interpreter, on the generic 256-bit
+   and on the 512-bit HIP C++ kernels (any pointer may be NULL). */
+int mq_tapes_info(mq_tapes* tapes, int32_t* n_asm, int32_t* n_generic_l8, int32_t* n_generic_l16);
+
 /* Static algorithmic cost of a tape; -1 if malformed. */
 double mq_tape_alg_ops(const mq_tape_batch* batch, int32_t t);
 

@@ -17,8 +17,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libmq.so")
 OBJDIR = os.path.join(HERE, "csrc", "_obj")
-SOURCES = ["mq_api.cpp", "tape_compiler.cpp", "qs_kernels.hip", "keccak.hip"]
-HEADERS = ["gprog.h", "bvops.h", "qs_launch.h", "tape_compiler.h"]
+SOURCES = ["mq_api.cpp", "tape_compiler.cpp", "qs_kernels.hip", "keccak.hip", "qsa.hip"]
+HEADERS = ["gprog.h", "bvops.h", "qs_launch.h", "tape_compiler.h", "qsa_table.h", "qsa_gen.inc"]
 ARCH = os.environ.get("MQ_OFFLOAD_ARCH", "gfx950")
 
 
@@ -47,6 +47,10 @@ def _stale(obj: str, src: str) -> bool:
 
 def build(force: bool = False, verbose: bool = False) -> str:
     hipcc = _hipcc()
+    gen = os.path.join(CSRC, "gen_qsa.py")
+    inc = os.path.join(CSRC, "qsa_gen.inc")
+    if force or not os.path.exists(inc) or os.path.getmtime(inc) < os.path.getmtime(gen):
+        subprocess.check_call([sys.executable, gen])
     os.makedirs(OBJDIR, exist_ok=True)
     jobs = []
     objs = []

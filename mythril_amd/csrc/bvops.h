@@ -20,16 +20,16 @@ MQ_DEV uint32_t limb_mask(int i, uint32_t W) {
   return W <= lo ? 0u : (W >= lo + 32u ? 0xFFFFFFFFu : ((1u << (W - lo)) - 1u));
 }
 
-template <int L>
-MQ_DEV void mask_w(uint32_t (&x)[L], uint32_t W) {
+template <int L, class T_x>
+MQ_DEV void mask_w(T_x& x, uint32_t W) {
   if (W >= 32u * L) return;
 #pragma unroll
   for (int i = 0; i < L; i++) x[i] &= limb_mask(i, W);
 }
 
 // sign-extend a canonical W-bit value to the full 32L bits (W uniform)
-template <int L>
-MQ_DEV void sext_full(uint32_t (&x)[L], uint32_t W) {
+template <int L, class T_x>
+MQ_DEV void sext_full(T_x& x, uint32_t W) {
   if (W >= 32u * L || W == 0) return;
   const uint32_t k = (W - 1) >> 5, b = (W - 1) & 31;
   uint32_t top = 0;
@@ -43,46 +43,46 @@ MQ_DEV void sext_full(uint32_t (&x)[L], uint32_t W) {
   }
 }
 
-template <int L>
-MQ_DEV void add_n(uint32_t (&r)[L], const uint32_t (&a)[L], const uint32_t (&b)[L]) {
+template <int L, class T_r, class T_a, class T_b>
+MQ_DEV void add_n(T_r& r, const T_a& a, const T_b& b) {
   uint32_t c = 0;
 #pragma unroll
   for (int i = 0; i < L; i++) r[i] = __builtin_addc(a[i], b[i], c, &c);
 }
 
-template <int L>
-MQ_DEV uint32_t sub_n(uint32_t (&r)[L], const uint32_t (&a)[L], const uint32_t (&b)[L]) {
+template <int L, class T_r, class T_a, class T_b>
+MQ_DEV uint32_t sub_n(T_r& r, const T_a& a, const T_b& b) {
   uint32_t c = 0;
 #pragma unroll
   for (int i = 0; i < L; i++) r[i] = __builtin_subc(a[i], b[i], c, &c);
   return c;  // borrow out: a < b
 }
 
-template <int L>
-MQ_DEV void neg_n(uint32_t (&x)[L]) {
+template <int L, class T_x>
+MQ_DEV void neg_n(T_x& x) {
   uint32_t c = 0;
 #pragma unroll
   for (int i = 0; i < L; i++) x[i] = __builtin_subc(0u, x[i], c, &c);
 }
 
-template <int L>
-MQ_DEV bool ult_n(const uint32_t (&a)[L], const uint32_t (&b)[L]) {
+template <int L, class T_a, class T_b>
+MQ_DEV bool ult_n(const T_a& a, const T_b& b) {
   uint32_t c = 0;
 #pragma unroll
   for (int i = 0; i < L; i++) (void)__builtin_subc(a[i], b[i], c, &c);
   return c != 0;
 }
 
-template <int L>
-MQ_DEV bool eq_n(const uint32_t (&a)[L], const uint32_t (&b)[L]) {
+template <int L, class T_a, class T_b>
+MQ_DEV bool eq_n(const T_a& a, const T_b& b) {
   bool e = true;
 #pragma unroll
   for (int i = 0; i < L; i++) e = e && (a[i] == b[i]);
   return e;
 }
 
-template <int L>
-MQ_DEV bool is_zero_n(const uint32_t (&a)[L]) {
+template <int L, class T_a>
+MQ_DEV bool is_zero_n(const T_a& a) {
   uint32_t acc = 0;
 #pragma unroll
   for (int i = 0; i < L; i++) acc |= a[i];
@@ -90,8 +90,8 @@ MQ_DEV bool is_zero_n(const uint32_t (&a)[L]) {
 }
 
 // r = a*b mod 2^(32L)   (row-wise schoolbook, L(L+1)/2 partial products)
-template <int L>
-MQ_DEV void mul_lo_n(uint32_t (&r)[L], const uint32_t (&a)[L], const uint32_t (&b)[L]) {
+template <int L, class T_r, class T_a, class T_b>
+MQ_DEV void mul_lo_n(T_r& r, const T_a& a, const T_b& b) {
   uint32_t t[L];
 #pragma unroll
   for (int i = 0; i < L; i++) t[i] = 0;
@@ -111,8 +111,8 @@ MQ_DEV void mul_lo_n(uint32_t (&r)[L], const uint32_t (&a)[L], const uint32_t (&
 }
 
 // full 2L-limb product
-template <int L>
-MQ_DEV void mul_full_n(uint32_t (&lo)[L], uint32_t (&hi)[L], const uint32_t (&a)[L], const uint32_t (&b)[L]) {
+template <int L, class T_lo, class T_hi, class T_a, class T_b>
+MQ_DEV void mul_full_n(T_lo& lo, T_hi& hi, const T_a& a, const T_b& b) {
   uint32_t t[2 * L];
 #pragma unroll
   for (int i = 0; i < 2 * L; i++) t[i] = 0;
@@ -136,8 +136,8 @@ MQ_DEV void mul_full_n(uint32_t (&lo)[L], uint32_t (&hi)[L], const uint32_t (&a)
 
 // ---------------------------------------------------------------- shifts
 // uniform right shift by s < 32L (zero fill)
-template <int L>
-MQ_DEV void shr_uni(uint32_t (&x)[L], uint32_t s) {
+template <int L, class T_x>
+MQ_DEV void shr_uni(T_x& x, uint32_t s) {
   const uint32_t ls = s >> 5, bs = s & 31;
 #pragma unroll
   for (int k = 1; k < L; k <<= 1) {
@@ -153,8 +153,8 @@ MQ_DEV void shr_uni(uint32_t (&x)[L], uint32_t s) {
 }
 
 // uniform left shift by s < 32L
-template <int L>
-MQ_DEV void shl_uni(uint32_t (&x)[L], uint32_t s) {
+template <int L, class T_x>
+MQ_DEV void shl_uni(T_x& x, uint32_t s) {
   const uint32_t ls = s >> 5, bs = s & 31;
 #pragma unroll
   for (int k = 1; k < L; k <<= 1) {
@@ -170,8 +170,8 @@ MQ_DEV void shl_uni(uint32_t (&x)[L], uint32_t s) {
 }
 
 // per-lane left shift by s < 32L
-template <int L>
-MQ_DEV void shl_var(uint32_t (&x)[L], uint32_t s) {
+template <int L, class T_x>
+MQ_DEV void shl_var(T_x& x, uint32_t s) {
   const uint32_t ls = s >> 5, bs = s & 31;
 #pragma unroll
   for (int k = 1; k < L; k <<= 1) {
@@ -185,8 +185,8 @@ MQ_DEV void shl_var(uint32_t (&x)[L], uint32_t s) {
 }
 
 // per-lane right shift by s < 32L with fill word (0 or ~0)
-template <int L>
-MQ_DEV void shr_var(uint32_t (&x)[L], uint32_t s, uint32_t fill) {
+template <int L, class T_x>
+MQ_DEV void shr_var(T_x& x, uint32_t s, uint32_t fill) {
   const uint32_t ls = s >> 5, bs = s & 31;
 #pragma unroll
   for (int k = 1; k < L; k <<= 1) {
@@ -199,8 +199,8 @@ MQ_DEV void shr_var(uint32_t (&x)[L], uint32_t s, uint32_t fill) {
 }
 
 // shift amount of a W-bit canonical value: returns true (and s) when amount < W
-template <int L>
-MQ_DEV bool shift_amount(const uint32_t (&b)[L], uint32_t W, uint32_t& s) {
+template <int L, class T_b>
+MQ_DEV bool shift_amount(const T_b& b, uint32_t W, uint32_t& s) {
   uint32_t hi = 0;
 #pragma unroll
   for (int i = 1; i < L; i++) hi |= b[i];
@@ -211,8 +211,8 @@ MQ_DEV bool shift_amount(const uint32_t (&b)[L], uint32_t W, uint32_t& s) {
 // ---------------------------------------------------------------- division
 // unsigned q = a / b, r = a % b at full 32L bits; b == 0 -> q = all ones, r = a.
 // Restoring radix-2 division, skipping the dividend limbs that are zero in every lane.
-template <int L>
-MQ_DEV void udivrem_n(uint32_t (&q)[L], uint32_t (&r)[L], const uint32_t (&a)[L], const uint32_t (&b)[L]) {
+template <int L, class T_q, class T_r, class T_a, class T_b>
+MQ_DEV void udivrem_n(T_q& q, T_r& r, const T_a& a, const T_b& b) {
   int top = 0;
 #pragma unroll
   for (int i = L - 1; i >= 0; i--) {

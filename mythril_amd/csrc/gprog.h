@@ -26,6 +26,9 @@ enum GOp : uint32_t {
   G_PUSH_TMP = 3,    // imm = temp slot
   G_STORE_TMP = 4,   // imm = temp slot; pops
   G_PUSH_BOOL = 5,   // imm = 0/1
+  G_PUSH_VAR_B = 6,  // Bool variable (same as G_PUSH_VAR for the C++ kernel)
+  G_PUSH_TMP_B = 7,  // Bool temp
+  G_STORE_TMP_B = 8, // Bool temp
   // Bool (limb 0 holds 0/1)
   G_NOT = 10,
   G_AND = 11,

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -16,6 +17,7 @@
 #include "../../include/mq.h"
 #include "gprog.h"
 #include "qs_launch.h"
+#include "qsa_table.h"
 #include "tape_compiler.h"
 
 using namespace mq;
@@ -65,6 +67,15 @@ struct mq_ctx {
   DevBuf counters;
   DevBuf best_tmp;  // scratch first-hit buffer for the synchronous API
   DevBuf verdict_buf;
+  // assembly interpreter (qsa.hip): handler byte offsets read back at context creation
+  bool qsa_ready = false;
+  std::vector<uint32_t> qsa_off;
+  int qsa_index[QK_COUNT][kQsaStack][kQsaVars + 1];
+  bool qsa_models_ok = false;   // model batch fits the preloaded-variable register file
+  uint32_t qsa_var_row[64];
+  DevBuf qsa_args;
+  int use_asm = 1;      // MQ_OPT_USE_ASM
+  int early_exit = 1;   // MQ_OPT_EARLY_EXIT
 };
 
 struct mq_tapes {
@@ -81,7 +92,11 @@ struct mq_tapes {
     int begin = 0, count = 0;  // range in descs
     int max_temps = 0;
   };
-  std::vector<Variant> variants;
+  // descs layout: [L8 QSA-eligible | L8 other | L16]; the QSA view (qdescs/qprog) holds the
+  // eligible tapes translated to threaded code, in the same order.
+  Variant l8_all, l8_rest, l16, qsa;
+  DevBuf qdescs, qprog, qargs;
+  QArgs qargs_host;
 };
 
 static thread_local std::string g_last_error;
@@ -132,6 +147,32 @@ const char* mq_strerror(int code) {
   }
 }
 
+// Read back the byte offset of every handler of the assembly interpreter (kernel mode 2).
+static int qsa_init(mq_ctx* c) {
+  for (int k = 0; k < QK_COUNT; k++)
+    for (int d = 0; d < kQsaStack; d++)
+      for (int v = 0; v <= kQsaVars; v++) c->qsa_index[k][d][v] = -1;
+  for (int h = 0; h < kQsaHandlers; h++) {
+    const QsaHandlerKey& key = kQsaHandlerKeys[h];
+    c->qsa_index[key.kind][key.d < 0 ? 0 : key.d][key.v + 1] = h;
+  }
+  DevBuf table;
+  HIPCHK(table.ensure(sizeof(uint32_t) * kQsaHandlers));
+  HIPCHK(hipMemsetAsync(table.p, 0xFF, sizeof(uint32_t) * kQsaHandlers, c->stream));
+  QArgs qa{};
+  qa.table_out = table.as<uint32_t>();
+  qa.mode = 2;
+  HIPCHK(c->qsa_args.upload(&qa, 1, c->stream));
+  HIPCHK(launch_qsa(c->qsa_args.as<QArgs>(), 1, 1, 0, c->stream));
+  c->qsa_off.resize(kQsaHandlers);
+  HIPCHK(hipMemcpyAsync(c->qsa_off.data(), table.p, sizeof(uint32_t) * kQsaHandlers, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  bool ok = true;
+  for (int h = 0; h < kQsaHandlers; h++) ok = ok && c->qsa_off[h] != 0xFFFFFFFFu && (c->qsa_off[h] & 3) == 0 && c->qsa_off[h] < (1u << 18);
+  c->qsa_ready = ok && std::getenv("MQ_DISABLE_QSA") == nullptr;
+  return MQ_OK;
+}
+
 int mq_ctx_create(int n_dev, const int* dev_ids, mq_ctx** out) {
   if (!out || n_dev != 1) return MQ_ERR_ARG;
   *out = nullptr;
@@ -156,6 +197,11 @@ int mq_ctx_create(int n_dev, const int* dev_ids, mq_ctx** out) {
   if (c->counters.ensure(4 * sizeof(unsigned long long)) != hipSuccess) {
     delete c;
     return MQ_ERR_NOMEM;
+  }
+  int rc = qsa_init(c);
+  if (rc) {
+    mq_ctx_destroy(c);
+    return rc;
   }
   *out = c;
   return MQ_OK;
@@ -212,7 +258,21 @@ int mq_models_upload(mq_ctx* c, const mq_model_batch* mb) {
   }
   if (else_soa.empty()) else_soa.push_back(0);
   c->have_models = false;
-  HIPCHK(c->vars.upload(mb->var_words, (size_t)std::max<int64_t>(rows * M, 1), c->stream));
+  // variable rows followed by one all-zero row (the QSA preload points absent limbs at it)
+  HIPCHK(c->vars.ensure(sizeof(uint32_t) * (size_t)(rows + 1) * M));
+  if (rows > 0) HIPCHK(hipMemcpyAsync(c->vars.p, mb->var_words, sizeof(uint32_t) * (size_t)rows * M, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemsetAsync((uint32_t*)c->vars.p + (size_t)rows * M, 0, sizeof(uint32_t) * M, c->stream));
+  c->qsa_models_ok = true;
+  for (int v = 0; v < 8; v++)
+    for (int l = 0; l < 8; l++) {
+      uint32_t row = (uint32_t)rows;  // zero row
+      if (v < mb->n_vars) {
+        if (mb->var_width[v] > 256) c->qsa_models_ok = false;
+        if ((uint32_t)l < vnl[v]) row = voff[v] + l;
+      }
+      c->qsa_var_row[8 * v + l] = row;
+    }
+  if ((rows + 1) * M * 4 > (int64_t)0xFFFFFFFFLL * 4) c->qsa_models_ok = false;
   HIPCHK(c->var_off.upload(voff.data(), voff.size(), c->stream));
   HIPCHK(c->var_nl.upload(vnl.data(), vnl.size(), c->stream));
   HIPCHK(c->funcs.upload(fd.data(), fd.size(), c->stream));
@@ -236,6 +296,66 @@ int mq_models_upload(mq_ctx* c, const mq_model_batch* mb) {
   return MQ_OK;
 }
 
+// Translate a compiled stack program into QSA threaded code; false if any instruction is
+// outside the assembly interpreter's set (those tapes run on the HIP C++ kernel).
+static bool qsa_translate(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_t>& out) {
+  out.clear();
+  if (x.L != 8 || x.depth > kQsaStack) return false;
+  auto word = [&](int kind, int d, int v, uint32_t imm) -> bool {
+    if (d < 0 || d >= kQsaStack || v < -1 || v >= kQsaVars || imm > 0xFFFFu) return false;
+    const int h = c->qsa_index[kind][d][v + 1];
+    if (h < 0) return false;
+    out.push_back((c->qsa_off[h] >> 2) | (imm << 16));
+    return true;
+  };
+  for (size_t pc = 0; pc < x.prog.size(); pc++) {
+    const uint32_t w = x.prog[pc];
+    const uint32_t op = w & 0xFFu, imm = w >> 12;
+    const int d = (int)((w >> 8) & 0xFu);
+    bool ok;
+    switch (op) {
+      case G_END: ok = word(QK_END, 0, -1, 0); break;
+      case G_PUSH_VAR: ok = imm < (uint32_t)kQsaVars && word(QK_PUSH_VAR, d, (int)imm, 0); break;
+      case G_PUSH_CONST: ok = word(QK_PUSH_CONST, d, -1, imm); break;
+      case G_PUSH_TMP: ok = word(QK_PUSH_TMP, d, -1, imm); break;
+      case G_PUSH_TMP_B: ok = word(QK_PUSH_TMP_BOOL, d, -1, imm); break;
+      case G_STORE_TMP: ok = d == 0 && word(QK_STORE_TMP, 0, -1, imm); break;
+      case G_STORE_TMP_B: ok = d == 0 && word(QK_STORE_TMP_BOOL, 0, -1, imm); break;
+      case G_PUSH_BOOL: ok = word(QK_PUSH_BOOL, d, -1, imm); break;
+      case G_NOT: ok = word(QK_NOT, d, -1, 0); break;
+      case G_AND: ok = word(QK_AND, d, -1, 0); break;
+      case G_OR: ok = word(QK_OR, d, -1, 0); break;
+      case G_XOR: ok = word(QK_XOR, d, -1, 0); break;
+      case G_IFF: ok = word(QK_IFF, d, -1, 0); break;
+      case G_IMPLIES: ok = word(QK_IMPLIES, d, -1, 0); break;
+      case G_BITE: ok = word(QK_BITE, d, -1, 0); break;
+      // unsigned predicates / bitwise / ite are exact on canonical values of any width <= 256
+      case G_EQ: ok = word(QK_EQ, d, -1, 0); break;
+      case G_ULT: ok = word(QK_ULT, d, -1, 0); break;
+      case G_ULE: ok = word(QK_ULE, d, -1, 0); break;
+      case G_UGT: ok = word(QK_UGT, d, -1, 0); break;
+      case G_UGE: ok = word(QK_UGE, d, -1, 0); break;
+      case G_BAND: ok = word(QK_BAND, d, -1, 0); break;
+      case G_BOR: ok = word(QK_BOR, d, -1, 0); break;
+      case G_BXOR: ok = word(QK_BXOR, d, -1, 0); break;
+      case G_ITE: ok = word(QK_ITE, d, -1, 0); break;
+      // signed predicates and wrapping arithmetic: full 256-bit width only (no masking)
+      case G_SLT: ok = imm == 256 && word(QK_SLT, d, -1, 0); break;
+      case G_SLE: ok = imm == 256 && word(QK_SLE, d, -1, 0); break;
+      case G_SGT: ok = imm == 256 && word(QK_SGT, d, -1, 0); break;
+      case G_SGE: ok = imm == 256 && word(QK_SGE, d, -1, 0); break;
+      case G_ADD: ok = imm == 256 && word(QK_ADD, d, -1, 0); break;
+      case G_SUB: ok = imm == 256 && word(QK_SUB, d, -1, 0); break;
+      case G_MUL: ok = imm == 256 && word(QK_MUL, d, -1, 0); break;
+      case G_NEG: ok = imm == 256 && word(QK_NEG, d, -1, 0); break;
+      case G_BNOT: ok = imm == 256 && word(QK_BNOT, d, -1, 0); break;
+      default: ok = false;
+    }
+    if (!ok) return false;
+  }
+  return true;
+}
+
 int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t* n_unsup_out) {
   if (!c || !tb || !out || tb->n_tapes < 0 || (tb->n_tapes > 0 && (!tb->tape_offsets || !tb->nodes))) return MQ_ERR_ARG;
   *out = nullptr;
@@ -254,34 +374,59 @@ int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t*
   // compile (independent per tape)
 #pragma omp parallel for schedule(dynamic, 64)
   for (int t = 0; t < tb->n_tapes; t++) ct[t] = compile_tape(tb, t, lim);
-  // order descriptors by variant (L)
-  std::vector<uint32_t> prog, consts;
-  std::vector<GDesc> descs;
-  for (int L : {8, 16}) {
-    mq_tapes::Variant v;
-    v.L = L;
+  // descriptor groups: [L8 QSA-eligible | L8 other | L16] (see mq_tapes)
+  std::vector<uint32_t> prog, consts, qprog;
+  std::vector<GDesc> descs, qdescs;
+  std::vector<uint32_t> qwords;
+  auto push_desc = [&](int t, const CompiledTape& x) {
+    GDesc d{};
+    d.prog_off = (uint32_t)prog.size();
+    d.prog_len = (uint32_t)x.prog.size();
+    d.tape = (uint32_t)t;
+    d.const_base = (uint32_t)consts.size();
+    d.n_nodes = x.n_nodes;
+    d.n_temps = (uint32_t)x.n_temps;
+    d.depth = (uint32_t)x.depth;
+    d.alg_ops = (uint32_t)std::min(x.alg_ops, 4.0e9);
+    prog.insert(prog.end(), x.prog.begin(), x.prog.end());
+    consts.insert(consts.end(), x.consts.begin(), x.consts.end());
+    descs.push_back(d);
+    return d;
+  };
+  std::vector<char> qsa_ok(tb->n_tapes, 0);
+  std::vector<std::vector<uint32_t>> qtr(tb->n_tapes);
+  if (c->qsa_ready)
+    for (int t = 0; t < tb->n_tapes; t++)
+      if (ct[t].supported && ct[t].L == 8) qsa_ok[t] = qsa_translate(c, ct[t], qtr[t]) ? 1 : 0;
+  T->qsa.begin = 0;
+  for (int pass = 0; pass < 3; pass++) {
+    mq_tapes::Variant& v = pass == 0 ? T->qsa : (pass == 1 ? T->l8_rest : T->l16);
+    v.L = pass == 2 ? 16 : 8;
     v.begin = (int)descs.size();
     for (int t = 0; t < tb->n_tapes; t++) {
       const CompiledTape& x = ct[t];
-      if (!x.supported || x.L != L) continue;
-      GDesc d{};
-      d.prog_off = (uint32_t)prog.size();
-      d.prog_len = (uint32_t)x.prog.size();
-      d.tape = (uint32_t)t;
-      d.const_base = (uint32_t)consts.size();
-      d.n_nodes = x.n_nodes;
-      d.n_temps = (uint32_t)x.n_temps;
-      d.depth = (uint32_t)x.depth;
-      d.alg_ops = (uint32_t)std::min(x.alg_ops, 4.0e9);
-      prog.insert(prog.end(), x.prog.begin(), x.prog.end());
-      consts.insert(consts.end(), x.consts.begin(), x.consts.end());
-      // pad so that the scalar loads of the last constant never run past the buffer
-      descs.push_back(d);
+      if (!x.supported) continue;
+      if (pass == 0 && !(x.L == 8 && qsa_ok[t])) continue;
+      if (pass == 1 && !(x.L == 8 && !qsa_ok[t])) continue;
+      if (pass == 2 && x.L != 16) continue;
+      GDesc d = push_desc(t, x);
+      if (pass == 0) {
+        d.prog_off = (uint32_t)qprog.size();
+        d.prog_len = (uint32_t)qtr[t].size();
+        qprog.insert(qprog.end(), qtr[t].begin(), qtr[t].end());
+        qdescs.push_back(d);
+      }
       v.max_temps = std::max(v.max_temps, x.n_temps);
     }
     v.count = (int)descs.size() - v.begin;
-    if (v.count) T->variants.push_back(v);
   }
+  T->l8_all.L = 8;
+  T->l8_all.begin = 0;
+  T->l8_all.count = T->qsa.count + T->l8_rest.count;
+  T->l8_all.max_temps = std::max(T->qsa.max_temps, T->l8_rest.max_temps);
+  // trailing END words: the dispatch tail prefetches one word past each program's END
+  qprog.push_back(c->qsa_ready ? c->qsa_off[c->qsa_index[QK_END][0][0]] / 4 : 0);
+  qprog.push_back(qprog.back());
   consts.resize(consts.size() + 16, 0);
   prog.push_back(gword(G_END, 0, 0));
   for (int t = 0; t < tb->n_tapes; t++) {
@@ -291,7 +436,11 @@ int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t*
     T->alg_ops[t] = ct[t].alg_ops;
   }
   if (descs.empty()) descs.push_back(GDesc{});
+  if (qdescs.empty()) qdescs.push_back(GDesc{});
   HIPCHK(T->descs.upload(descs.data(), descs.size(), c->stream));
+  HIPCHK(T->qdescs.upload(qdescs.data(), qdescs.size(), c->stream));
+  HIPCHK(T->qprog.upload(qprog.data(), qprog.size(), c->stream));
+  HIPCHK(T->qargs.ensure(sizeof(QArgs)));
   HIPCHK(T->prog.upload(prog.data(), prog.size(), c->stream));
   HIPCHK(T->consts.upload(consts.data(), consts.size(), c->stream));
   HIPCHK(T->unsup_dev.upload(T->unsupported.data(), T->unsupported.size(), c->stream));
@@ -331,6 +480,49 @@ static KArgs make_args(mq_ctx* c, mq_tapes* T, const mq_tapes::Variant& v) {
   return a;
 }
 
+// Launch every evaluation kernel for a compiled batch: the assembly interpreter for the
+// QSA-eligible tapes (when the model batch fits its register file), the HIP C++ kernels for
+// the rest.  verdicts == nullptr -> first-hit mode into best.
+static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, hipStream_t st) {
+  const bool use_qsa = c->qsa_ready && c->use_asm && c->qsa_models_ok && T->qsa.count > 0;
+  std::vector<mq_tapes::Variant> cpp;
+  if (use_qsa) cpp = {T->l8_rest, T->l16};
+  else cpp = {T->l8_all, T->l16};
+  if (use_qsa) {
+    KArgs k = make_args(c, T, T->qsa);
+    QArgs& q = T->qargs_host;
+    q = QArgs{};
+    q.descs = T->qdescs.p;
+    q.prog = T->qprog.p;
+    q.consts = T->consts.p;
+    q.vars = c->vars.p;
+    q.best = best;
+    q.counters = c->counters.as<unsigned long long>();
+    q.verdicts = verdicts;
+    q.M = (uint32_t)c->M;
+    q.index_base = (uint32_t)c->index_base;
+    q.n_desc = (uint32_t)T->qsa.count;
+    q.tapes_per_group = (uint32_t)k.tapes_per_group;
+    q.early_exit = verdicts ? 0u : (uint32_t)c->early_exit;
+    q.mode = verdicts ? 1u : 0u;
+    q.lds_wave_bytes = (uint32_t)T->qsa.max_temps * 2048u;
+    std::memcpy(q.var_row, c->qsa_var_row, sizeof(q.var_row));
+    HIPCHK(hipMemcpyAsync(T->qargs.p, &q, sizeof(QArgs), hipMemcpyHostToDevice, st));
+    const unsigned gx = (unsigned)((c->M + 255) / 256);
+    const unsigned gy = (unsigned)((T->qsa.count + k.tapes_per_group - 1) / k.tapes_per_group);
+    HIPCHK(launch_qsa(T->qargs.as<QArgs>(), gx, gy, (size_t)q.lds_wave_bytes * 4, st));
+  }
+  for (const auto& v : cpp) {
+    if (v.count <= 0) continue;
+    KArgs a = make_args(c, T, v);
+    a.best = best;
+    a.verdicts = verdicts;
+    a.early_exit = verdicts ? 0 : c->early_exit;
+    HIPCHK(launch_qs(a, v.L, verdicts != nullptr, st));
+  }
+  return MQ_OK;
+}
+
 int mq_launch_first_hit(mq_ctx* c, mq_tapes* T, int32_t* d_best, void* stream) {
   if (!c || !T || !d_best) return MQ_ERR_ARG;
   if (!c->have_models) return MQ_ERR_NO_MODELS;
@@ -338,12 +530,7 @@ int mq_launch_first_hit(mq_ctx* c, mq_tapes* T, int32_t* d_best, void* stream) {
   HIPCHK(hipSetDevice(c->device));
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
   HIPCHK(launch_init_best(d_best, T->n_tapes, st));
-  for (const auto& v : T->variants) {
-    KArgs a = make_args(c, T, v);
-    a.best = d_best;
-    HIPCHK(launch_qs(a, v.L, false, st));
-  }
-  return MQ_OK;
+  return launch_all(c, T, d_best, nullptr, st);
 }
 
 int mq_finalize_first_hit(mq_ctx* c, mq_tapes* T, int32_t* d_best, void* stream) {
@@ -419,12 +606,8 @@ int mq_eval_verdicts(mq_ctx* c, const mq_tape_batch* tb, uint8_t* bits, int32_t*
   const size_t nbytes = (size_t)T->n_tapes * (size_t)c->M;
   HIPCHK(c->verdict_buf.ensure(std::max<size_t>(nbytes, 1)));
   HIPCHK(hipMemsetAsync(c->verdict_buf.p, 0, std::max<size_t>(nbytes, 1), c->stream));
-  for (const auto& v : T->variants) {
-    KArgs a = make_args(c, T, v);
-    a.verdicts = c->verdict_buf.as<uint8_t>();
-    a.early_exit = 0;
-    HIPCHK(launch_qs(a, v.L, true, c->stream));
-  }
+  rc = launch_all(c, T, nullptr, c->verdict_buf.as<uint8_t>(), c->stream);
+  if (rc) return rc;
   std::vector<uint8_t> host(nbytes);
   if (nbytes) HIPCHK(hipMemcpyAsync(host.data(), c->verdict_buf.p, nbytes, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -444,6 +627,24 @@ int mq_eval_verdicts(mq_ctx* c, const mq_tape_batch* tb, uint8_t* bits, int32_t*
       first_hit_out[t] = h;
     }
   }
+  return MQ_OK;
+}
+
+int mq_ctx_set_option(mq_ctx* c, int option, int value) {
+  if (!c) return MQ_ERR_ARG;
+  switch (option) {
+    case MQ_OPT_USE_ASM: c->use_asm = value ? 1 : 0; return MQ_OK;
+    case MQ_OPT_EARLY_EXIT: c->early_exit = value ? 1 : 0; return MQ_OK;
+    case MQ_OPT_ASM_READY: return c->qsa_ready ? 1 : 0;
+    default: return MQ_ERR_ARG;
+  }
+}
+
+int mq_tapes_info(mq_tapes* T, int32_t* n_asm, int32_t* n_generic_l8, int32_t* n_generic_l16) {
+  if (!T) return MQ_ERR_ARG;
+  if (n_asm) *n_asm = T->qsa.count;
+  if (n_generic_l8) *n_generic_l8 = T->l8_rest.count;
+  if (n_generic_l16) *n_generic_l16 = T->l16.count;
   return MQ_OK;
 }
 

@@ -16,9 +16,39 @@
 
 namespace mq {
 
+// Uniform, read-only-for-the-launch data (programs, constants, descriptors, var/func tables)
+// is read through the CONSTANT address space: loads at uniform addresses then lower to
+// s_load (scalar cache) instead of global_load + readfirstlane.  Plain global pointers are
+// not provably unclobbered here (the kernel also stores: atomicMin, verdicts, LDS temps).
+typedef const __attribute__((address_space(4))) uint32_t* cu32p;
+typedef const __attribute__((address_space(4))) GDesc* cdescp;
+typedef const __attribute__((address_space(4))) FuncDev* cfuncp;
+#define CONSTP(T, p) ((T)(const void*)(p))
+
+template <int L>
+struct VecT;
+template <>
+struct VecT<8> { typedef uint32_t type __attribute__((ext_vector_type(8))); };
+template <>
+struct VecT<16> { typedef uint32_t type __attribute__((ext_vector_type(16))); };
+
+MQ_DEV GDesc load_desc(const GDesc* descs, int i) {
+  cu32p w = CONSTP(cu32p, descs) + (size_t)i * 8;
+  GDesc d;
+  d.prog_off = w[0];
+  d.prog_len = w[1];
+  d.tape = w[2];
+  d.const_base = w[3];
+  d.n_nodes = w[4];
+  d.n_temps = w[5];
+  d.depth = w[6];
+  d.alg_ops = w[7];
+  return d;
+}
+
 template <int L, int D>
 struct Stack {
-  uint32_t s[D][L];
+  typename VecT<L>::type s[D];
 };
 
 // Everything a handler may read; built once per wave from the kernel arguments and fully
@@ -34,7 +64,7 @@ struct Ctx {
   const uint32_t* entry_words;
   const uint32_t* else_words;
   int64_t M;
-  const uint32_t* consts;  // constants of the current tape
+  cu32p consts;            // constants of the current tape
   int64_t m;               // local model index of this lane (clamped to M-1)
   uint32_t* tmp;           // this wave's LDS temp region (slot, limb, lane)
   int lane;
@@ -52,7 +82,7 @@ MQ_DEV Ctx make_ctx(const KArgs& a, int64_t m, uint32_t* tmp, int lane) {
   c.entry_words = a.entry_words;
   c.else_words = a.else_words;
   c.M = a.M;
-  c.consts = a.consts;
+  c.consts = CONSTP(cu32p, a.consts);
   c.m = m;
   c.tmp = tmp;
   c.lane = lane;
@@ -68,8 +98,8 @@ struct HPushVar {
   H_DEV run(Stack<L, D>& S, uint32_t imm, uint32_t, const Ctx& cx) {
     uint32_t nl = 0, off = 0;
     if (imm < (uint32_t)cx.n_vars) {
-      off = cx.var_off[imm];
-      nl = cx.var_nl[imm];
+      off = CONSTP(cu32p, cx.var_off)[imm];
+      nl = CONSTP(cu32p, cx.var_nl)[imm];
     }
     const uint32_t* base = cx.vars + (int64_t)off * cx.M + cx.m;
 #pragma unroll
@@ -81,7 +111,7 @@ template <int L, int D>
 struct HPushConst {
   static constexpr int kMin = 0;
   H_DEV run(Stack<L, D>& S, uint32_t imm, uint32_t, const Ctx& cx) {
-    const uint32_t* c = cx.consts + imm;
+    cu32p c = cx.consts + imm;
 #pragma unroll
     for (int i = 0; i < L; i++) S.s[d][i] = c[i];
   }
@@ -270,8 +300,8 @@ struct HSext {  // imm = source width, imm2 = result width
 
 // ---------------------------------------------------------------- cold ops: operands copied
 // into X/Y, one shared implementation, result copied back (keeps code size bounded).
-template <int L, int D>
-MQ_DEV void load_xy(Stack<L, D>& S, int d, uint32_t (&X)[L], uint32_t (&Y)[L]) {
+template <int L, int D, class TX>
+MQ_DEV void load_xy(Stack<L, D>& S, int d, TX& X, TX& Y) {
   switch (d) {
 #define LXY(k)                                      \
   case k:                                           \
@@ -286,8 +316,8 @@ MQ_DEV void load_xy(Stack<L, D>& S, int d, uint32_t (&X)[L], uint32_t (&Y)[L]) {
 #undef LXY
   }
 }
-template <int L, int D>
-MQ_DEV void load_x(Stack<L, D>& S, int d, uint32_t (&X)[L]) {
+template <int L, int D, class TX>
+MQ_DEV void load_x(Stack<L, D>& S, int d, TX& X) {
   switch (d) {
 #define LX(k)                                                                   \
   case k:                                                                       \
@@ -297,8 +327,8 @@ MQ_DEV void load_x(Stack<L, D>& S, int d, uint32_t (&X)[L]) {
 #undef LX
   }
 }
-template <int L, int D>
-MQ_DEV void store_x(Stack<L, D>& S, int d, const uint32_t (&X)[L]) {
+template <int L, int D, class TX>
+MQ_DEV void store_x(Stack<L, D>& S, int d, const TX& X) {
   switch (d) {
 #define SX(k)                                                                   \
   case k:                                                                       \
@@ -310,13 +340,23 @@ MQ_DEV void store_x(Stack<L, D>& S, int d, const uint32_t (&X)[L]) {
 }
 
 // table lookup of a model function (UF or as-array): entries first, else value
-template <int L>
-MQ_DEV void func_lookup(const Ctx& cx, uint32_t f, uint32_t W, const uint32_t (&k0)[L], const uint32_t (&k1)[L],
-                        uint32_t (&out)[L]) {
+template <int L, class T0, class T1, class TO>
+MQ_DEV void func_lookup(const Ctx& cx, uint32_t f, uint32_t W, const T0& k0, const T1& k1, TO& out) {
 #pragma unroll
   for (int i = 0; i < L; i++) out[i] = 0;
   if (f >= (uint32_t)cx.n_funcs) return;
-  const FuncDev fd = cx.funcs[f];
+  FuncDev fd;
+  {
+    cu32p w = CONSTP(cu32p, cx.funcs) + (size_t)f * (sizeof(FuncDev) / 4);
+    fd.arity = w[0];
+    fd.nl_a0 = w[1];
+    fd.nl_a1 = w[2];
+    fd.nl_res = w[3];
+    fd.stride = w[4];
+    fd.entry_base = (int64_t)((uint64_t)w[6] | ((uint64_t)w[7] << 32));
+    fd.ptr_base = (int64_t)((uint64_t)w[8] | ((uint64_t)w[9] << 32));
+    fd.else_base = (int64_t)((uint64_t)w[10] | ((uint64_t)w[11] << 32));
+  }
   const int64_t M = cx.M;
   // else value (SoA, coalesced)
   const uint32_t* ev = cx.else_words + fd.else_base + cx.m;
@@ -502,7 +542,7 @@ MQ_DEV void dispatch(Stack<L, D>& S, int d, uint32_t imm, uint32_t imm2, const C
 }
 
 template <int L, int D>
-MQ_DEV bool run_tape(const uint32_t* __restrict__ prog, const Ctx& cx) {
+MQ_DEV bool run_tape(cu32p prog, const Ctx& cx) {
   Stack<L, D> S;
 #pragma unroll
   for (int k = 0; k < D; k++)
@@ -518,10 +558,13 @@ MQ_DEV bool run_tape(const uint32_t* __restrict__ prog, const Ctx& cx) {
     uint32_t imm2 = 0;
     if (op == G_EXTRACT || op == G_CONCAT || op == G_SEXT || op == G_UF1 || op == G_UF2) imm2 = prog[pc++];
     switch (op) {
-      case G_PUSH_VAR: dispatch<HPushVar, L, D>(S, d, imm, imm2, cx); break;
+      case G_PUSH_VAR:
+      case G_PUSH_VAR_B: dispatch<HPushVar, L, D>(S, d, imm, imm2, cx); break;
       case G_PUSH_CONST: dispatch<HPushConst, L, D>(S, d, imm, imm2, cx); break;
-      case G_PUSH_TMP: dispatch<HPushTmp, L, D>(S, d, imm, imm2, cx); break;
-      case G_STORE_TMP: dispatch<HStoreTmp, L, D>(S, d, imm, imm2, cx); break;
+      case G_PUSH_TMP:
+      case G_PUSH_TMP_B: dispatch<HPushTmp, L, D>(S, d, imm, imm2, cx); break;
+      case G_STORE_TMP:
+      case G_STORE_TMP_B: dispatch<HStoreTmp, L, D>(S, d, imm, imm2, cx); break;
       case G_PUSH_BOOL: dispatch<HPushBool, L, D>(S, d, imm, imm2, cx); break;
       case G_NOT: dispatch<HNot, L, D>(S, d, imm, imm2, cx); break;
       case G_AND: dispatch<HAnd, L, D>(S, d, imm, imm2, cx); break;
@@ -573,12 +616,12 @@ __global__ __launch_bounds__(256) void qs_first_hit_kernel(KArgs args) {
   const int32_t gfirst = (int32_t)(args.index_base + m0);
   uint64_t pairs = 0, nodes = 0, ops = 0;
   for (int i = gbeg; i < gend; i++) {
-    const GDesc dsc = args.descs[i];
+    const GDesc dsc = load_desc(args.descs, i);
     int32_t cur = __hip_atomic_load(&args.best[dsc.tape], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     cur = __builtin_amdgcn_readfirstlane(cur);
     if (args.early_exit && gfirst >= cur) continue;
-    cx.consts = args.consts + dsc.const_base;
-    const bool r = run_tape<L, D>(args.prog + dsc.prog_off, cx);
+    cx.consts = CONSTP(cu32p, args.consts) + dsc.const_base;
+    const bool r = run_tape<L, D>(CONSTP(cu32p, args.prog) + dsc.prog_off, cx);
     const uint64_t mask = __ballot(r && valid);
     const uint64_t vmask = __ballot(valid);
     pairs += __popcll(vmask);
@@ -608,9 +651,9 @@ __global__ __launch_bounds__(256) void qs_verdict_kernel(KArgs args) {
   const int gbeg = blockIdx.y * args.tapes_per_group;
   const int gend = min(gbeg + args.tapes_per_group, args.n_desc);
   for (int i = gbeg; i < gend; i++) {
-    const GDesc dsc = args.descs[i];
-    cx.consts = args.consts + dsc.const_base;
-    const bool r = run_tape<L, D>(args.prog + dsc.prog_off, cx);
+    const GDesc dsc = load_desc(args.descs, i);
+    cx.consts = CONSTP(cu32p, args.consts) + dsc.const_base;
+    const bool r = run_tape<L, D>(CONSTP(cu32p, args.prog) + dsc.prog_off, cx);
     if (valid) args.verdicts[(int64_t)dsc.tape * args.M + m] = r ? 1 : 0;
   }
 }

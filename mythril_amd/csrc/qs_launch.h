@@ -46,6 +46,31 @@ struct KArgs {
   int early_exit;
 };
 
+// argument block of the assembly interpreter (layout fixed by gen_qsa.py's prologue)
+struct QArgs {
+  const void* descs;             // 0x00 GDesc[] (prog_off indexes the QSA program words)
+  const void* prog;              // 0x08
+  const void* consts;            // 0x10
+  const void* vars;              // 0x18
+  int32_t* best;                 // 0x20
+  unsigned long long* counters;  // 0x28
+  uint8_t* verdicts;             // 0x30
+  uint32_t* table_out;           // 0x38 (mode 2)
+  uint32_t M;                    // 0x40
+  uint32_t index_base;           // 0x44
+  uint32_t n_desc;               // 0x48
+  uint32_t tapes_per_group;      // 0x4c
+  uint32_t early_exit;           // 0x50
+  uint32_t mode;                 // 0x54: 0 first-hit, 1 verdicts, 2 dump handler offsets
+  uint32_t lds_wave_bytes;       // 0x58
+  uint32_t pad;                  // 0x5c
+  uint32_t var_row[64];          // 0x60: limb row of var v limb l (v < 8), or the zero row
+};
+static_assert(sizeof(void*) == 8, "64-bit");
+static_assert(__builtin_offsetof(QArgs, M) == 0x40, "QArgs layout");
+static_assert(__builtin_offsetof(QArgs, var_row) == 0x60, "QArgs layout");
+
+hipError_t launch_qsa(const QArgs* d_args, unsigned gx, unsigned gy, size_t lds, hipStream_t st);
 hipError_t launch_qs(const KArgs& a, int L, bool verdict, hipStream_t st);
 hipError_t launch_init_best(int32_t* best, int n, hipStream_t st);
 hipError_t launch_finalize_best(int32_t* best, const uint8_t* unsupported, int n, hipStream_t st);

@@ -209,7 +209,7 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
         case MQ_OP_CONST: r = konst(i); break;
         case MQ_OP_VAR: {
           if (n.a > (uint32_t)kMaxImm) throw Fail{"var index too large"};
-          INode x = mk(G_PUSH_VAR, w, {}, n.a);
+          INode x = mk(w == 0 ? G_PUSH_VAR_B : G_PUSH_VAR, w, {}, n.a);
           x.leaf = true;
           r = B.add(x);
           break;
@@ -367,7 +367,7 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
       maxd = std::max(maxd, d + 1);
       const INode& n = B.nodes[x];
       if (hoist[x] && slot[x] >= 0) {
-        out.prog.push_back(gword(G_PUSH_TMP, d, slot[x]));
+        out.prog.push_back(gword(n.width == 0 ? G_PUSH_TMP_B : G_PUSH_TMP, d, slot[x]));
         return;
       }
       if (n.leaf) {
@@ -412,7 +412,7 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
           s = n_slots++;
         }
         slot[x] = s;
-        out.prog.push_back(gword(G_STORE_TMP, 0, s));
+        out.prog.push_back(gword(B.nodes[x].width == 0 ? G_STORE_TMP_B : G_STORE_TMP, 0, s));
       }
     }
     if (n_slots > max_temps) throw Fail{"too many temps"};

@@ -56,6 +56,8 @@ def load_library(path: str = LIB_PATH):
         L.mq_launch_first_hit.argtypes = [P, P, P, P]
         L.mq_finalize_first_hit.argtypes = [P, P, P, P]
         L.mq_counters.argtypes = [P, C.POINTER(C.c_double), C.c_int]
+        L.mq_ctx_set_option.argtypes = [P, C.c_int, C.c_int]
+        L.mq_tapes_info.argtypes = [P] + [C.POINTER(C.c_int32)] * 3
         L.mq_eval_verdicts.argtypes = [P, C.POINTER(MqTapeBatch), C.POINTER(C.c_uint8), C.POINTER(C.c_int32)]
         L.mq_keccak256.argtypes = [P, C.POINTER(C.c_uint8), C.POINTER(C.c_int64), C.c_int32, C.POINTER(C.c_uint8)]
         L.mq_tape_alg_ops.argtypes = [C.POINTER(MqTapeBatch), C.c_int32]
@@ -120,6 +122,12 @@ class CompiledTapes:
         self.handle = h
         self.n_unsupported = nu.value
 
+    def split(self):
+        """(tapes on the assembly interpreter, generic 256-bit, generic 512-bit)."""
+        a, b, c = C.c_int32(), C.c_int32(), C.c_int32()
+        _check(self.ev.lib.mq_tapes_info(self.handle, C.byref(a), C.byref(b), C.byref(c)), "mq_tapes_info")
+        return a.value, b.value, c.value
+
     def free(self) -> None:
         if self.handle:
             self.ev.lib.mq_tapes_free(self.handle)
@@ -144,6 +152,21 @@ class Evaluator:
         self.device = device
         self.n_models = 0
         self.index_base = 0
+
+    OPT_USE_ASM, OPT_EARLY_EXIT, OPT_ASM_READY = 1, 2, 3
+
+    def set_option(self, option: int, value: int) -> int:
+        rc = self.lib.mq_ctx_set_option(self.ctx, option, value)
+        if rc < 0:
+            _check(rc, "mq_ctx_set_option")
+        return rc
+
+    @property
+    def asm_ready(self) -> bool:
+        return self.set_option(self.OPT_ASM_READY, 0) == 1
+
+    def use_asm(self, on: bool) -> None:
+        self.set_option(self.OPT_USE_ASM, 1 if on else 0)
 
     def close(self) -> None:
         if getattr(self, "ctx", None):

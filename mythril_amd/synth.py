@@ -58,14 +58,14 @@ class _C2Expr:
 
 
 def c2_tape(rng: np.random.Generator, planted_vals: Optional[Sequence[int]], n_vars: int = 8,
-            n_cmp: int = 4, ops_per_side: int = 6) -> Tape:
+            n_cmp: int = 4, ops_per_side: int = 5) -> Tape:
     t = Tape()
     vals = planted_vals if planted_vals is not None else [0] * n_vars
     gen = _C2Expr(rng, t, n_vars, vals)
     cmps = []
     for i in range(n_cmp):
         a, va = gen.tree(ops_per_side)
-        b, vb = gen.tree(ops_per_side - 1)
+        b, vb = gen.tree(ops_per_side - 2)
         kind = "eq" if i == 0 else ("eq" if rng.random() < 0.3 else "ult")
         if kind == "eq":
             # EQ(a, b + c): planted -> c = a(p) - b(p); else c uniform (unsat w.p. ~1)
@@ -146,9 +146,10 @@ def fuzz_models(rng: np.random.Generator, var_widths: Sequence[int], n_models: i
 
 
 class _Fuzz:
-    def __init__(self, rng, tape: Tape, var_widths, funcs, max_width: int, ops=None):
+    def __init__(self, rng, tape: Tape, var_widths, funcs, max_width: int, ops=None, widths=None):
         self.rng, self.t, self.vw, self.funcs, self.maxw = rng, tape, var_widths, funcs, max_width
         self.ops = set(ops) if ops is not None else None
+        self.widths = widths
         self.pool = {}  # width -> list of bv nodes
 
     def allowed(self, op):
@@ -178,6 +179,8 @@ class _Fuzz:
         if r < 0.55 and self.allowed(Op.NEG):
             x = self.bv(w, depth - 1)
             return t.neg(x) if rng.random() < 0.5 else (t.bnot(x) if self.allowed(Op.BNOT) else x)
+        if self.widths is not None and r >= 0.65:
+            return self.bv_leaf(w)
         if r < 0.65 and self.allowed(Op.ITE):
             return t.ite(self.boolean(depth - 1), self.bv(w, depth - 1), self.bv(w, depth - 1))
         if r < 0.75 and self.allowed(Op.EXTRACT):
@@ -220,7 +223,7 @@ class _Fuzz:
             op = _PRED[int(rng.integers(len(_PRED)))]
             if not self.allowed(op):
                 op = Op.EQ
-            w = int(rng.choice([w for w in (1, 8, 32, 64, 160, 256, 512) if w <= self.maxw]))
+            w = int(rng.choice(self.widths or [w for w in (1, 8, 32, 64, 160, 256, 512) if w <= self.maxw]))
             a = self.bv(w, depth - 1)
             b = self.bv(w, depth - 1) if rng.random() < 0.7 else a
             if op == Op.EQ and rng.random() < 0.3:
@@ -245,16 +248,25 @@ class _Fuzz:
 
 
 def fuzz_tape(rng: np.random.Generator, var_widths: Sequence[int], funcs: Sequence[FuncSpec] = (),
-              depth: int = 4, max_width: int = 256, ops=None) -> Tape:
+              depth: int = 4, max_width: int = 256, ops=None, widths=None) -> Tape:
     t = Tape()
-    fz = _Fuzz(rng, t, var_widths, funcs, max_width, ops)
+    fz = _Fuzz(rng, t, var_widths, funcs, max_width, ops, widths)
     root = fz.boolean(depth)
     return t.finish(root)
 
 
+# the op set of the gfx950 assembly interpreter (full-width 256-bit arithmetic, Bool logic)
+ASM_OPS = frozenset({Op.ADD, Op.SUB, Op.MUL, Op.NEG, Op.BNOT, Op.BAND, Op.BOR, Op.BXOR, Op.ITE,
+                     Op.EQ, Op.ULT, Op.ULE, Op.SLT, Op.SLE})
+
+
 def fuzz_workload(seed: int, n_tapes: int, n_models: int, max_width: int = 256, depth: int = 4,
-                  with_funcs: bool = True, ops=None):
+                  with_funcs: bool = True, ops=None, asm_only: bool = False):
     rng = np.random.Generator(np.random.PCG64(seed))
+    if asm_only:
+        var_widths = [256] * 8
+        tapes = [fuzz_tape(rng, var_widths, (), depth, 256, ASM_OPS, widths=[256]) for _ in range(n_tapes)]
+        return TapeBatch(tapes), fuzz_models(rng, var_widths, n_models)
     widths = [w for w in (1, 8, 32, 64, 160, 256, 512) if w <= max_width]
     var_widths = [int(rng.choice(widths)) for _ in range(10)] + [256, 256, BOOL, 8]
     funcs: List[FuncSpec] = []

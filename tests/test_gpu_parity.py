@@ -146,3 +146,80 @@ def test_keccak_kernel(evaluator):
         assert d.hex() == k["digest"], k["name"]
     for m, d in zip(extra, out[len(msgs):]):
         assert d == keccak_ref.keccak256(m)
+
+
+# ---------------------------------------------------------------- assembly interpreter (qsa)
+def test_asm_interpreter_loaded(evaluator):
+    assert evaluator.asm_ready, "gfx950 assembly interpreter failed to load its handler table"
+
+
+def test_c2_runs_on_asm_path(evaluator):
+    tb, mb, exp = c2_workload(200, 3000, seed=4)
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    n_asm, n_l8, n_l16 = ct.split()
+    assert (n_asm, n_l8, n_l16) == (200, 0, 0)
+    assert (evaluator.first_hit(ct) == exp).all()
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_asm_fuzz_matches_oracle_and_generic(evaluator, seed):
+    from mythril_amd.synth import fuzz_workload as fw
+    tb, mb = fw(500 + seed, 80, 700, depth=6, asm_only=True)
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    assert ct.split()[0] == tb.n_tapes
+    v_asm, fh_asm = evaluator.verdicts(tb)
+    ref = cref.verdicts(tb, mb)
+    mism = np.argwhere(v_asm != ref)
+    assert len(mism) == 0, f"{len(mism)} asm mismatches, first {mism[:5]}"
+    fh_ref, _ = cref.first_hit(tb, mb)
+    assert (evaluator.first_hit(ct) == fh_ref).all()
+    evaluator.use_asm(False)
+    try:
+        v_gen, _ = evaluator.verdicts(tb)
+        assert (evaluator.first_hit(ct) == fh_ref).all()
+    finally:
+        evaluator.use_asm(True)
+    assert (v_gen == ref).all()
+
+
+def test_golden_vectors_generic_kernel(evaluator):
+    """The same golden fixtures with the assembly path disabled (HIP C++ interpreter only)."""
+    entries = load("shift_vectors.json") + load("vmtests_kats.json")
+    tapes = []
+    for e in entries:
+        exp = int(e["expected"], 16)
+        tapes.append(check_tape(e, exp))
+        tapes.append(check_tape(e, exp, negate=True))
+    tb = TapeBatch(tapes)
+    evaluator.upload_models(_one_model())
+    evaluator.use_asm(False)
+    try:
+        v, _ = evaluator.verdicts(tb)
+    finally:
+        evaluator.use_asm(True)
+    assert v[0::2, 0].all() and not v[1::2, 0].any()
+
+
+def test_asm_with_temps_and_bool_sharing(evaluator):
+    """Shared BV and Bool subterms go through LDS temps in the assembly interpreter."""
+    rng = np.random.default_rng(11)
+    M = 500
+    words = rng.integers(0, 1 << 32, size=(64, M), dtype=np.uint64).astype(np.uint32)
+    mb = ModelBatch([256] * 8, words)
+    tapes = []
+    for k in range(20):
+        t = Tape()
+        x, y, z = t.var(k % 8, 256), t.var((k + 3) % 8, 256), t.var((k + 5) % 8, 256)
+        s = t.mul(t.add(x, y), z)                   # shared BV subterm
+        c = t.ult(s, t.bnot(s))                      # shared Bool subterm
+        root = t.and_(t.or_(c, t.eq(s, x)), t.not_(t.and_(c, t.eq(t.band(s, y), t.const(k, 256)))),
+                      t.bite(c, t.ule(x, s), t.slt(s, y)))
+        tapes.append(t.finish(root))
+    tb = TapeBatch(tapes)
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    assert ct.split()[0] == len(tapes)
+    v, _ = evaluator.verdicts(tb)
+    assert (v == cref.verdicts(tb, mb)).all()
