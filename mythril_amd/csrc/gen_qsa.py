@@ -275,6 +275,9 @@ def frame():
         # wave / lane / model index
         "v_and_b32 v4, 63, v3",
         "v_lshrrev_b32 v5, 6, v3",
+        # gfx950 hazard: a VALU write of a VGPR followed by v_readfirstlane of it needs wait
+        # states, or the read returns the register's previous (stale) contents
+        "s_nop 1",
         "v_readfirstlane_b32 s34, v5",
         "s_nop 1",
         "s_lshl_b32 s35, s96, 8",
