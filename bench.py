@@ -76,6 +76,20 @@ def cpu_baseline(tb, mb, target_s: float):
                       f"(OpenMP {cores} threads), {dt:.1f} s", "seconds": dt}
 
 
+def pmc_traffic(workload_key: str):
+    """HBM bytes per launch of the evaluation kernel from the committed rocprofv3 PMC summary of
+    this exact workload (profiles/, FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; see
+    tools/rocpd_summary.py).  None if no summary matches."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            table = json.load(f)
+    except OSError:
+        return None
+    e = table.get(workload_key)
+    return None if e is None else {"bytes": e["fetch_bytes"] + e["write_bytes"], "source": e["source"]}
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -126,16 +140,14 @@ def main():
         print(f"[rank {rank}] first-hit mismatch on {len(bad)} tapes, e.g. {bad[:5]}", file=sys.stderr)
 
     ev.counters(reset=True)
-    kstart = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    kend = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    # HIP event pair recorded by libmq on `stream` around the evaluation kernel(s) of each launch
+    ev.time_kernels(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        kstart[i].record(stream)
         ev.launch_first_hit(ct, best.data_ptr(), sptr)
-        kend[i].record(stream)
         if world > 1:
             dist.all_reduce(best, op=dist.ReduceOp.MIN)
         ev.finalize_first_hit(ct, best.data_ptr(), sptr)
@@ -144,7 +156,10 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     pairs, node_evals, alg_ops = ev.counters(reset=True)
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in zip(kstart, kend)]))
+    ktimes = ev.kernel_times(reset=True)
+    ev.time_kernels(False)
+    assert len(ktimes) == args.steps, ktimes
+    kern_ms = float(np.mean(ktimes))
 
     stats = torch.tensor([elapsed, node_evals, alg_ops, float(ok)], dtype=torch.float64, device=dev)
     if world > 1:
@@ -163,6 +178,8 @@ def main():
         model_bytes = mb.var_words.nbytes
         tape_bytes = tb.nodes.nbytes + tb.consts.nbytes + 4 * tb.n_tapes
         hbm_gbs = (model_bytes + tape_bytes) / (kern_ms * 1e-3) / 1e9
+        wkey = f"c2:n{tb.n_tapes}:m{M}:s{args.seed}"
+        traffic = pmc_traffic(wkey)
         out = {
             "metric": "256-bit constraint-node x model evals/s",
             "value": node_evals / elapsed,
@@ -185,8 +202,11 @@ def main():
             },
             "roofline": {
                 "bound": "valu", "achieved": achieved_tops, "peak": VALU_PEAK_TOPS, "unit": "TOPS (int32 VALU)",
-                "frac": achieved_tops / VALU_PEAK_TOPS, "traffic": None,
-                "kernel": "qs_first_hit_kernel<8,8>", "kernel_ms": kern_ms,
+                "frac": achieved_tops / VALU_PEAK_TOPS,
+                "traffic": traffic["bytes"] if traffic else None,
+                "traffic_source": traffic["source"] if traffic else None,
+                "kernel": "mq::qsa_kernel (gfx950 threaded-code interpreter)", "kernel_ms": kern_ms,
+                "alg_bytes_per_launch": model_bytes + tape_bytes,
                 "alg_ops_per_launch": per_launch_ops,
                 "hbm_alg_GBps": hbm_gbs, "hbm_frac": hbm_gbs / HBM_PEAK_GBS,
             },

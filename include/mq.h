@@ -220,9 +220,16 @@ int mq_keccak256(mq_ctx* ctx, const uint8_t* data, const int64_t* offsets, int32
 /* Context options.  MQ_OPT_USE_ASM (default 1): run eligible 256-bit tapes on the gfx950
    assembly interpreter, the rest on the HIP C++ interpreter (0: HIP C++ for all — the A/B and
    parity cross-check).  MQ_OPT_EARLY_EXIT (default 1): waves skip a tape once a lower first
-   hit is published.  MQ_OPT_ASM_READY (query): returns 1 if the assembly interpreter loaded. */
-enum mq_option { MQ_OPT_USE_ASM = 1, MQ_OPT_EARLY_EXIT = 2, MQ_OPT_ASM_READY = 3 };
+   hit is published.  MQ_OPT_ASM_READY (query): returns 1 if the assembly interpreter loaded.
+   MQ_OPT_TIME_KERNELS (default 0): bracket the evaluation kernels of every launch with a HIP
+   event pair on the launch stream (read back with mq_kernel_times; setting it clears them). */
+enum mq_option { MQ_OPT_USE_ASM = 1, MQ_OPT_EARLY_EXIT = 2, MQ_OPT_ASM_READY = 3, MQ_OPT_TIME_KERNELS = 4 };
 int mq_ctx_set_option(mq_ctx* ctx, int option, int value);
+
+/* Device durations (ms) of the evaluation kernels of each launch since the last reset, in
+   launch order (MQ_OPT_TIME_KERNELS on).  Waits for those launches.  *n_out = number recorded
+   (may exceed max_out; only max_out are written).  reset != 0 forgets them. */
+int mq_kernel_times(mq_ctx* ctx, float* out_ms, int32_t max_out, int32_t* n_out, int reset);
 
 /* How a compiled batch is split: tapes on the assembly interpreter, on the generic 256-bit
    and on the 512-bit HIP C++ kernels (any pointer may be NULL). */

@@ -57,6 +57,7 @@ def load_library(path: str = LIB_PATH):
         L.mq_finalize_first_hit.argtypes = [P, P, P, P]
         L.mq_counters.argtypes = [P, C.POINTER(C.c_double), C.c_int]
         L.mq_ctx_set_option.argtypes = [P, C.c_int, C.c_int]
+        L.mq_kernel_times.argtypes = [P, C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_int32), C.c_int]
         L.mq_tapes_info.argtypes = [P] + [C.POINTER(C.c_int32)] * 3
         L.mq_eval_verdicts.argtypes = [P, C.POINTER(MqTapeBatch), C.POINTER(C.c_uint8), C.POINTER(C.c_int32)]
         L.mq_keccak256.argtypes = [P, C.POINTER(C.c_uint8), C.POINTER(C.c_int64), C.c_int32, C.POINTER(C.c_uint8)]
@@ -153,7 +154,7 @@ class Evaluator:
         self.n_models = 0
         self.index_base = 0
 
-    OPT_USE_ASM, OPT_EARLY_EXIT, OPT_ASM_READY = 1, 2, 3
+    OPT_USE_ASM, OPT_EARLY_EXIT, OPT_ASM_READY, OPT_TIME_KERNELS = 1, 2, 3, 4
 
     def set_option(self, option: int, value: int) -> int:
         rc = self.lib.mq_ctx_set_option(self.ctx, option, value)
@@ -214,6 +215,18 @@ class Evaluator:
     def finalize_first_hit(self, ct: CompiledTapes, device_ptr: int, stream: int = 0) -> None:
         _check(self.lib.mq_finalize_first_hit(self.ctx, ct.handle, C.c_void_p(device_ptr), C.c_void_p(stream or None)),
                "mq_finalize_first_hit")
+
+    def time_kernels(self, on: bool = True) -> None:
+        """Bracket the evaluation kernels of every launch with HIP events (clears old ones)."""
+        self.set_option(self.OPT_TIME_KERNELS, 1 if on else 0)
+
+    def kernel_times(self, reset: bool = True) -> List[float]:
+        """Per-launch device time (ms) of the evaluation kernels since the last reset."""
+        n = C.c_int32()
+        _check(self.lib.mq_kernel_times(self.ctx, None, 0, C.byref(n), 0), "mq_kernel_times")
+        buf = (C.c_float * max(n.value, 1))()
+        _check(self.lib.mq_kernel_times(self.ctx, buf, n.value, C.byref(n), 1 if reset else 0), "mq_kernel_times")
+        return [float(buf[i]) for i in range(n.value)]
 
     def counters(self, reset: bool = False):
         """(pairs evaluated, node-evals, algorithmic ops) accumulated on the device."""

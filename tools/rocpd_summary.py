@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 SQLite output (run_results.db) into the JSON kept under profiles/.
+
+  (kernels are keyed by name and grid size, so a launch-shape probe does not dilute averages)
+  kernel-trace db  -> per-kernel calls / total / average / min / max duration (ns)
+  --pmc db         -> per-kernel average of each counter per dispatch
+
+FETCH_SIZE / WRITE_SIZE are reported in KB as rocprofv3 gives them, plus the corrected byte
+count per dispatch: on gfx950 FETCH_SIZE counts half of the bytes of wide coalesced reads
+(MI355X_MICROARCH.md, HBM section), so fetch_bytes = 2 * 1024 * FETCH_SIZE.
+usage: rocpd_summary.py OUT.json kt=DB [pmc=DB ...]
+"""
+import json
+import sqlite3
+import sys
+
+
+def kernel_stats(db):
+    c = sqlite3.connect(db)
+    rows = c.execute(
+        "select name || ' grid=' || (grid_x*grid_y*grid_z), count(*), sum(duration), avg(duration), min(duration), max(duration), max(vgpr_count), max(sgpr_count), max(scratch_size), max(lds_size) "
+        "from kernels group by 1 order by sum(duration) desc").fetchall()
+    return [{"kernel": r[0], "calls": r[1], "total_ns": r[2], "avg_ns": r[3], "min_ns": r[4], "max_ns": r[5],
+             "vgpr": r[6], "sgpr": r[7], "scratch": r[8], "lds": r[9]} for r in rows]
+
+
+def pmc_stats(db):
+    c = sqlite3.connect(db)
+    rows = c.execute(
+        "select kernel_name || ' grid=' || grid_size, counter_name, count(*), avg(value) from counters_collection "
+        "group by 1, counter_name").fetchall()
+    out = {}
+    for k, name, n, v in rows:
+        d = out.setdefault(k, {"dispatches": n})
+        d[name] = v
+        if name == "FETCH_SIZE":
+            d["fetch_bytes_corrected"] = 2 * 1024 * v
+        if name == "WRITE_SIZE":
+            d["write_bytes"] = 1024 * v
+    return out
+
+
+def main():
+    out_path = sys.argv[1]
+    res = {"kernel_trace": None, "pmc": {}}
+    for arg in sys.argv[2:]:
+        kind, db = arg.split("=", 1)
+        if kind == "kt":
+            res["kernel_trace"] = kernel_stats(db)
+        else:
+            for k, d in pmc_stats(db).items():
+                res["pmc"].setdefault(k, {}).update(d)
+    with open(out_path, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res, indent=1)[:3000])
+
+
+if __name__ == "__main__":
+    main()
