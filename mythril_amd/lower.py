@@ -1,0 +1,212 @@
+"""Lowering pass: constraint terms -> tape IR, candidate models -> SoA model batch.
+
+This is the build's counterpart of the step ``model_cache.check_quick_sat(simplify(And(*constraints)).raw)``
+(reference ``mythril/support/model.py:101``): the conjunction handed to quick-sat is flattened
+into a postfix tape (include/mq.h) and the candidate models into the ``mq_model_batch`` layout.
+It lowers the z3-free terms of :mod:`mythril_amd.smt`; :mod:`mythril_amd.lower_z3` walks real
+z3 ASTs into the same :class:`SymbolTable` and tape.
+
+Fail closed: anything outside the vocabulary (array-valued ``ite``, array equality, functions of
+arity > 2, widths > 65535) raises :class:`LoweringError`; the query then keeps the reference's
+z3 evaluation path.
+
+``z3.simplify`` preserves equivalence over all interpretations and completion makes evaluation
+total, so lowering the raw conjunction or its simplified form yields the same verdict on every
+model ("Equivalence lets the lowering choose its input").
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Sequence, Tuple
+
+import numpy as np
+
+from . import smt as S
+from .exceptions import LoweringError
+from .models import FuncSpec, ModelBatch
+from .smt_model import Model
+from .tape import BOOL, NONE, Tape, TapeBatch, limbs, to_words
+
+MAX_WIDTH = 0xFFFF
+
+
+class SymbolTable:
+    """Free constants -> model variable indices; UFs and symbolic arrays -> model function ids.
+
+    A constant is identified by (name, width) — z3 declarations with equal names but different
+    sorts are different declarations.  A symbolic array ``Array(name, dom, rng)`` is read through
+    the model's interpretation of ``name`` (its ``as-array`` function, arity 1)."""
+
+    def __init__(self) -> None:
+        self.vars: Dict[Tuple[str, int], int] = {}
+        self.var_widths: List[int] = []
+        self.funcs: Dict[str, int] = {}
+        self.func_specs: List[FuncSpec] = []
+        self.func_names: List[str] = []
+
+    def var(self, name: str, width: int) -> int:
+        key = (name, width)
+        i = self.vars.get(key)
+        if i is None:
+            i = len(self.var_widths)
+            self.vars[key] = i
+            self.var_widths.append(width)
+        return i
+
+    def func(self, name: str, arg_widths: Sequence[int], result_width: int) -> int:
+        i = self.funcs.get(name)
+        spec = FuncSpec(len(arg_widths), result_width, tuple(arg_widths))
+        if i is None:
+            if not 1 <= len(arg_widths) <= 2:
+                raise LoweringError(f"function {name}: arity {len(arg_widths)} not supported")
+            i = len(self.func_specs)
+            self.funcs[name] = i
+            self.func_specs.append(spec)
+            self.func_names.append(name)
+        elif self.func_specs[i] != spec:
+            raise LoweringError(f"function {name} used with two signatures")
+        return i
+
+
+def _w(t: S.Term) -> int:
+    if t.width > MAX_WIDTH:
+        raise LoweringError(f"width {t.width} exceeds the tape format")
+    return t.width
+
+
+def lower_term(root: S.Term, syms: SymbolTable) -> Tape:
+    """Lower one Bool term (the quick-sat conjunction) to a tape; iterative over the DAG."""
+    if root.sort != "bool":
+        raise LoweringError("quick-sat root must be Bool")
+    tp = Tape()
+    node: Dict[int, int] = {}
+    for t in S.walk(root):
+        k = t.kind
+        a = [node[id(x)] for x in t.args]
+        if k == S.SYM:
+            r = tp.var(syms.var(t.params[0], _w(t)), _w(t))
+        elif k == S.VAL:
+            r = tp.const(t.params[0], _w(t))
+        elif k == S.TRUE:
+            r = tp.true()
+        elif k == S.FALSE:
+            r = tp.false()
+        elif k == S.NOT:
+            r = tp.not_(a[0])
+        elif k == S.AND:
+            r = tp.and_(*a)
+        elif k == S.OR:
+            r = tp.or_(*a)
+        elif k == S.XOR:
+            r = tp.xor(a[0], a[1])
+        elif k == S.IMPLIES:
+            r = tp.implies(a[0], a[1])
+        elif k == S.IFF:
+            r = tp.iff(a[0], a[1])
+        elif k == S.BITE:
+            r = tp.bite(a[0], a[1], a[2])
+        elif k == S.EQ:
+            if t.args[0].sort == "array":
+                raise LoweringError("array equality")
+            r = tp.eq(a[0], a[1])
+        elif k == S.BVULT:
+            r = tp.ult(a[0], a[1])
+        elif k == S.BVULE:
+            r = tp.ule(a[0], a[1])
+        elif k == S.BVSLT:
+            r = tp.slt(a[0], a[1])
+        elif k == S.BVSLE:
+            r = tp.sle(a[0], a[1])
+        elif k == S.UMUL_NOOVFL:
+            r = tp.umul_noovfl(a[0], a[1])
+        elif k == S.SMUL_NOOVFL:
+            r = tp.smul_noovfl(a[0], a[1])
+        elif k == S.SMUL_NOUDFL:
+            r = tp.smul_noudfl(a[0], a[1])
+        elif k in _BIN:
+            r = getattr(tp, _BIN[k])(a[0], a[1])
+        elif k == S.NEG:
+            r = tp.neg(a[0])
+        elif k == S.BNOT:
+            r = tp.bnot(a[0])
+        elif k == S.EXTRACT:
+            r = tp.extract(t.params[0], t.params[1], a[0])
+        elif k == S.CONCAT:
+            _w(t)
+            r = tp.concat(a[0], a[1])
+        elif k == S.ZEXT:
+            r = tp.zext(t.params[0], a[0])
+        elif k == S.SEXT:
+            r = tp.sext(t.params[0], a[0])
+        elif k == S.ITE:
+            r = tp.ite(a[0], a[1], a[2])
+        elif k == S.ARRAY_SYM:
+            r = tp.array_var(syms.func(t.params[0], (t.domain,), t.width), t.width)
+        elif k == S.CONST_ARRAY:
+            r = tp.const_array(a[0])
+        elif k == S.STORE:
+            r = tp.store(a[0], a[1], a[2])
+        elif k == S.SELECT:
+            r = tp.select(a[0], a[1])
+        elif k == S.APP:
+            name, dom = t.params
+            r = tp.uf(syms.func(name, dom, t.width), t.width, *a)
+        else:
+            raise LoweringError(f"term kind {k!r} not in the tape vocabulary")
+        node[id(t)] = r
+    return tp.finish(node[id(root)])
+
+
+_BIN = {S.ADD: "add", S.SUB: "sub", S.MUL: "mul", S.UDIV: "udiv", S.UREM: "urem", S.SDIV: "sdiv",
+        S.SREM: "srem", S.SMOD: "smod", S.BAND: "band", S.BOR: "bor", S.BXOR: "bxor",
+        S.SHL: "shl", S.LSHR: "lshr", S.ASHR: "ashr"}
+
+
+def lower_batch(roots: Sequence[S.Term], syms: SymbolTable = None):
+    """Lower N conjunctions over one shared symbol table.  Returns ``(TapeBatch | None, syms,
+    supported_mask)``: a root that fails to lower is replaced by a FALSE placeholder tape and
+    flagged unsupported (the caller routes it to z3)."""
+    syms = syms or SymbolTable()
+    tapes, ok = [], np.ones(len(roots), bool)
+    for i, r in enumerate(roots):
+        try:
+            tapes.append(lower_term(r, syms))
+        except (LoweringError, TypeError):
+            ok[i] = False
+            t = Tape()
+            tapes.append(t.finish(t.false()))
+    return (TapeBatch(tapes) if tapes else None), syms, ok
+
+
+def serialize_models(models: Sequence[Model], syms: SymbolTable, index_base: int = 0) -> ModelBatch:
+    """Candidate models (global order, index 0 = MRU) -> ``mq_model_batch`` (SoA u32 limbs +
+    per-function CSR tables), WITHOUT completion: an absent constant stays 0 / false and an
+    absent function has no entries and else 0."""
+    M = len(models)
+    widths = syms.var_widths
+    off = np.zeros(len(widths) + 1, np.int64)
+    off[1:] = np.cumsum([limbs(w) for w in widths])
+    words = np.zeros((int(off[-1]), M), np.uint32)
+    names = [None] * len(widths)
+    for (name, w), i in syms.vars.items():
+        names[i] = (name, w)
+    for m, mod in enumerate(models):
+        asg = mod.assignment
+        for i, (name, w) in enumerate(names):
+            v = asg.get(name)
+            if v is None:
+                continue
+            v = int(v) & ((1 << max(w, 1)) - 1)
+            words[off[i]:off[i + 1], m] = to_words(v, w)
+    fmodels = []
+    for mod in models:
+        fm = {}
+        for f, name in enumerate(syms.func_names):
+            interp = mod.functions.get(name)
+            if interp is not None:
+                fm[f] = interp
+        fmodels.append({"funcs": fm})
+    if not syms.func_specs:
+        return ModelBatch(widths, words, index_base=index_base)
+    fb = ModelBatch.from_python(widths or [], fmodels, syms.func_specs, index_base)
+    return ModelBatch(widths, words, syms.func_specs, fb.entry_ptr, fb.entry_words, fb.entry_base,
+                      fb.else_words, fb.else_base, index_base)

@@ -1,0 +1,431 @@
+"""Drop-in mirrors of the reference's quick-sat boundary, backed by the MI355X evaluator.
+
+Reference interface, kept name for name:
+
+* ``LRUCache``            ``mythril/support/support_utils.py:34-53``
+* ``ModelCache``          ``support_utils.py:56-70`` — ``check_quick_sat(constraints)`` returns the
+  first cached model (MRU first) under which the conjunction evaluates to literally ``true``,
+  bumps it to MRU, and is memoized per ``(self, constraints)`` by ``functools.lru_cache(2**10)``
+  (a memoized ``False`` or hit is returned again without re-evaluation and without a bump);
+* ``get_model``           ``mythril/support/model.py:68-130`` (gating, exceptions, quick-sat iff no
+  minimize/maximize, solver fallback in a ``ThreadPool(1)`` with timeout, cache insert on sat),
+  memoized by ``lru_cache(2**23)``;
+* ``model_cache``         ``model.py:25`` (the process-global instance).
+
+What changes is HOW ``check_quick_sat`` decides: instead of ``deepcopy(model).eval(...)`` per model
+in a Python loop (support_utils.py:62-64), the conjunction is lowered to a tape and evaluated against
+every cached model in one launch of the HIP kernels (``mq_eval_verdicts``, include/mq.h); the
+first-hit/bump/memo logic then runs exactly as the reference's loop would.
+
+Batching without changing semantics: :meth:`ModelCache.prefetch` evaluates N
+pending conjunctions against the current cache in ONE launch.  The queries are still answered
+one at a time, in the caller's order, through the unchanged ``check_quick_sat``: a bump reorders
+candidates exactly as in the sequential loop, and a model inserted mid-batch (a z3 fallback) is
+evaluated lazily for every still-pending conjunction in one more launch.  The answers are
+therefore identical to the sequential reference for any interleaving.
+
+Fail closed: a conjunction the lowering or the tape compiler cannot express is answered by the
+reference's own z3 eval loop where z3 exists (:mod:`mythril_amd.lower_z3`); without z3 it gets no
+quick answer (``False``) and goes to the solver, which is what a quick-sat miss does anyway.
+There is no CPU evaluator: if the HIP library or the GPU is missing, :class:`EvaluatorError` is
+raised.
+"""
+from __future__ import annotations
+
+import logging
+import math
+import os
+import sys
+import threading
+import time
+from collections import OrderedDict
+from functools import lru_cache
+from multiprocessing import TimeoutError as _PoolTimeout
+from multiprocessing.pool import ThreadPool
+from typing import Callable, Dict, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import smt as S
+from .exceptions import SolverTimeOutException, UnsatError
+from .smt_model import Model, as_record
+
+log = logging.getLogger(__name__)
+
+
+# ---------------------------------------------------------------------------- support_utils.py
+class Singleton(type):
+    """support_utils.py:14-31 (not thread-safe, as documented there)."""
+    _instances: Dict = {}
+
+    def __call__(cls, *args, **kwargs):
+        if cls not in cls._instances:
+            cls._instances[cls] = super().__call__(*args, **kwargs)
+        return cls._instances[cls]
+
+
+class LRUCache:
+    """support_utils.py:34-53: ``get`` moves the key to MRU (or returns -1); ``put`` re-inserts at
+    MRU and evicts the LRU entry when a NEW key arrives at capacity."""
+
+    def __init__(self, size: int):
+        self.size = size
+        self.lru_cache: "OrderedDict" = OrderedDict()
+
+    def get(self, key):
+        if key not in self.lru_cache:
+            return -1
+        self.lru_cache.move_to_end(key)
+        return self.lru_cache[key]
+
+    def put(self, key, value) -> None:
+        if key in self.lru_cache:
+            del self.lru_cache[key]
+        elif len(self.lru_cache) >= self.size:
+            self.lru_cache.popitem(last=False)
+        self.lru_cache[key] = value
+
+
+class Args(metaclass=Singleton):
+    """The hot-path subset of ``Args`` (mythril/support/support_args.py:5-27)."""
+
+    def __init__(self):
+        self.solver_timeout = 10000
+        self.pruning_factor = None
+        self.solver_log = None
+        self.parallel_solving = False
+
+
+args = Args()
+
+
+class TimeHandler(metaclass=Singleton):
+    """``time_handler`` (mythril/laser/ethereum/time_handler.py:5-18).  Before
+    ``start_execution`` the budget is unbounded (the reference would fail on ``None``)."""
+
+    def __init__(self):
+        self._start_time = None
+        self._execution_time = None
+
+    def start_execution(self, execution_time) -> None:
+        self._start_time = int(time.time() * 1000)
+        self._execution_time = execution_time * 1000
+
+    def time_remaining(self):
+        if self._start_time is None:
+            return math.inf
+        return self._execution_time - (int(time.time() * 1000) - self._start_time)
+
+
+time_handler = TimeHandler()
+
+
+# ---------------------------------------------------------------------------- verdict engine
+class VerdictEngine:
+    """Lowers conjunctions + candidate models and evaluates them on the GPU.
+
+    ``rows(exprs, models)`` -> one ``bool[len(models)]`` verdict row per expression (``None`` =
+    unsupported: fail closed).  Works on z3-free terms (:mod:`mythril_amd.smt`) and, on a z3 host,
+    on z3 ``BoolRef`` (lowered by :mod:`mythril_amd.lower_z3`)."""
+
+    def __init__(self, evaluator=None):
+        self._ev = evaluator
+        self.launches = 0
+        self.pairs = 0
+
+    @property
+    def evaluator(self):
+        if self._ev is None:
+            from .evaluator import default_evaluator
+            self._ev = default_evaluator()
+        return self._ev
+
+    def rows(self, exprs: Sequence, models: Sequence) -> List[Optional[np.ndarray]]:
+        if not exprs:
+            return []
+        if not models:
+            return [np.zeros(0, bool) for _ in exprs]
+        if all(isinstance(e, S.Term) for e in exprs):
+            from .lower import lower_batch, serialize_models
+            tb, syms, ok = lower_batch(exprs)
+            mb = serialize_models([as_record(m) for m in models], syms)
+        else:
+            from .lower_z3 import lower_batch_z3
+            tb, mb, ok = lower_batch_z3(exprs, models)
+        ev = self.evaluator
+        ev.upload_models(mb)
+        v, fh = ev.verdicts(tb)
+        self.launches += 1
+        self.pairs += tb.n_tapes * mb.n_models
+        out: List[Optional[np.ndarray]] = []
+        for i in range(len(exprs)):
+            out.append(v[i].copy() if ok[i] and fh[i] != -2 else None)
+        return out
+
+
+_UNSUPPORTED = object()
+
+
+# ---------------------------------------------------------------------------- ModelCache
+class ModelCache:
+    """support_utils.py:56-70 with the GPU verdict engine behind ``check_quick_sat``."""
+
+    def __init__(self, engine: Optional[VerdictEngine] = None):
+        self.model_cache = LRUCache(size=100)
+        self.engine = engine or VerdictEngine()
+        # expr -> {model: verdict} for conjunctions evaluated ahead of their check_quick_sat call
+        self._rows: Dict[object, object] = {}
+        self._pending: "OrderedDict[object, None]" = OrderedDict()
+        self.stats = {"queries": 0, "hits": 0, "unsupported": 0}
+
+    # support_utils.py:60-67
+    @lru_cache(maxsize=2 ** 10)
+    def check_quick_sat(self, constraints):
+        self.stats["queries"] += 1
+        order = list(reversed(self.model_cache.lru_cache.keys()))
+        row = self._verdicts(constraints, order)
+        if row is _UNSUPPORTED:
+            self.stats["unsupported"] += 1
+            return self._fallback(constraints, order)
+        for model, ok in zip(order, row):
+            if ok:
+                self.model_cache.put(model, self.model_cache.get(model) + 1)
+                self.stats["hits"] += 1
+                return model
+        return False
+
+    def put(self, key, value) -> None:
+        self.model_cache.put(key, value)
+
+    # -------------------------------------------------------------- batching
+    def prefetch(self, exprs: Iterable) -> None:
+        """Evaluate pending conjunctions against the current cache in one launch (a10)."""
+        exprs = [e for e in dict.fromkeys(exprs) if e not in self._rows]
+        order = list(reversed(self.model_cache.lru_cache.keys()))
+        for e in exprs:
+            self._rows[e] = {}
+            self._pending[e] = None
+        if exprs and order:
+            self._fill(exprs, order)
+
+    def check_quick_sat_batch(self, exprs: Sequence) -> list:
+        """``[check_quick_sat(e) for e in exprs]`` with one GPU launch for the whole batch."""
+        self.prefetch(exprs)
+        return [self.check_quick_sat(e) for e in exprs]
+
+    def _fill(self, exprs: List, models: List) -> None:
+        rows = self.engine.rows(exprs, models)
+        for e, r in zip(exprs, rows):
+            d = self._rows[e]
+            if d is _UNSUPPORTED:
+                continue
+            if r is None:
+                self._rows[e] = _UNSUPPORTED
+                continue
+            for m, ok in zip(models, r):
+                d[m] = bool(ok)
+
+    def _verdicts(self, expr, order):
+        if expr not in self._rows:
+            self._rows[expr] = {}
+            self._pending[expr] = None
+        d = self._rows[expr]
+        if d is not _UNSUPPORTED:
+            missing = [m for m in order if m not in d]
+            if missing:
+                # evaluate every still-pending conjunction against the new models in one launch
+                batch = [expr] + [e for e in self._pending if e is not expr and self._rows.get(e) is not _UNSUPPORTED]
+                self._fill(batch, missing)
+                d = self._rows[expr]
+        self._rows.pop(expr, None)
+        self._pending.pop(expr, None)
+        if d is _UNSUPPORTED:
+            return _UNSUPPORTED
+        return [d[m] for m in order]
+
+    def _fallback(self, constraints, order):
+        """Unsupported conjunction: the reference's own loop where z3 exists, else no quick answer."""
+        if isinstance(constraints, S.Term):
+            return False
+        from .lower_z3 import z3_quick_sat_loop
+        model = z3_quick_sat_loop(constraints, order)
+        if model is not False:
+            self.model_cache.put(model, self.model_cache.get(model) + 1)
+        return model
+
+
+# ---------------------------------------------------------------------------- model.py
+class SolverBackend:
+    """What ``solver_worker`` needs from an SMT solver (model.py:28-65): ``solve`` returns
+    ``(status, model_factory)`` with status in {"sat", "unsat", "unknown"} and ``model_factory()``
+    producing a fresh model object (``s.model()``, called twice at model.py:125-126)."""
+
+    def solve(self, constraints, minimize, maximize, timeout_ms) -> Tuple[str, Optional[Callable]]:
+        raise NotImplementedError
+
+
+class NoSolver(SolverBackend):
+    """No SMT solver available (this container / the GPU box have no z3): every miss is
+    ``unknown`` -> SolverTimeOutException, i.e. what the reference does when z3 gives up."""
+
+    def solve(self, constraints, minimize, maximize, timeout_ms):
+        return "unknown", None
+
+
+def _default_backend() -> SolverBackend:
+    try:
+        from .lower_z3 import Z3Backend
+        return Z3Backend()
+    except ImportError:
+        return NoSolver()
+
+
+model_cache = ModelCache()
+solver_backend: SolverBackend = None  # type: ignore[assignment]
+counters = {"get_model_calls": 0, "quick_sat_answers": 0, "solver_calls": 0}
+
+
+def set_solver_backend(backend: Optional[SolverBackend]) -> None:
+    global solver_backend
+    solver_backend = backend
+
+
+def solver_worker(constraints, minimize=(), maximize=(), solver_timeout=None):
+    """model.py:28-65 (the ``--solver-log`` dump is the harvest hook of :mod:`mythril_amd.corpus`)."""
+    backend = solver_backend or _default_backend()
+    return backend.solve(constraints, minimize, maximize, solver_timeout)
+
+
+def simplify(expr):
+    """``simplify`` (smt/expression.py:64-71).  Lowering does not depend on z3's rewrites
+    (equivalence-preserving), so on z3-free terms this is the identity."""
+    return expr
+
+
+@lru_cache(maxsize=2 ** 23)
+def get_model(constraints, minimize=(), maximize=(), solver_timeout=None):
+    """model.py:68-130."""
+    counters["get_model_calls"] += 1
+    solver_timeout = solver_timeout or args.solver_timeout
+    solver_timeout = min(solver_timeout, time_handler.time_remaining())
+    if solver_timeout <= 0:
+        raise SolverTimeOutException
+    for constraint in constraints:
+        if isinstance(constraint, bool) and not constraint:
+            raise UnsatError
+    if not isinstance(constraints, tuple):
+        constraints = constraints.get_all_constraints()
+    constraints = [c for c in constraints if not isinstance(c, bool)]
+
+    if len(maximize) + len(minimize) == 0:
+        ret_model = model_cache.check_quick_sat(simplify(S.And(*constraints)))
+        if ret_model:
+            counters["quick_sat_answers"] += 1
+            return ret_model
+    counters["solver_calls"] += 1
+    pool = ThreadPool(1)
+    try:
+        res = pool.apply_async(solver_worker, args=(constraints, minimize, maximize, solver_timeout))
+        try:
+            status, factory = res.get(None if math.isinf(solver_timeout) else solver_timeout / 1000.0)
+        except _PoolTimeout:
+            status, factory = "unknown", None
+        except Exception:
+            log.warning("Encountered an exception while solving expression")
+            status, factory = "unknown", None
+    finally:
+        pool.terminate()
+
+    if status == "sat":
+        model_cache.model_cache.put(factory(), 1)
+        return factory()
+    if status == "unknown":
+        raise SolverTimeOutException
+    raise UnsatError
+
+
+# ---------------------------------------------------------------------------- constraints.py
+class Constraints(list):
+    """``Constraints`` (mythril/laser/ethereum/state/constraints.py:12-131) over z3-free terms."""
+
+    def __init__(self, constraint_list=None):
+        super().__init__(self._get_smt_bool_list(constraint_list or []))
+
+    def is_possible(self, solver_timeout=None) -> bool:
+        """constraints.py:28-43: a timeout under the default timeout prunes the state."""
+        try:
+            get_model(self, solver_timeout=solver_timeout)
+        except SolverTimeOutException:
+            return solver_timeout is not None
+        except UnsatError:
+            return False
+        return True
+
+    def get_model(self, solver_timeout=None):
+        try:
+            return get_model(self, solver_timeout=solver_timeout)
+        except UnsatError:  # includes SolverTimeOutException
+            return None
+
+    def append(self, constraint) -> None:
+        super().append(simplify(constraint) if isinstance(constraint, S.Term) else S.BoolVal(constraint))
+
+    @property
+    def as_list(self):
+        return self.get_all_constraints()
+
+    def get_all_constraints(self):
+        from .function_managers import keccak_function_manager
+        return self[:] + [keccak_function_manager.create_conditions()]
+
+    def __copy__(self):
+        return Constraints(list.copy(self))
+
+    def copy(self):
+        return self.__copy__()
+
+    def __deepcopy__(self, memodict=None):
+        return Constraints(list(self))  # terms are immutable and interned
+
+    def __add__(self, constraints):
+        return Constraints(list(self) + self._get_smt_bool_list(constraints))
+
+    def __iadd__(self, constraints):
+        super().__iadd__(self._get_smt_bool_list(constraints))
+        return self
+
+    @staticmethod
+    def _get_smt_bool_list(constraints):
+        return [c if isinstance(c, S.Term) else S.BoolVal(c) for c in constraints]
+
+    def __hash__(self):
+        return tuple(self[:]).__hash__()
+
+
+def quick_sat_expr(constraints) -> Optional[S.Term]:
+    """The conjunction ``get_model`` hands to quick-sat for ``constraints`` (model.py:92-101),
+    or None when get_model would not reach quick-sat (a Python ``False`` constraint)."""
+    for c in constraints:
+        if isinstance(c, bool) and not c:
+            return None
+    cs = constraints if isinstance(constraints, tuple) else constraints.get_all_constraints()
+    return simplify(S.And(*[c for c in cs if not isinstance(c, bool)]))
+
+
+def is_possible_batch(states: Sequence[Constraints], solver_timeout=None) -> List[bool]:
+    """Batched ``[c.is_possible(solver_timeout) for c in states]`` — the per-transaction
+    reachability loop (svm.py:278-283) and per-fork pruning (svm.py:351-358) with one GPU launch
+    for all quick-sat queries.  Answers are identical to the sequential loop (see module doc)."""
+    exprs = [e for e in (quick_sat_expr(c) for c in states) if e is not None]
+    model_cache.prefetch(exprs)
+    return [c.is_possible(solver_timeout=solver_timeout) for c in states]
+
+
+def reset_caches() -> None:
+    """Tests only: clear both memo layers and the candidate cache (the reference never does)."""
+    global model_cache
+    get_model.cache_clear()
+    engine = model_cache.engine
+    model_cache = ModelCache(engine)
+    for k in counters:
+        counters[k] = 0

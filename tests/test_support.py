@@ -1,0 +1,260 @@
+"""Host-side drop-in boundary (mythril_amd.support) on CPU: the reference semantics of
+LRUCache / ModelCache.check_quick_sat / get_model / Constraints.is_possible
+(support_utils.py:34-67, model.py:68-130, constraints.py:28-55), with the verdict engine
+replaced by the oracle (tests only — the product engine is the GPU)."""
+import random
+
+import numpy as np
+import pytest
+
+import keccak_ref
+from oracle_engine import OracleEngine, ReferenceLoopCache, eval_under
+from mythril_amd import smt as S
+from mythril_amd import support as sp
+from mythril_amd.exceptions import SolverTimeOutException, UnsatError
+from mythril_amd.function_managers import ExponentFunctionManager, KeccakFunctionManager
+from mythril_amd.smt_model import Model
+
+
+@pytest.fixture
+def cache():
+    return sp.ModelCache(OracleEngine())
+
+
+@pytest.fixture
+def fresh(monkeypatch):
+    """Fresh process-global caches with the oracle engine and a scripted solver."""
+    sp.reset_caches()
+    sp.model_cache = sp.ModelCache(OracleEngine())
+    yield
+    sp.reset_caches()
+    sp.set_solver_backend(None)
+
+
+x = S.BitVecSym("x", 256)
+y = S.BitVecSym("y", 256)
+
+
+def test_lru_cache_semantics():
+    c = sp.LRUCache(3)
+    for k in "abc":
+        c.put(k, 1)
+    assert c.get("a") == 1 and list(c.lru_cache) == ["b", "c", "a"]
+    assert c.get("zz") == -1
+    c.put("d", 1)                      # evicts LRU "b"
+    assert list(c.lru_cache) == ["c", "a", "d"]
+    c.put("c", 5)                      # existing key: moved to MRU, nothing evicted
+    assert list(c.lru_cache) == ["a", "d", "c"] and c.lru_cache["c"] == 5
+
+
+def test_first_hit_is_mru_first_and_bumps(cache):
+    m1, m2, m3 = Model({"x": 5}), Model({"x": 7}), Model({"x": 5})
+    for m in (m1, m2, m3):
+        cache.put(m, 1)
+    expr = S.And(x == 5)
+    assert cache.check_quick_sat(expr) is m3           # MRU first
+    assert cache.model_cache.lru_cache[m3] == 2
+    e2 = S.ULT(x, S.BitVecVal(6, 256))
+    assert cache.check_quick_sat(e2) is m3
+    assert list(cache.model_cache.lru_cache) == [m1, m2, m3]
+    assert cache.check_quick_sat(S.And(x == 7)) is m2  # bump m2 to MRU
+    assert list(cache.model_cache.lru_cache) == [m1, m3, m2]
+
+
+def test_memoized_false_and_memoized_hit(cache):
+    expr = S.And(x == 9)
+    cache.put(Model({"x": 1}), 1)
+    assert cache.check_quick_sat(expr) is False
+    m9 = Model({"x": 9})
+    cache.put(m9, 1)
+    assert cache.check_quick_sat(expr) is False         # memoized False (lru_cache, support_utils.py:60)
+    e2 = S.And(x == 1)
+    m1 = cache.check_quick_sat(e2)
+    cache.put(m9, 1)
+    before = list(cache.model_cache.lru_cache)
+    assert cache.check_quick_sat(e2) is m1              # memo hit: same model, no bump
+    assert list(cache.model_cache.lru_cache) == before
+
+
+def test_model_completion_defaults(cache):
+    m = Model({})                                       # nothing assigned: x -> 0, b -> false
+    cache.put(m, 1)
+    assert cache.check_quick_sat(S.And(x == 0)) is m
+    assert cache.check_quick_sat(S.Not(S.BoolSym("b"))) is m
+    arr = S.Array("balance", 256, 256)
+    assert cache.check_quick_sat(arr[x] == 0) is m      # absent array -> K(0)
+    f = S.Function("keccak256_512", [512], 256)
+    assert cache.check_quick_sat(f(S.BitVecSym("k", 512)) == 0) is m
+
+
+def test_uf_and_array_tables(cache):
+    f = S.Function("keccak256_512", [512], 256)
+    k = S.BitVecSym("k", 512)
+    m = Model({"k": 3}, {"keccak256_512": ({(3,): 0xABC}, 7), "balance": ({(5,): 100}, 1)})
+    cache.put(m, 1)
+    bal = S.Array("balance", 256, 256)
+    assert cache.check_quick_sat(f(k) == 0xABC) is m
+    assert cache.check_quick_sat(S.And(bal[S.BitVecVal(5, 256)] == 100, bal[x] == 1)) is m
+    assert cache.check_quick_sat(S.Store(bal, x, S.BitVecVal(42, 256))[S.BitVecVal(0, 256)] == 42) is m
+    assert cache.check_quick_sat(S.And(f(k) == 7)) is False
+
+
+def test_unsupported_fails_closed(cache):
+    """A conjunction outside the tape vocabulary (here a ternary UF) gets no quick answer
+    without z3 (it goes to the solver, like any miss) and is counted as unsupported."""
+    cache.put(Model({"x": 1}), 1)
+    g = S.Function("g", [256, 256, 256], 256)
+    assert cache.check_quick_sat(S.And(g(x, x, x) == 0, x == 1)) is False
+    assert cache.stats["unsupported"] == 1
+    assert cache.check_quick_sat(x == 1) is not False
+
+
+def _random_expr(rng):
+    v = rng.randrange(6)
+    ops = [lambda: x == v, lambda: S.ULT(x, S.BitVecVal(v, 256)), lambda: S.UGT(y, S.BitVecVal(v, 256)),
+           lambda: S.And(x == v, y == (v + 1) % 6), lambda: S.Or(x == v, y == v), lambda: (x + y) == v]
+    return ops[rng.randrange(len(ops))]()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_batched_prefetch_is_sequentially_exact(seed):
+    """Queries answered through prefetch (one launch) + lazy evaluation of models inserted
+    mid-batch give exactly the sequential loop's answers and final LRU order."""
+    rng = random.Random(seed)
+    eng = OracleEngine()
+    gpu, ref = sp.ModelCache(eng), ReferenceLoopCache()
+    pool = [Model({"x": rng.randrange(6), "y": rng.randrange(6)}) for _ in range(130)]
+    for m in pool[:60]:
+        gpu.put(m, 1)
+        ref.put(m, 1)
+    nxt = 60
+    for rnd in range(3):
+        exprs = [_random_expr(rng) for _ in range(25)]
+        gpu.prefetch(exprs)
+        for e in exprs:
+            if rng.random() < 0.2 and nxt < len(pool):      # a z3 fallback inserting a new model
+                gpu.put(pool[nxt], 1)
+                ref.put(pool[nxt], 1)
+                nxt += 1
+            assert gpu.check_quick_sat(e) is ref.check_quick_sat(e)
+        assert list(gpu.model_cache.lru_cache) == list(ref.lru)
+        assert list(gpu.model_cache.lru_cache.values()) == list(ref.lru.values())
+    assert eng.launches < 3 * 25  # batching actually batches
+
+
+class ScriptedSolver(sp.SolverBackend):
+    def __init__(self, answers):
+        self.answers = answers
+        self.calls = 0
+
+    def solve(self, constraints, minimize, maximize, timeout_ms):
+        self.calls += 1
+        r = self.answers(constraints)
+        if isinstance(r, Model):
+            asg, fns = r.assignment, r.functions
+            return "sat", lambda: Model(asg, fns)
+        return r, None
+
+
+def test_get_model_gating_and_fallback(fresh):
+    solver = ScriptedSolver(lambda cs: Model({"x": 3}))
+    sp.set_solver_backend(solver)
+    c = sp.Constraints([x == 3])
+    m = sp.get_model(c)
+    assert solver.calls == 1 and m.assignment == {"x": 3}
+    cached = list(sp.model_cache.model_cache.lru_cache)
+    assert len(cached) == 1 and cached[0] is not m              # model.py:125-126 calls s.model() twice
+    c2 = sp.Constraints([S.ULT(x, S.BitVecVal(10, 256))])
+    assert sp.get_model(c2) is cached[0] and solver.calls == 1  # quick-sat hit: no solver call
+    assert sp.get_model(c2) is cached[0]                         # lru_cache(2**23) memo
+    sp.get_model(c2, minimize=(x,))                              # minimize bypasses quick-sat
+    assert solver.calls == 2
+    with pytest.raises(UnsatError):
+        sp.get_model((x == 1, False))                            # Python False -> UnsatError
+    sp.set_solver_backend(ScriptedSolver(lambda cs: "unsat"))
+    with pytest.raises(UnsatError) as ei:
+        sp.get_model(sp.Constraints([x == 77]))
+    assert not isinstance(ei.value, SolverTimeOutException)
+    sp.set_solver_backend(ScriptedSolver(lambda cs: "unknown"))
+    with pytest.raises(SolverTimeOutException):
+        sp.get_model(sp.Constraints([x == 78]))
+
+
+def test_timeout_budget(fresh):
+    sp.time_handler.start_execution(0)
+    try:
+        with pytest.raises(SolverTimeOutException):
+            sp.get_model(sp.Constraints([x == 1]))
+    finally:
+        sp.time_handler._start_time = None
+
+
+def test_is_possible_semantics(fresh):
+    sp.set_solver_backend(ScriptedSolver(lambda cs: "unknown"))
+    c = sp.Constraints([x == 5])
+    assert c.is_possible() is False                  # default timeout: timeout prunes
+    assert c.is_possible(solver_timeout=100) is True  # custom timeout: timeout keeps
+    sp.set_solver_backend(ScriptedSolver(lambda cs: "unsat"))
+    assert sp.Constraints([x == 6]).is_possible() is False
+    assert sp.Constraints([x == 6]).get_model() is None
+
+
+def test_is_possible_batch_matches_sequential(fresh):
+    rng = random.Random(5)
+
+    def answers(cs):
+        # a tiny exact "solver": search x, y in [0, 6) with the oracle
+        expr = S.And(*cs)
+        for xv in range(6):
+            for yv in range(6):
+                m = Model({"x": xv, "y": yv})
+                if eval_under(expr, m):
+                    return m
+        return "unsat"
+
+    states = [sp.Constraints([_random_expr(rng), _random_expr(rng)]) for _ in range(30)]
+    sp.set_solver_backend(ScriptedSolver(answers))
+    batch = sp.is_possible_batch(states)
+    order_batch = [(dict(m.assignment), v) for m, v in sp.model_cache.model_cache.lru_cache.items()]
+    sp.reset_caches()
+    sp.model_cache = sp.ModelCache(OracleEngine())
+    sp.set_solver_backend(ScriptedSolver(answers))
+    seq = [c.is_possible() for c in states]
+    order_seq = [(dict(m.assignment), v) for m, v in sp.model_cache.model_cache.lru_cache.items()]
+    assert batch == seq and order_batch == order_seq
+    assert any(seq) and not all(seq)
+
+
+def test_keccak_manager_shapes():
+    km = KeccakFunctionManager(hasher=keccak_ref.keccak256)
+    assert km.get_empty_keccak_hash().value == int.from_bytes(keccak_ref.keccak256(b""), "big")
+    c = km.create_keccak(S.BitVecVal(0, 256))
+    assert c.value == 0x290DECD9548B62A8D60345A988386FC84BA6BC95484008F6362F93160EF3E563
+    k = S.BitVecSym("k", 512)
+    h = km.create_keccak(k)
+    assert h.kind == S.APP and h.params[0] == "keccak256_512"
+    cond = km.create_conditions()
+    names = {t.params[0] for t in S.walk(cond) if t.kind == S.APP}
+    assert names == {"keccak256_512", "keccak256_512-1", "keccak256_256", "keccak256_256-1"}
+    lo, hi = km.interval(512)
+    v = (lo + 63) // 64 * 64
+    assert lo <= v < hi
+    # a model whose table maps k to an in-interval multiple of 64 and inverts it satisfies the axioms
+    good = Model({"k": 11}, {"keccak256_512": ({(11,): v}, 0), "keccak256_512-1": ({(v,): 11}, 0),
+                             "keccak256_256": ({(0,): c.value}, 0), "keccak256_256-1": ({(c.value,): 0}, 0)})
+    assert eval_under(cond, good)
+    bad = Model({"k": 11}, {"keccak256_512": ({(11,): v + 1}, 0), "keccak256_512-1": ({(v + 1,): 11}, 0),
+                            "keccak256_256": ({(0,): c.value}, 0), "keccak256_256-1": ({(c.value,): 0}, 0)})
+    assert not eval_under(cond, bad)
+
+
+def test_exponent_manager():
+    em = ExponentFunctionManager()
+    v, c = em.create_condition(S.BitVecVal(3, 256), S.BitVecVal(5, 256))
+    assert v.value == 243 and eval_under(c, Model({}, {"Power": ({(3, 5): 243}, 0)}))
+    e = S.BitVecSym("e", 256)
+    p, cond = em.create_condition(S.BitVecVal(256, 256), e)
+    table = {(256, i): pow(256, i, 2 ** 256) for i in range(32)}
+    table[(256, 33)] = 256
+    assert eval_under(cond, Model({"e": 33}, {"Power": (dict(table), 0)}))
+    assert not eval_under(cond, Model({"e": 33}, {"Power": ({(256, 33): 256}, 0)}))  # axioms missing
