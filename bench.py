@@ -36,14 +36,37 @@ VALU_PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12
 HBM_PEAK_GBS = 8000.0
 
 
+# config -> (default tapes, default models per GPU, seed, workload text, kernel that dominates)
+WORKLOADS = {
+    "c2": (10_000, 100_000, 2, "C2: synthetic 10^4 constraint tapes (ADD/MUL/AND/EQ/ULT, Bool-AND root) x 10^5 "
+           "random 256-bit models per GPU, seed 2, 10% planted", "mq::qsa_kernel (gfx950 threaded-code interpreter)"),
+    "c3": (1_000, 1_000_000, 3, "C3 substitute: 10^3 EVM-shaped path conjunctions over 3 txs (calldata bytes/words, "
+           "dispatch, SafeMath udiv/urem/smod, shifts, extract/concat/signext, balance table, storage store chains; "
+           "~1060 DAG nodes) x 10^6 models per GPU, seed 3, 10% planted", "qs_first_hit_kernel<8,8> (HIP C++ interpreter)"),
+}
+
+
+def build_workload(cfg: str, n_tapes: int, M: int, seed: int, rank: int, world: int):
+    """(tapes, this rank's model shard, expected global first hits)."""
+    if cfg == "c2":
+        from mythril_amd.synth import c2_workload
+        tb, mb_all, expected = c2_workload(n_tapes, M * world, seed=seed)
+        return tb, (mb_all.shard(rank * M, (rank + 1) * M) if world > 1 else mb_all), expected
+    from mythril_amd.synth_evm import c3_workload
+    tb, mb, expected, _ = c3_workload(n_tapes, M * world, seed=seed, shard=(rank * M, (rank + 1) * M))
+    return tb, mb, expected
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--tapes", type=int, default=10_000)
-    p.add_argument("--models", type=int, default=100_000, help="candidate models per GPU")
-    p.add_argument("--seed", type=int, default=2)
+    p.add_argument("--config", choices=sorted(WORKLOADS), default="c2",
+                   help="c2 = BASELINE configs[1] (the metric's workload); c3/c5 = EVM-shaped parity/scaling cases")
+    p.add_argument("--tapes", type=int, default=None)
+    p.add_argument("--models", type=int, default=None, help="candidate models per GPU")
+    p.add_argument("--seed", type=int, default=None)
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
@@ -72,7 +95,7 @@ def cpu_baseline(tb, mb, target_s: float):
         evals = mb.n_models if fh[t] < 0 else (fh[t] - mb.index_base + 1)
         node_evals += float(evals) * float(sizes[t])
     return {"value": node_evals / dt, "unit": "node-evals/s", "cores": cores, "kind": "port",
-            "sample": f"first {n} of {tb.n_tapes} C2 tapes x {mb.n_models} models, oracle/cref.c "
+            "sample": f"first {n} of {tb.n_tapes} tapes x {mb.n_models} models of the same workload, oracle/cref.c "
                       f"(OpenMP {cores} threads), {dt:.1f} s", "seconds": dt}
 
 
@@ -102,19 +125,21 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from mythril_amd.evaluator import Evaluator
-    from mythril_amd.synth import c2_workload
 
+    d_tapes, d_models, d_seed, workload_text, kernel_name = WORKLOADS[args.config]
+    args.tapes = args.tapes or d_tapes
+    args.models = args.models or d_models
+    args.seed = d_seed if args.seed is None else args.seed
     t_gen = time.perf_counter()
     M = args.models
-    tb, mb_all, expected = c2_workload(args.tapes, M * world, seed=args.seed)
-    mb = mb_all.shard(rank * M, (rank + 1) * M) if world > 1 else mb_all
+    tb, mb, expected = build_workload(args.config, args.tapes, M, args.seed, rank, world)
     t_gen = time.perf_counter() - t_gen
 
     ev = Evaluator(local)
     ev.upload_models(mb)
     ct = ev.compile(tb)
     if ct.n_unsupported:
-        raise SystemExit(f"{ct.n_unsupported} C2 tapes unsupported by the evaluator")
+        raise SystemExit(f"{ct.n_unsupported} {args.config} tapes unsupported by the evaluator")
     dev = torch.device("cuda", local)
     best = torch.empty(tb.n_tapes, dtype=torch.int32, device=dev)
     # a dedicated (non-null) stream: the kernels, the HIP events and RCCL all order on it
@@ -178,7 +203,7 @@ def main():
         model_bytes = mb.var_words.nbytes
         tape_bytes = tb.nodes.nbytes + tb.consts.nbytes + 4 * tb.n_tapes
         hbm_gbs = (model_bytes + tape_bytes) / (kern_ms * 1e-3) / 1e9
-        wkey = f"c2:n{tb.n_tapes}:m{M}:s{args.seed}"
+        wkey = f"{args.config}:n{tb.n_tapes}:m{M}:s{args.seed}"
         traffic = pmc_traffic(wkey)
         out = {
             "metric": "256-bit constraint-node x model evals/s",
@@ -194,8 +219,7 @@ def main():
             "dtype": "u32",
             "data": "synthetic",
             "config": {
-                "workload": "C2: synthetic 10^4 constraint tapes (ADD/MUL/AND/EQ/ULT, Bool-AND root) x 10^5 "
-                            "random 256-bit models per GPU, seed 2, 10% planted",
+                "workload": workload_text,
                 "n_tapes": tb.n_tapes, "models_per_gpu": M, "models_total": M * world,
                 "avg_tape_nodes": float(tb.sizes().mean()), "seed": args.seed,
                 "parallelism": f"model-axis shard x{world} + RCCL min-allreduce" if world > 1 else "single GPU",
@@ -205,7 +229,7 @@ def main():
                 "frac": achieved_tops / VALU_PEAK_TOPS,
                 "traffic": traffic["bytes"] if traffic else None,
                 "traffic_source": traffic["source"] if traffic else None,
-                "kernel": "mq::qsa_kernel (gfx950 threaded-code interpreter)", "kernel_ms": kern_ms,
+                "kernel": kernel_name, "kernel_ms": kern_ms,
                 "alg_bytes_per_launch": model_bytes + tape_bytes,
                 "alg_ops_per_launch": per_launch_ops,
                 "hbm_alg_GBps": hbm_gbs, "hbm_frac": hbm_gbs / HBM_PEAK_GBS,

@@ -54,6 +54,9 @@ struct DevBuf {
 
 }  // namespace
 
+// the assembly interpreter keeps temps in LDS (2 KB per temp per wave, 4 waves per workgroup)
+static constexpr int kQsaMaxTemps = 16;
+
 struct mq_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -66,6 +69,7 @@ struct mq_ctx {
   DevBuf vars, var_off, var_nl, funcs, entry_ptr, entry_words, else_words;
   DevBuf counters;
   DevBuf best_tmp;  // scratch first-hit buffer for the synchronous API
+  DevBuf scratch;   // per-wave temp slots of the HIP C++ interpreter (persistent grid)
   DevBuf verdict_buf;
   // assembly interpreter (qsa.hip): handler byte offsets read back at context creation
   bool qsa_ready = false;
@@ -407,7 +411,8 @@ int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t*
   std::vector<std::vector<uint32_t>> qtr(tb->n_tapes);
   if (c->qsa_ready)
     for (int t = 0; t < tb->n_tapes; t++)
-      if (ct[t].supported && ct[t].L == 8) qsa_ok[t] = qsa_translate(c, ct[t], qtr[t]) ? 1 : 0;
+      if (ct[t].supported && ct[t].L == 8 && ct[t].n_temps <= kQsaMaxTemps)
+        qsa_ok[t] = qsa_translate(c, ct[t], qtr[t]) ? 1 : 0;
   T->qsa.begin = 0;
   for (int pass = 0; pass < 3; pass++) {
     mq_tapes::Variant& v = pass == 0 ? T->qsa : (pass == 1 ? T->l8_rest : T->l16);
@@ -462,6 +467,10 @@ int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t*
 
 void mq_tapes_free(mq_tapes* t) { delete t; }
 
+// Workgroups of the persistent HIP C++ kernels: 8 per CU on 256 CUs; each strides over the
+// (model tile, tape group) items.  Bounds the temp scratch to grid * 4 waves * temps * 2 KB.
+static constexpr int64_t kPersistentGroups = 2048;
+
 static KArgs make_args(mq_ctx* c, mq_tapes* T, const mq_tapes::Variant& v) {
   KArgs a{};
   a.descs = T->descs.as<GDesc>() + v.begin;
@@ -487,6 +496,11 @@ static KArgs make_args(mq_ctx* c, mq_tapes* T, const mq_tapes::Variant& v) {
   a.counters = c->counters.as<unsigned long long>();
   a.tmp_words_per_wave = v.max_temps * v.L * 64;
   a.early_exit = 1;
+  const int64_t groups = (int64_t(v.count) + tpg - 1) / tpg;
+  a.tiles = tiles;
+  a.n_items = tiles * groups;
+  a.grid = (int)std::min<int64_t>(a.n_items, kPersistentGroups);
+  a.scratch = nullptr;
   return a;
 }
 
@@ -551,6 +565,11 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
   for (const auto& v : cpp) {
     if (v.count <= 0) continue;
     KArgs a = make_args(c, T, v);
+    const size_t scratch_bytes = (size_t)a.grid * 4 * (size_t)a.tmp_words_per_wave * 4;
+    if (scratch_bytes) {
+      HIPCHK(c->scratch.ensure(scratch_bytes));
+      a.scratch = c->scratch.as<uint32_t>();
+    }
     a.best = best;
     a.verdicts = verdicts;
     a.early_exit = verdicts ? 0 : c->early_exit;

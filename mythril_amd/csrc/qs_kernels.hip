@@ -602,34 +602,42 @@ MQ_DEV bool run_tape(cu32p prog, const Ctx& cx) {
 
 // ---------------------------------------------------------------- kernels
 // grid.x: model tiles of 64*WAVES models; grid.y: groups of tapes_per_group descriptors.
+// Persistent grid: workgroup w handles items w, w + grid, ... with item = group * tiles + tile
+// (model tiles of 256 fastest, so low candidate indices are evaluated first and their hits
+// feed the early exit).  A wave's temp slots live in HBM at a fixed per-(workgroup, wave)
+// offset: coalesced 256-byte rows, L1/L2-resident, no LDS occupancy limit on the temp count.
 template <int L, int D>
 __global__ __launch_bounds__(256) void qs_first_hit_kernel(KArgs args) {
-  extern __shared__ uint32_t lds_tmp[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t m0 = (int64_t)blockIdx.x * 256 + wave * 64;
-  if (m0 >= args.M) return;
-  const int64_t m = m0 + lane;
-  const bool valid = m < args.M;
-  Ctx cx = make_ctx(args, valid ? m : args.M - 1, lds_tmp + (size_t)wave * args.tmp_words_per_wave, lane);
-  const int gbeg = blockIdx.y * args.tapes_per_group;
-  const int gend = min(gbeg + args.tapes_per_group, args.n_desc);
-  const int32_t gfirst = (int32_t)(args.index_base + m0);
+  uint32_t* tmp = args.scratch + ((size_t)blockIdx.x * 4 + wave) * (size_t)args.tmp_words_per_wave;
   uint64_t pairs = 0, nodes = 0, ops = 0;
-  for (int i = gbeg; i < gend; i++) {
-    const GDesc dsc = load_desc(args.descs, i);
-    int32_t cur = __hip_atomic_load(&args.best[dsc.tape], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    cur = __builtin_amdgcn_readfirstlane(cur);
-    if (args.early_exit && gfirst >= cur) continue;
-    cx.consts = CONSTP(cu32p, args.consts) + dsc.const_base;
-    const bool r = run_tape<L, D>(CONSTP(cu32p, args.prog) + dsc.prog_off, cx);
-    const uint64_t mask = __ballot(r && valid);
+  for (int64_t item = blockIdx.x; item < args.n_items; item += gridDim.x) {
+    const int64_t tile = item % args.tiles;
+    const int group = (int)(item / args.tiles);
+    const int64_t m0 = tile * 256 + wave * 64;
+    if (m0 >= args.M) continue;
+    const int64_t m = m0 + lane;
+    const bool valid = m < args.M;
+    Ctx cx = make_ctx(args, valid ? m : args.M - 1, tmp, lane);
+    const int gbeg = group * args.tapes_per_group;
+    const int gend = min(gbeg + args.tapes_per_group, args.n_desc);
+    const int32_t gfirst = (int32_t)(args.index_base + m0);
     const uint64_t vmask = __ballot(valid);
-    pairs += __popcll(vmask);
-    nodes += (uint64_t)__popcll(vmask) * dsc.n_nodes;
-    ops += (uint64_t)__popcll(vmask) * dsc.alg_ops;
-    if (mask != 0 && lane == 0) {
-      const int32_t hit = (int32_t)(args.index_base + m0 + __builtin_ctzll(mask));
-      atomicMin(&args.best[dsc.tape], hit);
+    for (int i = gbeg; i < gend; i++) {
+      const GDesc dsc = load_desc(args.descs, i);
+      int32_t cur = __hip_atomic_load(&args.best[dsc.tape], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      cur = __builtin_amdgcn_readfirstlane(cur);
+      if (args.early_exit && gfirst >= cur) continue;
+      cx.consts = CONSTP(cu32p, args.consts) + dsc.const_base;
+      const bool r = run_tape<L, D>(CONSTP(cu32p, args.prog) + dsc.prog_off, cx);
+      const uint64_t mask = __ballot(r && valid);
+      pairs += __popcll(vmask);
+      nodes += (uint64_t)__popcll(vmask) * dsc.n_nodes;
+      ops += (uint64_t)__popcll(vmask) * dsc.alg_ops;
+      if (mask != 0 && lane == 0) {
+        const int32_t hit = (int32_t)(args.index_base + m0 + __builtin_ctzll(mask));
+        atomicMin(&args.best[dsc.tape], hit);
+      }
     }
   }
   if (lane == 0 && args.counters) {
@@ -641,20 +649,24 @@ __global__ __launch_bounds__(256) void qs_first_hit_kernel(KArgs args) {
 
 template <int L, int D>
 __global__ __launch_bounds__(256) void qs_verdict_kernel(KArgs args) {
-  extern __shared__ uint32_t lds_tmp[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t m0 = (int64_t)blockIdx.x * 256 + wave * 64;
-  if (m0 >= args.M) return;
-  const int64_t m = m0 + lane;
-  const bool valid = m < args.M;
-  Ctx cx = make_ctx(args, valid ? m : args.M - 1, lds_tmp + (size_t)wave * args.tmp_words_per_wave, lane);
-  const int gbeg = blockIdx.y * args.tapes_per_group;
-  const int gend = min(gbeg + args.tapes_per_group, args.n_desc);
-  for (int i = gbeg; i < gend; i++) {
-    const GDesc dsc = load_desc(args.descs, i);
-    cx.consts = CONSTP(cu32p, args.consts) + dsc.const_base;
-    const bool r = run_tape<L, D>(CONSTP(cu32p, args.prog) + dsc.prog_off, cx);
-    if (valid) args.verdicts[(int64_t)dsc.tape * args.M + m] = r ? 1 : 0;
+  uint32_t* tmp = args.scratch + ((size_t)blockIdx.x * 4 + wave) * (size_t)args.tmp_words_per_wave;
+  for (int64_t item = blockIdx.x; item < args.n_items; item += gridDim.x) {
+    const int64_t tile = item % args.tiles;
+    const int group = (int)(item / args.tiles);
+    const int64_t m0 = tile * 256 + wave * 64;
+    if (m0 >= args.M) continue;
+    const int64_t m = m0 + lane;
+    const bool valid = m < args.M;
+    Ctx cx = make_ctx(args, valid ? m : args.M - 1, tmp, lane);
+    const int gbeg = group * args.tapes_per_group;
+    const int gend = min(gbeg + args.tapes_per_group, args.n_desc);
+    for (int i = gbeg; i < gend; i++) {
+      const GDesc dsc = load_desc(args.descs, i);
+      cx.consts = CONSTP(cu32p, args.consts) + dsc.const_base;
+      const bool r = run_tape<L, D>(CONSTP(cu32p, args.prog) + dsc.prog_off, cx);
+      if (valid) args.verdicts[(int64_t)dsc.tape * args.M + m] = r ? 1 : 0;
+    }
   }
 }
 
@@ -674,13 +686,9 @@ __global__ void qs_finalize_best(int32_t* best, const uint8_t* unsupported, int 
 // ---------------------------------------------------------------- host launchers
 template <int L, int D>
 static hipError_t launch_variant(const KArgs& a, bool verdict, hipStream_t st) {
-  if (a.n_desc <= 0) return hipSuccess;
-  const int64_t tiles = (a.M + 255) / 256;
-  const int groups = (a.n_desc + a.tapes_per_group - 1) / a.tapes_per_group;
-  dim3 grid((unsigned)tiles, (unsigned)groups);
-  const size_t lds = (size_t)a.tmp_words_per_wave * 4 * 4;
-  if (verdict) hipLaunchKernelGGL((qs_verdict_kernel<L, D>), grid, dim3(256), lds, st, a);
-  else hipLaunchKernelGGL((qs_first_hit_kernel<L, D>), grid, dim3(256), lds, st, a);
+  if (a.n_desc <= 0 || a.grid <= 0) return hipSuccess;
+  if (verdict) hipLaunchKernelGGL((qs_verdict_kernel<L, D>), dim3((unsigned)a.grid), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((qs_first_hit_kernel<L, D>), dim3((unsigned)a.grid), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

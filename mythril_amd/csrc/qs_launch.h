@@ -42,8 +42,12 @@ struct KArgs {
   int32_t* best;                 // first-hit accumulator (global index, INT32_MAX = none)
   uint8_t* verdicts;             // verdict mode: [tape][M] bytes
   unsigned long long* counters;  // [0] pairs evaluated, [1] node-evals, [2] algorithmic ops
-  int tmp_words_per_wave;        // LDS temp words per wave
+  int tmp_words_per_wave;        // temp words per wave (slot, limb, lane)
   int early_exit;
+  uint32_t* scratch;             // per-wave temp slots in HBM: [gridDim.x * 4][tmp_words_per_wave]
+  int64_t tiles;                 // model tiles of 256
+  int64_t n_items;               // tiles x tape groups; workgroups stride over them
+  int grid;                      // workgroups launched (persistent, <= n_items)
 };
 
 // argument block of the assembly interpreter (layout fixed by gen_qsa.py's prologue)

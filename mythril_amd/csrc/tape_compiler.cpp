@@ -303,11 +303,31 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
     }
     std::vector<char> hoist(NI, 0);
     std::vector<int> units;  // hoisted nodes in topological (index) order, then root
-    for (int x = 0; x < NI; x++)
-      if (live[x] && x != root && !B.nodes[x].leaf && uses[x] > 1) {
+    // Rematerialisation: a shared node whose expression is tiny and cheap (a calldata byte
+    // `ite(slt(i, size), cd_i, 0)`, a masked extract) is re-evaluated at each use instead of
+    // occupying a temp slot: temps cost 2 KB per wave and their count bounds what compiles.
+    // remat_cost(x) = nodes re-emitted per extra use (hoisted kids and leaves are free pushes).
+    std::vector<int> remat_cost(NI, 0);
+    auto expensive = [&](uint32_t g) {
+      return g == G_MUL || g == G_UDIV || g == G_UREM || g == G_SDIV || g == G_SREM || g == G_SMOD ||
+             g == G_UF1 || g == G_UF2 || g == G_KECCAK || g == G_UMUL_NOOVFL || g == G_SMUL_NOOVFL ||
+             g == G_SMUL_NOUDFL || g == G_SHL || g == G_LSHR || g == G_ASHR;
+    };
+    for (int x = 0; x < NI; x++) {
+      if (!live[x]) continue;
+      const INode& n = B.nodes[x];
+      if (n.leaf) continue;
+      int c = expensive(n.gop) ? 1000 : 1;
+      for (int k = 0; k < n.nk; k++) {
+        const int kid = n.kid[k];
+        if (!B.nodes[kid].leaf && !hoist[kid]) c += remat_cost[kid];
+      }
+      remat_cost[x] = c;
+      if (x != root && uses[x] > 1 && c > lim.remat_max_nodes) {
         hoist[x] = 1;
         units.push_back(x);
       }
+    }
     units.push_back(root);
 
     // stack need with hoisted nodes as leaves (Sethi-Ullman)

@@ -24,8 +24,9 @@ struct CompiledTape {
 struct CompileLimits {
   int max_depth_l8 = 8;
   int max_depth_l16 = 6;
-  int max_temps_l8 = 16;
-  int max_temps_l16 = 8;
+  int max_temps_l8 = 64;      // temps live in a per-wave global scratch slot (64 x 2 KB)
+  int max_temps_l16 = 32;     // (32 x 4 KB)
+  int remat_max_nodes = 3;    // shared sub-terms up to this many cheap nodes are re-evaluated
 };
 
 // Compile tape t of the batch. n_funcs/funcs describe the model function table (result

@@ -16,7 +16,7 @@ model ("Equivalence lets the lowering choose its input").
 """
 from __future__ import annotations
 
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -36,12 +36,26 @@ class SymbolTable:
     sorts are different declarations.  A symbolic array ``Array(name, dom, rng)`` is read through
     the model's interpretation of ``name`` (its ``as-array`` function, arity 1)."""
 
-    def __init__(self) -> None:
+    def __init__(self, derive_constant_lookups: bool = True) -> None:
         self.vars: Dict[Tuple[str, int], int] = {}
         self.var_widths: List[int] = []
         self.funcs: Dict[str, int] = {}
         self.func_specs: List[FuncSpec] = []
         self.func_names: List[str] = []
+        self.derive = derive_constant_lookups
+        self.derived: Dict[int, Tuple[str, Tuple[int, ...]]] = {}  # var index -> (function, const args)
+
+    def derived_var(self, fname: str, args: Tuple[int, ...], width: int) -> int:
+        """A model-only quantity: the interpretation of function/array ``fname`` at CONSTANT
+        arguments (``select(<tx>_calldata, 4)``, ``keccak256_256(c)``).  Its value is fixed per
+        model, so it is looked up once per model at serialization (entries, then else value —
+        the same rule the kernel applies) and stored as an SoA column like any constant."""
+        key = ("@" + fname + ":" + ",".join(str(a) for a in args), width)
+        i = self.vars.get(key)
+        if i is None:
+            i = self.var(key[0], width)
+            self.derived[i] = (fname, tuple(args))
+        return i
 
     def var(self, name: str, width: int) -> int:
         key = (name, width)
@@ -79,6 +93,14 @@ def lower_term(root: S.Term, syms: SymbolTable) -> Tape:
         raise LoweringError("quick-sat root must be Bool")
     tp = Tape()
     node: Dict[int, int] = {}
+
+    def arr_node(arr: S.Term, r: int) -> int:
+        if r >= 0:
+            return r
+        r = tp.array_var(syms.func(arr.params[0], (arr.domain,), arr.width), arr.width)
+        node[id(arr)] = r
+        return r
+
     for t in S.walk(root):
         k = t.kind
         a = [node[id(x)] for x in t.args]
@@ -140,16 +162,25 @@ def lower_term(root: S.Term, syms: SymbolTable) -> Tape:
         elif k == S.ITE:
             r = tp.ite(a[0], a[1], a[2])
         elif k == S.ARRAY_SYM:
-            r = tp.array_var(syms.func(t.params[0], (t.domain,), t.width), t.width)
+            r = -1  # materialised at its first table use (a symbol only read at constant indices
+            #         never enters the model's function tables)
         elif k == S.CONST_ARRAY:
             r = tp.const_array(a[0])
         elif k == S.STORE:
-            r = tp.store(a[0], a[1], a[2])
+            r = tp.store(arr_node(t.args[0], a[0]), a[1], a[2])
         elif k == S.SELECT:
-            r = tp.select(a[0], a[1])
+            arr, idx = t.args
+            if syms.derive and arr.kind == S.ARRAY_SYM and idx.kind == S.VAL:
+                r = tp.var(syms.derived_var(arr.params[0], (idx.params[0],), _w(t)), _w(t))
+            else:
+                r = tp.select(arr_node(arr, a[0]), a[1])
         elif k == S.APP:
             name, dom = t.params
-            r = tp.uf(syms.func(name, dom, t.width), t.width, *a)
+            fid = syms.func(name, dom, t.width)
+            if syms.derive and all(x.kind == S.VAL for x in t.args):
+                r = tp.var(syms.derived_var(name, tuple(x.params[0] for x in t.args), _w(t)), _w(t))
+            else:
+                r = tp.uf(fid, t.width, *a)
         else:
             raise LoweringError(f"term kind {k!r} not in the tape vocabulary")
         node[id(t)] = r
@@ -161,7 +192,7 @@ _BIN = {S.ADD: "add", S.SUB: "sub", S.MUL: "mul", S.UDIV: "udiv", S.UREM: "urem"
         S.SHL: "shl", S.LSHR: "lshr", S.ASHR: "ashr"}
 
 
-def lower_batch(roots: Sequence[S.Term], syms: SymbolTable = None):
+def lower_batch(roots: Sequence[S.Term], syms: Optional[SymbolTable] = None):
     """Lower N conjunctions over one shared symbol table.  Returns ``(TapeBatch | None, syms,
     supported_mask)``: a root that fails to lower is replaced by a FALSE placeholder tape and
     flagged unsupported (the caller routes it to z3)."""
@@ -192,7 +223,12 @@ def serialize_models(models: Sequence[Model], syms: SymbolTable, index_base: int
     for m, mod in enumerate(models):
         asg = mod.assignment
         for i, (name, w) in enumerate(names):
-            v = asg.get(name)
+            if i in syms.derived:
+                fname, fargs = syms.derived[i]
+                interp = mod.functions.get(fname)
+                v = 0 if interp is None else interp[0].get(fargs, interp[1])
+            else:
+                v = asg.get(name)
             if v is None:
                 continue
             v = int(v) & ((1 << max(w, 1)) - 1)

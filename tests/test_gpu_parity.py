@@ -224,3 +224,56 @@ def test_asm_with_temps_and_bool_sharing(evaluator):
     assert ct.split()[0] == len(tapes)
     v, _ = evaluator.verdicts(tb)
     assert (v == cref.verdicts(tb, mb)).all()
+
+
+# ---------------------------------------------------------------- EVM-shaped C3 tapes (HIP C++ interpreter)
+def test_c3_evm_tapes_match_oracle(evaluator):
+    from mythril_amd.synth_evm import c3_workload
+    tb, mb, exp, _ = c3_workload(80, 4000, seed=3, planted_frac=0.3)
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    assert ct.n_unsupported == 0
+    fh = evaluator.first_hit(ct)
+    ref, _ = cref.first_hit(tb, mb)
+    assert (ref == exp).all()
+    assert (fh == ref).all(), np.flatnonzero(fh != ref)[:10]
+    v, fh2 = evaluator.verdicts(tb)
+    assert (v == cref.verdicts(tb, mb)).all()
+    assert (fh2 == ref).all()
+
+
+def test_c3_shard_index_base(evaluator):
+    from mythril_amd.synth_evm import c3_workload
+    tb, mb, exp, _ = c3_workload(40, 3000, seed=5, planted_frac=0.5, shard=(1100, 2900))
+    assert mb.index_base == 1100
+    evaluator.upload_models(mb)
+    fh = evaluator.first_hit(tb)
+    ref, _ = cref.first_hit(tb, mb)
+    assert (fh == ref).all()
+    inside = (exp >= 1100) & (exp < 2900)
+    assert (fh[inside] == exp[inside]).all()
+
+
+def test_many_shared_subterms_use_hbm_temps(evaluator):
+    """> 16 live shared sub-terms: temps in per-wave HBM scratch (persistent C++ kernel)."""
+    rng = np.random.default_rng(3)
+    M = 777
+    mb = ModelBatch([256] * 4, rng.integers(0, 1 << 32, (32, M), dtype=np.uint64).astype(np.uint32))
+    tapes = []
+    for k in range(12):
+        t = Tape()
+        v = [t.var(i, 256) for i in range(4)]
+        shared = [t.mul(v[i % 4], t.add(v[(i + 1) % 4], t.const(i + k, 256))) for i in range(40)]
+        # every shared product is used by two comparisons of the root: all 40 live at once
+        pairs = [t.ult(shared[i], shared[i + 1]) for i in range(39)]
+        root = t.or_(t.and_(*pairs[: 3 + k]), t.xor(pairs[-1], t.and_(*pairs[3 + k:])))
+        tapes.append(t.finish(root))
+    tb = TapeBatch(tapes)
+    from mythril_amd.evaluator import compile_info
+    assert max(compile_info(tb, i).n_temps for i in range(tb.n_tapes)) > 16
+    evaluator.upload_models(mb)
+    v, fh = evaluator.verdicts(tb)
+    assert (fh != -2).all()
+    assert (v == cref.verdicts(tb, mb)).all()
+    ref, _ = cref.first_hit(tb, mb)
+    assert (evaluator.first_hit(tb) == ref).all()

@@ -1,0 +1,123 @@
+"""Lowering pass (mythril_amd.lower) on CPU: the z3-free term layer keeps the reference's operator
+meanings (bitvec.py:63-246, bitvec_helper.py), and lowering choices (derived constant lookups,
+shared sub-terms) never change a verdict — checked with the oracle."""
+import random
+
+import numpy as np
+import pytest
+
+import cref
+from oracle_engine import eval_under
+from mythril_amd import smt as S
+from mythril_amd.exceptions import LoweringError
+from mythril_amd.lower import SymbolTable, lower_batch, lower_term, serialize_models
+from mythril_amd.smt_model import Model
+
+M256 = (1 << 256) - 1
+
+
+def _s(v, w=256):
+    return v - (1 << w) if v >> (w - 1) else v
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_operator_meanings_match_reference(seed):
+    rng = random.Random(seed)
+    a, b = S.BitVecSym("a", 256), S.BitVecSym("b", 256)
+    for _ in range(40):
+        va = rng.choice([0, 1, M256, 1 << 255, rng.getrandbits(256), rng.getrandbits(8)])
+        vb = rng.choice([0, 1, M256, 1 << 255, rng.getrandbits(256), rng.getrandbits(8), 300])
+        m = Model({"a": va, "b": vb})
+        q = 0 if vb == 0 else abs(_s(va)) // abs(_s(vb)) * (1 if (_s(va) < 0) == (_s(vb) < 0) else -1)
+        sdiv = (-1 & M256 if _s(va) >= 0 else 1) if vb == 0 else q & M256
+        checks = [
+            (a / b == S.BitVecVal(sdiv, 256), True),                      # '/' is bvsdiv (bitvec.py:96-103)
+            (a < b, _s(va) < _s(vb)),                                      # '<' is signed (bitvec.py:138-147)
+            (S.ULT(a, b), va < vb),
+            (S.ULE(a, b), va <= vb),                                       # Or(ULT, ==) (bitvec_helper.py:105-112)
+            (S.UGE(a, b), va >= vb),
+            (a >> b == S.BitVecVal((_s(va) >> min(vb, 256)) & M256, 256), True),   # '>>' is bvashr
+            (S.LShR(a, b) == S.BitVecVal(0 if vb >= 256 else va >> vb, 256), True),
+            (S.BVMulNoOverflow(a, b, False), va * vb < (1 << 256)),
+            (S.BVAddNoOverflow(a, b, False), va + vb < (1 << 256)),
+            (S.BVSubNoUnderflow(a, b, False), vb <= va),
+            (S.Extract(7, 0, a) == (va & 0xFF), True),                     # mixed-width == zero-pads (bitvec.py:16-22)
+            (S.URem(a, b) == S.BitVecVal(va if vb == 0 else va % vb, 256), True),
+        ]
+        for term, expect in checks:
+            assert eval_under(term, m) == expect, (term, va, vb)
+
+
+def _evm_exprs(rng, n):
+    cd = S.Array("1_calldata", 256, 8)
+    bal = S.Array("balance", 256, 256)
+    kec = S.Function("keccak256_256", [256], 256)
+    pw = S.Function("Power", [256, 256], 256)
+    cds = S.BitVecSym("1_calldatasize", 256)
+    snd = S.BitVecSym("sender_1", 256)
+    out = []
+    for _ in range(n):
+        bytes_ = [S.If(S.BitVecVal(i, 256) < cds, cd[S.BitVecVal(i, 256)], S.BitVecVal(0, 8)) for i in range(4)]
+        sel = S.Concat(*bytes_)
+        terms = [sel == rng.getrandbits(3), S.UGE(bal[snd], S.BitVecVal(rng.getrandbits(3), 256)),
+                 kec(S.BitVecVal(rng.getrandbits(2), 256)) == rng.getrandbits(2),
+                 pw(S.BitVecVal(256, 256), S.BitVecVal(rng.getrandbits(1), 256)) == 1,
+                 cd[S.Extract(255, 0, snd)] == rng.getrandbits(2)]
+        out.append(S.And(*rng.sample(terms, 3)))
+    return out
+
+
+def _evm_models(rng, n):
+    out = []
+    for _ in range(n):
+        out.append(Model({"1_calldatasize": rng.randrange(6), "sender_1": rng.randrange(3)},
+                         {"1_calldata": ({(i,): rng.getrandbits(3) for i in range(rng.randrange(5))}, rng.getrandbits(2)),
+                          "balance": ({(i,): rng.getrandbits(3) for i in range(rng.randrange(3))}, rng.getrandbits(3)),
+                          "keccak256_256": ({(rng.getrandbits(2),): rng.getrandbits(2)}, rng.getrandbits(2)),
+                          "Power": ({(256, 0): 1, (256, 1): rng.choice([1, 256])}, 0)}))
+    return out
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_derived_constant_lookups_preserve_verdicts(seed):
+    rng = random.Random(seed)
+    exprs = _evm_exprs(rng, 60)
+    models = _evm_models(rng, 120)
+    res = []
+    for derive in (True, False):
+        tb, syms, ok = lower_batch(exprs, SymbolTable(derive_constant_lookups=derive))
+        assert ok.all()
+        mb = serialize_models(models, syms)
+        res.append(cref.verdicts(tb, mb))
+        if derive:
+            assert len(syms.derived) > 0
+    assert (res[0] == res[1]).all()
+    assert res[0].any() and not res[0].all()
+
+
+def test_lowering_fails_closed():
+    g = S.Function("g", [8, 8, 8], 8)
+    v = S.BitVecSym("v", 8)
+    with pytest.raises(LoweringError):
+        lower_term(g(v, v, v) == 0, SymbolTable())
+    with pytest.raises(LoweringError):
+        lower_term(S.BitVecSym("w", 70000) == 0, SymbolTable())
+    tb, syms, ok = lower_batch([g(v, v, v) == 0, v == 1])
+    assert list(ok) == [False, True]
+
+
+def test_shared_subterms_are_shared_in_tape():
+    x = S.BitVecSym("x", 256)
+    w = (x * x + x) * (x * x + x)
+    tp = lower_term(S.And(w == 0, S.ULT(x * x, w)), SymbolTable())
+    ops = [n[0] for n in tp.nodes]
+    assert ops.count(32) == 2  # x*x and the outer product, each once (MUL = 32)
+
+
+def test_deep_conjunction_is_iterative():
+    x = S.BitVecSym("x", 256)
+    e = x
+    for i in range(5000):
+        e = e + 1
+    tp = lower_term(e == 5000, SymbolTable())
+    assert len(tp) > 5000
