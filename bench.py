@@ -43,6 +43,12 @@ WORKLOADS = {
     "c3": (1_000, 1_000_000, 3, "C3 substitute: 10^3 EVM-shaped path conjunctions over 3 txs (calldata bytes/words, "
            "dispatch, SafeMath udiv/urem/smod, shifts, extract/concat/signext, balance table, storage store chains; "
            "~1060 DAG nodes) x 10^6 models per GPU, seed 3, 10% planted", "qs_first_hit_kernel<8,8> (HIP C++ interpreter)"),
+    "c4": (200, 1_000_000, 4, "C4: 200 keccak-heavy token-transfer paths over 2 txs (balances[key] = storage at "
+           "keccak256(key ++ slot), store chains, keccak UF axioms of keccak_function_manager) x 10^6 "
+           "keccak-consistent models per GPU, keccak256_512 evaluated IN-KERNEL (keccak-f[1600]), seed 4, 10% planted",
+           "qs_first_hit_kernel<16,6,keccak> (HIP C++ interpreter + keccak-f[1600])"),
+    "c5": (256, 1_250_000, 5, "C5: 256 deep EVM-shaped paths over 5 txs (~1900 DAG nodes) x 1.25*10^6 models per GPU "
+           "(10^7 over 8 GPUs), seed 5, 10% planted", "qs_first_hit_kernel<8,8> (HIP C++ interpreter)"),
 }
 
 
@@ -52,8 +58,17 @@ def build_workload(cfg: str, n_tapes: int, M: int, seed: int, rank: int, world: 
         from mythril_amd.synth import c2_workload
         tb, mb_all, expected = c2_workload(n_tapes, M * world, seed=seed)
         return tb, (mb_all.shard(rank * M, (rank + 1) * M) if world > 1 else mb_all), expected
-    from mythril_amd.synth_evm import c3_workload
-    tb, mb, expected, _ = c3_workload(n_tapes, M * world, seed=seed, shard=(rank * M, (rank + 1) * M))
+    from mythril_amd import synth_evm
+    shard = (rank * M, (rank + 1) * M)
+    if cfg == "c4":
+        from mythril_amd.evaluator import default_evaluator
+        tb, mb, expected, _ = synth_evm.c4_workload(n_tapes, M * world, seed=seed, shard=shard, interpret_keccak=True,
+                                                    hasher_many=default_evaluator().keccak256_array)
+    elif cfg == "c5":
+        tb, mb, expected, _ = synth_evm.c3_workload(n_tapes, M * world, seed=seed, shard=shard, n_tx=5,
+                                                    checks_per_tx=(10, 14))
+    else:
+        tb, mb, expected, _ = synth_evm.c3_workload(n_tapes, M * world, seed=seed, shard=shard)
     return tb, mb, expected
 
 

@@ -74,6 +74,11 @@ enum GOp : uint32_t {
   G_UF1 = 60,        // imm = function id; result width from the function table
   G_UF2 = 61,
   G_KECCAK = 62,     // imm = argument width (bits, multiple of 8)
+  // else-first ternaries: operands d-2 (else), d-1 (cond), d (then); result in d-2.  Chosen by
+  // the compiler when the else operand is the deep one (select over a store chain lowers to
+  // ite(k == i, v, <rest of the chain>)), so the chain costs O(1) stack slots, not 2 per store.
+  G_ITE_EF = 63,
+  G_BITE_EF = 9,
   G_NUM_OPS = 64
 };
 

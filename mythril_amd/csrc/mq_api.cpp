@@ -99,10 +99,11 @@ struct mq_tapes {
     int L = 0;
     int begin = 0, count = 0;  // range in descs
     int max_temps = 0;
+    bool keccak = false;
   };
   // descs layout: [L8 QSA-eligible | L8 other | L16]; the QSA view (qdescs/qprog) holds the
   // eligible tapes translated to threaded code, in the same order.
-  Variant l8_all, l8_rest, l16, qsa;
+  Variant l8_all, l8_rest, l16, l16k, qsa;   // l16k: tapes with interpreted keccak
   DevBuf qdescs, qprog, qargs;
   QArgs qargs_host;
   QArgs qargs_dev_copy;      // what qargs currently holds on the device
@@ -414,16 +415,18 @@ int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t*
       if (ct[t].supported && ct[t].L == 8 && ct[t].n_temps <= kQsaMaxTemps)
         qsa_ok[t] = qsa_translate(c, ct[t], qtr[t]) ? 1 : 0;
   T->qsa.begin = 0;
-  for (int pass = 0; pass < 3; pass++) {
-    mq_tapes::Variant& v = pass == 0 ? T->qsa : (pass == 1 ? T->l8_rest : T->l16);
-    v.L = pass == 2 ? 16 : 8;
+  for (int pass = 0; pass < 4; pass++) {
+    mq_tapes::Variant& v = pass == 0 ? T->qsa : (pass == 1 ? T->l8_rest : (pass == 2 ? T->l16 : T->l16k));
+    v.L = pass >= 2 ? 16 : 8;
+    v.keccak = pass == 3;
     v.begin = (int)descs.size();
     for (int t = 0; t < tb->n_tapes; t++) {
       const CompiledTape& x = ct[t];
       if (!x.supported) continue;
       if (pass == 0 && !(x.L == 8 && qsa_ok[t])) continue;
       if (pass == 1 && !(x.L == 8 && !qsa_ok[t])) continue;
-      if (pass == 2 && x.L != 16) continue;
+      if (pass == 2 && !(x.L == 16 && !x.keccak)) continue;
+      if (pass == 3 && !x.keccak) continue;
       GDesc d = push_desc(t, x);
       if (pass == 0) {
         d.prog_off = (uint32_t)qprog.size();
@@ -510,8 +513,8 @@ static KArgs make_args(mq_ctx* c, mq_tapes* T, const mq_tapes::Variant& v) {
 static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, hipStream_t st) {
   const bool use_qsa = c->qsa_ready && c->use_asm && c->qsa_models_ok && T->qsa.count > 0;
   std::vector<mq_tapes::Variant> cpp;
-  if (use_qsa) cpp = {T->l8_rest, T->l16};
-  else cpp = {T->l8_all, T->l16};
+  if (use_qsa) cpp = {T->l8_rest, T->l16, T->l16k};
+  else cpp = {T->l8_all, T->l16, T->l16k};
   hipEvent_t kend = nullptr;
   if (c->time_kernels) {
     if (c->kev_used == c->kev.size()) {
@@ -574,7 +577,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     a.verdicts = verdicts;
     a.early_exit = verdicts ? 0 : c->early_exit;
     HIPCHK(start_timer());
-    HIPCHK(launch_qs(a, v.L, verdicts != nullptr, st));
+    HIPCHK(launch_qs(a, v.L, v.keccak, verdicts != nullptr, st));
   }
   if (kend) {
     HIPCHK(start_timer());
@@ -724,7 +727,7 @@ int mq_tapes_info(mq_tapes* T, int32_t* n_asm, int32_t* n_generic_l8, int32_t* n
   if (!T) return MQ_ERR_ARG;
   if (n_asm) *n_asm = T->qsa.count;
   if (n_generic_l8) *n_generic_l8 = T->l8_rest.count;
-  if (n_generic_l16) *n_generic_l16 = T->l16.count;
+  if (n_generic_l16) *n_generic_l16 = T->l16.count + T->l16k.count;
   return MQ_OK;
 }
 

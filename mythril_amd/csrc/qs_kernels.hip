@@ -273,6 +273,22 @@ struct HIte {
   }
 };
 template <int L, int D>
+struct HIteEF {  // else at d-2, cond at d-1, then at d
+  static constexpr int kMin = 2;
+  H_DEV run(Stack<L, D>& S, uint32_t, uint32_t, const Ctx&) {
+    const bool c = (S.s[d - 1][0] & 1u) != 0;
+#pragma unroll
+    for (int i = 0; i < L; i++) S.s[d - 2][i] = c ? S.s[d][i] : S.s[d - 2][i];
+  }
+};
+template <int L, int D>
+struct HBIteEF {
+  static constexpr int kMin = 2;
+  H_DEV run(Stack<L, D>& S, uint32_t, uint32_t, const Ctx&) {
+    S.s[d - 2][0] = S.s[d - 1][0] ? S.s[d][0] : S.s[d - 2][0];
+  }
+};
+template <int L, int D>
 struct HExtract {  // imm = lo, imm2 = result width
   static constexpr int kMin = 0;
   H_DEV run(Stack<L, D>& S, uint32_t lo, uint32_t W, const Ctx&) {
@@ -382,6 +398,80 @@ MQ_DEV void func_lookup(const Ctx& cx, uint32_t f, uint32_t W, const T0& k0, con
     }
   }
   mask_w<L>(out, W);
+}
+
+// ---------------------------------------------------------------- interpreted keccak256
+// keccak256 (Ethereum padding) of the big-endian bytes of S[d] (imm = width in bits, a multiple
+// of 8, <= 512 -> one 136-byte block); the digest read big-endian replaces S[d] (256 bits).
+// kfm.py:56-69 semantics; only bit-exact with UF table lookup on keccak-consistent models.
+__constant__ uint64_t kKeccakRC[24] = {
+    0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808Aull, 0x8000000080008000ull,
+    0x000000000000808Bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
+    0x000000000000008Aull, 0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000Aull,
+    0x000000008000808Bull, 0x800000000000008Bull, 0x8000000000008089ull, 0x8000000000008003ull,
+    0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800Aull, 0x800000008000000Aull,
+    0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
+
+MQ_DEV uint64_t krol(uint64_t v, int n) { return n ? (v << n) | (v >> (64 - n)) : v; }
+
+__device__ __noinline__ void keccak_f1600(uint64_t* A) {
+  constexpr int R[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
+  uint64_t a[25];
+#pragma unroll
+  for (int i = 0; i < 25; i++) a[i] = A[i];
+  for (int r = 0; r < 24; r++) {
+    uint64_t C[5], Dd[5], B[25];
+#pragma unroll
+    for (int x = 0; x < 5; x++) C[x] = a[x] ^ a[x + 5] ^ a[x + 10] ^ a[x + 15] ^ a[x + 20];
+#pragma unroll
+    for (int x = 0; x < 5; x++) Dd[x] = C[(x + 4) % 5] ^ krol(C[(x + 1) % 5], 1);
+#pragma unroll
+    for (int i = 0; i < 25; i++) a[i] ^= Dd[i % 5];
+#pragma unroll
+    for (int x = 0; x < 5; x++)
+#pragma unroll
+      for (int y = 0; y < 5; y++) B[y + 5 * ((2 * x + 3 * y) % 5)] = krol(a[x + 5 * y], R[x + 5 * y]);
+#pragma unroll
+    for (int y = 0; y < 5; y++)
+#pragma unroll
+      for (int x = 0; x < 5; x++) a[x + 5 * y] = B[x + 5 * y] ^ ((~B[(x + 1) % 5 + 5 * y]) & B[(x + 2) % 5 + 5 * y]);
+    a[0] ^= kKeccakRC[r];
+  }
+#pragma unroll
+  for (int i = 0; i < 25; i++) A[i] = a[i];
+}
+
+template <int L, int D>
+MQ_DEV void keccak_op(Stack<L, D>& S, int d, uint32_t W) {
+  uint32_t X[L];
+  load_x<L, D>(S, d, X);
+  const uint32_t nbytes = W >> 3;
+  // full-width byte reversal, then shift the message to byte 0: message byte p = LE byte p
+  uint32_t R[L];
+#pragma unroll
+  for (int k = 0; k < L; k++) R[k] = __builtin_bswap32(X[L - 1 - k]);
+  shr_uni<L>(R, 8u * (4u * L - nbytes));
+  // padding: 0x01 right after the message (bytes >= nbytes are zero after the shift)
+#pragma unroll
+  for (int k = 0; k < L; k++)
+    if ((uint32_t)k == (nbytes >> 2)) R[k] |= 1u << (8u * (nbytes & 3u));
+  uint64_t A[25];
+#pragma unroll
+  for (int w = 0; w < 25; w++) A[w] = (2 * w + 1 < L) ? ((uint64_t)R[2 * w] | ((uint64_t)R[2 * w + 1] << 32)) : 0ull;
+  // nbytes == 4L (a 512-bit argument): the 0x01 pad byte is byte 64, outside R
+  if (nbytes >= 4u * L) A[nbytes >> 3] |= 1ull << (8u * (nbytes & 7u));
+  A[16] |= 0x8000000000000000ull;
+  keccak_f1600(A);
+#pragma unroll
+  for (int i = 0; i < L; i++) {
+    uint32_t v = 0;
+    if (i < 8) {
+      const uint64_t q = A[(7 - i) >> 1];
+      v = __builtin_bswap32((uint32_t)(((7 - i) & 1) ? (q >> 32) : q));
+    }
+    X[i] = v;
+  }
+  store_x<L, D>(S, d, X);
 }
 
 template <int L, int D>
@@ -541,7 +631,7 @@ MQ_DEV void dispatch(Stack<L, D>& S, int d, uint32_t imm, uint32_t imm2, const C
   }
 }
 
-template <int L, int D>
+template <int L, int D, bool K>
 MQ_DEV bool run_tape(cu32p prog, const Ctx& cx) {
   Stack<L, D> S;
 #pragma unroll
@@ -591,9 +681,14 @@ MQ_DEV bool run_tape(cu32p prog, const Ctx& cx) {
       case G_BXOR: dispatch<HBXor, L, D>(S, d, imm, imm2, cx); break;
       case G_BNOT: dispatch<HBNot, L, D>(S, d, imm, imm2, cx); break;
       case G_ITE: dispatch<HIte, L, D>(S, d, imm, imm2, cx); break;
+      case G_ITE_EF: dispatch<HIteEF, L, D>(S, d, imm, imm2, cx); break;
+      case G_BITE_EF: dispatch<HBIteEF, L, D>(S, d, imm, imm2, cx); break;
       case G_EXTRACT: dispatch<HExtract, L, D>(S, d, imm, imm2, cx); break;
       case G_CONCAT: dispatch<HConcat, L, D>(S, d, imm, imm2, cx); break;
       case G_SEXT: dispatch<HSext, L, D>(S, d, imm, imm2, cx); break;
+      case G_KECCAK:
+        if constexpr (K) keccak_op<L, D>(S, d, imm);
+        break;
       default: cold_op<L, D>(S, op, d, imm, imm2, cx); break;
     }
   }
@@ -606,7 +701,7 @@ MQ_DEV bool run_tape(cu32p prog, const Ctx& cx) {
 // (model tiles of 256 fastest, so low candidate indices are evaluated first and their hits
 // feed the early exit).  A wave's temp slots live in HBM at a fixed per-(workgroup, wave)
 // offset: coalesced 256-byte rows, L1/L2-resident, no LDS occupancy limit on the temp count.
-template <int L, int D>
+template <int L, int D, bool K>
 __global__ __launch_bounds__(256) void qs_first_hit_kernel(KArgs args) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t* tmp = args.scratch + ((size_t)blockIdx.x * 4 + wave) * (size_t)args.tmp_words_per_wave;
@@ -629,7 +724,7 @@ __global__ __launch_bounds__(256) void qs_first_hit_kernel(KArgs args) {
       cur = __builtin_amdgcn_readfirstlane(cur);
       if (args.early_exit && gfirst >= cur) continue;
       cx.consts = CONSTP(cu32p, args.consts) + dsc.const_base;
-      const bool r = run_tape<L, D>(CONSTP(cu32p, args.prog) + dsc.prog_off, cx);
+      const bool r = run_tape<L, D, K>(CONSTP(cu32p, args.prog) + dsc.prog_off, cx);
       const uint64_t mask = __ballot(r && valid);
       pairs += __popcll(vmask);
       nodes += (uint64_t)__popcll(vmask) * dsc.n_nodes;
@@ -647,7 +742,7 @@ __global__ __launch_bounds__(256) void qs_first_hit_kernel(KArgs args) {
   }
 }
 
-template <int L, int D>
+template <int L, int D, bool K>
 __global__ __launch_bounds__(256) void qs_verdict_kernel(KArgs args) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t* tmp = args.scratch + ((size_t)blockIdx.x * 4 + wave) * (size_t)args.tmp_words_per_wave;
@@ -664,7 +759,7 @@ __global__ __launch_bounds__(256) void qs_verdict_kernel(KArgs args) {
     for (int i = gbeg; i < gend; i++) {
       const GDesc dsc = load_desc(args.descs, i);
       cx.consts = CONSTP(cu32p, args.consts) + dsc.const_base;
-      const bool r = run_tape<L, D>(CONSTP(cu32p, args.prog) + dsc.prog_off, cx);
+      const bool r = run_tape<L, D, K>(CONSTP(cu32p, args.prog) + dsc.prog_off, cx);
       if (valid) args.verdicts[(int64_t)dsc.tape * args.M + m] = r ? 1 : 0;
     }
   }
@@ -684,17 +779,18 @@ __global__ void qs_finalize_best(int32_t* best, const uint8_t* unsupported, int 
 }
 
 // ---------------------------------------------------------------- host launchers
-template <int L, int D>
+template <int L, int D, bool K>
 static hipError_t launch_variant(const KArgs& a, bool verdict, hipStream_t st) {
   if (a.n_desc <= 0 || a.grid <= 0) return hipSuccess;
-  if (verdict) hipLaunchKernelGGL((qs_verdict_kernel<L, D>), dim3((unsigned)a.grid), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((qs_first_hit_kernel<L, D>), dim3((unsigned)a.grid), dim3(256), 0, st, a);
+  if (verdict) hipLaunchKernelGGL((qs_verdict_kernel<L, D, K>), dim3((unsigned)a.grid), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((qs_first_hit_kernel<L, D, K>), dim3((unsigned)a.grid), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
-hipError_t launch_qs(const KArgs& a, int L, bool verdict, hipStream_t st) {
-  if (L == 8) return launch_variant<8, 8>(a, verdict, st);
-  if (L == 16) return launch_variant<16, 6>(a, verdict, st);
+hipError_t launch_qs(const KArgs& a, int L, bool keccak, bool verdict, hipStream_t st) {
+  if (keccak) return L == 16 ? launch_variant<16, 6, true>(a, verdict, st) : hipErrorInvalidValue;
+  if (L == 8) return launch_variant<8, 8, false>(a, verdict, st);
+  if (L == 16) return launch_variant<16, 6, false>(a, verdict, st);
   return hipErrorInvalidValue;
 }
 

@@ -142,10 +142,14 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
            n.op == MQ_OP_UMUL_NOOVFL || n.op == MQ_OP_SMUL_NOOVFL || n.op == MQ_OP_SMUL_NOUDFL) &&
           nd[n.a].width != nd[n.b].width)
         throw Fail{"predicate operand width mismatch"};
-      if (n.op == MQ_OP_KECCAK) throw Fail{"interpreted keccak not supported in the evaluator yet"};
+      if (n.op == MQ_OP_KECCAK) {
+        const int aw = nd[n.a].width;
+        if (aw == 0 || aw % 8 || aw > 512 || n.width != 256) throw Fail{"keccak argument must be 8..512 bits, bytes"};
+        out.keccak = true;
+      }
     }
     if (kind[nn - 1] != K_BOOL) throw Fail{"root is not Bool"};
-    if (maxw <= 256) out.L = 8;
+    if (maxw <= 256 && !out.keccak) out.L = 8;
     else if (maxw <= 512) out.L = 16;
     else throw Fail{"width > 512"};
     const int L = out.L;
@@ -266,6 +270,7 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
         case MQ_OP_SEXT: r = B.add(mk(G_SEXT, w, {A()}, (uint32_t)aw, (uint32_t)w)); break;
         case MQ_OP_ITE: r = B.add(mk(G_ITE, w, {A(), Bk(), Ck()}, w)); break;
         case MQ_OP_STORE: case MQ_OP_CONST_ARRAY: case MQ_OP_ARRAY_VAR: r = -1; break;
+        case MQ_OP_KECCAK: r = B.add(mk(G_KECCAK, 256, {A()}, (uint32_t)aw)); break;
         case MQ_OP_SELECT: r = select(n.a, Bk(), w); break;
         case MQ_OP_UF: {
           if (n.a > (uint32_t)kMaxImm) throw Fail{"function id too large"};
@@ -349,7 +354,15 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
           need[x] = fwd;
         }
       } else {
-        need[x] = std::max({nd_of(n.kid[0]), nd_of(n.kid[1]) + 1, nd_of(n.kid[2]) + 2});
+        const int c0 = nd_of(n.kid[0]), c1 = nd_of(n.kid[1]), c2 = nd_of(n.kid[2]);
+        const int fwd = std::max({c0, c1 + 1, c2 + 2});
+        const int ef = std::max({c2, c0 + 1, c1 + 2});  // else, cond, then
+        if ((n.gop == G_ITE || n.gop == G_BITE) && ef < fwd) {
+          swap[x] = 1;
+          need[x] = ef;
+        } else {
+          need[x] = fwd;
+        }
       }
     }
 
@@ -408,9 +421,16 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
         }
         d += 1;
       } else if (n.nk == 3) {
-        emit(n.kid[0], d);
-        emit(n.kid[1], d + 1);
-        emit(n.kid[2], d + 2);
+        if (swap[x]) {
+          emit(n.kid[2], d);
+          emit(n.kid[0], d + 1);
+          emit(n.kid[1], d + 2);
+          g = n.gop == G_ITE ? G_ITE_EF : G_BITE_EF;
+        } else {
+          emit(n.kid[0], d);
+          emit(n.kid[1], d + 1);
+          emit(n.kid[2], d + 2);
+        }
         d += 2;
       }
       if (n.imm > (uint32_t)kMaxImm) throw Fail{"immediate too large"};

@@ -13,6 +13,7 @@ struct CompiledTape {
   bool supported = false;
   std::string why;               // reason when unsupported
   int L = 0;                     // limbs per value (8 or 16)
+  bool keccak = false;           // uses interpreted keccak (G_KECCAK): runs on the L=16 keccak kernel
   int depth = 0;                 // max stack slots used
   int n_temps = 0;               // LDS temp slots
   std::vector<uint32_t> prog;    // instruction words, terminated by G_END

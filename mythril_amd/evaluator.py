@@ -246,6 +246,19 @@ class Evaluator:
         return v, fh
 
     # ------------------------------------------------------------ keccak
+    def keccak256_array(self, msgs: np.ndarray) -> np.ndarray:
+        """keccak256 of each row of a uint8 [n, len] array on the GPU -> uint8 [n, 32]."""
+        msgs = np.ascontiguousarray(msgs, dtype=np.uint8)
+        n, ln = msgs.shape
+        out = np.zeros((n, 32), np.uint8)
+        if n == 0:
+            return out
+        offs = np.arange(n + 1, dtype=np.int64) * ln
+        data = msgs.reshape(-1) if msgs.size else np.zeros(1, np.uint8)
+        _check(self.lib.mq_keccak256(self.ctx, data.ctypes.data_as(C.POINTER(C.c_uint8)), offs.ctypes.data_as(C.POINTER(C.c_int64)),
+                                     n, out.ctypes.data_as(C.POINTER(C.c_uint8))), "mq_keccak256")
+        return out
+
     def keccak256(self, messages: Sequence[bytes]) -> List[bytes]:
         msgs = [bytes(m) for m in messages]
         offs = np.zeros(len(msgs) + 1, np.int64)

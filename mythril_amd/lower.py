@@ -36,13 +36,16 @@ class SymbolTable:
     sorts are different declarations.  A symbolic array ``Array(name, dom, rng)`` is read through
     the model's interpretation of ``name`` (its ``as-array`` function, arity 1)."""
 
-    def __init__(self, derive_constant_lookups: bool = True) -> None:
+    def __init__(self, derive_constant_lookups: bool = True, interpret_keccak: bool = False) -> None:
         self.vars: Dict[Tuple[str, int], int] = {}
         self.var_widths: List[int] = []
         self.funcs: Dict[str, int] = {}
         self.func_specs: List[FuncSpec] = []
         self.func_names: List[str] = []
         self.derive = derive_constant_lookups
+        # lower keccak256_<n>(x) to in-kernel keccak-f[1600] instead of the model's UF table:
+        # exact only for keccak-consistent candidate sets (C4), never for z3 models in general
+        self.interpret_keccak = interpret_keccak
         self.derived: Dict[int, Tuple[str, Tuple[int, ...]]] = {}  # var index -> (function, const args)
 
     def derived_var(self, fname: str, args: Tuple[int, ...], width: int) -> int:
@@ -174,6 +177,10 @@ def lower_term(root: S.Term, syms: SymbolTable) -> Tape:
                 r = tp.var(syms.derived_var(arr.params[0], (idx.params[0],), _w(t)), _w(t))
             else:
                 r = tp.select(arr_node(arr, a[0]), a[1])
+        elif k == S.KECCAK:
+            r = tp.keccak(a[0])
+        elif k == S.APP and syms.interpret_keccak and _is_keccak_uf(t.params[0]):
+            r = tp.keccak(a[0])
         elif k == S.APP:
             name, dom = t.params
             fid = syms.func(name, dom, t.width)
@@ -185,6 +192,11 @@ def lower_term(root: S.Term, syms: SymbolTable) -> Tape:
             raise LoweringError(f"term kind {k!r} not in the tape vocabulary")
         node[id(t)] = r
     return tp.finish(node[id(root)])
+
+
+def _is_keccak_uf(name: str) -> bool:
+    """``keccak256_<n>`` (keccak_function_manager.py:77), not its inverse ``keccak256_<n>-1``."""
+    return name.startswith("keccak256_") and name[10:].isdigit()
 
 
 _BIN = {S.ADD: "add", S.SUB: "sub", S.MUL: "mul", S.UDIV: "udiv", S.UREM: "urem", S.SDIV: "sdiv",

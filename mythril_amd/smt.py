@@ -40,6 +40,7 @@ BAND, BOR, BXOR, BNOT = "bvand", "bvor", "bvxor", "bvnot"
 SHL, LSHR, ASHR = "bvshl", "bvlshr", "bvashr"
 EXTRACT, CONCAT, ZEXT, SEXT, ITE = "extract", "concat", "zero_extend", "sign_extend", "ite"
 SELECT, STORE, CONST_ARRAY, ARRAY_SYM, APP = "select", "store", "K", "array", "app"
+KECCAK = "keccak256"   # interpreted keccak (not a reference constructor: see Keccak256)
 
 _INTERN: "weakref.WeakValueDictionary[tuple, Term]" = weakref.WeakValueDictionary()
 
@@ -306,7 +307,10 @@ def Concat(*args) -> Term:
     acc = args[0]
     _bv(acc)
     for x in args[1:]:
-        acc = Term(CONCAT, "bv", acc.width + _bv(x), (acc, x))
+        if acc.kind == VAL and x.kind == VAL:   # concrete: folded, as z3's simplify does
+            acc = BitVecVal((acc.params[0] << x.width) | x.params[0], acc.width + x.width)
+        else:
+            acc = Term(CONCAT, "bv", acc.width + _bv(x), (acc, x))
     return acc
 
 
@@ -314,6 +318,8 @@ def Extract(high: int, low: int, bv: Term) -> Term:
     w = _bv(bv)
     if not 0 <= low <= high < w:
         raise TypeError(f"Extract({high},{low}) out of range for width {w}")
+    if bv.kind == VAL:
+        return BitVecVal(bv.params[0] >> low, high - low + 1)
     return Term(EXTRACT, "bv", high - low + 1, (bv,), (int(high), int(low)))
 
 
@@ -404,6 +410,17 @@ class Function:
             if _bv(x) != w:
                 raise TypeError(f"{self.name}: argument width {x.width} != {w}")
         return Term(APP, "bv", self.range, args, (self.name, self.domain))
+
+
+def Keccak256(data: Term) -> Term:
+    """INTERPRETED keccak256 of the big-endian bytes of ``data`` (256-bit result).  Not z3's
+    semantics — Mythril models hashes as the UF ``keccak256_<n>`` — and only equal to it on
+    keccak-consistent models.  Concrete inputs are what ``find_concrete_keccak``
+    hashes (keccak_function_manager.py:56-69)."""
+    w = _bv(data)
+    if w % 8:
+        raise TypeError("keccak input width must be a multiple of 8")
+    return Term(KECCAK, "bv", 256, (data,))
 
 
 def walk(root: Term) -> List[Term]:

@@ -57,7 +57,7 @@ BLOCK = 1 << 16  # models are generated in independently seeded blocks (any rank
 
 
 class _Block:
-    def __init__(self, seed: int, b: int, n: int, n_tx: int):
+    def __init__(self, seed: int, b: int, n: int, n_tx: int, address_args: bool = False):
         rng = np.random.Generator(np.random.PCG64([seed, b]))
         self.sender, self.value, self.cds, self.cdata = [], [], [], []
         for _ in range(n_tx):
@@ -71,7 +71,15 @@ class _Block:
             v[rng.random(n) < 0.4] = 0
             self.value.append(_to_limbs(v))
             self.cds.append(_to_limbs(rng.integers(4, 100, n, dtype=np.uint64)))
-            self.cdata.append(rng.integers(0, 256, (N_BYTES, n), dtype=np.uint64).astype(np.uint8))
+            cd = rng.integers(0, 256, (N_BYTES, n), dtype=np.uint64).astype(np.uint8)
+            if address_args:
+                # first ABI argument is an address: 12 zero bytes + an actor (90 %) or random bytes
+                cd[4:16] = 0
+                who2 = rng.integers(0, 10, n)
+                for a, addr in enumerate(ACTORS):
+                    pick = (who2 // 3) == a
+                    cd[16:36, pick] = np.frombuffer(addr.to_bytes(20, "big"), np.uint8)[:, None]
+            self.cdata.append(cd)
         # balance: entries for the three actors + else value, all < 2^62
         self.bal_vals = rng.integers(0, 1 << 62, (3, n), dtype=np.uint64)
         self.bal_else = rng.integers(0, 1 << 62, n, dtype=np.uint64)
@@ -82,9 +90,10 @@ class EvmModels:
     Senders are actors 90 % of the time, call values are 0 (40 %) or < 2^40, calldatasize is
     uniform in [4, 100), calldata bytes are uniform, balances have entries for the 3 actors."""
 
-    def __init__(self, seed: int, M: int, n_tx: int, lo: int = 0, hi: int = None):
+    def __init__(self, seed: int, M: int, n_tx: int, lo: int = 0, hi: int = None, address_args: bool = False):
         hi = M if hi is None else hi
         self.seed, self.M, self.n_tx, self.lo, self.hi = seed, M, n_tx, lo, hi
+        self.address_args = address_args
         blocks = [self._block(b) for b in range(lo // BLOCK, (hi + BLOCK - 1) // BLOCK)] if hi > lo else []
         off = lo - (lo // BLOCK) * BLOCK
         n = hi - lo
@@ -103,7 +112,20 @@ class EvmModels:
 
     def _block(self, b: int) -> _Block:
         n = min(BLOCK, self.M - b * BLOCK)
-        return _Block(self.seed, b, n, self.n_tx)
+        return _Block(self.seed, b, n, self.n_tx, self.address_args)
+
+    def derived_column(self, fname: str, args, nl: int, n: int) -> np.ndarray:
+        """Interpretation of ``fname`` at constant ``args`` for every stored model."""
+        r = np.zeros((nl, n), np.uint32)
+        if fname.endswith("_calldata"):
+            k, idx = int(fname.split("_")[0]) - 1, args[0]
+            if idx < N_BYTES:
+                r[0] = self.cdata[k][idx].astype(np.uint32)
+            return r
+        raise ValueError(f"no derived column for {fname}{args}")
+
+    def extra_table(self, fname: str, spec):
+        return None
 
     # witness values of GLOBAL model m as Python ints (any m: its block is regenerated)
     @staticmethod
@@ -135,11 +157,7 @@ class EvmModels:
             nl = limbs(w)
             if i in syms.derived:
                 fname, args = syms.derived[i]
-                k = int(fname.split("_")[0]) - 1
-                idx = args[0]
-                col = self.cdata[k][idx, lo:hi].astype(np.uint32) if idx < N_BYTES else np.zeros(n, np.uint32)
-                r = np.zeros((nl, n), np.uint32)
-                r[0] = col
+                r = self.derived_column(fname, args, nl, n)
             elif name.startswith("sender_"):
                 r = self.sender[int(name[7:]) - 1][:, lo:hi]
             elif name.startswith("call_value"):
@@ -156,7 +174,18 @@ class EvmModels:
             spec = syms.func_specs[f]
             funcs.append(spec)
             if fname != "balance":
-                raise ValueError(f"EvmModels has no table for {fname}")
+                t = self.extra_table(fname, spec)
+                if t is None:
+                    raise ValueError(f"EvmModels has no table for {fname}")
+                ptr, ent, els = t
+                ebase.append(wpos)
+                ewords.append(ent.reshape(-1))
+                wpos += ent.size
+                eptr.append(ptr)
+                elb.append(epos)
+                elw.append(els.reshape(-1))
+                epos += els.size
+                continue
             # 3 entries per model: key = actor (8 limbs), value (8 limbs)
             ent = np.zeros((n, 3, 16), np.uint32)
             for a in range(3):
@@ -241,7 +270,7 @@ def evm_path(rng: np.random.Generator, wit: Dict, n_tx: int, checks_per_tx: Tupl
         snd, cv, cds, B = wit["sender"][k], wit["value"][k], wit["cds"][k], wit["bytes"][k]
         W0, W1, W2 = _word_val(B, cds, 0), _word_val(B, cds, 4), _word_val(B, cds, 36)
         w0, w1, w2 = tx.word(0), tx.word(4), tx.word(36)
-        cs.append(_holds(S.Or(*[tx.sender == a for a in ACTORS]), snd in ACTORS))
+        cs.append(S.Or(*[tx.sender == a for a in ACTORS]))  # always asserted (symbolic.py:217-219)
         cs.append(_holds(S.ULT(tx.cds, S.BitVecVal(4, 256)), cds < 4))
         sel = W0 >> 224
         form = int(rng.integers(3))
@@ -324,10 +353,182 @@ def c3_workload(n_tapes: int = 1000, n_models: int = 1_000_000, seed: int = 3, p
     planted = rng.random(n_tapes) < planted_frac
     for t in range(n_tapes):
         if planted[t]:
-            p = int(rng.integers(n_models))
-            wit = models.witness(p)
+            while True:  # the caller is always an actor (transaction/symbolic.py:217-219)
+                p = int(rng.integers(n_models))
+                wit = models.witness(p)
+                if all(x in ACTORS for x in wit["sender"]):
+                    break
             expected[t] = p
         else:
             wit = ghost.witness(t)
         tapes.append(lower_term(evm_path(rng, wit, n_tx, checks_per_tx), syms))
+    return TapeBatch(tapes), models.batch(syms), expected, syms
+
+
+# ====================================================================== C4: keccak-heavy mappings
+def _be_bytes(words: np.ndarray) -> np.ndarray:
+    """[nl, n] u32 little-endian limbs -> [n, 4*nl] big-endian bytes."""
+    nl = words.shape[0]
+    le = np.ascontiguousarray(words.T).view(np.uint8).reshape(-1, 4 * nl)
+    return le[:, ::-1]
+
+
+def _digest_limbs(dig: np.ndarray) -> np.ndarray:
+    """[n, 32] digests (big-endian integers) -> [8, n] u32 limbs."""
+    le = np.ascontiguousarray(dig[:, ::-1])
+    return np.ascontiguousarray(le.view(np.uint32).T)
+
+
+class KeccakModels(EvmModels):
+    """Keccak-consistent candidates: for every mapping key the path hashes —
+    ``sender_k ++ slot`` and ``to_k ++ slot`` (to = the address argument) — and for the concrete
+    constructor key ``CREATOR ++ slot``, the model's ``keccak256_512`` table holds the TRUE
+    keccak256 and ``keccak256_512-1`` the inverse entry.  UF table lookup (z3 semantics) and the
+    in-kernel keccak-f[1600] then agree on every model."""
+
+    SLOT = 1
+
+    def __init__(self, seed, M, n_tx, lo=0, hi=None, hasher_many=None):
+        super().__init__(seed, M, n_tx, lo, hi, address_args=True)
+        self.hasher_many = hasher_many
+        self._tables = None
+
+    def keys(self) -> List[np.ndarray]:
+        """[n, 64] big-endian 512-bit keys per stored model: the 3 actors, then per tx sender / to."""
+        n = self.hi - self.lo
+        slot = np.zeros((8, n), np.uint32)
+        slot[0] = self.SLOT
+        out = [np.concatenate([_be_bytes(np.repeat(_int_limbs(a)[:, None], n, 1)), _be_bytes(slot)], 1) for a in ACTORS]
+        for k in range(self.n_tx):
+            out.append(np.concatenate([_be_bytes(self.sender[k]), _be_bytes(slot)], 1))
+            # address word: calldata bytes 4..35 (zero past calldatasize) masked to 160 bits
+            to = np.zeros((32, n), np.uint8)
+            idx = np.arange(16, 36)[:, None]
+            to[12:32] = np.where(idx < self.cds[k][0][None, :], self.cdata[k][16:36], 0)
+            out.append(np.concatenate([to.T, _be_bytes(slot)], 1))
+        return out
+
+    def _build(self):
+        if self._tables is not None:
+            return self._tables
+        keys = self.keys()
+        n = self.hi - self.lo
+        E = len(keys)
+        digests = [self.hasher_many(k) for k in keys]
+        fwd = np.zeros((n, E, 24), np.uint32)   # key (16 limbs LE) + value (8 limbs)
+        inv = np.zeros((n, E, 24), np.uint32)   # key (8) + value (16)
+        for e, (k, dg) in enumerate(zip(keys, digests)):
+            key_limbs = np.ascontiguousarray(k[:, ::-1]).view(np.uint32)      # [n, 16] LE limbs
+            val_limbs = _digest_limbs(dg).T                                    # [n, 8]
+            fwd[:, e, :16] = key_limbs
+            fwd[:, e, 16:] = val_limbs
+            inv[:, e, :8] = val_limbs
+            inv[:, e, 8:] = key_limbs
+        ptr = np.arange(n + 1, dtype=np.int64) * E
+        self._tables = {"keccak256_512": (ptr, fwd, np.zeros((n, 8), np.uint32)),
+                        "keccak256_512-1": (ptr, inv, np.zeros((n, 16), np.uint32))}
+        return self._tables
+
+    def extra_table(self, fname, spec):
+        return self._build().get(fname)
+
+    def derived_column(self, fname, args, nl, n):
+        if fname in ("keccak256_512", "keccak256_512-1"):
+            ptr, ent, els = self._build()[fname]
+            kl = 16 if fname == "keccak256_512" else 8
+            key = _int_limbs(args[0], kl)
+            r = np.zeros((nl, n), np.uint32)
+            found = np.zeros(n, bool)
+            for e in range(ent.shape[1]):
+                hit = (ent[:, e, :kl] == key[None, :]).all(1) & ~found
+                r[:, hit] = ent[hit, e, kl:kl + nl].T
+                found |= hit
+            return r
+        return super().derived_column(fname, args, nl, n)
+
+
+def c4_path(rng: np.random.Generator, wit: Dict, n_tx: int, hasher_many) -> S.Term:
+    """A token-transfer path per tx over ``balances[...]`` mappings (storage slot keccak256 of
+    key ++ slot, instructions.py:1017-1055) plus the manager's axioms for every keccak input on
+    the path (keccak_function_manager.py:116-179)."""
+    from .function_managers import KeccakFunctionManager
+
+    def h(v: int) -> int:
+        return int.from_bytes(bytes(hasher_many(np.frombuffer(v.to_bytes(64, "big"), np.uint8)[None, :])[0]), "big")
+
+    km = KeccakFunctionManager(hasher=lambda b: h(int.from_bytes(b, "big")).to_bytes(32, "big"))
+    slot = S.BitVecVal(KeccakModels.SLOT, 256)
+    # constructor: initial balances of the three actors (concrete keys -> concrete hashes)
+    storage = S.K(256, 256, 0)
+    wst = {}
+    for a, addr in enumerate(ACTORS):
+        amount = 10 ** 24 >> a
+        storage = S.Store(storage, km.create_keccak(S.Concat(S.BitVecVal(addr, 256), slot)), amount)
+        wst[h((addr << 256) | KeccakModels.SLOT)] = amount
+    cs: List[S.Term] = []
+    m160 = (1 << 160) - 1
+    for k in range(n_tx):
+        tx = _Tx(k + 1)
+        snd, cds, B = wit["sender"][k], wit["cds"][k], wit["bytes"][k]
+        W0, W1, W2 = _word_val(B, cds, 0), _word_val(B, cds, 4), _word_val(B, cds, 36)
+        w0, w1, w2 = tx.word(0), tx.word(4), tx.word(36)
+        cs.append(S.Or(*[tx.sender == a for a in ACTORS]))
+        cs.append(_holds(S.ULT(tx.cds, S.BitVecVal(68, 256)), cds < 68))
+        cs.append(S.Extract(255, 224, w0) == (W0 >> 224))
+        to = w1 & m160
+        TO = W1 & m160
+        cs.append(_holds(to == 0, TO == 0))
+        hf = km.create_keccak(S.Concat(tx.sender, slot))
+        ht = km.create_keccak(S.Concat(to, slot))
+        HF, HT = h((snd << 256) | KeccakModels.SLOT), h((TO << 256) | KeccakModels.SLOT)
+        bal_f, bal_t = S.Select(storage, hf), S.Select(storage, ht)
+        BF, BT = wst.get(HF, 0), wst.get(HT, 0)
+        cs.append(_holds(S.UGE(bal_f, w2), BF >= W2))
+        storage = S.Store(storage, hf, bal_f - w2)
+        wst[HF] = (BF - W2) & M256
+        BT = wst.get(HT, 0)
+        bal_t = S.Select(storage, ht)
+        cs.append(_holds(S.UGE(bal_t + w2, bal_t), ((BT + W2) & M256) >= BT))
+        storage = S.Store(storage, ht, bal_t + w2)
+        wst[HT] = (BT + W2) & M256
+    # sender's balance after the path is read back (storage chain over every keccak key)
+    cs.append(_holds(S.UGT(S.Select(storage, km.create_keccak(S.Concat(_Tx(1).sender, slot))), S.BitVecVal(0, 256)),
+                     wst.get(h((wit["sender"][0] << 256) | KeccakModels.SLOT), 0) > 0))
+    return S.And(*cs, km.create_conditions())
+
+
+def c4_workload(n_tapes: int = 200, n_models: int = 1_000_000, seed: int = 4, planted_frac: float = 0.1,
+                n_tx: int = 2, shard: Tuple[int, int] = None, hasher_many=None, interpret_keccak: bool = False):
+    """Config C4: keccak-heavy mapping/storage tapes x keccak-consistent models.
+
+    ``interpret_keccak`` lowers ``keccak256_512(x)`` to the in-kernel keccak-f[1600]
+    (MQ_OP_KECCAK) instead of the model's UF table; on these models both give the same verdicts.
+    ``hasher_many``: uint8 [n, len] -> uint8 [n, 32] (the GPU keccak kernel in the product)."""
+    if hasher_many is None:
+        from .evaluator import default_evaluator
+        hasher_many = default_evaluator().keccak256_array
+    rng = np.random.Generator(np.random.PCG64(seed))
+    lo, hi = shard if shard else (0, n_models)
+    models = KeccakModels(seed, n_models, n_tx, lo, hi, hasher_many)
+    ghost = EvmModels(seed + 1_000_003, max(1, n_tapes), n_tx, 0, 0, address_args=True)
+    syms = SymbolTable(interpret_keccak=interpret_keccak)
+    tapes, expected = [], np.full(n_tapes, -1, np.int32)
+    planted = rng.random(n_tapes) < planted_frac
+    def hashed_keys_are_concrete(w) -> bool:
+        # the manager's axioms hold under true hashes only for keys equal to a concrete (actor)
+        # key; keccak-consistent witnesses therefore send to actors with a full address argument
+        return all(w["cds"][k] >= 36 and _word_val(w["bytes"][k], w["cds"][k], 4) in ACTORS
+                   and w["sender"][k] in ACTORS for k in range(n_tx))
+
+    for t in range(n_tapes):
+        if planted[t]:
+            while True:
+                p = int(rng.integers(n_models))
+                wit = models.witness(p)
+                if hashed_keys_are_concrete(wit):
+                    break
+            expected[t] = p
+        else:
+            wit = ghost.witness(t)
+        tapes.append(lower_term(c4_path(rng, wit, n_tx, hasher_many), syms))
     return TapeBatch(tapes), models.batch(syms), expected, syms

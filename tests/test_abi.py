@@ -76,9 +76,17 @@ def test_compile_rejects_what_it_cannot_do():
     ci = evaluator.compile_info(tb, 0)
     assert not ci.supported and "512" in ci.why
     t = Tape()
-    k = t.keccak(t.var(0, 512))
+    k = t.keccak(t.var(0, 520))   # one keccak block holds at most 64 argument bytes here
     tb = TapeBatch([t.finish(t.eq(k, t.const(3, 256)))])
     assert not evaluator.compile_info(tb, 0).supported
+
+
+def test_interpreted_keccak_compiles_to_the_l16_kernel():
+    t = Tape()
+    k = t.keccak(t.var(0, 512))
+    tb = TapeBatch([t.finish(t.eq(k, t.const(3, 256)))])
+    ci = evaluator.compile_info(tb, 0)
+    assert ci.supported and ci.limbs == 16
 
 
 def test_shared_subterms_use_temps():

@@ -277,3 +277,62 @@ def test_many_shared_subterms_use_hbm_temps(evaluator):
     assert (v == cref.verdicts(tb, mb)).all()
     ref, _ = cref.first_hit(tb, mb)
     assert (evaluator.first_hit(tb) == ref).all()
+
+
+# ---------------------------------------------------------------- C4: keccak-heavy, in-kernel keccak-f
+def _gpu_hasher(evaluator):
+    return evaluator.keccak256_array
+
+
+@pytest.mark.parametrize("interpret", [False, True])
+def test_c4_keccak_tapes_match_oracle(evaluator, interpret):
+    from mythril_amd.synth_evm import c4_workload
+    tb, mb, exp, syms = c4_workload(40, 1500, seed=4, planted_frac=0.4, hasher_many=evaluator.keccak256_array,
+                                    interpret_keccak=interpret)
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    assert ct.n_unsupported == 0
+    if interpret:
+        assert ct.split()[2] == tb.n_tapes  # all on the L=16 keccak kernel
+    fh = evaluator.first_hit(ct)
+    ref, _ = cref.first_hit(tb, mb)
+    assert (ref == exp).all()
+    assert (fh == ref).all(), np.flatnonzero(fh != ref)[:10]
+    v, _ = evaluator.verdicts(tb)
+    assert (v == cref.verdicts(tb, mb)).all()
+
+
+def test_keccak_op_all_widths(evaluator):
+    """Interpreted keccak of 1..64-byte arguments (the padding byte moves through every lane
+    position, including the 64-byte case where it leaves the value registers)."""
+    rng = np.random.default_rng(11)
+    widths = [8 * k for k in range(1, 65)]
+    M = 70
+    mb = ModelBatch(widths, np.vstack([rng.integers(0, 1 << 32, ((w + 31) // 32, M), dtype=np.uint64).astype(np.uint32)
+                                       for w in widths]))
+    tapes = []
+    for v, w in enumerate(widths):
+        t = Tape()
+        k = t.keccak(t.var(v, w))
+        # compare against the model-0 digest computed by the oracle, plus a low-byte predicate
+        val = sum(int(mb.var_words[int(mb.var_word_offsets()[v]) + i, 0]) << (32 * i) for i in range((w + 31) // 32))
+        dig = int.from_bytes(keccak_ref.keccak256(val.to_bytes(w // 8, "big")), "big")
+        tapes.append(t.finish(t.eq(k, t.const(dig, 256))))
+        t2 = Tape()
+        k2 = t2.keccak(t2.var(v, w))
+        tapes.append(t2.finish(t2.ult(t2.extract(7, 0, k2), t2.const(100, 8))))
+    tb = TapeBatch(tapes)
+    evaluator.upload_models(mb)
+    v_gpu, fh = evaluator.verdicts(tb)
+    assert (fh != -2).all()
+    assert v_gpu[0::2, 0].all()
+    assert (v_gpu == cref.verdicts(tb, mb)).all()
+
+
+def test_c5_deep_tapes_match_oracle(evaluator):
+    from mythril_amd.synth_evm import c3_workload
+    tb, mb, exp, _ = c3_workload(16, 3000, seed=5, planted_frac=0.5, n_tx=5, checks_per_tx=(10, 14))
+    evaluator.upload_models(mb)
+    fh = evaluator.first_hit(tb)
+    ref, _ = cref.first_hit(tb, mb)
+    assert (ref == exp).all() and (fh == ref).all()
