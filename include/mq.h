@@ -140,6 +140,8 @@ typedef struct mq_tape_batch {
  *     stride_f = sum_i limbs(arg_width[i]) + limbs(result_width): args first, then value.
  *     else value of (f, m): else_words[else_base[f] + m*limbs(result_width) ..].
  *     A function absent from a model has no entries and else value 0 (z3 completion).
+ *   Variable words are reduced mod 2^width on upload (bits above a width are ignored); function
+ *   entry keys must already be canonical (they are matched word for word).
  */
 typedef struct mq_func_desc {
   uint16_t arity;          /* 1 or 2 */

@@ -111,6 +111,8 @@ for d in range(1, D):
 for d in range(2, D):
     H(("BITE", d), [f"s_and_b64 s[34:35], {B(d - 2)}, {B(d - 1)}", f"s_andn2_b64 s[36:37], {B(d)}, {B(d - 2)}",
                     f"s_or_b64 {B(d - 2)}, s[34:35], s[36:37]"])
+    H(("BITE_EF", d), [f"s_and_b64 s[34:35], {B(d - 1)}, {B(d)}", f"s_andn2_b64 s[36:37], {B(d - 2)}, {B(d - 1)}",
+                       f"s_or_b64 {B(d - 2)}, s[34:35], s[36:37]"])
 
 
 # ---------------------------------------------------------------- 256-bit predicates
@@ -179,6 +181,8 @@ for d in range(D):
     H(("BNOT", d), [f"v_not_b32 {S(d, l)}, {S(d, l)}" for l in range(L)])
 for d in range(2, D):
     H(("ITE", d), [f"v_cndmask_b32_e64 {S(d - 2, l)}, {S(d, l)}, {S(d - 1, l)}, {B(d - 2)}" for l in range(L)])
+    # else-first ternaries (gprog.h G_ITE_EF / G_BITE_EF): else at d-2, cond at d-1, then at d
+    H(("ITE_EF", d), [f"v_cndmask_b32_e64 {S(d - 2, l)}, {S(d - 2, l)}, {S(d, l)}, {B(d - 1)}" for l in range(L)])
 
 
 def mul_body(d):

@@ -70,6 +70,7 @@ struct mq_ctx {
   DevBuf counters;
   DevBuf best_tmp;  // scratch first-hit buffer for the synchronous API
   DevBuf scratch;   // per-wave temp slots of the HIP C++ interpreter (persistent grid)
+  DevBuf rowmask;   // per-row masks applied to uploaded variable words
   DevBuf verdict_buf;
   // assembly interpreter (qsa.hip): handler byte offsets read back at context creation
   bool qsa_ready = false;
@@ -277,6 +278,24 @@ int mq_models_upload(mq_ctx* c, const mq_model_batch* mb) {
   HIPCHK(c->vars.ensure(sizeof(uint32_t) * (size_t)(rows + 1) * M));
   if (rows > 0) HIPCHK(hipMemcpyAsync(c->vars.p, mb->var_words, sizeof(uint32_t) * (size_t)rows * M, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemsetAsync((uint32_t*)c->vars.p + (size_t)rows * M, 0, sizeof(uint32_t) * M, c->stream));
+  {
+    // canonical values: bits above a variable's width are cleared on the device (the kernels
+    // and the asm interpreter read rows unmasked)
+    std::vector<uint32_t> rowmask((size_t)rows + 1, 0xFFFFFFFFu);
+    bool need = false;
+    for (int v = 0; v < mb->n_vars; v++) {
+      const int w = mb->var_width[v];
+      const uint32_t top = w == 0 ? 1u : ((w % 32) ? ((1u << (w % 32)) - 1u) : 0xFFFFFFFFu);
+      if (top != 0xFFFFFFFFu) {
+        rowmask[voff[v] + vnl[v] - 1] = top;
+        need = true;
+      }
+    }
+    if (need) {
+      HIPCHK(c->rowmask.upload(rowmask.data(), rowmask.size(), c->stream));
+      HIPCHK(launch_mask_rows(c->vars.as<uint32_t>(), c->rowmask.as<uint32_t>(), rows, M, c->stream));
+    }
+  }
   c->qsa_models_ok = true;
   for (int v = 0; v < 8; v++)
     for (int l = 0; l < 8; l++) {
@@ -354,6 +373,8 @@ static bool qsa_translate(const mq_ctx* c, const CompiledTape& x, std::vector<ui
       case G_BOR: ok = word(QK_BOR, d, -1, 0); break;
       case G_BXOR: ok = word(QK_BXOR, d, -1, 0); break;
       case G_ITE: ok = word(QK_ITE, d, -1, 0); break;
+      case G_ITE_EF: ok = word(QK_ITE_EF, d, -1, 0); break;
+      case G_BITE_EF: ok = word(QK_BITE_EF, d, -1, 0); break;
       // signed predicates and wrapping arithmetic: full 256-bit width only (no masking)
       case G_SLT: ok = imm == 256 && word(QK_SLT, d, -1, 0); break;
       case G_SLE: ok = imm == 256 && word(QK_SLE, d, -1, 0); break;

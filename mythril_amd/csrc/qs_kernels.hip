@@ -414,11 +414,10 @@ __constant__ uint64_t kKeccakRC[24] = {
 
 MQ_DEV uint64_t krol(uint64_t v, int n) { return n ? (v << n) | (v >> (64 - n)) : v; }
 
-__device__ __noinline__ void keccak_f1600(uint64_t* A) {
+// state by reference and inlined: the 25 lanes stay in VGPRs (a pointer argument to a
+// non-inlined function put them in scratch memory)
+MQ_DEV void keccak_f1600(uint64_t (&a)[25]) {
   constexpr int R[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
-  uint64_t a[25];
-#pragma unroll
-  for (int i = 0; i < 25; i++) a[i] = A[i];
   for (int r = 0; r < 24; r++) {
     uint64_t C[5], Dd[5], B[25];
 #pragma unroll
@@ -437,8 +436,6 @@ __device__ __noinline__ void keccak_f1600(uint64_t* A) {
       for (int x = 0; x < 5; x++) a[x + 5 * y] = B[x + 5 * y] ^ ((~B[(x + 1) % 5 + 5 * y]) & B[(x + 2) % 5 + 5 * y]);
     a[0] ^= kKeccakRC[r];
   }
-#pragma unroll
-  for (int i = 0; i < 25; i++) A[i] = a[i];
 }
 
 template <int L, int D>
@@ -763,6 +760,18 @@ __global__ __launch_bounds__(256) void qs_verdict_kernel(KArgs args) {
       if (valid) args.verdicts[(int64_t)dsc.tape * args.M + m] = r ? 1 : 0;
     }
   }
+}
+
+__global__ void qs_mask_rows(uint32_t* vars, const uint32_t* rowmask, int64_t rows, int64_t M) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < rows * M) vars[i] &= rowmask[i / M];
+}
+
+hipError_t launch_mask_rows(uint32_t* vars, const uint32_t* rowmask, int64_t rows, int64_t M, hipStream_t st) {
+  const int64_t n = rows * M;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(qs_mask_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, vars, rowmask, rows, M);
+  return hipGetLastError();
 }
 
 __global__ void qs_init_best(int32_t* best, int n) {

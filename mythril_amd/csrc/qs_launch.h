@@ -77,6 +77,7 @@ static_assert(__builtin_offsetof(QArgs, var_row) == 0x60, "QArgs layout");
 hipError_t launch_qsa(const QArgs* d_args, unsigned gx, unsigned gy, size_t lds, hipStream_t st);
 hipError_t launch_qs(const KArgs& a, int L, bool keccak, bool verdict, hipStream_t st);
 hipError_t launch_init_best(int32_t* best, int n, hipStream_t st);
+hipError_t launch_mask_rows(uint32_t* vars, const uint32_t* rowmask, int64_t rows, int64_t M, hipStream_t st);
 hipError_t launch_finalize_best(int32_t* best, const uint8_t* unsupported, int n, hipStream_t st);
 hipError_t launch_keccak(const uint8_t* data, const int64_t* offsets, int n, uint8_t* out, hipStream_t st);
 

@@ -315,7 +315,9 @@ def test_keccak_op_all_widths(evaluator):
         t = Tape()
         k = t.keccak(t.var(v, w))
         # compare against the model-0 digest computed by the oracle, plus a low-byte predicate
+        # raw words are NOT masked to the width: the upload must reduce them mod 2^w
         val = sum(int(mb.var_words[int(mb.var_word_offsets()[v]) + i, 0]) << (32 * i) for i in range((w + 31) // 32))
+        val &= (1 << w) - 1
         dig = int.from_bytes(keccak_ref.keccak256(val.to_bytes(w // 8, "big")), "big")
         tapes.append(t.finish(t.eq(k, t.const(dig, 256))))
         t2 = Tape()
