@@ -100,6 +100,7 @@ struct mq_tapes {
     int L = 0;
     int begin = 0, count = 0;  // range in descs
     int max_temps = 0;
+    int max_depth = 1;
     bool keccak = false;
   };
   // descs layout: [L8 QSA-eligible | L8 other | L16]; the QSA view (qdescs/qprog) holds the
@@ -456,6 +457,7 @@ int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t*
         qdescs.push_back(d);
       }
       v.max_temps = std::max(v.max_temps, x.n_temps);
+      v.max_depth = std::max(v.max_depth, x.depth);
     }
     v.count = (int)descs.size() - v.begin;
   }
@@ -463,6 +465,7 @@ int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t*
   T->l8_all.begin = 0;
   T->l8_all.count = T->qsa.count + T->l8_rest.count;
   T->l8_all.max_temps = std::max(T->qsa.max_temps, T->l8_rest.max_temps);
+  T->l8_all.max_depth = std::max(T->qsa.max_depth, T->l8_rest.max_depth);
   // trailing END words: the dispatch tail prefetches one word past each program's END
   qprog.push_back(c->qsa_ready ? c->qsa_off[c->qsa_index[QK_END][0][0]] / 4 : 0);
   qprog.push_back(qprog.back());
@@ -491,16 +494,17 @@ int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t*
 
 void mq_tapes_free(mq_tapes* t) { delete t; }
 
-// Workgroups of the persistent HIP C++ kernels: 8 per CU on 256 CUs; each strides over the
-// (model tile, tape group) items.  Bounds the temp scratch to grid * 4 waves * temps * 2 KB.
-static constexpr int64_t kPersistentGroups = 2048;
+// Workgroups (one wave each) of the persistent HIP C++ kernels: 16 per CU on 256 CUs; each
+// strides over the (model tile, tape group) items.  Bounds the temp scratch to
+// grid * temps * 2 KB (L = 8).
+static constexpr int64_t kPersistentGroups = 4096;
 
 static KArgs make_args(mq_ctx* c, mq_tapes* T, const mq_tapes::Variant& v) {
   KArgs a{};
   a.descs = T->descs.as<GDesc>() + v.begin;
   a.n_desc = v.count;
-  const int64_t tiles = (c->M + 255) / 256;
-  // ~8k workgroups: enough to fill 256 CUs many times over with a short tail
+  const int64_t tiles = (c->M + 63) / 64;
+  // ~8k (tile, tape group) items: enough to fill 256 CUs many times over with a short tail
   int64_t tpg = (int64_t(v.count) * tiles + 8191) / 8192;
   tpg = std::max<int64_t>(1, std::min<int64_t>(tpg, v.count));
   a.tapes_per_group = (int)tpg;
@@ -525,6 +529,7 @@ static KArgs make_args(mq_ctx* c, mq_tapes* T, const mq_tapes::Variant& v) {
   a.n_items = tiles * groups;
   a.grid = (int)std::min<int64_t>(a.n_items, kPersistentGroups);
   a.scratch = nullptr;
+  a.stack_slots = std::max(1, v.max_depth);
   return a;
 }
 
@@ -589,7 +594,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
   for (const auto& v : cpp) {
     if (v.count <= 0) continue;
     KArgs a = make_args(c, T, v);
-    const size_t scratch_bytes = (size_t)a.grid * 4 * (size_t)a.tmp_words_per_wave * 4;
+    const size_t scratch_bytes = (size_t)a.grid * (size_t)a.tmp_words_per_wave * 4;
     if (scratch_bytes) {
       HIPCHK(c->scratch.ensure(scratch_bytes));
       a.scratch = c->scratch.as<uint32_t>();

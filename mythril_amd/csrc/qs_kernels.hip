@@ -1,12 +1,23 @@
-// qs_kernels.hip — gfx950 quick-sat kernels: N constraint tapes x M candidate models.
+// qs_kernels.hip — gfx950 quick-sat kernels (general vocabulary): N constraint tapes x M models.
 //
 // Replaces the per-model Python/z3 loop of ModelCache.check_quick_sat
-// (mythril/support/support_utils.py:60-67): lane = one candidate model (index m), the
-// wave runs the SAME compiled tape (wave-uniform instruction stream read through the scalar
-// cache, handlers specialized per register-stack slot), and the per-lane Bool verdict is
-// reduced with a wave ballot; the lowest satisfying lane is published with an agent-scope
-// atomicMin on first_hit[tape] (global candidate index, INT32_MAX = none).  Waves whose first
-// model index is already >= the published minimum skip the tape (first-hit early exit).
+// (mythril/support/support_utils.py:60-67): lane = one candidate model (index m), the wave
+// runs the SAME compiled tape (wave-uniform instruction stream read through the scalar cache),
+// and the per-lane Bool verdict is reduced with a wave ballot; the lowest satisfying lane is
+// published with an agent-scope atomicMin on first_hit[tape] (global candidate index,
+// INT32_MAX = none).  Waves whose first model index is already >= the published minimum skip
+// the tape (first-hit early exit).
+//
+// Operand stack in LDS.  The straight-line stack programs of gprog.h address stack slots by a
+// runtime (wave-uniform) depth d.  A register-resident stack forced a per-slot specialisation of
+// every handler, and the switch joins of that dispatch made the register allocator copy the
+// whole stack around each node (~440 VALU per node measured with rocprofv3 on the C3 workload,
+// profiles/r01_c3_pmc.json).  Here slot d lives in LDS at a uniform offset; a handler reads its
+// operands into registers, computes, and writes the canonical result back, so nothing is live
+// across the dispatch.  Layout per wave: [slot][limb group of 4][lane] of uint4, i.e.
+// ds_read_b128 / ds_write_b128 with consecutive lanes on consecutive 16-byte words (no bank
+// conflicts).  Every slot holds a canonical L-limb value (zeros above its width), so a reader
+// may skip limb groups above its operand width, and values <= 32 bits take 1-limb fast paths.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -16,21 +27,8 @@
 
 namespace mq {
 
-// Uniform, read-only-for-the-launch data (programs, constants, descriptors, var/func tables)
-// is read through the CONSTANT address space: loads at uniform addresses then lower to
-// s_load (scalar cache) instead of global_load + readfirstlane.  Plain global pointers are
-// not provably unclobbered here (the kernel also stores: atomicMin, verdicts, LDS temps).
 typedef const __attribute__((address_space(4))) uint32_t* cu32p;
-typedef const __attribute__((address_space(4))) GDesc* cdescp;
-typedef const __attribute__((address_space(4))) FuncDev* cfuncp;
 #define CONSTP(T, p) ((T)(const void*)(p))
-
-template <int L>
-struct VecT;
-template <>
-struct VecT<8> { typedef uint32_t type __attribute__((ext_vector_type(8))); };
-template <>
-struct VecT<16> { typedef uint32_t type __attribute__((ext_vector_type(16))); };
 
 MQ_DEV GDesc load_desc(const GDesc* descs, int i) {
   cu32p w = CONSTP(cu32p, descs) + (size_t)i * 8;
@@ -46,13 +44,7 @@ MQ_DEV GDesc load_desc(const GDesc* descs, int i) {
   return d;
 }
 
-template <int L, int D>
-struct Stack {
-  typename VecT<L>::type s[D];
-};
-
-// Everything a handler may read; built once per wave from the kernel arguments and fully
-// scalar-replaced after inlining (uniform fields stay in SGPRs).
+// Everything a handler may read; uniform fields stay in SGPRs.
 struct Ctx {
   const uint32_t* vars;
   const uint32_t* var_off;
@@ -66,11 +58,12 @@ struct Ctx {
   int64_t M;
   cu32p consts;            // constants of the current tape
   int64_t m;               // local model index of this lane (clamped to M-1)
-  uint32_t* tmp;           // this wave's LDS temp region (slot, limb, lane)
+  uint32_t* tmp;           // this wave's temp slots in HBM (slot, limb, lane)
+  uint4* stk;              // this wave's LDS operand stack, offset by the lane
   int lane;
 };
 
-MQ_DEV Ctx make_ctx(const KArgs& a, int64_t m, uint32_t* tmp, int lane) {
+MQ_DEV Ctx make_ctx(const KArgs& a, int64_t m, uint32_t* tmp, uint4* stk, int lane) {
   Ctx c;
   c.vars = a.vars;
   c.var_off = a.var_off;
@@ -85,279 +78,456 @@ MQ_DEV Ctx make_ctx(const KArgs& a, int64_t m, uint32_t* tmp, int lane) {
   c.consts = CONSTP(cu32p, a.consts);
   c.m = m;
   c.tmp = tmp;
+  c.stk = stk + lane;
   c.lane = lane;
   return c;
 }
 
-#define H_DEV template <int d> __device__ __forceinline__ static void
+MQ_DEV uint32_t nl_of_w(uint32_t W) { return W == 0 ? 1u : (W + 31u) >> 5; }
+
+// ---------------------------------------------------------------- LDS stack access
+template <int L>
+MQ_DEV void sld(const Ctx& cx, int d, uint32_t (&x)[L], uint32_t nl = L) {
+  const uint4* p = cx.stk + (d * (L / 4)) * 64;
+#pragma unroll
+  for (int g = 0; g < L / 4; g++) {
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (g == 0 || (uint32_t)(4 * g) < nl) v = p[g * 64];
+    x[4 * g] = v.x;
+    x[4 * g + 1] = v.y;
+    x[4 * g + 2] = v.z;
+    x[4 * g + 3] = v.w;
+  }
+}
+template <int L>
+MQ_DEV void sst(const Ctx& cx, int d, const uint32_t (&x)[L]) {
+  uint4* p = cx.stk + (d * (L / 4)) * 64;
+#pragma unroll
+  for (int g = 0; g < L / 4; g++) p[g * 64] = make_uint4(x[4 * g], x[4 * g + 1], x[4 * g + 2], x[4 * g + 3]);
+}
+template <int L>
+MQ_DEV uint32_t sld0(const Ctx& cx, int d) {
+  return reinterpret_cast<const uint32_t*>(cx.stk + (d * (L / 4)) * 64)[0];
+}
+// a value of at most 32 bits: limb 0, zeros above (keeps the slot canonical)
+template <int L>
+MQ_DEV void sst0(const Ctx& cx, int d, uint32_t v) {
+  uint4* p = cx.stk + (d * (L / 4)) * 64;
+  p[0] = make_uint4(v, 0u, 0u, 0u);
+#pragma unroll
+  for (int g = 1; g < L / 4; g++) p[g * 64] = make_uint4(0u, 0u, 0u, 0u);
+}
+// Bool results: limb 0 only.  Bool slots are only ever read through limb 0 (Bool connectives,
+// ite conditions, temps copy all limbs but their Bool readers again look at limb 0).
+template <int L>
+MQ_DEV void sstb(const Ctx& cx, int d, bool b) {
+  reinterpret_cast<uint32_t*>(cx.stk + (d * (L / 4)) * 64)[0] = b ? 1u : 0u;
+}
+
+MQ_DEV uint32_t mask32(uint32_t W) { return W >= 32u ? 0xFFFFFFFFu : ((1u << W) - 1u); }
 
 // ---------------------------------------------------------------- leaves
-template <int L, int D>
-struct HPushVar {
-  static constexpr int kMin = 0;
-  H_DEV run(Stack<L, D>& S, uint32_t imm, uint32_t, const Ctx& cx) {
-    uint32_t nl = 0, off = 0;
-    if (imm < (uint32_t)cx.n_vars) {
-      off = CONSTP(cu32p, cx.var_off)[imm];
-      nl = CONSTP(cu32p, cx.var_nl)[imm];
+template <int L>
+MQ_DEV void h_push_var(const Ctx& cx, int d, uint32_t imm) {
+  uint32_t nl = 0, off = 0;
+  if (imm < (uint32_t)cx.n_vars) {
+    off = CONSTP(cu32p, cx.var_off)[imm];
+    nl = CONSTP(cu32p, cx.var_nl)[imm];
+  }
+  const uint32_t* base = cx.vars + (int64_t)off * cx.M + cx.m;
+  if (nl == 1) {
+    sst0<L>(cx, d, base[0]);
+    return;
+  }
+  uint32_t x[L];
+#pragma unroll
+  for (int i = 0; i < L; i++) x[i] = ((uint32_t)i < nl) ? base[(int64_t)i * cx.M] : 0u;
+  sst<L>(cx, d, x);
+}
+
+template <int L>
+MQ_DEV void h_push_const(const Ctx& cx, int d, uint32_t imm) {
+  cu32p c = cx.consts + imm;
+  uint32_t x[L];
+#pragma unroll
+  for (int i = 0; i < L; i++) x[i] = c[i];
+  sst<L>(cx, d, x);
+}
+
+template <int L>
+MQ_DEV void h_push_tmp(const Ctx& cx, int d, uint32_t imm) {
+  const uint32_t* p = cx.tmp + (imm * L) * 64 + cx.lane;
+  uint32_t x[L];
+#pragma unroll
+  for (int i = 0; i < L; i++) x[i] = p[i * 64];
+  sst<L>(cx, d, x);
+}
+
+template <int L>
+MQ_DEV void h_store_tmp(const Ctx& cx, int d, uint32_t imm) {
+  uint32_t x[L];
+  sld<L>(cx, d, x);
+  uint32_t* p = cx.tmp + (imm * L) * 64 + cx.lane;
+#pragma unroll
+  for (int i = 0; i < L; i++) p[i * 64] = x[i];
+}
+
+// ---------------------------------------------------------------- predicates (W = operand width)
+template <int L>
+MQ_DEV void h_eq(const Ctx& cx, int d, uint32_t W) {
+  if (W <= 32u) {
+    sstb<L>(cx, d - 1, sld0<L>(cx, d - 1) == sld0<L>(cx, d));
+    return;
+  }
+  const uint32_t nl = nl_of_w(W);
+  uint32_t x[L], y[L];
+  sld<L>(cx, d - 1, x, nl);
+  sld<L>(cx, d, y, nl);
+  sstb<L>(cx, d - 1, eq_n<L>(x, y));
+}
+
+// kind: 0 ult, 1 ule, 2 ugt, 3 uge ; signed compares flip the sign bit at W-1 first
+template <int L>
+MQ_DEV void h_cmp(const Ctx& cx, int d, uint32_t W, int kind, bool sgn) {
+  if (W <= 32u) {
+    uint32_t a = sld0<L>(cx, d - 1), b = sld0<L>(cx, d);
+    if (sgn) {
+      const uint32_t sb = 1u << (W - 1u);
+      a ^= sb;
+      b ^= sb;
     }
-    const uint32_t* base = cx.vars + (int64_t)off * cx.M + cx.m;
+    const bool r = kind == 0 ? a < b : kind == 1 ? a <= b : kind == 2 ? a > b : a >= b;
+    sstb<L>(cx, d - 1, r);
+    return;
+  }
+  const uint32_t nl = nl_of_w(W);
+  uint32_t x[L], y[L];
+  sld<L>(cx, d - 1, x, nl);
+  sld<L>(cx, d, y, nl);
+  if (sgn) {
+    sext_full<L>(x, W);
+    sext_full<L>(y, W);
+    x[L - 1] ^= 0x80000000u;
+    y[L - 1] ^= 0x80000000u;
+  }
+  bool r;
+  if (kind == 0) r = ult_n<L>(x, y);
+  else if (kind == 1) r = !ult_n<L>(y, x);
+  else if (kind == 2) r = ult_n<L>(y, x);
+  else r = !ult_n<L>(x, y);
+  sstb<L>(cx, d - 1, r);
+}
+
+// ---------------------------------------------------------------- arithmetic (W = result width)
+template <int L>
+MQ_DEV void h_add_sub(const Ctx& cx, int d, uint32_t W, bool sub) {
+  if (W <= 32u) {
+    const uint32_t a = sld0<L>(cx, d - 1), b = sld0<L>(cx, d);
+    sst0<L>(cx, d - 1, (sub ? a - b : a + b) & mask32(W));
+    return;
+  }
+  uint32_t x[L], y[L];
+  sld<L>(cx, d - 1, x);
+  sld<L>(cx, d, y);
+  if (sub) (void)sub_n<L>(x, x, y);
+  else add_n<L>(x, x, y);
+  mask_w<L>(x, W);
+  sst<L>(cx, d - 1, x);
+}
+
+template <int L>
+MQ_DEV void h_mul(const Ctx& cx, int d, uint32_t W) {
+  if (W <= 32u) {
+    sst0<L>(cx, d - 1, (sld0<L>(cx, d - 1) * sld0<L>(cx, d)) & mask32(W));
+    return;
+  }
+  uint32_t x[L], y[L], r[L];
+  sld<L>(cx, d - 1, x);
+  sld<L>(cx, d, y);
+  mul_lo_n<L>(r, x, y);
+  mask_w<L>(r, W);
+  sst<L>(cx, d - 1, r);
+}
+
+template <int L>
+MQ_DEV void h_neg_not(const Ctx& cx, int d, uint32_t W, bool is_not) {
+  if (W <= 32u) {
+    const uint32_t a = sld0<L>(cx, d);
+    sst0<L>(cx, d, (is_not ? ~a : 0u - a) & mask32(W));
+    return;
+  }
+  uint32_t x[L];
+  sld<L>(cx, d, x);
+  if (is_not) {
 #pragma unroll
-    for (int i = 0; i < L; i++) S.s[d][i] = ((uint32_t)i < nl) ? base[(int64_t)i * cx.M] : 0u;
+    for (int i = 0; i < L; i++) x[i] = ~x[i];
+  } else {
+    neg_n<L>(x);
   }
-};
+  mask_w<L>(x, W);
+  sst<L>(cx, d, x);
+}
 
-template <int L, int D>
-struct HPushConst {
-  static constexpr int kMin = 0;
-  H_DEV run(Stack<L, D>& S, uint32_t imm, uint32_t, const Ctx& cx) {
-    cu32p c = cx.consts + imm;
+// bitwise: 0 and, 1 or, 2 xor
+template <int L>
+MQ_DEV void h_bitwise(const Ctx& cx, int d, uint32_t W, int kind) {
+  if (W <= 32u) {
+    const uint32_t a = sld0<L>(cx, d - 1), b = sld0<L>(cx, d);
+    sst0<L>(cx, d - 1, kind == 0 ? (a & b) : kind == 1 ? (a | b) : (a ^ b));
+    return;
+  }
+  const uint32_t nl = nl_of_w(W);
+  uint32_t x[L], y[L];
+  sld<L>(cx, d - 1, x, nl);
+  sld<L>(cx, d, y, nl);
 #pragma unroll
-    for (int i = 0; i < L; i++) S.s[d][i] = c[i];
-  }
-};
+  for (int i = 0; i < L; i++) x[i] = kind == 0 ? (x[i] & y[i]) : kind == 1 ? (x[i] | y[i]) : (x[i] ^ y[i]);
+  sst<L>(cx, d - 1, x);
+}
 
-template <int L, int D>
-struct HPushTmp {
-  static constexpr int kMin = 0;
-  H_DEV run(Stack<L, D>& S, uint32_t imm, uint32_t, const Ctx& cx) {
-    const uint32_t* p = cx.tmp + (imm * L) * 64 + cx.lane;
+// ite: cond at slot c, then at t, else at e, result to r
+template <int L>
+MQ_DEV void h_ite(const Ctx& cx, int c, int t, int e, int r, uint32_t W) {
+  const bool cond = (sld0<L>(cx, c) & 1u) != 0;
+  if (W <= 32u) {
+    const uint32_t a = sld0<L>(cx, t), b = sld0<L>(cx, e);
+    sst0<L>(cx, r, cond ? a : b);
+    return;
+  }
+  const uint32_t nl = nl_of_w(W);
+  uint32_t x[L], y[L];
+  sld<L>(cx, t, x, nl);
+  sld<L>(cx, e, y, nl);
 #pragma unroll
-    for (int i = 0; i < L; i++) S.s[d][i] = p[i * 64];
-  }
-};
+  for (int i = 0; i < L; i++) x[i] = cond ? x[i] : y[i];
+  sst<L>(cx, r, x);
+}
 
-template <int L, int D>
-struct HStoreTmp {
-  static constexpr int kMin = 0;
-  H_DEV run(Stack<L, D>& S, uint32_t imm, uint32_t, const Ctx& cx) {
-    uint32_t* p = cx.tmp + (imm * L) * 64 + cx.lane;
+template <int L>
+MQ_DEV void h_extract(const Ctx& cx, int d, uint32_t lo, uint32_t W) {
+  if (lo + W <= 32u) {
+    sst0<L>(cx, d, (sld0<L>(cx, d) >> lo) & mask32(W));
+    return;
+  }
+  uint32_t x[L];
+  sld<L>(cx, d, x, nl_of_w(lo + W));
+  shr_uni<L>(x, lo);
+  mask_w<L>(x, W);
+  sst<L>(cx, d, x);
+}
+
+template <int L>
+MQ_DEV void h_concat(const Ctx& cx, int d, uint32_t wl, uint32_t W) {
+  if (W <= 32u) {
+    sst0<L>(cx, d - 1, (sld0<L>(cx, d - 1) << wl) | sld0<L>(cx, d));
+    return;
+  }
+  uint32_t x[L], y[L];
+  sld<L>(cx, d - 1, x, nl_of_w(W - wl));
+  sld<L>(cx, d, y, nl_of_w(wl));
+  shl_uni<L>(x, wl);
 #pragma unroll
-    for (int i = 0; i < L; i++) p[i * 64] = S.s[d][i];
-  }
-};
+  for (int i = 0; i < L; i++) x[i] |= y[i];
+  sst<L>(cx, d - 1, x);
+}
 
-template <int L, int D>
-struct HPushBool {
-  static constexpr int kMin = 0;
-  H_DEV run(Stack<L, D>& S, uint32_t imm, uint32_t, const Ctx&) { S.s[d][0] = imm & 1u; }
-};
+template <int L>
+MQ_DEV void h_sext(const Ctx& cx, int d, uint32_t w0, uint32_t W) {
+  uint32_t x[L];
+  sld<L>(cx, d, x, nl_of_w(w0));
+  sext_full<L>(x, w0);
+  mask_w<L>(x, W);
+  sst<L>(cx, d, x);
+}
 
-// ---------------------------------------------------------------- Bool connectives (limb 0)
-template <int L, int D>
-struct HNot {
-  static constexpr int kMin = 0;
-  H_DEV run(Stack<L, D>& S, uint32_t, uint32_t, const Ctx&) { S.s[d][0] ^= 1u; }
-};
+// ---------------------------------------------------------------- division
+// per-lane bit length of a canonical value
+template <int L>
+MQ_DEV uint32_t bitlen_n(const uint32_t (&a)[L]) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < L; i++) r = a[i] ? 32u * i + 32u - (uint32_t)__clz(a[i]) : r;
+  return r;
+}
 
-#define BOOL_BIN(NAME, EXPR)                                                 \
-  template <int L, int D>                                                    \
-  struct NAME {                                                              \
-    static constexpr int kMin = 1;                                           \
-    H_DEV run(Stack<L, D>& S, uint32_t, uint32_t, const Ctx&) {              \
-      const uint32_t x = S.s[d - 1][0], y = S.s[d][0];                       \
-      S.s[d - 1][0] = (EXPR);                                                \
-    }                                                                        \
-  };
-BOOL_BIN(HAnd, x & y)
-BOOL_BIN(HOr, x | y)
-BOOL_BIN(HXor, x ^ y)
-BOOL_BIN(HIff, (x == y) ? 1u : 0u)
-BOOL_BIN(HImplies, (x ^ 1u) | y)
-
-template <int L, int D>
-struct HBIte {
-  static constexpr int kMin = 2;
-  H_DEV run(Stack<L, D>& S, uint32_t, uint32_t, const Ctx&) {
-    S.s[d - 2][0] = S.s[d - 2][0] ? S.s[d - 1][0] : S.s[d][0];
-  }
-};
-
-// ---------------------------------------------------------------- predicates (imm = operand width)
-template <int L, int D>
-struct HEq {
-  static constexpr int kMin = 1;
-  H_DEV run(Stack<L, D>& S, uint32_t, uint32_t, const Ctx&) {
-    S.s[d - 1][0] = eq_n<L>(S.s[d - 1], S.s[d]) ? 1u : 0u;
-  }
-};
-
-// kind: 0 ult, 1 ule, 2 ugt, 3 uge ; signed variants flip the sign bits first
-template <int L, int D, int KIND, bool SIGNED>
-struct HCmpT {
-  static constexpr int kMin = 1;
-  H_DEV run(Stack<L, D>& S, uint32_t W, uint32_t, const Ctx&) {
-    if (SIGNED) {
-      sext_full<L>(S.s[d - 1], W);
-      sext_full<L>(S.s[d], W);
-      S.s[d - 1][L - 1] ^= 0x80000000u;
-      S.s[d][L - 1] ^= 0x80000000u;
+// q = a / b, r = a % b (unsigned, full 32L bits); b == 0 -> q = all ones, r = a (SMT-LIB).
+// Divisors < 2^32 in every lane: schoolbook 64/32 long division (L steps).  Otherwise
+// restoring division over only the quotient's bit length (bitlen(a) - bitlen(b) + 1 steps,
+// the wave's maximum), with the divisor pre-aligned to the dividend's top bit.
+template <int L>
+MQ_DEV void udivrem_fast(uint32_t (&q)[L], uint32_t (&r)[L], const uint32_t (&a)[L], const uint32_t (&b)[L]) {
+  const bool bz = is_zero_n<L>(b);
+  uint32_t bhi = 0;
+#pragma unroll
+  for (int i = 1; i < L; i++) bhi |= b[i];
+  if (__ballot(bhi != 0u) == 0) {
+    const uint32_t dv = bz ? 1u : b[0];
+    uint32_t rem = 0;
+#pragma unroll
+    for (int i = L - 1; i >= 0; i--) {
+      const uint64_t n = ((uint64_t)rem << 32) | a[i];
+      const uint64_t qq = n / dv;
+      q[i] = (uint32_t)qq;
+      rem = (uint32_t)(n - qq * dv);
     }
-    bool r;
-    if (KIND == 0) r = ult_n<L>(S.s[d - 1], S.s[d]);
-    else if (KIND == 1) r = !ult_n<L>(S.s[d], S.s[d - 1]);
-    else if (KIND == 2) r = ult_n<L>(S.s[d], S.s[d - 1]);
-    else r = !ult_n<L>(S.s[d - 1], S.s[d]);
-    S.s[d - 1][0] = r ? 1u : 0u;
-  }
-};
-template <int L, int D> struct HUlt : HCmpT<L, D, 0, false> {};
-template <int L, int D> struct HUle : HCmpT<L, D, 1, false> {};
-template <int L, int D> struct HUgt : HCmpT<L, D, 2, false> {};
-template <int L, int D> struct HUge : HCmpT<L, D, 3, false> {};
-template <int L, int D> struct HSlt : HCmpT<L, D, 0, true> {};
-template <int L, int D> struct HSle : HCmpT<L, D, 1, true> {};
-template <int L, int D> struct HSgt : HCmpT<L, D, 2, true> {};
-template <int L, int D> struct HSge : HCmpT<L, D, 3, true> {};
-
-// ---------------------------------------------------------------- arithmetic (imm = result width)
-template <int L, int D>
-struct HAdd {
-  static constexpr int kMin = 1;
-  H_DEV run(Stack<L, D>& S, uint32_t W, uint32_t, const Ctx&) {
-    add_n<L>(S.s[d - 1], S.s[d - 1], S.s[d]);
-    mask_w<L>(S.s[d - 1], W);
-  }
-};
-template <int L, int D>
-struct HSub {
-  static constexpr int kMin = 1;
-  H_DEV run(Stack<L, D>& S, uint32_t W, uint32_t, const Ctx&) {
-    (void)sub_n<L>(S.s[d - 1], S.s[d - 1], S.s[d]);
-    mask_w<L>(S.s[d - 1], W);
-  }
-};
-template <int L, int D>
-struct HMul {
-  static constexpr int kMin = 1;
-  H_DEV run(Stack<L, D>& S, uint32_t W, uint32_t, const Ctx&) {
-    mul_lo_n<L>(S.s[d - 1], S.s[d - 1], S.s[d]);
-    mask_w<L>(S.s[d - 1], W);
-  }
-};
-template <int L, int D>
-struct HNeg {
-  static constexpr int kMin = 0;
-  H_DEV run(Stack<L, D>& S, uint32_t W, uint32_t, const Ctx&) {
-    neg_n<L>(S.s[d]);
-    mask_w<L>(S.s[d], W);
-  }
-};
-#define BV_BITWISE(NAME, OP)                                                 \
-  template <int L, int D>                                                    \
-  struct NAME {                                                              \
-    static constexpr int kMin = 1;                                           \
-    H_DEV run(Stack<L, D>& S, uint32_t, uint32_t, const Ctx&) {              \
-      _Pragma("unroll") for (int i = 0; i < L; i++) S.s[d - 1][i] OP S.s[d][i]; \
-    }                                                                        \
-  };
-BV_BITWISE(HBAnd, &=)
-BV_BITWISE(HBOr, |=)
-BV_BITWISE(HBXor, ^=)
-template <int L, int D>
-struct HBNot {
-  static constexpr int kMin = 0;
-  H_DEV run(Stack<L, D>& S, uint32_t W, uint32_t, const Ctx&) {
 #pragma unroll
-    for (int i = 0; i < L; i++) S.s[d][i] = ~S.s[d][i];
-    mask_w<L>(S.s[d], W);
-  }
-};
-template <int L, int D>
-struct HIte {
-  static constexpr int kMin = 2;
-  H_DEV run(Stack<L, D>& S, uint32_t, uint32_t, const Ctx&) {
-    const bool c = (S.s[d - 2][0] & 1u) != 0;
+    for (int i = 0; i < L; i++) r[i] = i == 0 ? rem : 0u;
+  } else {
+    const int la = (int)bitlen_n<L>(a), lb = (int)bitlen_n<L>(b);
+    const int k = bz ? -1 : la - lb;  // the quotient has at most k+1 bits
+    uint32_t bs[L];
 #pragma unroll
-    for (int i = 0; i < L; i++) S.s[d - 2][i] = c ? S.s[d - 1][i] : S.s[d][i];
-  }
-};
-template <int L, int D>
-struct HIteEF {  // else at d-2, cond at d-1, then at d
-  static constexpr int kMin = 2;
-  H_DEV run(Stack<L, D>& S, uint32_t, uint32_t, const Ctx&) {
-    const bool c = (S.s[d - 1][0] & 1u) != 0;
+    for (int i = 0; i < L; i++) {
+      bs[i] = b[i];
+      q[i] = 0;
+      r[i] = a[i];
+    }
+    shl_var<L>(bs, k > 0 ? (uint32_t)k : 0u);
+    for (int it = 0; __ballot(it <= k) != 0; it++) {
+      if (it <= k) {
+        uint32_t t[L];
+        const uint32_t borrow = sub_n<L>(t, r, bs);
+        const uint32_t bit = (uint32_t)(k - it);
+        if (!borrow) {
 #pragma unroll
-    for (int i = 0; i < L; i++) S.s[d - 2][i] = c ? S.s[d][i] : S.s[d - 2][i];
-  }
-};
-template <int L, int D>
-struct HBIteEF {
-  static constexpr int kMin = 2;
-  H_DEV run(Stack<L, D>& S, uint32_t, uint32_t, const Ctx&) {
-    S.s[d - 2][0] = S.s[d - 1][0] ? S.s[d][0] : S.s[d - 2][0];
-  }
-};
-template <int L, int D>
-struct HExtract {  // imm = lo, imm2 = result width
-  static constexpr int kMin = 0;
-  H_DEV run(Stack<L, D>& S, uint32_t lo, uint32_t W, const Ctx&) {
-    shr_uni<L>(S.s[d], lo);
-    mask_w<L>(S.s[d], W);
-  }
-};
-template <int L, int D>
-struct HConcat {  // imm = low operand width
-  static constexpr int kMin = 1;
-  H_DEV run(Stack<L, D>& S, uint32_t wl, uint32_t, const Ctx&) {
-    shl_uni<L>(S.s[d - 1], wl);
+          for (int i = 0; i < L; i++) {
+            r[i] = t[i];
+            q[i] |= ((uint32_t)i == (bit >> 5)) ? (1u << (bit & 31u)) : 0u;
+          }
+        }
 #pragma unroll
-    for (int i = 0; i < L; i++) S.s[d - 1][i] |= S.s[d][i];
+        for (int i = 0; i < L; i++) bs[i] = __builtin_amdgcn_alignbit(i + 1 < L ? bs[i + 1] : 0u, bs[i], 1u);
+      }
+    }
   }
-};
-template <int L, int D>
-struct HSext {  // imm = source width, imm2 = result width
-  static constexpr int kMin = 0;
-  H_DEV run(Stack<L, D>& S, uint32_t w0, uint32_t W, const Ctx&) {
-    sext_full<L>(S.s[d], w0);
-    mask_w<L>(S.s[d], W);
-  }
-};
-
-// ---------------------------------------------------------------- cold ops: operands copied
-// into X/Y, one shared implementation, result copied back (keeps code size bounded).
-template <int L, int D, class TX>
-MQ_DEV void load_xy(Stack<L, D>& S, int d, TX& X, TX& Y) {
-  switch (d) {
-#define LXY(k)                                      \
-  case k:                                           \
-    if constexpr (k >= 1 && k < D) {                \
-      _Pragma("unroll") for (int i = 0; i < L; i++) { \
-        X[i] = S.s[k - 1][i];                       \
-        Y[i] = S.s[k][i];                           \
-      }                                             \
-    }                                               \
-    break;
-    LXY(0) LXY(1) LXY(2) LXY(3) LXY(4) LXY(5) LXY(6) LXY(7) LXY(8) LXY(9) LXY(10) LXY(11)
-#undef LXY
-  }
-}
-template <int L, int D, class TX>
-MQ_DEV void load_x(Stack<L, D>& S, int d, TX& X) {
-  switch (d) {
-#define LX(k)                                                                   \
-  case k:                                                                       \
-    if constexpr (k < D) { _Pragma("unroll") for (int i = 0; i < L; i++) X[i] = S.s[k][i]; } \
-    break;
-    LX(0) LX(1) LX(2) LX(3) LX(4) LX(5) LX(6) LX(7) LX(8) LX(9) LX(10) LX(11)
-#undef LX
-  }
-}
-template <int L, int D, class TX>
-MQ_DEV void store_x(Stack<L, D>& S, int d, const TX& X) {
-  switch (d) {
-#define SX(k)                                                                   \
-  case k:                                                                       \
-    if constexpr (k < D) { _Pragma("unroll") for (int i = 0; i < L; i++) S.s[k][i] = X[i]; } \
-    break;
-    SX(0) SX(1) SX(2) SX(3) SX(4) SX(5) SX(6) SX(7) SX(8) SX(9) SX(10) SX(11)
-#undef SX
+#pragma unroll
+  for (int i = 0; i < L; i++) {
+    q[i] = bz ? 0xFFFFFFFFu : q[i];
+    r[i] = bz ? a[i] : r[i];
   }
 }
 
+template <int L>
+MQ_DEV void h_div(const Ctx& cx, int d, uint32_t op, uint32_t W) {
+  uint32_t x[L], y[L], Q[L], R[L];
+  const uint32_t nl = nl_of_w(W);
+  sld<L>(cx, d - 1, x, nl);
+  sld<L>(cx, d, y, nl);
+  if (op == G_UDIV || op == G_UREM) {
+    udivrem_fast<L>(Q, R, x, y);
+    if (op == G_UDIV) {
+#pragma unroll
+      for (int i = 0; i < L; i++) R[i] = Q[i];
+    }
+    mask_w<L>(R, W);
+    sst<L>(cx, d - 1, R);
+    return;
+  }
+  sext_full<L>(x, W);
+  sext_full<L>(y, W);
+  const bool sa = (x[L - 1] >> 31) != 0, sb = (y[L - 1] >> 31) != 0;
+  uint32_t NA[L], NB[L];
+#pragma unroll
+  for (int i = 0; i < L; i++) {
+    NA[i] = x[i];
+    NB[i] = y[i];
+  }
+  if (sa) neg_n<L>(NA);
+  if (sb) neg_n<L>(NB);
+  udivrem_fast<L>(Q, R, NA, NB);
+  if (op == G_SDIV) {
+#pragma unroll
+    for (int i = 0; i < L; i++) R[i] = Q[i];
+    if (sa != sb) neg_n<L>(R);
+  } else if (op == G_SREM) {
+    if (sa) neg_n<L>(R);
+  } else {  // smod: sign of the divisor
+    if (!is_zero_n<L>(R)) {
+      if (sa && !sb) {
+        neg_n<L>(R);
+        add_n<L>(R, R, y);
+      } else if (!sa && sb) {
+        add_n<L>(R, R, y);
+      } else if (sa && sb) {
+        neg_n<L>(R);
+      }
+    }
+  }
+  mask_w<L>(R, W);
+  sst<L>(cx, d - 1, R);
+}
+
+// ---------------------------------------------------------------- shifts by a stack value
+template <int L>
+MQ_DEV void h_shift(const Ctx& cx, int d, uint32_t op, uint32_t W) {
+  const uint32_t nl = nl_of_w(W);
+  uint32_t x[L], y[L];
+  sld<L>(cx, d - 1, x, nl);
+  sld<L>(cx, d, y, nl);
+  uint32_t s;
+  const bool ok = shift_amount<L>(y, W, s);
+  if (op == G_SHL) {
+    shl_var<L>(x, ok ? s : 0u);
+#pragma unroll
+    for (int i = 0; i < L; i++) x[i] = ok ? x[i] : 0u;
+    mask_w<L>(x, W);
+  } else if (op == G_LSHR) {
+    shr_var<L>(x, ok ? s : 0u, 0u);
+#pragma unroll
+    for (int i = 0; i < L; i++) x[i] = ok ? x[i] : 0u;
+  } else {
+    sext_full<L>(x, W);
+    const uint32_t fill = (x[L - 1] >> 31) ? 0xFFFFFFFFu : 0u;
+    shr_var<L>(x, ok ? s : (32u * L - 1u), fill);
+    mask_w<L>(x, W);
+  }
+  sst<L>(cx, d - 1, x);
+}
+
+// ---------------------------------------------------------------- overflow predicates
+template <int L>
+MQ_DEV void h_mul_ovfl(const Ctx& cx, int d, uint32_t op, uint32_t W) {
+  uint32_t X[L], Y[L];
+  sld<L>(cx, d - 1, X);
+  sld<L>(cx, d, Y);
+  uint32_t LO[L], HI[L];
+  bool res;
+  if (op == G_UMUL_NOOVFL) {
+    mul_full_n<L>(LO, HI, X, Y);
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < L; i++) acc |= HI[i] | (LO[i] & ~limb_mask(i, W));
+    res = acc == 0;
+  } else {
+    sext_full<L>(X, W);
+    sext_full<L>(Y, W);
+    const bool sa = (X[L - 1] >> 31) != 0, sb = (Y[L - 1] >> 31) != 0;
+    if (sa) neg_n<L>(X);
+    if (sb) neg_n<L>(Y);
+    mul_full_n<L>(LO, HI, X, Y);
+    // compare |p| (2L limbs) with 2^(W-1)
+    const uint32_t hb = W - 1, hk = hb >> 5, hbit = 1u << (hb & 31);
+    bool gt = false, eq = true;
+#pragma unroll
+    for (int i = 2 * L - 1; i >= 0; i--) {
+      const uint32_t pw = (i < L) ? LO[i] : HI[i - L];
+      const uint32_t tw = ((uint32_t)i == hk) ? hbit : 0u;
+      gt = eq ? (pw > tw) : gt;
+      eq = eq && (pw == tw);
+    }
+    const bool neg = sa != sb;
+    const bool pz = is_zero_n<L>(LO) && is_zero_n<L>(HI);
+    if (op == G_SMUL_NOOVFL) res = (neg || pz) ? true : (!gt && !eq);
+    else res = (!neg || pz) ? true : !gt;
+  }
+  sstb<L>(cx, d - 1, res);
+}
+
+// ---------------------------------------------------------------- model functions
 // table lookup of a model function (UF or as-array): entries first, else value
-template <int L, class T0, class T1, class TO>
-MQ_DEV void func_lookup(const Ctx& cx, uint32_t f, uint32_t W, const T0& k0, const T1& k1, TO& out) {
+template <int L>
+MQ_DEV void func_lookup(const Ctx& cx, uint32_t f, uint32_t W, const uint32_t (&k0)[L], const uint32_t (&k1)[L],
+                        uint32_t (&out)[L]) {
 #pragma unroll
   for (int i = 0; i < L; i++) out[i] = 0;
   if (f >= (uint32_t)cx.n_funcs) return;
@@ -397,7 +567,24 @@ MQ_DEV void func_lookup(const Ctx& cx, uint32_t f, uint32_t W, const T0& k0, con
       break;
     }
   }
-  mask_w<L>(out, W);
+  mask_w<L>(out, W == 0 ? 1u : W);  // Bool range: limb 0 holds 0/1
+}
+
+template <int L>
+MQ_DEV void h_uf(const Ctx& cx, int d, uint32_t op, uint32_t f, uint32_t W) {
+  uint32_t X[L], Y[L], R[L];
+  if (op == G_UF1) {
+    sld<L>(cx, d, X);
+#pragma unroll
+    for (int i = 0; i < L; i++) Y[i] = 0;
+    func_lookup<L>(cx, f, W, X, Y, R);
+    sst<L>(cx, d, R);
+  } else {
+    sld<L>(cx, d - 1, X);
+    sld<L>(cx, d, Y);
+    func_lookup<L>(cx, f, W, X, Y, R);
+    sst<L>(cx, d - 1, R);
+  }
 }
 
 // ---------------------------------------------------------------- interpreted keccak256
@@ -414,8 +601,7 @@ __constant__ uint64_t kKeccakRC[24] = {
 
 MQ_DEV uint64_t krol(uint64_t v, int n) { return n ? (v << n) | (v >> (64 - n)) : v; }
 
-// state by reference and inlined: the 25 lanes stay in VGPRs (a pointer argument to a
-// non-inlined function put them in scratch memory)
+// state by reference and inlined: the 25 lanes stay in VGPRs
 MQ_DEV void keccak_f1600(uint64_t (&a)[25]) {
   constexpr int R[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
   for (int r = 0; r < 24; r++) {
@@ -438,10 +624,10 @@ MQ_DEV void keccak_f1600(uint64_t (&a)[25]) {
   }
 }
 
-template <int L, int D>
-MQ_DEV void keccak_op(Stack<L, D>& S, int d, uint32_t W) {
+template <int L>
+MQ_DEV void h_keccak(const Ctx& cx, int d, uint32_t W) {
   uint32_t X[L];
-  load_x<L, D>(S, d, X);
+  sld<L>(cx, d, X);
   const uint32_t nbytes = W >> 3;
   // full-width byte reversal, then shift the message to byte 0: message byte p = LE byte p
   uint32_t R[L];
@@ -468,173 +654,12 @@ MQ_DEV void keccak_op(Stack<L, D>& S, int d, uint32_t W) {
     }
     X[i] = v;
   }
-  store_x<L, D>(S, d, X);
+  sst<L>(cx, d, X);
 }
 
-template <int L, int D>
-MQ_DEV void cold_op(Stack<L, D>& S, uint32_t op, int d, uint32_t imm, uint32_t imm2, const Ctx& cx) {
-  uint32_t X[L], Y[L], R[L];
-  if (op == G_UF1) {
-    load_x<L, D>(S, d, X);
-#pragma unroll
-    for (int i = 0; i < L; i++) Y[i] = 0;
-    func_lookup<L>(cx, imm, imm2, X, Y, R);
-    store_x<L, D>(S, d, R);
-    return;
-  }
-  load_xy<L, D>(S, d, X, Y);
-  const uint32_t W = (op == G_UF2) ? imm2 : imm;
-  switch (op) {
-    case G_UF2:
-      func_lookup<L>(cx, imm, imm2, X, Y, R);
-      break;
-    case G_UDIV:
-    case G_UREM: {
-      uint32_t Q[L];
-      udivrem_n<L>(Q, R, X, Y);
-      if (op == G_UDIV) {
-#pragma unroll
-        for (int i = 0; i < L; i++) R[i] = Q[i];
-      }
-      mask_w<L>(R, W);
-      break;
-    }
-    case G_SDIV:
-    case G_SREM:
-    case G_SMOD: {
-      sext_full<L>(X, W);
-      sext_full<L>(Y, W);
-      const bool sa = (X[L - 1] >> 31) != 0, sb = (Y[L - 1] >> 31) != 0;
-      uint32_t NA[L], NB[L], Q[L], U[L];
-#pragma unroll
-      for (int i = 0; i < L; i++) {
-        NA[i] = X[i];
-        NB[i] = Y[i];
-      }
-      if (sa) neg_n<L>(NA);  // per-lane: the compiler predicates with exec masks
-      if (sb) neg_n<L>(NB);
-      udivrem_n<L>(Q, U, NA, NB);
-      if (op == G_SDIV) {
-#pragma unroll
-        for (int i = 0; i < L; i++) R[i] = Q[i];
-        if (sa != sb) neg_n<L>(R);
-      } else if (op == G_SREM) {
-#pragma unroll
-        for (int i = 0; i < L; i++) R[i] = U[i];
-        if (sa) neg_n<L>(R);
-      } else {
-        const bool uz = is_zero_n<L>(U);
-#pragma unroll
-        for (int i = 0; i < L; i++) R[i] = U[i];
-        if (!uz) {
-          if (sa && !sb) {
-            neg_n<L>(R);
-            add_n<L>(R, R, Y);
-          } else if (!sa && sb) {
-            add_n<L>(R, R, Y);
-          } else if (sa && sb) {
-            neg_n<L>(R);
-          }
-        }
-      }
-      mask_w<L>(R, W);
-      break;
-    }
-    case G_SHL: {
-      uint32_t s;
-      const bool ok = shift_amount<L>(Y, W, s);
-#pragma unroll
-      for (int i = 0; i < L; i++) R[i] = X[i];
-      shl_var<L>(R, ok ? s : 0u);
-#pragma unroll
-      for (int i = 0; i < L; i++) R[i] = ok ? R[i] : 0u;
-      mask_w<L>(R, W);
-      break;
-    }
-    case G_LSHR: {
-      uint32_t s;
-      const bool ok = shift_amount<L>(Y, W, s);
-#pragma unroll
-      for (int i = 0; i < L; i++) R[i] = X[i];
-      shr_var<L>(R, ok ? s : 0u, 0u);
-#pragma unroll
-      for (int i = 0; i < L; i++) R[i] = ok ? R[i] : 0u;
-      break;
-    }
-    case G_ASHR: {
-      uint32_t s;
-      const bool ok = shift_amount<L>(Y, W, s);
-      sext_full<L>(X, W);
-      const uint32_t fill = (X[L - 1] >> 31) ? 0xFFFFFFFFu : 0u;
-#pragma unroll
-      for (int i = 0; i < L; i++) R[i] = X[i];
-      shr_var<L>(R, ok ? s : (32u * L - 1u), fill);
-      mask_w<L>(R, W);
-      break;
-    }
-    case G_UMUL_NOOVFL: {
-      uint32_t LO[L], HI[L];
-      mul_full_n<L>(LO, HI, X, Y);
-      uint32_t acc = 0;
-#pragma unroll
-      for (int i = 0; i < L; i++) acc |= HI[i] | (LO[i] & ~limb_mask(i, W));
-      R[0] = acc == 0 ? 1u : 0u;
-      break;
-    }
-    case G_SMUL_NOOVFL:
-    case G_SMUL_NOUDFL: {
-      sext_full<L>(X, W);
-      sext_full<L>(Y, W);
-      const bool sa = (X[L - 1] >> 31) != 0, sb = (Y[L - 1] >> 31) != 0;
-      if (sa) neg_n<L>(X);
-      if (sb) neg_n<L>(Y);
-      uint32_t LO[L], HI[L];
-      mul_full_n<L>(LO, HI, X, Y);
-      // compare |p| (2L limbs) with 2^(W-1)
-      const uint32_t hb = W - 1, hk = hb >> 5, hbit = 1u << (hb & 31);
-      bool gt = false, eq = true;
-#pragma unroll
-      for (int i = 2 * L - 1; i >= 0; i--) {
-        const uint32_t pw = (i < L) ? LO[i] : HI[i - L];
-        const uint32_t tw = ((uint32_t)i == hk) ? hbit : 0u;
-        gt = eq ? (pw > tw) : gt;
-        eq = eq && (pw == tw);
-      }
-      const bool neg = sa != sb;
-      const bool pz = is_zero_n<L>(LO) && is_zero_n<L>(HI);
-      bool ok;
-      if (op == G_SMUL_NOOVFL) ok = (neg || pz) ? true : (!gt && !eq);
-      else ok = (!neg || pz) ? true : !gt;
-      R[0] = ok ? 1u : 0u;
-      break;
-    }
-    default:
-      break;
-  }
-  store_x<L, D>(S, d - 1, R);
-}
-
-// ---------------------------------------------------------------- dispatch
-template <template <int, int> class H, int L, int D>
-MQ_DEV void dispatch(Stack<L, D>& S, int d, uint32_t imm, uint32_t imm2, const Ctx& cx) {
-  using T = H<L, D>;
-  switch (d) {
-#define DC(k)                                                           \
-  case k:                                                               \
-    if constexpr (k >= T::kMin && k < D) T::template run<k>(S, imm, imm2, cx); \
-    break;
-    DC(0) DC(1) DC(2) DC(3) DC(4) DC(5) DC(6) DC(7) DC(8) DC(9) DC(10) DC(11)
-#undef DC
-  }
-}
-
-template <int L, int D, bool K>
+// ---------------------------------------------------------------- interpreter
+template <int L, bool K>
 MQ_DEV bool run_tape(cu32p prog, const Ctx& cx) {
-  Stack<L, D> S;
-#pragma unroll
-  for (int k = 0; k < D; k++)
-#pragma unroll
-    for (int i = 0; i < L; i++) S.s[k][i] = 0;
   uint32_t pc = 0;
   for (;;) {
     const uint32_t ins = prog[pc++];
@@ -646,71 +671,91 @@ MQ_DEV bool run_tape(cu32p prog, const Ctx& cx) {
     if (op == G_EXTRACT || op == G_CONCAT || op == G_SEXT || op == G_UF1 || op == G_UF2) imm2 = prog[pc++];
     switch (op) {
       case G_PUSH_VAR:
-      case G_PUSH_VAR_B: dispatch<HPushVar, L, D>(S, d, imm, imm2, cx); break;
-      case G_PUSH_CONST: dispatch<HPushConst, L, D>(S, d, imm, imm2, cx); break;
+      case G_PUSH_VAR_B: h_push_var<L>(cx, d, imm); break;
+      case G_PUSH_CONST: h_push_const<L>(cx, d, imm); break;
       case G_PUSH_TMP:
-      case G_PUSH_TMP_B: dispatch<HPushTmp, L, D>(S, d, imm, imm2, cx); break;
+      case G_PUSH_TMP_B: h_push_tmp<L>(cx, d, imm); break;
       case G_STORE_TMP:
-      case G_STORE_TMP_B: dispatch<HStoreTmp, L, D>(S, d, imm, imm2, cx); break;
-      case G_PUSH_BOOL: dispatch<HPushBool, L, D>(S, d, imm, imm2, cx); break;
-      case G_NOT: dispatch<HNot, L, D>(S, d, imm, imm2, cx); break;
-      case G_AND: dispatch<HAnd, L, D>(S, d, imm, imm2, cx); break;
-      case G_OR: dispatch<HOr, L, D>(S, d, imm, imm2, cx); break;
-      case G_XOR: dispatch<HXor, L, D>(S, d, imm, imm2, cx); break;
-      case G_IFF: dispatch<HIff, L, D>(S, d, imm, imm2, cx); break;
-      case G_IMPLIES: dispatch<HImplies, L, D>(S, d, imm, imm2, cx); break;
-      case G_BITE: dispatch<HBIte, L, D>(S, d, imm, imm2, cx); break;
-      case G_EQ: dispatch<HEq, L, D>(S, d, imm, imm2, cx); break;
-      case G_ULT: dispatch<HUlt, L, D>(S, d, imm, imm2, cx); break;
-      case G_ULE: dispatch<HUle, L, D>(S, d, imm, imm2, cx); break;
-      case G_UGT: dispatch<HUgt, L, D>(S, d, imm, imm2, cx); break;
-      case G_UGE: dispatch<HUge, L, D>(S, d, imm, imm2, cx); break;
-      case G_SLT: dispatch<HSlt, L, D>(S, d, imm, imm2, cx); break;
-      case G_SLE: dispatch<HSle, L, D>(S, d, imm, imm2, cx); break;
-      case G_SGT: dispatch<HSgt, L, D>(S, d, imm, imm2, cx); break;
-      case G_SGE: dispatch<HSge, L, D>(S, d, imm, imm2, cx); break;
-      case G_ADD: dispatch<HAdd, L, D>(S, d, imm, imm2, cx); break;
-      case G_SUB: dispatch<HSub, L, D>(S, d, imm, imm2, cx); break;
-      case G_MUL: dispatch<HMul, L, D>(S, d, imm, imm2, cx); break;
-      case G_NEG: dispatch<HNeg, L, D>(S, d, imm, imm2, cx); break;
-      case G_BAND: dispatch<HBAnd, L, D>(S, d, imm, imm2, cx); break;
-      case G_BOR: dispatch<HBOr, L, D>(S, d, imm, imm2, cx); break;
-      case G_BXOR: dispatch<HBXor, L, D>(S, d, imm, imm2, cx); break;
-      case G_BNOT: dispatch<HBNot, L, D>(S, d, imm, imm2, cx); break;
-      case G_ITE: dispatch<HIte, L, D>(S, d, imm, imm2, cx); break;
-      case G_ITE_EF: dispatch<HIteEF, L, D>(S, d, imm, imm2, cx); break;
-      case G_BITE_EF: dispatch<HBIteEF, L, D>(S, d, imm, imm2, cx); break;
-      case G_EXTRACT: dispatch<HExtract, L, D>(S, d, imm, imm2, cx); break;
-      case G_CONCAT: dispatch<HConcat, L, D>(S, d, imm, imm2, cx); break;
-      case G_SEXT: dispatch<HSext, L, D>(S, d, imm, imm2, cx); break;
-      case G_KECCAK:
-        if constexpr (K) keccak_op<L, D>(S, d, imm);
+      case G_STORE_TMP_B: h_store_tmp<L>(cx, d, imm); break;
+      case G_PUSH_BOOL: sstb<L>(cx, d, (imm & 1u) != 0); break;
+      // Bool connectives: limb 0
+      case G_NOT: sstb<L>(cx, d, (sld0<L>(cx, d) & 1u) == 0); break;
+      case G_AND: sstb<L>(cx, d - 1, (sld0<L>(cx, d - 1) & sld0<L>(cx, d) & 1u) != 0); break;
+      case G_OR: sstb<L>(cx, d - 1, ((sld0<L>(cx, d - 1) | sld0<L>(cx, d)) & 1u) != 0); break;
+      case G_XOR: sstb<L>(cx, d - 1, ((sld0<L>(cx, d - 1) ^ sld0<L>(cx, d)) & 1u) != 0); break;
+      case G_IFF: sstb<L>(cx, d - 1, (sld0<L>(cx, d - 1) & 1u) == (sld0<L>(cx, d) & 1u)); break;
+      case G_IMPLIES: sstb<L>(cx, d - 1, (((sld0<L>(cx, d - 1) ^ 1u) | sld0<L>(cx, d)) & 1u) != 0); break;
+      case G_BITE: {
+        const bool c = (sld0<L>(cx, d - 2) & 1u) != 0;
+        sstb<L>(cx, d - 2, ((c ? sld0<L>(cx, d - 1) : sld0<L>(cx, d)) & 1u) != 0);
         break;
-      default: cold_op<L, D>(S, op, d, imm, imm2, cx); break;
+      }
+      case G_BITE_EF: {
+        const bool c = (sld0<L>(cx, d - 1) & 1u) != 0;
+        sstb<L>(cx, d - 2, ((c ? sld0<L>(cx, d) : sld0<L>(cx, d - 2)) & 1u) != 0);
+        break;
+      }
+      case G_EQ: h_eq<L>(cx, d, imm); break;
+      case G_ULT: h_cmp<L>(cx, d, imm, 0, false); break;
+      case G_ULE: h_cmp<L>(cx, d, imm, 1, false); break;
+      case G_UGT: h_cmp<L>(cx, d, imm, 2, false); break;
+      case G_UGE: h_cmp<L>(cx, d, imm, 3, false); break;
+      case G_SLT: h_cmp<L>(cx, d, imm, 0, true); break;
+      case G_SLE: h_cmp<L>(cx, d, imm, 1, true); break;
+      case G_SGT: h_cmp<L>(cx, d, imm, 2, true); break;
+      case G_SGE: h_cmp<L>(cx, d, imm, 3, true); break;
+      case G_ADD: h_add_sub<L>(cx, d, imm, false); break;
+      case G_SUB: h_add_sub<L>(cx, d, imm, true); break;
+      case G_MUL: h_mul<L>(cx, d, imm); break;
+      case G_NEG: h_neg_not<L>(cx, d, imm, false); break;
+      case G_BNOT: h_neg_not<L>(cx, d, imm, true); break;
+      case G_BAND: h_bitwise<L>(cx, d, imm, 0); break;
+      case G_BOR: h_bitwise<L>(cx, d, imm, 1); break;
+      case G_BXOR: h_bitwise<L>(cx, d, imm, 2); break;
+      case G_ITE: h_ite<L>(cx, d - 2, d - 1, d, d - 2, imm); break;
+      case G_ITE_EF: h_ite<L>(cx, d - 1, d, d - 2, d - 2, imm); break;
+      case G_EXTRACT: h_extract<L>(cx, d, imm, imm2); break;
+      case G_CONCAT: h_concat<L>(cx, d, imm, imm2); break;
+      case G_SEXT: h_sext<L>(cx, d, imm, imm2); break;
+      case G_UDIV:
+      case G_UREM:
+      case G_SDIV:
+      case G_SREM:
+      case G_SMOD: h_div<L>(cx, d, op, imm); break;
+      case G_SHL:
+      case G_LSHR:
+      case G_ASHR: h_shift<L>(cx, d, op, imm); break;
+      case G_UMUL_NOOVFL:
+      case G_SMUL_NOOVFL:
+      case G_SMUL_NOUDFL: h_mul_ovfl<L>(cx, d, op, imm); break;
+      case G_UF1:
+      case G_UF2: h_uf<L>(cx, d, op, imm, imm2); break;
+      case G_KECCAK:
+        if constexpr (K) h_keccak<L>(cx, d, imm);
+        break;
+      default: break;
     }
   }
-  return (S.s[0][0] & 1u) != 0;
+  return (sld0<L>(cx, 0) & 1u) != 0;
 }
 
 // ---------------------------------------------------------------- kernels
-// grid.x: model tiles of 64*WAVES models; grid.y: groups of tapes_per_group descriptors.
-// Persistent grid: workgroup w handles items w, w + grid, ... with item = group * tiles + tile
-// (model tiles of 256 fastest, so low candidate indices are evaluated first and their hits
-// feed the early exit).  A wave's temp slots live in HBM at a fixed per-(workgroup, wave)
-// offset: coalesced 256-byte rows, L1/L2-resident, no LDS occupancy limit on the temp count.
-template <int L, int D, bool K>
-__global__ __launch_bounds__(256) void qs_first_hit_kernel(KArgs args) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t* tmp = args.scratch + ((size_t)blockIdx.x * 4 + wave) * (size_t)args.tmp_words_per_wave;
+// One wave per workgroup; a persistent grid strides over items (model tile of 64, tape group),
+// item = group * tiles + tile (low candidate indices first, feeding the early exit).  A wave's
+// operand stack lives in LDS (stack_slots x L x 256 B), its temp slots in HBM scratch.
+template <int L, bool K>
+__global__ __launch_bounds__(64) void qs_first_hit_kernel(KArgs args) {
+  extern __shared__ uint4 lds_stack[];
+  const int lane = threadIdx.x & 63;
+  uint32_t* tmp = args.scratch + (size_t)blockIdx.x * (size_t)args.tmp_words_per_wave;
   uint64_t pairs = 0, nodes = 0, ops = 0;
   for (int64_t item = blockIdx.x; item < args.n_items; item += gridDim.x) {
     const int64_t tile = item % args.tiles;
     const int group = (int)(item / args.tiles);
-    const int64_t m0 = tile * 256 + wave * 64;
-    if (m0 >= args.M) continue;
+    const int64_t m0 = tile * 64;
     const int64_t m = m0 + lane;
     const bool valid = m < args.M;
-    Ctx cx = make_ctx(args, valid ? m : args.M - 1, tmp, lane);
+    Ctx cx = make_ctx(args, valid ? m : args.M - 1, tmp, lds_stack, lane);
     const int gbeg = group * args.tapes_per_group;
     const int gend = min(gbeg + args.tapes_per_group, args.n_desc);
     const int32_t gfirst = (int32_t)(args.index_base + m0);
@@ -721,7 +766,7 @@ __global__ __launch_bounds__(256) void qs_first_hit_kernel(KArgs args) {
       cur = __builtin_amdgcn_readfirstlane(cur);
       if (args.early_exit && gfirst >= cur) continue;
       cx.consts = CONSTP(cu32p, args.consts) + dsc.const_base;
-      const bool r = run_tape<L, D, K>(CONSTP(cu32p, args.prog) + dsc.prog_off, cx);
+      const bool r = run_tape<L, K>(CONSTP(cu32p, args.prog) + dsc.prog_off, cx);
       const uint64_t mask = __ballot(r && valid);
       pairs += __popcll(vmask);
       nodes += (uint64_t)__popcll(vmask) * dsc.n_nodes;
@@ -739,24 +784,24 @@ __global__ __launch_bounds__(256) void qs_first_hit_kernel(KArgs args) {
   }
 }
 
-template <int L, int D, bool K>
-__global__ __launch_bounds__(256) void qs_verdict_kernel(KArgs args) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t* tmp = args.scratch + ((size_t)blockIdx.x * 4 + wave) * (size_t)args.tmp_words_per_wave;
+template <int L, bool K>
+__global__ __launch_bounds__(64) void qs_verdict_kernel(KArgs args) {
+  extern __shared__ uint4 lds_stack[];
+  const int lane = threadIdx.x & 63;
+  uint32_t* tmp = args.scratch + (size_t)blockIdx.x * (size_t)args.tmp_words_per_wave;
   for (int64_t item = blockIdx.x; item < args.n_items; item += gridDim.x) {
     const int64_t tile = item % args.tiles;
     const int group = (int)(item / args.tiles);
-    const int64_t m0 = tile * 256 + wave * 64;
-    if (m0 >= args.M) continue;
+    const int64_t m0 = tile * 64;
     const int64_t m = m0 + lane;
     const bool valid = m < args.M;
-    Ctx cx = make_ctx(args, valid ? m : args.M - 1, tmp, lane);
+    Ctx cx = make_ctx(args, valid ? m : args.M - 1, tmp, lds_stack, lane);
     const int gbeg = group * args.tapes_per_group;
     const int gend = min(gbeg + args.tapes_per_group, args.n_desc);
     for (int i = gbeg; i < gend; i++) {
       const GDesc dsc = load_desc(args.descs, i);
       cx.consts = CONSTP(cu32p, args.consts) + dsc.const_base;
-      const bool r = run_tape<L, D, K>(CONSTP(cu32p, args.prog) + dsc.prog_off, cx);
+      const bool r = run_tape<L, K>(CONSTP(cu32p, args.prog) + dsc.prog_off, cx);
       if (valid) args.verdicts[(int64_t)dsc.tape * args.M + m] = r ? 1 : 0;
     }
   }
@@ -788,18 +833,19 @@ __global__ void qs_finalize_best(int32_t* best, const uint8_t* unsupported, int 
 }
 
 // ---------------------------------------------------------------- host launchers
-template <int L, int D, bool K>
+template <int L, bool K>
 static hipError_t launch_variant(const KArgs& a, bool verdict, hipStream_t st) {
   if (a.n_desc <= 0 || a.grid <= 0) return hipSuccess;
-  if (verdict) hipLaunchKernelGGL((qs_verdict_kernel<L, D, K>), dim3((unsigned)a.grid), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((qs_first_hit_kernel<L, D, K>), dim3((unsigned)a.grid), dim3(256), 0, st, a);
+  const size_t lds = (size_t)a.stack_slots * L * 64 * 4;
+  if (verdict) hipLaunchKernelGGL((qs_verdict_kernel<L, K>), dim3((unsigned)a.grid), dim3(64), lds, st, a);
+  else hipLaunchKernelGGL((qs_first_hit_kernel<L, K>), dim3((unsigned)a.grid), dim3(64), lds, st, a);
   return hipGetLastError();
 }
 
 hipError_t launch_qs(const KArgs& a, int L, bool keccak, bool verdict, hipStream_t st) {
-  if (keccak) return L == 16 ? launch_variant<16, 6, true>(a, verdict, st) : hipErrorInvalidValue;
-  if (L == 8) return launch_variant<8, 8, false>(a, verdict, st);
-  if (L == 16) return launch_variant<16, 6, false>(a, verdict, st);
+  if (keccak) return L == 16 ? launch_variant<16, true>(a, verdict, st) : hipErrorInvalidValue;
+  if (L == 8) return launch_variant<8, false>(a, verdict, st);
+  if (L == 16) return launch_variant<16, false>(a, verdict, st);
   return hipErrorInvalidValue;
 }
 

@@ -44,10 +44,11 @@ struct KArgs {
   unsigned long long* counters;  // [0] pairs evaluated, [1] node-evals, [2] algorithmic ops
   int tmp_words_per_wave;        // temp words per wave (slot, limb, lane)
   int early_exit;
-  uint32_t* scratch;             // per-wave temp slots in HBM: [gridDim.x * 4][tmp_words_per_wave]
-  int64_t tiles;                 // model tiles of 256
+  uint32_t* scratch;             // per-wave temp slots in HBM: [gridDim.x][tmp_words_per_wave]
+  int64_t tiles;                 // model tiles of 64 (one wave = one workgroup)
   int64_t n_items;               // tiles x tape groups; workgroups stride over them
   int grid;                      // workgroups launched (persistent, <= n_items)
+  int stack_slots;               // LDS operand-stack slots per wave (max program depth)
 };
 
 // argument block of the assembly interpreter (layout fixed by gen_qsa.py's prologue)
