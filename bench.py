@@ -84,6 +84,10 @@ def parse():
     p.add_argument("--seed", type=int, default=None)
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                   help="nccl (= RCCL over xGMI, the product path); gloo stages the 4N-byte reduce through "
+                        "the host and lets a 1-GPU box rehearse N>1 with --device 0")
+    p.add_argument("--device", type=int, default=None, help="override LOCAL_RANK -> device mapping (rehearsal)")
     return p.parse_args()
 
 
@@ -133,11 +137,26 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.device is not None:
+        local = args.device
     import torch
     import torch.distributed as dist
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+
+    def all_reduce(t, op):
+        if world == 1:
+            return
+        if args.dist_backend == "nccl":
+            dist.all_reduce(t, op=op)
+        else:
+            h = t.cpu()
+            dist.all_reduce(h, op=op)
+            t.copy_(h)
 
     from mythril_amd.evaluator import Evaluator
 
@@ -165,8 +184,7 @@ def main():
 
     def step():
         ev.launch_first_hit(ct, best.data_ptr(), sptr)
-        if world > 1:
-            dist.all_reduce(best, op=dist.ReduceOp.MIN)
+        all_reduce(best, dist.ReduceOp.MIN)
         ev.finalize_first_hit(ct, best.data_ptr(), sptr)
 
     for _ in range(args.warmup):
@@ -187,10 +205,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        ev.launch_first_hit(ct, best.data_ptr(), sptr)
-        if world > 1:
-            dist.all_reduce(best, op=dist.ReduceOp.MIN)
-        ev.finalize_first_hit(ct, best.data_ptr(), sptr)
+        step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -204,11 +219,11 @@ def main():
     stats = torch.tensor([elapsed, node_evals, alg_ops, float(ok)], dtype=torch.float64, device=dev)
     if world > 1:
         mx = stats.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        all_reduce(mx, dist.ReduceOp.MAX)
         sm = stats.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        all_reduce(sm, dist.ReduceOp.SUM)
         mn = stats.clone()
-        dist.all_reduce(mn, op=dist.ReduceOp.MIN)
+        all_reduce(mn, dist.ReduceOp.MIN)
         elapsed, node_evals, alg_ops, ok = float(mx[0]), float(sm[1]), float(sm[2]), bool(mn[3] > 0)
     hits = int((got >= 0).sum())
 
