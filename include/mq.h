@@ -193,6 +193,16 @@ int mq_models_upload(mq_ctx* ctx, const mq_model_batch* models);
 int mq_tapes_upload(mq_ctx* ctx, const mq_tape_batch* batch, mq_tapes** out, int32_t* n_unsupported_out);
 void mq_tapes_free(mq_tapes* tapes);
 
+/* Batch-level hoisting: sub-terms shared by several tapes of the batch depend only on the model,
+   so the lowering can replace them by derived model variables.  Column program k (a tape whose
+   LAST node is the BV/Bool value to store, not necessarily Bool) is evaluated once per model and
+   written into model variable var_index[k] before every evaluation launch of `tapes`; columns
+   of level j may read columns of levels < j.  The uploaded model batch must contain the target
+   variables with matching widths (their uploaded values are overwritten).  MQ_ERR_TAPE if a
+   program is not supported (the caller then lowers without hoisting). */
+int mq_tapes_set_columns(mq_tapes* tapes, const mq_tape_batch* programs, const int32_t* var_index,
+                         const int32_t* level, int32_t n_columns);
+
 /* check_quick_sat over the batch (support_utils.py:60-67): first_hit_out[t] = smallest
    global candidate index whose model satisfies tape t, MQ_NO_HIT, or MQ_UNSUPPORTED. */
 int mq_eval_first_hit(mq_ctx* ctx, const mq_tape_batch* batch, int32_t* first_hit_out, mq_stats* stats);
@@ -213,6 +223,7 @@ int mq_counters(mq_ctx* ctx, double* out3, int reset);
    bits_out has ceil(n_tapes*M/8) bytes.  Unsupported tapes yield all-zero rows and are
    reported through first_hit_out (may be NULL). */
 int mq_eval_verdicts(mq_ctx* ctx, const mq_tape_batch* batch, uint8_t* bits_out, int32_t* first_hit_out);
+int mq_eval_tapes_verdicts(mq_ctx* ctx, mq_tapes* tapes, uint8_t* bits_out, int32_t* first_hit_out);
 
 /* Concrete keccak256 (Ethereum padding 0x01) of n messages on the GPU (keccak-f[1600] kernel);
    message i = data[offsets[i] .. offsets[i+1]), digests_out = 32*n bytes.

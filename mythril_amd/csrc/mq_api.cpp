@@ -110,6 +110,14 @@ struct mq_tapes {
   QArgs qargs_host;
   QArgs qargs_dev_copy;      // what qargs currently holds on the device
   bool qargs_valid = false;
+  // batch-level hoisting: column programs evaluated once per model before the tapes, one
+  // launch per (nesting level, kernel variant); GDesc.tape = the model variable written
+  struct ColumnLevel {
+    Variant v8, v16, v16k;
+  };
+  std::vector<ColumnLevel> clevels;
+  std::vector<int32_t> col_var, col_width;
+  DevBuf cdescs, cprog, cconsts;
 };
 
 static thread_local std::string g_last_error;
@@ -494,6 +502,74 @@ int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t*
 
 void mq_tapes_free(mq_tapes* t) { delete t; }
 
+int mq_tapes_set_columns(mq_tapes* T, const mq_tape_batch* progs, const int32_t* var_index, const int32_t* level,
+                         int32_t n_columns) {
+  if (!T || n_columns < 0 || (n_columns > 0 && (!progs || !var_index || !level || progs->n_tapes != n_columns)))
+    return MQ_ERR_ARG;
+  mq_ctx* c = T->ctx;
+  HIPCHK(hipSetDevice(c->device));
+  T->clevels.clear();
+  T->col_var.assign(var_index, var_index + n_columns);
+  T->col_width.assign(n_columns, 0);
+  if (n_columns == 0) return MQ_OK;
+  CompileLimits lim;
+  lim.value_root = true;
+  std::vector<CompiledTape> ct(n_columns);
+#pragma omp parallel for schedule(dynamic, 16)
+  for (int k = 0; k < n_columns; k++) ct[k] = compile_tape(progs, k, lim);
+  int max_level = 0;
+  for (int k = 0; k < n_columns; k++) {
+    if (!ct[k].supported) {
+      g_last_error = "column program " + std::to_string(k) + " unsupported: " + ct[k].why;
+      return MQ_ERR_TAPE;
+    }
+    if (level[k] < 0) return MQ_ERR_ARG;
+    max_level = std::max(max_level, (int)level[k]);
+    const int64_t last = progs->tape_offsets[k + 1] - 1;
+    T->col_width[k] = progs->nodes[last].width;
+  }
+  std::vector<uint32_t> prog, consts;
+  std::vector<GDesc> descs;
+  T->clevels.resize((size_t)max_level + 1);
+  for (int lv = 0; lv <= max_level; lv++) {
+    for (int pass = 0; pass < 3; pass++) {
+      mq_tapes::Variant& v = pass == 0 ? T->clevels[lv].v8 : (pass == 1 ? T->clevels[lv].v16 : T->clevels[lv].v16k);
+      v.L = pass == 0 ? 8 : 16;
+      v.keccak = pass == 2;
+      v.begin = (int)descs.size();
+      for (int k = 0; k < n_columns; k++) {
+        const CompiledTape& x = ct[k];
+        if (level[k] != lv) continue;
+        if (pass == 0 && !(x.L == 8 && !x.keccak)) continue;
+        if (pass == 1 && !(x.L == 16 && !x.keccak)) continue;
+        if (pass == 2 && !x.keccak) continue;
+        GDesc d{};
+        d.prog_off = (uint32_t)prog.size();
+        d.prog_len = (uint32_t)x.prog.size();
+        d.tape = (uint32_t)var_index[k];
+        d.const_base = (uint32_t)consts.size();
+        d.n_nodes = x.n_nodes;
+        d.n_temps = (uint32_t)x.n_temps;
+        d.depth = (uint32_t)x.depth;
+        d.alg_ops = (uint32_t)std::min(x.alg_ops, 4.0e9);
+        prog.insert(prog.end(), x.prog.begin(), x.prog.end());
+        consts.insert(consts.end(), x.consts.begin(), x.consts.end());
+        descs.push_back(d);
+        v.max_temps = std::max(v.max_temps, x.n_temps);
+        v.max_depth = std::max(v.max_depth, x.depth);
+      }
+      v.count = (int)descs.size() - v.begin;
+    }
+  }
+  consts.resize(consts.size() + 16, 0);
+  prog.push_back(gword(G_END, 0, 0));
+  HIPCHK(T->cdescs.upload(descs.data(), descs.size(), c->stream));
+  HIPCHK(T->cprog.upload(prog.data(), prog.size(), c->stream));
+  HIPCHK(T->cconsts.upload(consts.data(), consts.size(), c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return MQ_OK;
+}
+
 // Workgroups (one wave each) of the persistent HIP C++ kernels: 16 per CU on 256 CUs; each
 // strides over the (model tile, tape group) items.  Bounds the temp scratch to
 // grid * temps * 2 KB (L = 8).
@@ -533,6 +609,15 @@ static KArgs make_args(mq_ctx* c, mq_tapes* T, const mq_tapes::Variant& v) {
   return a;
 }
 
+static KArgs make_col_args(mq_ctx* c, mq_tapes* T, const mq_tapes::Variant& v) {
+  KArgs a = make_args(c, T, v);
+  a.descs = T->cdescs.as<GDesc>() + v.begin;
+  a.prog = T->cprog.as<uint32_t>();
+  a.consts = T->cconsts.as<uint32_t>();
+  a.mode = 2;
+  return a;
+}
+
 // Launch every evaluation kernel for a compiled batch: the assembly interpreter for the
 // QSA-eligible tapes (when the model batch fits its register file), the HIP C++ kernels for
 // the rest.  verdicts == nullptr -> first-hit mode into best.
@@ -560,6 +645,27 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     started = true;
     return hipEventRecord(c->kev[c->kev_used - 1].first, st);
   };
+  // hoisted columns first (they write model variable rows the tapes read)
+  for (size_t i = 0; i < T->col_var.size(); i++) {
+    const int v = T->col_var[i];
+    if (v < 0 || v >= c->n_vars || nl_of(c->var_width[v]) != nl_of(T->col_width[i])) {
+      g_last_error = "column target variable does not match the uploaded model batch";
+      return MQ_ERR_ARG;
+    }
+  }
+  for (const auto& lv : T->clevels) {
+    for (const mq_tapes::Variant* v : {&lv.v8, &lv.v16, &lv.v16k}) {
+      if (v->count <= 0) continue;
+      KArgs a = make_col_args(c, T, *v);
+      const size_t scratch_bytes = (size_t)a.grid * (size_t)a.tmp_words_per_wave * 4;
+      if (scratch_bytes) {
+        HIPCHK(c->scratch.ensure(scratch_bytes));
+        a.scratch = c->scratch.as<uint32_t>();
+      }
+      HIPCHK(start_timer());
+      HIPCHK(launch_columns(a, v->L, v->keccak, st));
+    }
+  }
   if (use_qsa) {
     KArgs k = make_args(c, T, T->qsa);
     QArgs& q = T->qargs_host;
@@ -708,6 +814,15 @@ int mq_eval_verdicts(mq_ctx* c, const mq_tape_batch* tb, uint8_t* bits, int32_t*
   int rc = mq_tapes_upload(c, tb, &T, nullptr);
   if (rc) return rc;
   std::unique_ptr<mq_tapes> guard(T);
+  return mq_eval_tapes_verdicts(c, T, bits, first_hit_out);
+}
+
+int mq_eval_tapes_verdicts(mq_ctx* c, mq_tapes* T, uint8_t* bits, int32_t* first_hit_out) {
+  if (!c || !T || !bits) return MQ_ERR_ARG;
+  if (!c->have_models) return MQ_ERR_NO_MODELS;
+  if (T->ctx != c) return MQ_ERR_STATE;
+  HIPCHK(hipSetDevice(c->device));
+  int rc;
   const size_t nbytes = (size_t)T->n_tapes * (size_t)c->M;
   HIPCHK(c->verdict_buf.ensure(std::max<size_t>(nbytes, 1)));
   HIPCHK(hipMemsetAsync(c->verdict_buf.p, 0, std::max<size_t>(nbytes, 1), c->stream));

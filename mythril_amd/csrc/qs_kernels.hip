@@ -807,6 +807,64 @@ __global__ __launch_bounds__(64) void qs_verdict_kernel(KArgs args) {
   }
 }
 
+// Column programs of batch-level hoisting (tape.py ColumnSet): each descriptor evaluates a
+// sub-term shared by many tapes ONCE per model and writes its value into model variable
+// dsc.tape's rows, which the batch's tapes then read as an ordinary variable.  One launch per
+// nesting level (a level only reads columns written by earlier launches on the same stream).
+template <int L, bool K>
+__global__ __launch_bounds__(64) void qs_column_kernel(KArgs args) {
+  extern __shared__ uint4 lds_stack[];
+  const int lane = threadIdx.x & 63;
+  uint32_t* tmp = args.scratch + (size_t)blockIdx.x * (size_t)args.tmp_words_per_wave;
+  uint64_t nodes = 0, ops = 0;
+  for (int64_t item = blockIdx.x; item < args.n_items; item += gridDim.x) {
+    const int64_t tile = item % args.tiles;
+    const int group = (int)(item / args.tiles);
+    const int64_t m = tile * 64 + lane;
+    const bool valid = m < args.M;
+    Ctx cx = make_ctx(args, valid ? m : args.M - 1, tmp, lds_stack, lane);
+    const int gbeg = group * args.tapes_per_group;
+    const int gend = min(gbeg + args.tapes_per_group, args.n_desc);
+    const uint32_t nvalid = (uint32_t)__popcll(__ballot(valid));
+    for (int i = gbeg; i < gend; i++) {
+      const GDesc dsc = load_desc(args.descs, i);
+      cx.consts = CONSTP(cu32p, args.consts) + dsc.const_base;
+      (void)run_tape<L, K>(CONSTP(cu32p, args.prog) + dsc.prog_off, cx);
+      uint32_t x[L];
+      sld<L>(cx, 0, x);
+      const uint32_t off = CONSTP(cu32p, args.var_off)[dsc.tape];
+      const uint32_t nl = CONSTP(cu32p, args.var_nl)[dsc.tape];
+      if (valid) {
+        uint32_t* dst = const_cast<uint32_t*>(args.vars) + (int64_t)off * args.M + m;
+#pragma unroll
+        for (int l = 0; l < L; l++)
+          if ((uint32_t)l < nl) dst[(int64_t)l * args.M] = x[l];
+      }
+      nodes += (uint64_t)nvalid * dsc.n_nodes;
+      ops += (uint64_t)nvalid * dsc.alg_ops;
+    }
+  }
+  if (lane == 0 && args.counters) {
+    atomicAdd(&args.counters[1], (unsigned long long)nodes);
+    atomicAdd(&args.counters[2], (unsigned long long)ops);
+  }
+}
+
+template <int L, bool K>
+static hipError_t launch_column_variant(const KArgs& a, hipStream_t st) {
+  if (a.n_desc <= 0 || a.grid <= 0) return hipSuccess;
+  const size_t lds = (size_t)a.stack_slots * L * 64 * 4;
+  hipLaunchKernelGGL((qs_column_kernel<L, K>), dim3((unsigned)a.grid), dim3(64), lds, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_columns(const KArgs& a, int L, bool keccak, hipStream_t st) {
+  if (keccak) return L == 16 ? launch_column_variant<16, true>(a, st) : hipErrorInvalidValue;
+  if (L == 8) return launch_column_variant<8, false>(a, st);
+  if (L == 16) return launch_column_variant<16, false>(a, st);
+  return hipErrorInvalidValue;
+}
+
 __global__ void qs_mask_rows(uint32_t* vars, const uint32_t* rowmask, int64_t rows, int64_t M) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < rows * M) vars[i] &= rowmask[i / M];

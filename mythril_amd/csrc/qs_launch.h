@@ -49,6 +49,7 @@ struct KArgs {
   int64_t n_items;               // tiles x tape groups; workgroups stride over them
   int grid;                      // workgroups launched (persistent, <= n_items)
   int stack_slots;               // LDS operand-stack slots per wave (max program depth)
+  int mode;                      // 0 first hit, 1 verdicts, 2 columns (GDesc.tape = target var)
 };
 
 // argument block of the assembly interpreter (layout fixed by gen_qsa.py's prologue)
@@ -77,6 +78,7 @@ static_assert(__builtin_offsetof(QArgs, var_row) == 0x60, "QArgs layout");
 
 hipError_t launch_qsa(const QArgs* d_args, unsigned gx, unsigned gy, size_t lds, hipStream_t st);
 hipError_t launch_qs(const KArgs& a, int L, bool keccak, bool verdict, hipStream_t st);
+hipError_t launch_columns(const KArgs& a, int L, bool keccak, hipStream_t st);
 hipError_t launch_init_best(int32_t* best, int n, hipStream_t st);
 hipError_t launch_mask_rows(uint32_t* vars, const uint32_t* rowmask, int64_t rows, int64_t M, hipStream_t st);
 hipError_t launch_finalize_best(int32_t* best, const uint8_t* unsupported, int n, hipStream_t st);

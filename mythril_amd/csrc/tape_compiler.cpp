@@ -148,7 +148,7 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
         out.keccak = true;
       }
     }
-    if (kind[nn - 1] != K_BOOL) throw Fail{"root is not Bool"};
+    if (kind[nn - 1] != K_BOOL && !(lim.value_root && kind[nn - 1] == K_BV)) throw Fail{"root is not Bool"};
     if (maxw <= 256 && !out.keccak) out.L = 8;
     else if (maxw <= 512) out.L = 16;
     else throw Fail{"width > 512"};

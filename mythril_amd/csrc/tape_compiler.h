@@ -28,6 +28,7 @@ struct CompileLimits {
   int max_temps_l8 = 64;      // temps live in a per-wave global scratch slot (64 x 2 KB)
   int max_temps_l16 = 32;     // (32 x 4 KB)
   int remat_max_nodes = 3;    // shared sub-terms up to this many cheap nodes are re-evaluated
+  bool value_root = false;    // column program: any BV/Bool root, its value is the result
 };
 
 // Compile tape t of the batch. n_funcs/funcs describe the model function table (result

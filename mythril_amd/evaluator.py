@@ -60,6 +60,8 @@ def load_library(path: str = LIB_PATH):
         L.mq_kernel_times.argtypes = [P, C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_int32), C.c_int]
         L.mq_tapes_info.argtypes = [P] + [C.POINTER(C.c_int32)] * 3
         L.mq_eval_verdicts.argtypes = [P, C.POINTER(MqTapeBatch), C.POINTER(C.c_uint8), C.POINTER(C.c_int32)]
+        L.mq_eval_tapes_verdicts.argtypes = [P, P, C.POINTER(C.c_uint8), C.POINTER(C.c_int32)]
+        L.mq_tapes_set_columns.argtypes = [P, C.POINTER(MqTapeBatch), C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_int32]
         L.mq_keccak256.argtypes = [P, C.POINTER(C.c_uint8), C.POINTER(C.c_int64), C.c_int32, C.POINTER(C.c_uint8)]
         L.mq_tape_alg_ops.argtypes = [C.POINTER(MqTapeBatch), C.c_int32]
         L.mq_tape_alg_ops.restype = C.c_double
@@ -122,6 +124,15 @@ class CompiledTapes:
         _check(ev.lib.mq_tapes_upload(ev.ctx, C.byref(s), C.byref(h), C.byref(nu)), "mq_tapes_upload")
         self.handle = h
         self.n_unsupported = nu.value
+        cols = getattr(tb, "columns", None)
+        self.n_columns = 0
+        if cols is not None and cols.n:
+            cs, ckeep = as_tape_batch(cols.programs)
+            vi = np.ascontiguousarray(cols.var_index, np.int32)
+            lv = np.ascontiguousarray(cols.level, np.int32)
+            _check(ev.lib.mq_tapes_set_columns(h, C.byref(cs), vi.ctypes.data_as(C.POINTER(C.c_int32)),
+                                               lv.ctypes.data_as(C.POINTER(C.c_int32)), cols.n), "mq_tapes_set_columns")
+            self.n_columns = cols.n
 
     def split(self):
         """(tapes on the assembly interpreter, generic 256-bit, generic 512-bit)."""
@@ -234,15 +245,20 @@ class Evaluator:
         _check(self.lib.mq_counters(self.ctx, out, 1 if reset else 0), "mq_counters")
         return float(out[0]), float(out[1]), float(out[2])
 
-    def verdicts(self, tb: TapeBatch):
+    def verdicts(self, tapes):
         """Full N x M verdict matrix (bool) and first-hit (parity dumps)."""
-        n = tb.n_tapes * self.n_models
+        own = not isinstance(tapes, CompiledTapes)
+        ct = self.compile(tapes) if own else tapes
+        n = ct.n_tapes * self.n_models
         bits = np.zeros((n + 7) // 8, np.uint8)
-        fh = np.zeros(tb.n_tapes, np.int32)
-        s, keep = as_tape_batch(tb)
-        _check(self.lib.mq_eval_verdicts(self.ctx, C.byref(s), bits.ctypes.data_as(C.POINTER(C.c_uint8)),
-                                         fh.ctypes.data_as(C.POINTER(C.c_int32))), "mq_eval_verdicts")
-        v = np.unpackbits(bits, bitorder="little")[:n].reshape(tb.n_tapes, self.n_models).astype(bool)
+        fh = np.zeros(ct.n_tapes, np.int32)
+        try:
+            _check(self.lib.mq_eval_tapes_verdicts(self.ctx, ct.handle, bits.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                                   fh.ctypes.data_as(C.POINTER(C.c_int32))), "mq_eval_tapes_verdicts")
+        finally:
+            if own:
+                ct.free()
+        v = np.unpackbits(bits, bitorder="little")[:n].reshape(ct.n_tapes, self.n_models).astype(bool)
         return v, fh
 
     # ------------------------------------------------------------ keccak

@@ -24,7 +24,7 @@ from . import smt as S
 from .exceptions import LoweringError
 from .models import FuncSpec, ModelBatch
 from .smt_model import Model
-from .tape import BOOL, NONE, Tape, TapeBatch, limbs, to_words
+from .tape import BOOL, NONE, ColumnSet, Tape, TapeBatch, limbs, to_words
 
 MAX_WIDTH = 0xFFFF
 
@@ -47,6 +47,7 @@ class SymbolTable:
         # exact only for keccak-consistent candidate sets (C4), never for z3 models in general
         self.interpret_keccak = interpret_keccak
         self.derived: Dict[int, Tuple[str, Tuple[int, ...]]] = {}  # var index -> (function, const args)
+        self.hoisted_vars = set()   # variables computed on the device from column programs
 
     def derived_var(self, fname: str, args: Tuple[int, ...], width: int) -> int:
         """A model-only quantity: the interpretation of function/array ``fname`` at CONSTANT
@@ -90,10 +91,13 @@ def _w(t: S.Term) -> int:
     return t.width
 
 
-def lower_term(root: S.Term, syms: SymbolTable) -> Tape:
-    """Lower one Bool term (the quick-sat conjunction) to a tape; iterative over the DAG."""
-    if root.sort != "bool":
+def lower_term(root: S.Term, syms: SymbolTable, hoisted: Optional[Dict[int, int]] = None,
+               value_root: bool = False) -> Tape:
+    """Lower one Bool term (the quick-sat conjunction) to a tape; iterative over the DAG.
+    ``hoisted``: id(term) -> variable index of terms replaced by derived columns."""
+    if root.sort != "bool" and not value_root:
         raise LoweringError("quick-sat root must be Bool")
+    hoisted = hoisted or {}
     tp = Tape()
     node: Dict[int, int] = {}
 
@@ -104,8 +108,11 @@ def lower_term(root: S.Term, syms: SymbolTable) -> Tape:
         node[id(arr)] = r
         return r
 
-    for t in S.walk(root):
+    for t in _walk_cut(root, hoisted):
         k = t.kind
+        if id(t) in hoisted and t is not root:
+            node[id(t)] = tp.var(hoisted[id(t)], _w(t))
+            continue
         a = [node[id(x)] for x in t.args]
         if k == S.SYM:
             r = tp.var(syms.var(t.params[0], _w(t)), _w(t))
@@ -191,7 +198,74 @@ def lower_term(root: S.Term, syms: SymbolTable) -> Tape:
         else:
             raise LoweringError(f"term kind {k!r} not in the tape vocabulary")
         node[id(t)] = r
-    return tp.finish(node[id(root)])
+    return tp.finish(node[id(root)], value_root=value_root)
+
+
+def _walk_cut(root: S.Term, cut: Dict[int, int]) -> List[S.Term]:
+    """Postfix order of the DAG under ``root`` that does not descend into ``cut`` terms."""
+    order: List[S.Term] = []
+    seen = set()
+    stack = [(root, False)]
+    while stack:
+        t, done = stack.pop()
+        if done:
+            order.append(t)
+            continue
+        if id(t) in seen:
+            continue
+        seen.add(id(t))
+        stack.append((t, True))
+        if id(t) in cut and t is not root:
+            continue
+        for a in reversed(t.args):
+            if id(a) not in seen:
+                stack.append((a, False))
+    return order
+
+
+_LEAVES = frozenset({S.SYM, S.VAL, S.TRUE, S.FALSE, S.ARRAY_SYM})
+
+
+def shared_subterms(roots: Sequence[S.Term], min_nodes: int = 8, min_tapes: int = 2) -> List[S.Term]:
+    """Maximal sub-terms (BV/Bool sorted, >= ``min_nodes`` tree nodes) that occur in at least
+    ``min_tapes`` of the roots — candidates for batch-level hoisting into model columns."""
+    count: Dict[int, int] = {}
+    terms: Dict[int, S.Term] = {}
+    for r in roots:
+        for t in S.walk(r):
+            if t.kind in _LEAVES or t.sort == "array" or t is r:
+                continue
+            count[id(t)] = count.get(id(t), 0) + 1
+            terms[id(t)] = t
+    size: Dict[int, int] = {}
+
+    def tree_size(t: S.Term) -> int:   # capped tree size (cheap, memoised)
+        s = size.get(id(t))
+        if s is None:
+            s = 1 + sum(0 if a.kind in _LEAVES else tree_size(a) for a in t.args)
+            s = min(s, 1 << 20)
+            size[id(t)] = s
+        return s
+
+    eligible = {i for i, c in count.items() if c >= min_tapes and terms[i].width <= 512}
+    chosen: Dict[int, S.Term] = {}
+    for r in roots:   # top-down: the first eligible term on every path is maximal for that root
+        stack = list(r.args)
+        seen = set()
+        while stack:
+            t = stack.pop()
+            if id(t) in seen or t.kind in _LEAVES:
+                continue
+            seen.add(id(t))
+            if id(t) in eligible:
+                for w in S.walk(t):   # iterative: sizes of deep chains without recursion limits
+                    if w.kind not in _LEAVES:
+                        tree_size(w)
+                if tree_size(t) >= min_nodes:
+                    chosen[id(t)] = t
+                    continue
+            stack.extend(t.args)
+    return list(chosen.values())
 
 
 def _is_keccak_uf(name: str) -> bool:
@@ -204,20 +278,52 @@ _BIN = {S.ADD: "add", S.SUB: "sub", S.MUL: "mul", S.UDIV: "udiv", S.UREM: "urem"
         S.SHL: "shl", S.LSHR: "lshr", S.ASHR: "ashr"}
 
 
-def lower_batch(roots: Sequence[S.Term], syms: Optional[SymbolTable] = None):
+def lower_batch(roots: Sequence[S.Term], syms: Optional[SymbolTable] = None, hoist: bool = False,
+                hoist_min_nodes: int = 8):
     """Lower N conjunctions over one shared symbol table.  Returns ``(TapeBatch | None, syms,
     supported_mask)``: a root that fails to lower is replaced by a FALSE placeholder tape and
-    flagged unsupported (the caller routes it to z3)."""
+    flagged unsupported (the caller routes it to z3).
+
+    ``hoist``: sub-terms shared by several roots are evaluated once per model into derived
+    columns (``TapeBatch.columns``, variables named ``@h<k>``) instead of once per (tape, model).
+    Verdicts are unchanged: a sub-term's value depends only on the model."""
     syms = syms or SymbolTable()
+    hoisted: Dict[int, int] = {}
+    col_terms: List[S.Term] = []
+    if hoist and len(roots) > 1:
+        col_terms = shared_subterms(roots, hoist_min_nodes)
+        for k, t in enumerate(col_terms):
+            hoisted[id(t)] = syms.var(f"@h{k}", t.width)
+            syms.hoisted_vars.add(hoisted[id(t)])
     tapes, ok = [], np.ones(len(roots), bool)
     for i, r in enumerate(roots):
         try:
-            tapes.append(lower_term(r, syms))
+            tapes.append(lower_term(r, syms, hoisted))
         except (LoweringError, TypeError):
             ok[i] = False
             t = Tape()
             tapes.append(t.finish(t.false()))
-    return (TapeBatch(tapes) if tapes else None), syms, ok
+    tb = TapeBatch(tapes) if tapes else None
+    if tb is not None and col_terms:
+        progs, levels = [], []
+        lvl: Dict[int, int] = {}
+        for t in col_terms:   # column programs; a column may read columns nested inside it
+            inner = [h for h in _walk_cut(t, hoisted) if id(h) in hoisted and h is not t]
+            lvl[id(t)] = 0
+            progs.append(lower_term(t, syms, hoisted, value_root=True))
+        # levels: longest chain of nested columns (terms are acyclic)
+        changed = True
+        while changed:
+            changed = False
+            for t in col_terms:
+                inner = [h for h in _walk_cut(t, hoisted) if id(h) in hoisted and h is not t]
+                want = 1 + max((lvl[id(h)] for h in inner), default=-1)
+                if want > lvl[id(t)]:
+                    lvl[id(t)] = want
+                    changed = True
+        levels = [lvl[id(t)] for t in col_terms]
+        tb.columns = ColumnSet(TapeBatch(progs), [hoisted[id(t)] for t in col_terms], levels)
+    return tb, syms, ok
 
 
 def serialize_models(models: Sequence[Model], syms: SymbolTable, index_base: int = 0) -> ModelBatch:

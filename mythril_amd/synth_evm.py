@@ -31,7 +31,7 @@ from typing import Dict, List, Sequence, Tuple
 import numpy as np
 
 from . import smt as S
-from .lower import SymbolTable, lower_term
+from .lower import SymbolTable, lower_batch, lower_term
 from .models import FuncSpec, ModelBatch
 from .tape import TapeBatch, limbs
 
@@ -340,7 +340,8 @@ def evm_path(rng: np.random.Generator, wit: Dict, n_tx: int, checks_per_tx: Tupl
 
 
 def c3_workload(n_tapes: int = 1000, n_models: int = 1_000_000, seed: int = 3, planted_frac: float = 0.1,
-                n_tx: int = 3, shard: Tuple[int, int] = None, checks_per_tx: Tuple[int, int] = (3, 6)):
+                n_tx: int = 3, shard: Tuple[int, int] = None, checks_per_tx: Tuple[int, int] = (3, 6),
+                hoist: bool = False):
     """Config C3 substitute: ``n_tapes`` EVM-shaped path conjunctions over ``n_tx`` transactions x
     ``n_models`` candidates.  ``shard=(lo, hi)`` materialises only candidates [lo, hi) (multi-GPU);
     tapes and expected first hits are global.  Returns (tapes, models, expected, symbols)."""
@@ -349,7 +350,7 @@ def c3_workload(n_tapes: int = 1000, n_models: int = 1_000_000, seed: int = 3, p
     models = EvmModels(seed, n_models, n_tx, lo, hi)
     ghost = EvmModels(seed + 1_000_003, max(1, n_tapes), n_tx, 0, 0)
     syms = SymbolTable()
-    tapes, expected = [], np.full(n_tapes, -1, np.int32)
+    roots, expected = [], np.full(n_tapes, -1, np.int32)
     planted = rng.random(n_tapes) < planted_frac
     for t in range(n_tapes):
         if planted[t]:
@@ -361,8 +362,10 @@ def c3_workload(n_tapes: int = 1000, n_models: int = 1_000_000, seed: int = 3, p
             expected[t] = p
         else:
             wit = ghost.witness(t)
-        tapes.append(lower_term(evm_path(rng, wit, n_tx, checks_per_tx), syms))
-    return TapeBatch(tapes), models.batch(syms), expected, syms
+        roots.append(evm_path(rng, wit, n_tx, checks_per_tx))
+    tb, syms, ok = lower_batch(roots, syms, hoist=hoist)
+    assert ok.all()
+    return tb, models.batch(syms), expected, syms
 
 
 # ====================================================================== C4: keccak-heavy mappings
@@ -498,7 +501,8 @@ def c4_path(rng: np.random.Generator, wit: Dict, n_tx: int, hasher_many) -> S.Te
 
 
 def c4_workload(n_tapes: int = 200, n_models: int = 1_000_000, seed: int = 4, planted_frac: float = 0.1,
-                n_tx: int = 2, shard: Tuple[int, int] = None, hasher_many=None, interpret_keccak: bool = False):
+                n_tx: int = 2, shard: Tuple[int, int] = None, hasher_many=None, interpret_keccak: bool = False,
+                hoist: bool = False):
     """Config C4: keccak-heavy mapping/storage tapes x keccak-consistent models.
 
     ``interpret_keccak`` lowers ``keccak256_512(x)`` to the in-kernel keccak-f[1600]
@@ -512,7 +516,7 @@ def c4_workload(n_tapes: int = 200, n_models: int = 1_000_000, seed: int = 4, pl
     models = KeccakModels(seed, n_models, n_tx, lo, hi, hasher_many)
     ghost = EvmModels(seed + 1_000_003, max(1, n_tapes), n_tx, 0, 0, address_args=True)
     syms = SymbolTable(interpret_keccak=interpret_keccak)
-    tapes, expected = [], np.full(n_tapes, -1, np.int32)
+    roots, expected = [], np.full(n_tapes, -1, np.int32)
     planted = rng.random(n_tapes) < planted_frac
     def hashed_keys_are_concrete(w) -> bool:
         # the manager's axioms hold under true hashes only for keys equal to a concrete (actor)
@@ -530,5 +534,7 @@ def c4_workload(n_tapes: int = 200, n_models: int = 1_000_000, seed: int = 4, pl
             expected[t] = p
         else:
             wit = ghost.witness(t)
-        tapes.append(lower_term(c4_path(rng, wit, n_tx, hasher_many), syms))
-    return TapeBatch(tapes), models.batch(syms), expected, syms
+        roots.append(c4_path(rng, wit, n_tx, hasher_many))
+    tb, syms, ok = lower_batch(roots, syms, hoist=hoist)
+    assert ok.all()
+    return tb, models.batch(syms), expected, syms

@@ -155,9 +155,14 @@ class Tape:
     def root(self) -> int:
         return len(self.nodes) - 1
 
-    def finish(self, root: int) -> "Tape":
-        """Make ``root`` the last node (the evaluated root) — re-emits the live DAG in postfix order."""
-        self._bool(root)
+    def finish(self, root: int, value_root: bool = False) -> "Tape":
+        """Make ``root`` the last node (the evaluated root) — re-emits the live DAG in postfix order.
+        ``value_root``: a BV/Bool root whose VALUE is the result (column programs of hoisting)."""
+        if value_root:
+            if self.kind[root] == "array":
+                raise SortError("a column program's root cannot be an array")
+        else:
+            self._bool(root)
         if root == len(self.nodes) - 1:
             return self
         out = Tape()
@@ -440,6 +445,7 @@ class TapeBatch:
         if self.consts.size == 0:
             self.consts = np.zeros(1, np.uint32)
         self.offsets = np.asarray(offsets, dtype=np.int64)
+        self.columns = None  # Optional[ColumnSet]: model-level sub-terms hoisted out of the batch
 
     @classmethod
     def from_arrays(cls, nodes: np.ndarray, offsets: np.ndarray, consts: np.ndarray) -> "TapeBatch":
@@ -450,6 +456,7 @@ class TapeBatch:
         if self.consts.size == 0:
             self.consts = np.zeros(1, np.uint32)
         self.n_tapes = len(self.offsets) - 1
+        self.columns = None
         return self
 
     def tape_nodes(self, t: int) -> np.ndarray:
@@ -464,3 +471,21 @@ class TapeBatch:
         offs[1:] = np.cumsum([len(c) for c in chunks])
         nodes = np.concatenate(chunks) if chunks else np.zeros(0, NODE_DTYPE)
         return TapeBatch.from_arrays(nodes, offs, self.consts)
+
+
+class ColumnSet:
+    """Sub-terms shared by several tapes of a batch, hoisted into derived model columns.
+
+    A shared sub-term depends only on the model, so it is evaluated once per model (column program
+    ``programs`` tape k, BV/Bool root) and written into model variable ``var_index[k]``; the tapes
+    of the batch read it as a variable.  ``level[k]``: columns of level j only read columns of
+    levels < j (one launch per level)."""
+
+    def __init__(self, programs: "TapeBatch", var_index: Sequence[int], level: Sequence[int]):
+        self.programs = programs
+        self.var_index = np.asarray(var_index, dtype=np.int32)
+        self.level = np.asarray(level, dtype=np.int32)
+
+    @property
+    def n(self) -> int:
+        return int(self.var_index.size)

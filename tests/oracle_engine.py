@@ -72,3 +72,24 @@ class ReferenceLoopCache:
                 break
         self.memo[expr] = res
         return res
+
+
+def apply_columns(tb, mb):
+    """Oracle evaluation of a hoisted batch's column programs (tape.py ColumnSet), level by level,
+    written into the model variables they define (the device does this in qs_column_kernel)."""
+    from mythril_amd.models import ModelBatch
+    from mythril_amd.tape import to_words
+    cols = tb.columns
+    words = mb.var_words.copy()
+    out = ModelBatch(mb.var_widths, words, mb.funcs, mb.entry_ptr, mb.entry_words, mb.entry_base,
+                     mb.else_words, mb.else_base, mb.index_base)
+    off = out.var_word_offsets()
+    for lvl in sorted(set(int(x) for x in cols.level)):
+        for k in np.flatnonzero(cols.level == lvl):
+            v = int(cols.var_index[k])
+            w = int(mb.var_widths[v])
+            nodes = cols.programs.tape_nodes(int(k))
+            for m in range(mb.n_models):
+                val = pyoracle.eval_nodes(nodes, cols.programs.consts, out, m)[-1]
+                out.var_words[off[v]:off[v + 1], m] = to_words(int(val), w)
+    return out

@@ -338,3 +338,51 @@ def test_c5_deep_tapes_match_oracle(evaluator):
     fh = evaluator.first_hit(tb)
     ref, _ = cref.first_hit(tb, mb)
     assert (ref == exp).all() and (fh == ref).all()
+
+
+# ---------------------------------------------------------------- batch-level hoisting (column programs)
+def test_c3_hoisted_columns_match_unhoisted_oracle(evaluator):
+    from mythril_amd.synth_evm import c3_workload
+    plain = c3_workload(60, 3000, seed=3, planted_frac=0.3)
+    tb, mb, exp, _ = c3_workload(60, 3000, seed=3, planted_frac=0.3, hoist=True)
+    assert tb.columns.n > 0
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    assert ct.n_unsupported == 0 and ct.n_columns == tb.columns.n
+    fh = evaluator.first_hit(ct)
+    ref, _ = cref.first_hit(plain[0], plain[1])
+    assert (ref == exp).all() and (fh == ref).all(), np.flatnonzero(fh != ref)[:10]
+    v, _ = evaluator.verdicts(ct)
+    assert (v == cref.verdicts(plain[0], plain[1])).all()
+
+
+def test_hoisting_nested_levels_on_gpu(evaluator):
+    from mythril_amd import smt as S
+    from mythril_amd.lower import lower_batch, serialize_models
+    from mythril_amd.smt_model import Model
+    x, y = S.BitVecSym("x", 256), S.BitVecSym("y", 256)
+    inner = (x * y + x) * (y + x) + (x ^ y)
+    outer = (inner * inner + x) * (inner - y) + (inner & y)
+    b8 = S.Extract(7, 0, inner)
+    roots = [S.ULT(outer, S.BitVecVal(1 << (250 - i), 256)) for i in range(4)] + \
+            [S.ULT(inner, S.BitVecVal(1 << 255, 256)), S.And(b8 == 3, S.ULT(outer, x)), S.ULT(b8, S.BitVecVal(100, 8))]
+    rng = np.random.default_rng(5)
+    models = [Model({"x": int(rng.integers(1 << 62)) << 190, "y": int(rng.integers(1 << 62))}) for _ in range(500)]
+    tb, syms, _ = lower_batch(roots, hoist=True, hoist_min_nodes=3)
+    assert tb.columns.n >= 2 and tb.columns.level.max() >= 1
+    tb2, syms2, _ = lower_batch(roots)
+    evaluator.upload_models(serialize_models(models, syms))
+    v, fh = evaluator.verdicts(tb)
+    ref = cref.verdicts(tb2, serialize_models(models, syms2))
+    assert (v == ref).all()
+
+
+def test_c4_hoisted_in_kernel_keccak(evaluator):
+    from mythril_amd.synth_evm import c4_workload
+    plain = c4_workload(30, 1200, seed=14, planted_frac=0.4, hasher_many=evaluator.keccak256_array)
+    tb, mb, exp, _ = c4_workload(30, 1200, seed=14, planted_frac=0.4, hasher_many=evaluator.keccak256_array,
+                                 interpret_keccak=True, hoist=True)
+    evaluator.upload_models(mb)
+    fh = evaluator.first_hit(tb)
+    ref, _ = cref.first_hit(plain[0], plain[1])
+    assert (ref == exp).all() and (fh == ref).all()

@@ -121,3 +121,32 @@ def test_deep_conjunction_is_iterative():
         e = e + 1
     tp = lower_term(e == 5000, SymbolTable())
     assert len(tp) > 5000
+
+
+def test_batch_hoisting_preserves_verdicts():
+    """Sub-terms shared across the tapes of a batch become model columns: same verdicts (oracle),
+    far fewer nodes per tape."""
+    from mythril_amd.synth_evm import c3_workload
+    from oracle_engine import apply_columns
+    plain = c3_workload(24, 60, seed=13, planted_frac=0.5)
+    hoisted = c3_workload(24, 60, seed=13, planted_frac=0.5, hoist=True)
+    tb, mb = hoisted[0], hoisted[1]
+    assert tb.columns is not None and tb.columns.n > 0
+    assert tb.sizes().mean() < 0.5 * plain[0].sizes().mean()
+    mb_full = apply_columns(tb, mb)
+    assert (cref.verdicts(tb, mb_full) == cref.verdicts(plain[0], plain[1])).all()
+
+
+def test_hoisting_levels_nest():
+    x, y = S.BitVecSym("x", 256), S.BitVecSym("y", 256)
+    inner = (x * y + x) * (y + x) + (x ^ y)
+    outer = (inner * inner + x) * (inner - y) + (inner & y)
+    roots = [S.ULT(outer, S.BitVecVal(i, 256)) for i in range(3)] + [S.ULT(inner, S.BitVecVal(9, 256))]
+    tb, syms, ok = lower_batch(roots, hoist=True, hoist_min_nodes=3)
+    assert tb.columns.n == 2 and sorted(tb.columns.level.tolist()) == [0, 1]
+    from oracle_engine import apply_columns
+    from mythril_amd.smt_model import Model
+    models = [Model({"x": i * 7 + 1, "y": i * 3 + 2}) for i in range(30)]
+    mb = apply_columns(tb, serialize_models(models, syms))
+    tb2, syms2, _ = lower_batch(roots)
+    assert (cref.verdicts(tb, mb) == cref.verdicts(tb2, serialize_models(models, syms2))).all()
