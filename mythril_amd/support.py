@@ -128,6 +128,8 @@ class VerdictEngine:
     unsupported: fail closed).  Works on z3-free terms (:mod:`mythril_amd.smt`) and, on a z3 host,
     on z3 ``BoolRef`` (lowered by :mod:`mythril_amd.lower_z3`)."""
 
+    hoist_min_batch = 8
+
     def __init__(self, evaluator=None):
         self._ev = evaluator
         self.launches = 0
@@ -147,7 +149,9 @@ class VerdictEngine:
             return [np.zeros(0, bool) for _ in exprs]
         if all(isinstance(e, S.Term) for e in exprs):
             from .lower import lower_batch, serialize_models
-            tb, syms, ok = lower_batch(exprs)
+            # states forked from a common parent share constraint prefixes: hoist what a batch
+            # shares into once-per-model columns (lower.py lower_batch)
+            tb, syms, ok = lower_batch(exprs, hoist=len(exprs) >= self.hoist_min_batch)
             mb = serialize_models([as_record(m) for m in models], syms)
         else:
             from .lower_z3 import lower_batch_z3
