@@ -151,14 +151,25 @@ class VerdictEngine:
             from .lower import lower_batch, serialize_models
             # states forked from a common parent share constraint prefixes: hoist what a batch
             # shares into once-per-model columns (lower.py lower_batch)
+            records = [as_record(m) for m in models]
             tb, syms, ok = lower_batch(exprs, hoist=len(exprs) >= self.hoist_min_batch)
-            mb = serialize_models([as_record(m) for m in models], syms)
+            mb = serialize_models(records, syms)
         else:
             from .lower_z3 import lower_batch_z3
             tb, mb, ok = lower_batch_z3(exprs, models)
         ev = self.evaluator
         ev.upload_models(mb)
-        v, fh = ev.verdicts(tb)
+        try:
+            v, fh = ev.verdicts(tb)
+        except Exception:
+            if getattr(tb, "columns", None) is None:
+                raise
+            # a column program the compiler rejects (mq_tapes_set_columns -> MQ_ERR_TAPE):
+            # evaluate the batch without hoisting instead
+            tb, syms, ok = lower_batch(exprs)
+            mb = serialize_models(records, syms)
+            ev.upload_models(mb)
+            v, fh = ev.verdicts(tb)
         self.launches += 1
         self.pairs += tb.n_tapes * mb.n_models
         out: List[Optional[np.ndarray]] = []
