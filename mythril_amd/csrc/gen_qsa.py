@@ -189,20 +189,22 @@ def mul_body(d):
     """S[d-1] = S[d-1] * S[d] mod 2^256: product scanning (Comba) columns 0..7, 64-bit column
     accumulator v[4:5] (v_mad_u64_u32 with carry-out) + overflow word v6; carries are added
     through three rotating SGPR pairs so every VALU carry read is >= 2 instructions after its
-    write."""
+    write.  Column 0 has no carries; each later column's first carry-add writes the overflow word
+    (no reset move); the accumulator shift (v4, v5) <- (v5, v6) is one v_pk_mov_b32; column 7's
+    low word goes straight to S[d-1][7] after its last product."""
     a, b = d - 1, d
     C = ["s[34:35]", "s[36:37]", "s[38:39]"]
-    out = ["v_mov_b64 v[4:5], 0", "v_mov_b32 v6, 0"]
-    for k in range(L):
+    out = [f"v_mad_u64_u32 v[4:5], s[60:61], {S(a, 0)}, {S(b, 0)}, 0",
+           f"v_mov_b32 {T(0)}, v4", "v_mov_b32 v4, v5", "v_mov_b32 v5, 0"]
+    for k in range(1, L):
         prods = [(i, k - i) for i in range(k + 1)]
         if k == L - 1:
             # last column: only the low word matters, no carry tracking
             for i, j in prods:
                 out.append(f"v_mad_u64_u32 v[4:5], s[60:61], {S(a, i)}, {S(b, j)}, v[4:5]")
-            out.append(f"v_mov_b32 {T(7)}, v4")
             break
         mads = [f"v_mad_u64_u32 v[4:5], {C[t % 3]}, {S(a, i)}, {S(b, j)}, v[4:5]" for t, (i, j) in enumerate(prods)]
-        adds = [f"v_addc_co_u32_e64 v6, s[60:61], 0, v6, {C[t % 3]}" for t in range(len(prods))]
+        adds = [f"v_addc_co_u32_e64 v6, s[60:61], 0, {'0' if t == 0 else 'v6'}, {C[t % 3]}" for t in range(len(prods))]
         seq = []
         n = len(prods)
         # m0 m1 m2 a0 m3 a1 m4 a2 ... then flush
@@ -211,16 +213,14 @@ def mul_body(d):
             if t >= 2:
                 seq.append(adds[t - 2])
         tail = [adds[t] for t in range(max(0, n - 2), n)]
-        if n == 1:
-            seq += ["s_nop 1"] + tail
-        elif n == 2:
+        if n == 2:
             seq += ["s_nop 0"] + tail
         else:
             seq += tail
         out += seq
-        out += [f"v_mov_b32 {T(k)}, v4", "v_mov_b32 v4, v5", "v_mov_b32 v5, v6", "v_mov_b32 v6, 0"]
+        out += [f"v_mov_b32 {T(k)}, v4", "v_mov_b32 v4, v5", "v_mov_b32 v5, v6"]
     out += [f"v_mov_b64 {S2(a, l)}, v[{TBASE + l}:{TBASE + l + 1}]" for l in range(0, 6, 2)]
-    out += [f"v_mov_b32 {S(a, 6)}, {T(6)}", f"v_mov_b32 {S(a, 7)}, {T(7)}"]
+    out += [f"v_mov_b32 {S(a, 6)}, {T(6)}", f"v_mov_b32 {S(a, 7)}, v4"]
     return out
 
 

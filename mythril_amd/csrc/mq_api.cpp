@@ -668,6 +668,13 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
   }
   if (use_qsa) {
     KArgs k = make_args(c, T, T->qsa);
+    // the assembly interpreter's grid is (256-model tiles) x (tape groups): size the groups for
+    // ~8k workgroups with ITS tile count (make_args sizes them for the 64-model C++ tiles)
+    {
+      const int64_t tiles256 = (c->M + 255) / 256;
+      int64_t tpg = (int64_t(T->qsa.count) * tiles256 + 8191) / 8192;
+      k.tapes_per_group = (int)std::max<int64_t>(1, std::min<int64_t>(tpg, T->qsa.count));
+    }
     QArgs& q = T->qargs_host;
     q = QArgs{};
     q.descs = T->qdescs.p;

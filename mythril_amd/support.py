@@ -201,13 +201,22 @@ class ModelCache:
         row = self._verdicts(constraints, order)
         if row is _UNSUPPORTED:
             self.stats["unsupported"] += 1
+            self._record(constraints, order, -2)
             return self._fallback(constraints, order)
-        for model, ok in zip(order, row):
+        for i, (model, ok) in enumerate(zip(order, row)):
             if ok:
+                self._record(constraints, order, i)
                 self.model_cache.put(model, self.model_cache.get(model) + 1)
                 self.stats["hits"] += 1
                 return model
+        self._record(constraints, order, -1)
         return False
+
+    recorder = None  # corpus.Recorder: harvest every evaluated query (enable_dump)
+
+    def _record(self, constraints, order, answer: int) -> None:
+        if self.recorder is not None and order:
+            self.recorder.record(constraints, order, answer)
 
     def put(self, key, value) -> None:
         self.model_cache.put(key, value)
@@ -434,6 +443,13 @@ def is_possible_batch(states: Sequence[Constraints], solver_timeout=None) -> Lis
     exprs = [e for e in (quick_sat_expr(c) for c in states) if e is not None]
     model_cache.prefetch(exprs)
     return [c.is_possible(solver_timeout=solver_timeout) for c in states]
+
+
+def enable_dump(directory: Optional[str]) -> None:
+    """Harvest hook next to ``--solver-log`` (model.py:51-62): record every quick-sat query of the
+    process-global cache into ``directory`` (mythril_amd.corpus format); None disables it."""
+    from .corpus import Recorder
+    model_cache.recorder = Recorder(directory) if directory else None
 
 
 def reset_caches() -> None:
