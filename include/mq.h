@@ -248,6 +248,11 @@ int mq_kernel_times(mq_ctx* ctx, float* out_ms, int32_t max_out, int32_t* n_out,
    and on the 512-bit HIP C++ kernels (any pointer may be NULL). */
 int mq_tapes_info(mq_tapes* tapes, int32_t* n_asm, int32_t* n_generic_l8, int32_t* n_generic_l16);
 
+/* After a launch: how the assembly-eligible tapes were split between the preloaded-variable
+   kernel (*n_p) and the general kernel (*n_g); *live = 0 when the batch fell back to the HIP C++
+   kernel for the current model batch.  Returns 0 or MQ_ERR_ARG. */
+int mq_tapes_qsa_split(mq_tapes* tapes, int32_t* n_p, int32_t* n_g, int32_t* live);
+
 /* Static algorithmic cost of a tape; -1 if malformed. */
 double mq_tape_alg_ops(const mq_tape_batch* batch, int32_t t);
 
@@ -256,6 +261,11 @@ double mq_tape_alg_ops(const mq_tape_batch* batch, int32_t t);
    copied into why[why_len].  Returns 0 or MQ_ERR_ARG. */
 int mq_tape_compile_info(const mq_tape_batch* batch, int32_t t, int32_t* supported, int32_t* limbs,
                          int32_t* depth, int32_t* n_temps, int32_t* prog_words, char* why, int32_t why_len);
+
+/* Host-only: the compiled stack program of tape t (gprog.h instruction words, G_END last) into
+   words[cap]; *n_words = its length (also when cap is too small, then nothing is copied).
+   Returns 0, MQ_ERR_ARG, or MQ_ERR_TAPE when the tape does not compile. */
+int mq_tape_program(const mq_tape_batch* batch, int32_t t, uint32_t* words, int32_t cap, int32_t* n_words);
 
 /* Library version string. */
 const char* mq_version(void);

@@ -1,29 +1,43 @@
 #!/usr/bin/env python3
-"""Generate the gfx950 threaded-code tape interpreter ("QSA") as inline assembly.
+"""Generate the gfx950 threaded-code tape interpreters ("QSA") as inline assembly.
 
 Why assembly: the evaluator is an interpreter whose operand stack must live in statically
-named VGPRs.  Expressed in HIP C++, every dispatch join made the register allocator shuffle
-the whole stack (thousands of v_mov per tape, SGPR spills; profiles/r01_*): 137 VALU + 68 SALU
-per tape node against ~18 algorithmic ops.  Here the register file is fixed by hand:
+named VGPRs and whose dispatch must be ONE indirect jump.  Expressed in HIP C++, every dispatch
+join made the register allocator shuffle the whole stack (profiles/r01_*), and the AMDGPU backend
+lowers a `switch` (and computed goto) to a compare tree: the LDS-stack C++ interpreter measures
+~67 SALU + 26 branches per tape node on C3 (profiles/r01_c3b_pmc.json).  Here every handler ends
+with the dispatch tail NEXT (decode the prefetched word, prefetch the next, s_setpc).
 
+Two variants are generated from the same handler code (one asm statement each, label prefixes
+.Lqsa / .Lqsg):
+
+  P ("preload", qsa_kernel):  the wave's 64 models' first 8 variables are preloaded into VGPRs
+     once per workgroup; PUSH_VAR is a register copy.  C2-shaped batches.
+  G ("general", qsg_kernel):  no preload; variables are pushed from the model rows in HBM
+     (PUSH_MEM: the loads are issued by the push and waited for by the first consumer), and
+     v[8:71] are the work registers of the table-lookup subroutine (UF1).  EVM-shaped batches.
+
+Register map (both):
   VGPR  v1       LDS temp address (wave base + lane*8)
-        v2       model byte offset m*4 (clamped)          v3 tid, v[4:7] scratch / MUL accumulator
-        v[8:71]  the wave's 64 models' variables V[v][l] = v(8+8v+l), preloaded once
+        v2       model byte offset m*4 (clamped)          v3 sign mask of signed division
+        v[4:7]   scratch / MUL accumulator / division step
+        v[8:71]  P: preloaded variables V[v][l] = v(8+8v+l);  G: UF1 work registers
         v[72:119] operand stack S[d][l] = v(72+8d+l), d < 6 (256-bit values, 8 x u32 limbs)
-        v[120:127] MUL partial-product column results
+        v[120:127] MUL column results / division + lookup operand
   SGPR  s[48:59] Bool stack B[d] = s[48+2d : 49+2d] as 64-lane masks (Bool ops are SALU)
         s[12:13] handler base, s[14:15] program pointer, s16 next word, s17 immediate
+        s[74:75] M*4 (model row stride in bytes), s[76:77] subroutine return address,
+        s[78:79] / s98 / s99 subroutine scratch
 
-Programs are direct-threaded: each 32-bit word = (handler byte offset / 4) | imm << 16; every
-handler ends with the dispatch tail NEXT (prefetch word n+2, decode word n+1, s_setpc).
-Handler offsets are read back once per context by launching the kernel in mode 2.
+Programs are direct-threaded: each 32-bit word = (handler byte offset / 4) | imm << 16.
+Handler offsets are read back once per context by launching each kernel in mode 2.
 
 gfx950 hazard rule respected throughout: a VALU that writes an SGPR/VCC is followed by >= 2
 wait states before a VALU reads that SGPR (carry chains get s_nop 1; the MUL interleaves three
-carry registers).
+carry registers) and >= 4 before a SALU reads it.
 
-Outputs: qsa_gen.inc (the asm text as a C string literal + clobber list) and qsa_table.h
-(handler enumeration used by the host-side translator in mq_api.cpp).
+Outputs: qsa_gen.inc (the two asm texts as C string literals + clobber list) and qsa_table.h
+(handler enumerations used by the host-side translator in mq_api.cpp).
 """
 from __future__ import annotations
 
@@ -31,7 +45,7 @@ import os
 import sys
 
 D = 6          # stack slots
-NV = 8         # preloaded variables
+NV = 8         # preloaded variables (P)
 L = 8          # limbs (256-bit)
 VBASE, SBASE, TBASE = 8, 72, 120
 BBASE = 48
@@ -61,6 +75,14 @@ def T(k):
     return f"v{TBASE + k}"
 
 
+def W(k):  # division / lookup operand registers v[120:127]
+    return f"v{TBASE + k}"
+
+
+def W2(k):
+    return f"v[{TBASE + k}:{TBASE + k + 1}]"
+
+
 NEXT = [
     "s_waitcnt lgkmcnt(0)",
     "s_and_b32 s18, s16, 0xffff",
@@ -74,48 +96,24 @@ NEXT = [
     "s_setpc_b64 s[18:19]",
 ]
 
-handlers = []  # (key, body lines)
+VMWAIT = "s_waitcnt vmcnt(0)"
 
 
-def H(key, body, tail=True):
-    handlers.append((key, list(body) + (NEXT if tail else [])))
+def zero_limbs(d, lo):
+    """S[d][lo..7] = 0 (64-bit moves where aligned)."""
+    out = []
+    l = lo
+    while l < L:
+        if l % 2 == 0 and l + 1 < L:
+            out.append(f"v_mov_b64 {S2(d, l)}, 0")
+            l += 2
+        else:
+            out.append(f"v_mov_b32 {S(d, l)}, 0")
+            l += 1
+    return out
 
 
-# ---------------------------------------------------------------- leaves
-H(("END",), ["s_branch .Lqsa_tape_end"], tail=False)
-for d in range(D):
-    for v in range(NV):
-        H(("PUSH_VAR", d, v), [f"v_mov_b64 {S2(d, l)}, {V2(v, l)}" for l in range(0, L, 2)])
-    H(("PUSH_CONST", d), ["s_lshl_b32 s34, s17, 2", "s_load_dwordx8 s[64:71], s[20:21], s34", "s_waitcnt lgkmcnt(0)"]
-      + [f"v_mov_b64 {S2(d, l)}, s[{64 + l}:{65 + l}]" for l in range(0, L, 2)])
-    H(("PUSH_TMP", d), ["s_lshl_b32 s34, s17, 11", "v_add_u32 v5, s34, v1"]
-      + [f"ds_read_b64 {S2(d, l)}, v5 offset:{256 * l}" for l in range(0, L, 2)] + ["s_waitcnt lgkmcnt(0)"])
-    H(("PUSH_TMP_BOOL", d), ["s_lshl_b32 s34, s17, 11", "v_add_u32 v5, s34, v1", "ds_read_b32 v6, v5",
-                             "s_waitcnt lgkmcnt(0)", f"v_cmp_ne_u32_e64 {B(d)}, 0, v6"])
-    H(("PUSH_BOOL", d), ["s_cmp_lg_u32 s17, 0", f"s_cselect_b64 {B(d)}, -1, 0"])
-H(("STORE_TMP", 0), ["s_lshl_b32 s34, s17, 11", "v_add_u32 v5, s34, v1"]
-  + [f"ds_write_b64 v5, {S2(0, l)} offset:{256 * l}" for l in range(0, L, 2)])
-H(("STORE_TMP_BOOL", 0), ["s_lshl_b32 s34, s17, 11", "v_add_u32 v5, s34, v1",
-                          f"v_cndmask_b32_e64 v6, 0, 1, {B(0)}", "ds_write_b32 v5, v6"])
-
-# ---------------------------------------------------------------- Bool (SALU on lane masks)
-for d in range(D):
-    H(("NOT", d), [f"s_not_b64 {B(d)}, {B(d)}"])
-for d in range(1, D):
-    a, b = B(d - 1), B(d)
-    H(("AND", d), [f"s_and_b64 {a}, {a}, {b}"])
-    H(("OR", d), [f"s_or_b64 {a}, {a}, {b}"])
-    H(("XOR", d), [f"s_xor_b64 {a}, {a}, {b}"])
-    H(("IFF", d), [f"s_xnor_b64 {a}, {a}, {b}"])
-    H(("IMPLIES", d), [f"s_orn2_b64 {a}, {b}, {a}"])
-for d in range(2, D):
-    H(("BITE", d), [f"s_and_b64 s[34:35], {B(d - 2)}, {B(d - 1)}", f"s_andn2_b64 s[36:37], {B(d)}, {B(d - 2)}",
-                    f"s_or_b64 {B(d - 2)}, s[34:35], s[36:37]"])
-    H(("BITE_EF", d), [f"s_and_b64 s[34:35], {B(d - 1)}, {B(d)}", f"s_andn2_b64 s[36:37], {B(d - 2)}, {B(d - 1)}",
-                       f"s_or_b64 {B(d - 2)}, s[34:35], s[36:37]"])
-
-
-# ---------------------------------------------------------------- 256-bit predicates
+# ---------------------------------------------------------------- handler bodies
 def eq_body(d):
     """8 limb compares into 8 distinct SGPR pairs, then a SALU AND tree (every SALU read is
     >= 4 instructions after the VALU write)."""
@@ -146,19 +144,6 @@ def flip_signs(d):
     return [f"v_xor_b32 {S(d - 1, 7)}, 0x80000000, {S(d - 1, 7)}", f"v_xor_b32 {S(d, 7)}, 0x80000000, {S(d, 7)}"]
 
 
-for d in range(1, D):
-    a, b = d - 1, d
-    H(("EQ", d), eq_body(d))
-    for signed in (False, True):
-        pre = flip_signs(d) if signed else []
-        p = "S" if signed else "U"
-        H((p + "LT", d), pre + lt_chain(a, b, B(a)))                       # a < b
-        H((p + "GT", d), pre + lt_chain(b, a, B(a)))                       # b < a
-        H((p + "LE", d), pre + lt_chain(b, a, "s[38:39]") + ["s_nop 1", f"s_not_b64 {B(a)}, s[38:39]"])  # !(b < a)
-        H((p + "GE", d), pre + lt_chain(a, b, "s[38:39]") + ["s_nop 1", f"s_not_b64 {B(a)}, s[38:39]"])  # !(a < b)
-
-
-# ---------------------------------------------------------------- 256-bit arithmetic
 def carry_chain(first, rest, n=L):
     out = [first(0)]
     for l in range(1, n):
@@ -167,31 +152,12 @@ def carry_chain(first, rest, n=L):
     return out
 
 
-for d in range(1, D):
-    a, b = d - 1, d
-    H(("ADD", d), carry_chain(lambda l: f"v_add_co_u32 {S(a, l)}, vcc, {S(a, l)}, {S(b, l)}",
-                              lambda l: f"v_addc_co_u32 {S(a, l)}, vcc, {S(a, l)}, {S(b, l)}, vcc"))
-    H(("SUB", d), carry_chain(lambda l: f"v_sub_co_u32 {S(a, l)}, vcc, {S(a, l)}, {S(b, l)}",
-                              lambda l: f"v_subb_co_u32 {S(a, l)}, vcc, {S(a, l)}, {S(b, l)}, vcc"))
-    for nm, ins in (("BAND", "v_and_b32"), ("BOR", "v_or_b32"), ("BXOR", "v_xor_b32")):
-        H((nm, d), [f"{ins} {S(a, l)}, {S(a, l)}, {S(b, l)}" for l in range(L)])
-for d in range(D):
-    H(("NEG", d), carry_chain(lambda l: f"v_sub_co_u32 {S(d, l)}, vcc, 0, {S(d, l)}",
-                              lambda l: f"v_subb_co_u32 {S(d, l)}, vcc, 0, {S(d, l)}, vcc"))
-    H(("BNOT", d), [f"v_not_b32 {S(d, l)}, {S(d, l)}" for l in range(L)])
-for d in range(2, D):
-    H(("ITE", d), [f"v_cndmask_b32_e64 {S(d - 2, l)}, {S(d, l)}, {S(d - 1, l)}, {B(d - 2)}" for l in range(L)])
-    # else-first ternaries (gprog.h G_ITE_EF / G_BITE_EF): else at d-2, cond at d-1, then at d
-    H(("ITE_EF", d), [f"v_cndmask_b32_e64 {S(d - 2, l)}, {S(d - 2, l)}, {S(d, l)}, {B(d - 1)}" for l in range(L)])
-
-
 def mul_body(d):
     """S[d-1] = S[d-1] * S[d] mod 2^256: product scanning (Comba) columns 0..7, 64-bit column
     accumulator v[4:5] (v_mad_u64_u32 with carry-out) + overflow word v6; carries are added
     through three rotating SGPR pairs so every VALU carry read is >= 2 instructions after its
     write.  Column 0 has no carries; each later column's first carry-add writes the overflow word
-    (no reset move); the accumulator shift (v4, v5) <- (v5, v6) is one v_pk_mov_b32; column 7's
-    low word goes straight to S[d-1][7] after its last product."""
+    (no reset move); column 7's low word goes straight to S[d-1][7] after its last product."""
     a, b = d - 1, d
     C = ["s[34:35]", "s[36:37]", "s[38:39]"]
     out = [f"v_mad_u64_u32 v[4:5], s[60:61], {S(a, 0)}, {S(b, 0)}, 0",
@@ -224,12 +190,367 @@ def mul_body(d):
     return out
 
 
-for d in range(1, D):
-    H(("MUL", d), mul_body(d))
+def lshr_body(d, q, arith):
+    """S[d] >>= 32q + s in place (s = imm, 0..31): limb l = (S[l+q+1] : S[l+q]) >> s, ascending
+    so every source is read before it is overwritten; ASHR fills with the sign word v4."""
+    out = [f"v_ashrrev_i32 v4, 31, {S(d, 7)}"] if arith else []
+    for l in range(L):
+        src = l + q
+        if src + 1 <= L - 1:
+            out.append(f"v_alignbit_b32 {S(d, l)}, {S(d, src + 1)}, {S(d, src)}, s17")
+        elif src == L - 1:
+            out.append(f"v_alignbit_b32 {S(d, l)}, v4, {S(d, L - 1)}, s17" if arith
+                       else f"v_lshrrev_b32 {S(d, l)}, s17, {S(d, L - 1)}")
+        else:
+            out.append(f"v_mov_b32 {S(d, l)}, {'v4' if arith else 0}")
+    return out
+
+
+def shl_body(d, q, bits):
+    """S[d] <<= 32q + s in place, descending.  bits: s != 0 and imm = 32 - s
+    (limb l = (S[l-q] : S[l-q-1]) >> (32 - s)); otherwise a pure word move."""
+    out = []
+    for l in range(L - 1, -1, -1):
+        src = l - q
+        if src < 0:
+            out.append(f"v_mov_b32 {S(d, l)}, 0")
+        elif not bits:
+            if src != l:
+                out.append(f"v_mov_b32 {S(d, l)}, {S(d, src)}")
+        elif src >= 1:
+            out.append(f"v_alignbit_b32 {S(d, l)}, {S(d, src)}, {S(d, src - 1)}, s17")
+        else:
+            out.append(f"v_alignbit_b32 {S(d, l)}, {S(d, 0)}, 0, s17")
+    return out
+
+
+def copy_to_w(d):
+    return [f"v_mov_b64 {W2(l)}, {S2(d, l)}" for l in range(0, L, 2)]
+
+
+def copy_from_w(d):
+    return [f"v_mov_b64 {S2(d, l)}, {W2(l)}" for l in range(0, L, 2)]
+
+
+def divc_body(x, kind, pfx):
+    """Division of slot x by a constant divisor c (|c| < 2^32, from the tape constants at imm:
+    {d_norm, v, shift, |c|}).  kinds: UDIVC UREMC SREMC SMODCP SMODCN SDIVCP SDIVCN (P/N = sign
+    of c).  bvsrem / bvsmod / bvsdiv at 256 bits (SMT-LIB)."""
+    out = ["s_lshl_b32 s34, s17, 2", "s_load_dwordx4 s[64:67], s[20:21], s34"] + copy_to_w(x) + ["s_waitcnt lgkmcnt(0)"]
+    signed = kind not in ("UDIVC", "UREMC")
+    if signed:
+        out.append(f"s_call_b64 s[76:77], {pfx}_sub_abs")       # v3 = sign(a) mask, W = |a|
+    out.append(f"s_call_b64 s[76:77], {pfx}_sub_udiv32")         # W = q, v4 = r
+    if kind == "UDIVC":
+        out += copy_from_w(x)
+    elif kind == "UREMC":
+        out += [f"v_mov_b32 {S(x, 0)}, v4"] + zero_limbs(x, 1)
+    elif kind == "SREMC":
+        # r with the dividend's sign: -r = (2^32 - r, ~0, ..) when r != 0
+        out += ["v_sub_u32 v5, 0, v4",
+                "v_cmp_ne_u32_e64 s[34:35], 0, v3",
+                "v_cmp_ne_u32_e64 s[36:37], 0, v4",
+                "s_nop 3",
+                "s_and_b64 s[36:37], s[36:37], s[34:35]",
+                f"v_cndmask_b32_e64 {S(x, 0)}, v4, v5, s[34:35]",
+                "v_cndmask_b32_e64 v6, 0, -1, s[36:37]"]
+        out += [f"v_mov_b32 {S(x, l)}, v6" for l in range(1, L)]
+    elif kind == "SMODCP":
+        # c > 0: t = (a < 0 && r != 0) ? c - r : r   (non-negative, < c)
+        out += ["v_sub_u32 v5, s67, v4",
+                "v_cmp_ne_u32_e64 s[34:35], 0, v3",
+                "v_cmp_ne_u32_e64 s[36:37], 0, v4",
+                "s_nop 3",
+                "s_and_b64 s[36:37], s[36:37], s[34:35]",
+                "s_nop 0",
+                f"v_cndmask_b32_e64 {S(x, 0)}, v4, v5, s[36:37]"] + zero_limbs(x, 1)
+    elif kind == "SMODCN":
+        # c < 0: result = -t, t = a >= 0 ? (r != 0 ? |c| - r : 0) : r
+        out += ["v_sub_u32 v5, s67, v4",
+                "v_cmp_ne_u32_e64 s[36:37], 0, v4",
+                "v_cmp_ne_u32_e64 s[34:35], 0, v3",
+                "s_nop 1",
+                "v_cndmask_b32_e64 v5, 0, v5, s[36:37]",
+                "v_cndmask_b32_e64 v5, v5, v4, s[34:35]",
+                "v_sub_u32 v4, 0, v5",
+                "v_cmp_ne_u32_e64 s[36:37], 0, v5",
+                f"v_mov_b32 {S(x, 0)}, v4",
+                "s_nop 1",
+                "v_cndmask_b32_e64 v6, 0, -1, s[36:37]"]
+        out += [f"v_mov_b32 {S(x, l)}, v6" for l in range(1, L)]
+    elif kind in ("SDIVCP", "SDIVCN"):
+        # q negated when the operand signs differ
+        if kind == "SDIVCN":
+            out.append("v_not_b32 v3, v3")
+        out.append(f"s_call_b64 s[76:77], {pfx}_sub_cneg")
+        out += copy_from_w(x)
+    return out
+
+
+def sub_abs_cneg(pfx):
+    """_sub_abs: v3 = sign mask of W, then _sub_cneg: W = (W ^ v3) - v3 (256-bit: subtracting the
+    all-ones word v3 from every limb with borrow = adding 1 to ~W when v3 = ~0)."""
+    out = [f"{pfx}_sub_abs:", f"v_ashrrev_i32 v3, 31, {W(7)}", f"{pfx}_sub_cneg:"]
+    out += [f"v_xor_b32 {W(l)}, {W(l)}, v3" for l in range(L)]
+    out += carry_chain(lambda l: f"v_sub_co_u32 {W(l)}, vcc, {W(l)}, v3",
+                       lambda l: f"v_subb_co_u32 {W(l)}, vcc, {W(l)}, v3, vcc")
+    out += ["s_setpc_b64 s[76:77]"]
+    return out
+
+
+def sub_udiv32(pfx):
+    """W[0..7] = W / c, v4 = W mod c for a 32-bit divisor c (wave-uniform), by 2-by-1 word division
+    with a precomputed reciprocal (Moller & Granlund, "Improved division by invariant integers",
+    2011, Alg. 4): s64 = c << sh (normalised), s65 = floor((2^64-1)/s64) - 2^32, s66 = sh.
+    The numerator is normalised limb by limb on the fly ((W[i]:W[i-1]) >> (32-sh)); quotient
+    words overwrite W[i] (W[i-1] is still unread when step i writes).  ~14 VALU per limb."""
+    out = [f"{pfx}_sub_udiv32:",
+           "s_cmp_eq_u32 s66, 0",
+           "s_cselect_b64 s[70:71], 0, -1",          # all lanes when sh != 0
+           "s_sub_u32 s68, 32, s66",
+           f"v_lshrrev_b32 v5, s68, {W(7)}",
+           "v_cndmask_b32_e64 v5, 0, v5, s[70:71]"]   # r = top bits shifted out (0 when sh == 0)
+    for i in range(L - 1, -1, -1):
+        lo = W(i - 1) if i > 0 else "0"
+        out += [f"v_alignbit_b32 v4, {W(i)}, {lo}, s68",
+                f"v_cndmask_b32_e64 v4, {W(i)}, v4, s[70:71]",      # u0 = normalised limb i
+                "v_mad_u64_u32 v[6:7], s[34:35], s65, v5, v[4:5]",    # (q1:q0) = v*r + (r:u0)
+                "v_add_u32 v7, 1, v7",
+                "v_mul_lo_u32 v5, v7, s64",
+                "v_sub_u32 v5, v4, v5",                               # r = u0 - q1*d
+                "v_cmp_gt_u32_e64 s[36:37], v5, v6",
+                "v_add_u32 v4, s64, v5",
+                "v_add_u32 v6, -1, v7",
+                "s_nop 1",
+                "v_cndmask_b32_e64 v5, v5, v4, s[36:37]",
+                "v_cndmask_b32_e64 v7, v7, v6, s[36:37]",
+                "v_cmp_le_u32_e64 s[38:39], s64, v5",
+                "v_subrev_u32 v4, s64, v5",
+                "v_add_u32 v6, 1, v7",
+                "s_nop 1",
+                "v_cndmask_b32_e64 v5, v5, v4, s[38:39]",
+                f"v_cndmask_b32_e64 {W(i)}, v7, v6, s[38:39]"]
+    out += ["v_lshrrev_b32 v4, s66, v5", "s_setpc_b64 s[76:77]"]
+    return out
+
+
+def sub_uf1(pfx):
+    """Arity-1 model function lookup (UF / as-array select, z3 completion: the else value when no
+    entry matches): key W[0..7] (canonical), s98 = function id; result in v[8:15].
+    FuncDev (qs_launch.h) of the function gives nl_a0 / nl_res / stride and the offsets of its
+    entry rows, per-model entry ranges (entry_ptr) and SoA else block.  Per lane the entries are
+    scanned in order and the first match wins (mq.h model layout); the wave loops over the
+    longest list with finished lanes masked off."""
+    P = pfx
+    out = [f"{P}_sub_uf1:"]
+    out += [f"v_mov_b64 v[{8 + l}:{9 + l}], 0" for l in range(0, 8, 2)]
+    out += ["s_load_dwordx8 s[64:71], s[10:11], 0x160",       # funcs, entry_ptr, entry_words, else_words
+            "s_load_dword s99, s[10:11], 0x180",             # n_funcs
+            "s_waitcnt lgkmcnt(0)",
+            "s_cmp_ge_u32 s98, s99",
+            f"s_cbranch_scc1 {P}_uf_ret",
+            "s_mul_i32 s34, s98, 48",
+            "s_add_u32 s78, s64, s34",
+            "s_addc_u32 s79, s65, 0",
+            "s_load_dword s36, s[78:79], 0x4",                # nl_a0
+            "s_load_dword s37, s[78:79], 0xc",                # nl_res
+            "s_load_dword s38, s[78:79], 0x10",               # stride (words)
+            "s_load_dwordx2 s[64:65], s[78:79], 0x18",        # entry_base
+            "s_load_dwordx2 s[60:61], s[78:79], 0x20",        # ptr_base
+            "s_load_dwordx2 s[34:35], s[78:79], 0x28",        # else_base
+            "s_waitcnt lgkmcnt(0)",
+            "s_lshl_b64 s[34:35], s[34:35], 2",
+            "s_add_u32 s70, s70, s34",
+            "s_addc_u32 s71, s71, s35",                       # else rows
+            "s_lshl_b64 s[60:61], s[60:61], 3",
+            "s_add_u32 s66, s66, s60",
+            "s_addc_u32 s67, s67, s61",                       # this function's entry_ptr[M+1]
+            "s_lshl_b64 s[64:65], s[64:65], 2",
+            "s_add_u32 s68, s68, s64",
+            "s_addc_u32 s69, s69, s65",                       # entry 0 of the function
+            "s_lshl_b32 s39, s38, 2",                         # stride bytes
+            "s_lshl_b32 s98, s36, 2",                        # value offset in an entry
+            # else value: nl_res SoA rows
+            "s_mov_b64 s[34:35], s[70:71]"]
+    for l in range(L):
+        out += [f"s_cmp_le_u32 s37, {l}", f"s_cbranch_scc1 {P}_uf_else_done",
+                f"global_load_dword v{8 + l}, v2, s[34:35]",
+                "s_add_u32 s34, s34, s74", "s_addc_u32 s35, s35, s75"]
+    out += [f"{P}_uf_else_done:",
+            "v_lshlrev_b32 v4, 1, v2",                        # m*8
+            "global_load_dword v5, v4, s[66:67]",             # first entry of (f, m)
+            "global_load_dword v6, v4, s[66:67] offset:8",    # end
+            "v_mov_b32 v7, s39",
+            "s_waitcnt vmcnt(0)",
+            "v_mad_u64_u32 v[16:17], s[34:35], v5, v7, s[68:69]",   # &entry[lo]
+            "s_mov_b64 s[60:61], exec",
+            f"{P}_uf_loop:",
+            "v_cmp_lt_u32_e64 s[34:35], v5, v6",
+            "s_nop 3",
+            "s_and_b64 exec, exec, s[34:35]",
+            f"s_cbranch_execz {P}_uf_done"]
+    for l in range(L):
+        out += [f"s_cmp_le_u32 s36, {l}", f"s_cbranch_scc1 {P}_uf_kl_done",
+                f"global_load_dword v{20 + l}, v[16:17], off offset:{4 * l}"]
+    out += [f"{P}_uf_kl_done:", "s_waitcnt vmcnt(0)", "v_mov_b32 v28, 0"]
+    for l in range(L):
+        out += [f"s_cmp_le_u32 s36, {l}", f"s_cbranch_scc1 {P}_uf_kc_done",
+                f"v_xor_b32 v29, v{20 + l}, {W(l)}", "v_or_b32 v28, v28, v29"]
+    out += [f"{P}_uf_kc_done:",
+            "v_cmp_eq_u32_e64 s[34:35], 0, v28",
+            "v_add_co_u32 v30, vcc, s98, v16",
+            "s_nop 1",
+            "v_addc_co_u32 v31, vcc, 0, v17, vcc",
+            "s_nop 3",
+            "s_and_saveexec_b64 s[78:79], s[34:35]",
+            f"s_cbranch_execz {P}_uf_nomatch"]
+    for l in range(L):
+        out += [f"s_cmp_le_u32 s37, {l}", f"s_cbranch_scc1 {P}_uf_vl_done",
+                f"global_load_dword v{8 + l}, v[30:31], off offset:{4 * l}"]
+    out += [f"{P}_uf_vl_done:", "s_waitcnt vmcnt(0)",
+            f"{P}_uf_nomatch:",
+            "s_andn2_b64 exec, s[78:79], s[34:35]",           # matched lanes are done
+            "v_add_u32 v5, 1, v5",
+            "v_add_co_u32 v16, vcc, v16, v7",
+            "s_nop 1",
+            "v_addc_co_u32 v17, vcc, 0, v17, vcc",
+            f"s_branch {P}_uf_loop",
+            f"{P}_uf_done:",
+            "s_mov_b64 exec, s[60:61]",
+            f"{P}_uf_ret:",
+            "s_setpc_b64 s[76:77]"]
+    return out
+
+
+# ---------------------------------------------------------------- handler table
+def make_handlers(variant, pfx):
+    """(key, body lines) for the variant; key = (kind, d, v)."""
+    G = variant == "g"
+    hs = []
+
+    def H(key, body, tail=True, reads_stack=True):
+        pre = [VMWAIT] if (G and reads_stack) else []
+        hs.append((key, pre + list(body) + (NEXT if tail else [])))
+
+    H(("END",), [f"s_branch {pfx}_tape_end"], tail=False, reads_stack=False)
+    # ---- leaves
+    for d in range(D):
+        if not G:
+            for v in range(NV):
+                H(("PUSH_VAR", d, v), [f"v_mov_b64 {S2(d, l)}, {V2(v, l)}" for l in range(0, L, 2)], reads_stack=False)
+                H(("PUSH_VARB", d, v), [f"v_cmp_ne_u32_e64 {B(d)}, 0, v{VBASE + 8 * v}", "s_nop 3"], reads_stack=False)
+        else:
+            # variable row imm: loads in flight until the next stack reader's vmcnt wait
+            for n in range(1, L + 1):
+                body = ["s_mul_i32 s34, s17, s29", "s_mul_hi_u32 s35, s17, s29", "s_lshl_b64 s[34:35], s[34:35], 2",
+                        "s_add_u32 s34, s34, s90", "s_addc_u32 s35, s35, s91"]
+                for l in range(n):
+                    body.append(f"global_load_dword {S(d, l)}, v2, s[34:35]")
+                    if l < n - 1:
+                        body += ["s_add_u32 s34, s34, s74", "s_addc_u32 s35, s35, s75"]
+                body += zero_limbs(d, n)
+                H(("PUSH_MEM", d, n - 1), body, reads_stack=False)
+            H(("PUSH_MEMB", d), ["s_mul_i32 s34, s17, s29", "s_mul_hi_u32 s35, s17, s29", "s_lshl_b64 s[34:35], s[34:35], 2",
+                                 "s_add_u32 s34, s34, s90", "s_addc_u32 s35, s35, s91",
+                                 "global_load_dword v4, v2, s[34:35]", "s_waitcnt vmcnt(0)",
+                                 f"v_cmp_ne_u32_e64 {B(d)}, 0, v4", "s_nop 3"], reads_stack=False)
+        H(("PUSH_CONST", d), ["s_lshl_b32 s34, s17, 2", "s_load_dwordx8 s[64:71], s[20:21], s34", "s_waitcnt lgkmcnt(0)"]
+          + [f"v_mov_b64 {S2(d, l)}, s[{64 + l}:{65 + l}]" for l in range(0, L, 2)], reads_stack=False)
+        H(("PUSH_TMP", d), ["s_lshl_b32 s34, s17, 11", "v_add_u32 v5, s34, v1"]
+          + [f"ds_read_b64 {S2(d, l)}, v5 offset:{256 * l}" for l in range(0, L, 2)] + ["s_waitcnt lgkmcnt(0)"],
+          reads_stack=False)
+        H(("PUSH_TMP_BOOL", d), ["s_lshl_b32 s34, s17, 11", "v_add_u32 v5, s34, v1", "ds_read_b32 v6, v5",
+                                 "s_waitcnt lgkmcnt(0)", f"v_cmp_ne_u32_e64 {B(d)}, 0, v6", "s_nop 3"], reads_stack=False)
+        H(("PUSH_BOOL", d), ["s_cmp_lg_u32 s17, 0", f"s_cselect_b64 {B(d)}, -1, 0"], reads_stack=False)
+    H(("STORE_TMP", 0), ["s_lshl_b32 s34, s17, 11", "v_add_u32 v5, s34, v1"]
+      + [f"ds_write_b64 v5, {S2(0, l)} offset:{256 * l}" for l in range(0, L, 2)])
+    H(("STORE_TMP_BOOL", 0), ["s_lshl_b32 s34, s17, 11", "v_add_u32 v5, s34, v1",
+                              f"v_cndmask_b32_e64 v6, 0, 1, {B(0)}", "ds_write_b32 v5, v6"], reads_stack=False)
+    # ---- Bool (SALU on lane masks)
+    for d in range(D):
+        H(("NOT", d), [f"s_not_b64 {B(d)}, {B(d)}"], reads_stack=False)
+    for d in range(1, D):
+        a, b = B(d - 1), B(d)
+        H(("AND", d), [f"s_and_b64 {a}, {a}, {b}"], reads_stack=False)
+        H(("OR", d), [f"s_or_b64 {a}, {a}, {b}"], reads_stack=False)
+        H(("XOR", d), [f"s_xor_b64 {a}, {a}, {b}"], reads_stack=False)
+        H(("IFF", d), [f"s_xnor_b64 {a}, {a}, {b}"], reads_stack=False)
+        H(("IMPLIES", d), [f"s_orn2_b64 {a}, {b}, {a}"], reads_stack=False)
+    for d in range(2, D):
+        H(("BITE", d), [f"s_and_b64 s[34:35], {B(d - 2)}, {B(d - 1)}", f"s_andn2_b64 s[36:37], {B(d)}, {B(d - 2)}",
+                        f"s_or_b64 {B(d - 2)}, s[34:35], s[36:37]"], reads_stack=False)
+        H(("BITE_EF", d), [f"s_and_b64 s[34:35], {B(d - 1)}, {B(d)}", f"s_andn2_b64 s[36:37], {B(d - 2)}, {B(d - 1)}",
+                           f"s_or_b64 {B(d - 2)}, s[34:35], s[36:37]"], reads_stack=False)
+    # ---- 256-bit predicates (unsigned compares are exact on canonical values of any width)
+    for d in range(1, D):
+        a, b = d - 1, d
+        H(("EQ", d), eq_body(d))
+        for signed in (False, True):
+            pre = flip_signs(d) if signed else []
+            p = "S" if signed else "U"
+            H((p + "LT", d), pre + lt_chain(a, b, B(a)))
+            H((p + "GT", d), pre + lt_chain(b, a, B(a)))
+            H((p + "LE", d), pre + lt_chain(b, a, "s[38:39]") + ["s_nop 3", f"s_not_b64 {B(a)}, s[38:39]"])
+            H((p + "GE", d), pre + lt_chain(a, b, "s[38:39]") + ["s_nop 3", f"s_not_b64 {B(a)}, s[38:39]"])
+        # signed compare below 256 bits: flip bit W-1 of both operands, then compare unsigned
+        for p in range(L):
+            H(("FLIP2", d, p), ["s_lshl_b32 s34, 1, s17", f"v_xor_b32 {S(d - 1, p)}, s34, {S(d - 1, p)}",
+                                f"v_xor_b32 {S(d, p)}, s34, {S(d, p)}"])
+    # ---- 256-bit arithmetic (results below 256 bits are re-masked by MASK*)
+    for d in range(1, D):
+        a, b = d - 1, d
+        H(("ADD", d), carry_chain(lambda l: f"v_add_co_u32 {S(a, l)}, vcc, {S(a, l)}, {S(b, l)}",
+                                  lambda l: f"v_addc_co_u32 {S(a, l)}, vcc, {S(a, l)}, {S(b, l)}, vcc"))
+        H(("SUB", d), carry_chain(lambda l: f"v_sub_co_u32 {S(a, l)}, vcc, {S(a, l)}, {S(b, l)}",
+                                  lambda l: f"v_subb_co_u32 {S(a, l)}, vcc, {S(a, l)}, {S(b, l)}, vcc"))
+        for nm, ins in (("BAND", "v_and_b32"), ("BOR", "v_or_b32"), ("BXOR", "v_xor_b32")):
+            H((nm, d), [f"{ins} {S(a, l)}, {S(a, l)}, {S(b, l)}" for l in range(L)])
+        H(("MUL", d), mul_body(d))
+    for d in range(D):
+        H(("NEG", d), carry_chain(lambda l: f"v_sub_co_u32 {S(d, l)}, vcc, 0, {S(d, l)}",
+                                  lambda l: f"v_subb_co_u32 {S(d, l)}, vcc, 0, {S(d, l)}, vcc"))
+        H(("BNOT", d), [f"v_not_b32 {S(d, l)}, {S(d, l)}" for l in range(L)])
+    for d in range(2, D):
+        H(("ITE", d), [f"v_cndmask_b32_e64 {S(d - 2, l)}, {S(d, l)}, {S(d - 1, l)}, {B(d - 2)}" for l in range(L)])
+        # else-first ternaries (gprog.h G_ITE_EF / G_BITE_EF): else at d-2, cond at d-1, then at d
+        H(("ITE_EF", d), [f"v_cndmask_b32_e64 {S(d - 2, l)}, {S(d - 2, l)}, {S(d, l)}, {B(d - 1)}" for l in range(L)])
+    # ---- width handling, constant shifts, sign extension (any slot, in place)
+    for d in range(D):
+        for n in range(1, L + 1):
+            # keep n limbs, the top one masked to imm bits (MASKP) or whole (MASKZ)
+            H(("MASKP", d, n - 1), ["s_lshl_b32 s34, 1, s17", "s_add_u32 s34, s34, -1",
+                                    f"v_and_b32 {S(d, n - 1)}, s34, {S(d, n - 1)}"] + zero_limbs(d, n))
+            if n < L:
+                H(("MASKZ", d, n - 1), zero_limbs(d, n))
+        for q in range(L):
+            H(("LSHRI", d, q), lshr_body(d, q, False))
+            H(("ASHRI", d, q), lshr_body(d, q, True))
+            H(("SHLI", d, q), shl_body(d, q, True))
+            if q:
+                H(("SHLW", d, q), shl_body(d, q, False))
+        for p in range(L):
+            fill = [f"v_ashrrev_i32 v4, 31, {S(d, p)}"] + [f"v_mov_b32 {S(d, l)}, v4" for l in range(p + 1, L)]
+            H(("SEXTB", d, p), [f"v_bfe_i32 {S(d, p)}, {S(d, p)}, 0, s17"] + fill)
+            if p < L - 1:
+                H(("SEXTA", d, p), fill)
+    # ---- division by a constant (operand slot x = d - 1 of the binary op)
+    for x in range(D - 1):
+        for kind in ("UDIVC", "UREMC", "SREMC", "SMODCP", "SMODCN", "SDIVCP", "SDIVCN"):
+            H((kind, x), divc_body(x, kind, pfx))
+    # ---- model function lookup (G: uses v[8:31])
+    if G:
+        for d in range(D):
+            H(("UF1", d), copy_to_w(d) + ["s_mov_b32 s98, s17", f"s_call_b64 s[76:77], {pfx}_sub_uf1"]
+              + [f"v_mov_b64 {S2(d, l)}, v[{8 + l}:{9 + l}]" for l in range(0, L, 2)])
+            H(("UF1B", d), copy_to_w(d) + ["s_mov_b32 s98, s17", f"s_call_b64 s[76:77], {pfx}_sub_uf1",
+                                            "v_and_b32 v4, 1, v8", f"v_cmp_ne_u32_e64 {B(d)}, 0, v4", "s_nop 3"])
+    subs = sub_abs_cneg(pfx) + sub_udiv32(pfx) + (sub_uf1(pfx) if G else [])
+    return hs, subs
 
 
 # ---------------------------------------------------------------- kernel frame
-def frame():
+def frame(variant, pfx, handlers, subs):
+    G = variant == "g"
     P = []
     P += [
         "s_mov_b64 s[10:11], %0",
@@ -253,29 +574,28 @@ def frame():
         "s_mov_b32 s99, s86",
         # handler base
         "s_getpc_b64 s[12:13]",
-        ".Lqsa_pc:",
-        "s_add_u32 s12, s12, .Lqsa_hbase - .Lqsa_pc",
+        f"{pfx}_pc:",
+        f"s_add_u32 s12, s12, {pfx}_hbase - {pfx}_pc",
         "s_addc_u32 s13, s13, 0",
         # mode 2: dump handler offsets (block 0, lane 0)
         "s_cmp_eq_u32 s31, 2",
-        "s_cbranch_scc0 .Lqsa_main",
+        f"s_cbranch_scc0 {pfx}_main",
         "s_or_b32 s34, s96, s97",
         "s_cmp_eq_u32 s34, 0",
-        "s_cbranch_scc0 .Lqsa_end",
+        f"s_cbranch_scc0 {pfx}_end",
         "v_cmp_eq_u32_e64 s[34:35], 0, v3",
-        "s_nop 1",
+        "s_nop 3",
         "s_and_saveexec_b64 s[36:37], s[34:35]",
         "v_mov_b32 v4, 0",
     ]
     for k in range(len(handlers)):
-        P.append(f"v_mov_b32 v5, .Lqh_{k} - .Lqsa_hbase")
+        P.append(f"v_mov_b32 v5, {pfx}_h{k} - {pfx}_hbase")
         P.append(f"global_store_dword v4, v5, s[78:79] offset:{4 * k}")
     P += [
-        f"v_mov_b32 v5, {len(handlers)}",
         "s_waitcnt vmcnt(0)",
         "s_mov_b64 exec, s[36:37]",
-        "s_branch .Lqsa_end",
-        ".Lqsa_main:",
+        f"s_branch {pfx}_end",
+        f"{pfx}_main:",
         # wave / lane / model index
         "v_and_b32 v4, 63, v3",
         "v_lshrrev_b32 v5, 6, v3",
@@ -288,7 +608,7 @@ def frame():
         "s_lshl_b32 s36, s34, 6",
         "s_add_u32 s35, s35, s36",
         "s_cmp_ge_u32 s35, s29",
-        "s_cbranch_scc1 .Lqsa_end",
+        f"s_cbranch_scc1 {pfx}_end",
         "s_add_u32 s28, s98, s35",            # gfirst
         "v_add_u32 v2, s35, v4",               # m
         "v_cmp_lt_u32_e64 s[62:63], v2, s29",  # valid
@@ -305,39 +625,41 @@ def frame():
         "s_add_u32 s25, s24, s83",
         "s_min_u32 s25, s25, s82",
     ]
-    # preload variables: 64 limb rows (row index table at args+0x60; the host points missing
-    # limbs / vars at an all-zero row)
-    for c in range(4):
-        P += [f"s_load_dwordx16 s[64:79], s[10:11], {0x60 + 64 * c:#x}", "s_waitcnt lgkmcnt(0)"]
-        for j in range(16):
-            idx = 16 * c + j
-            v, l = idx // 8, idx % 8
-            P += [f"s_mul_i32 s34, s{64 + j}, s29", f"s_mul_hi_u32 s35, s{64 + j}, s29",
-                  "s_lshl_b64 s[34:35], s[34:35], 2", "s_add_u32 s34, s34, s90", "s_addc_u32 s35, s35, s91",
-                  f"global_load_dword v{VBASE + 8 * v + l}, v2, s[34:35]"]
-    P += ["s_waitcnt vmcnt(0)"]
+    if not G:
+        # preload variables: 64 limb rows (row index table at args+0x60; the host points missing
+        # limbs / vars at an all-zero row)
+        for c in range(4):
+            P += [f"s_load_dwordx16 s[64:79], s[10:11], {0x60 + 64 * c:#x}", "s_waitcnt lgkmcnt(0)"]
+            for j in range(16):
+                idx = 16 * c + j
+                v, l = idx // 8, idx % 8
+                P += [f"s_mul_i32 s34, s{64 + j}, s29", f"s_mul_hi_u32 s35, s{64 + j}, s29",
+                      "s_lshl_b64 s[34:35], s[34:35], 2", "s_add_u32 s34, s34, s90", "s_addc_u32 s35, s35, s91",
+                      f"global_load_dword v{VBASE + 8 * v + l}, v2, s[34:35]"]
+        P += ["s_waitcnt vmcnt(0)"]
+    P += ["s_lshl_b32 s74, s29, 2", "s_lshr_b32 s75, s29, 30"]   # M*4 (after the preload's s[64:79] use)
     # tape loop
     P += [
-        ".Lqsa_tape_loop:",
+        f"{pfx}_tape_loop:",
         "s_cmp_ge_u32 s24, s25",
-        "s_cbranch_scc1 .Lqsa_tapes_done",
+        f"s_cbranch_scc1 {pfx}_tapes_done",
         "s_lshl_b32 s34, s24, 5",
         "s_add_u32 s34, s22, s34",
         "s_addc_u32 s35, s23, 0",
         "s_load_dwordx8 s[80:87], s[34:35], 0x0",
         "s_waitcnt lgkmcnt(0)",
         "s_lshl_b32 s34, s82, 2",
-        "s_add_u32 s72, s26, s34",           # s[72:73] = &best[tape] (handlers never touch s72-s87)
+        "s_add_u32 s72, s26, s34",           # s[72:73] = &best[tape] (handlers never touch s72-s73, s80-s87)
         "s_addc_u32 s73, s27, 0",
         "s_cmp_eq_u32 s31, 1",
-        "s_cbranch_scc1 .Lqsa_run",
+        f"s_cbranch_scc1 {pfx}_run",
         "s_cmp_eq_u32 s30, 0",
-        "s_cbranch_scc1 .Lqsa_run",
+        f"s_cbranch_scc1 {pfx}_run",
         "s_load_dword s34, s[72:73], 0x0 glc",
         "s_waitcnt lgkmcnt(0)",
         "s_cmp_ge_i32 s28, s34",
-        "s_cbranch_scc1 .Lqsa_next_tape",
-        ".Lqsa_run:",
+        f"s_cbranch_scc1 {pfx}_next_tape",
+        f"{pfx}_run:",
         "s_lshl_b32 s34, s83, 2",
         "s_add_u32 s20, s88, s34",
         "s_addc_u32 s21, s89, 0",
@@ -348,7 +670,7 @@ def frame():
         "s_add_u32 s14, s14, 4",
         "s_addc_u32 s15, s15, 0",
     ] + NEXT + [
-        ".Lqsa_tape_end:",
+        f"{pfx}_tape_end:",
         "s_waitcnt lgkmcnt(0)",
         "s_and_b64 s[34:35], s[48:49], s[62:63]",
         "s_bcnt1_i32_b64 s38, s[62:63]",
@@ -363,9 +685,9 @@ def frame():
         "s_add_u32 s44, s44, s60",
         "s_addc_u32 s45, s45, s61",
         "s_cmp_eq_u32 s31, 1",
-        "s_cbranch_scc1 .Lqsa_store_verdict",
+        f"s_cbranch_scc1 {pfx}_store_verdict",
         "s_cmp_eq_u64 s[34:35], 0",
-        "s_cbranch_scc1 .Lqsa_next_tape",
+        f"s_cbranch_scc1 {pfx}_next_tape",
         "s_ff1_i32_b64 s38, s[34:35]",
         "s_add_u32 s38, s38, s28",
         "s_mov_b64 s[60:61], exec",
@@ -374,8 +696,8 @@ def frame():
         "v_mov_b32 v6, 0",
         "global_atomic_smin v6, v5, s[72:73]",
         "s_mov_b64 exec, s[60:61]",
-        "s_branch .Lqsa_next_tape",
-        ".Lqsa_store_verdict:",
+        f"s_branch {pfx}_next_tape",
+        f"{pfx}_store_verdict:",
         "s_mul_i32 s38, s82, s29",
         "s_mul_hi_u32 s39, s82, s29",
         "s_add_u32 s38, s38, s94",
@@ -386,10 +708,10 @@ def frame():
         "s_mov_b64 exec, s[62:63]",
         "global_store_byte v6, v5, s[38:39]",
         "s_mov_b64 exec, s[60:61]",
-        ".Lqsa_next_tape:",
+        f"{pfx}_next_tape:",
         "s_add_u32 s24, s24, 1",
-        "s_branch .Lqsa_tape_loop",
-        ".Lqsa_tapes_done:",
+        f"s_branch {pfx}_tape_loop",
+        f"{pfx}_tapes_done:",
         "s_mov_b64 s[60:61], exec",
         "s_mov_b64 exec, 1",
         "v_mov_b32 v6, 0",
@@ -404,44 +726,55 @@ def frame():
         "global_atomic_add_x2 v6, v[4:5], s[92:93] offset:16",
         "s_waitcnt vmcnt(0)",
         "s_mov_b64 exec, s[60:61]",
-        "s_branch .Lqsa_end",
-        ".Lqsa_hbase:",
+        f"s_branch {pfx}_end",
     ]
+    P += subs
+    P.append(f"{pfx}_hbase:")
     for k, (key, body) in enumerate(handlers):
-        P.append(f".Lqh_{k}:  ; {' '.join(map(str, key))}")
+        P.append(f"{pfx}_h{k}:  ; {' '.join(map(str, key))}")
         P += body
-    P.append(".Lqsa_end:")
+    P.append(f"{pfx}_end:")
     return P
 
 
+VARIANTS = (("p", ".Lqsa", "QSA_ASM_TEXT_P", "P"), ("g", ".Lqsg", "QSA_ASM_TEXT_G", "G"))
+
+
 def main():
-    lines = frame()
-    text = "\n".join(lines) + "\n"
     clob = [f'"v{i}"' for i in range(1, 128)] + [f'"s{i}"' for i in range(10, 100) if i not in (32, 33)]
     clob += ['"vcc"', '"scc"', '"memory"']
+    gen = {}
+    for variant, pfx, macro, suffix in VARIANTS:
+        hs, subs = make_handlers(variant, pfx)
+        gen[variant] = (hs, frame(variant, pfx, hs, subs), macro, suffix)
     with open(os.path.join(HERE, "qsa_gen.inc"), "w") as f:
         f.write("// GENERATED by gen_qsa.py — do not edit\n")
-        f.write("#define QSA_ASM_TEXT \\\n")
-        for ln in text.splitlines():
-            f.write('  "' + ln.replace('"', '\\"') + '\\n" \\\n')
-        f.write("  \"\"\n")
+        for variant, (hs, lines, macro, suffix) in gen.items():
+            f.write(f"#define {macro} \\\n")
+            for ln in lines:
+                f.write('  "' + ln.replace('"', '\\"') + '\\n" \\\n')
+            f.write("  \"\"\n")
         f.write("#define QSA_CLOBBERS " + ", ".join(clob) + "\n")
-    names = sorted({k[0] for k, _ in handlers})
+    names = sorted({k[0] for hs, *_ in gen.values() for k, _ in hs})
     with open(os.path.join(HERE, "qsa_table.h"), "w") as f:
-        f.write("// GENERATED by gen_qsa.py — handler enumeration of the QSA interpreter\n")
+        f.write("// GENERATED by gen_qsa.py — handler enumerations of the QSA interpreters\n")
         f.write("#ifndef MQ_QSA_TABLE_H\n#define MQ_QSA_TABLE_H\nnamespace mq {\n")
-        f.write(f"constexpr int kQsaStack = {D};\nconstexpr int kQsaVars = {NV};\nconstexpr int kQsaHandlers = {len(handlers)};\n")
+        f.write(f"constexpr int kQsaStack = {D};\nconstexpr int kQsaVars = {NV};\nconstexpr int kQsaSel = {L};\n")
         f.write("enum QsaKind {\n" + "".join(f"  QK_{n},\n" for n in names) + "  QK_COUNT\n};\n")
         f.write("struct QsaHandlerKey { int kind, d, v; };\n")
-        f.write("static const QsaHandlerKey kQsaHandlerKeys[] = {\n")
-        for key, _ in handlers:
-            kind = key[0]
-            d = key[1] if len(key) > 1 else -1
-            v = key[2] if len(key) > 2 else -1
-            f.write(f"  {{QK_{kind}, {d}, {v}}},\n")
-        f.write("};\n}  // namespace mq\n#endif\n")
-    nins = sum(1 for ln in lines if ln and not ln.startswith(".L"))
-    print(f"handlers={len(handlers)} asm_lines={nins}", file=sys.stderr)
+        for variant, (hs, lines, macro, suffix) in gen.items():
+            f.write(f"constexpr int kQsaHandlers{suffix} = {len(hs)};\n")
+            f.write(f"static const QsaHandlerKey kQsaHandlerKeys{suffix}[] = {{\n")
+            for key, _ in hs:
+                kind = key[0]
+                d = key[1] if len(key) > 1 else -1
+                v = key[2] if len(key) > 2 else -1
+                f.write(f"  {{QK_{kind}, {d}, {v}}},\n")
+            f.write("};\n")
+        f.write("}  // namespace mq\n#endif\n")
+    for variant, (hs, lines, *_ ) in gen.items():
+        nins = sum(1 for ln in lines if ln and not ln.startswith(".L"))
+        print(f"{variant}: handlers={len(hs)} asm_lines={nins}", file=sys.stderr)
 
 
 if __name__ == "__main__":

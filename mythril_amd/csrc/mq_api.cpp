@@ -72,13 +72,17 @@ struct mq_ctx {
   DevBuf scratch;   // per-wave temp slots of the HIP C++ interpreter (persistent grid)
   DevBuf rowmask;   // per-row masks applied to uploaded variable words
   DevBuf verdict_buf;
-  // assembly interpreter (qsa.hip): handler byte offsets read back at context creation
+  // assembly interpreters (qsa.hip): handler byte offsets read back at context creation;
+  // k = 0 the P kernel (preloaded variables), k = 1 the G kernel (general)
   bool qsa_ready = false;
-  std::vector<uint32_t> qsa_off;
-  int qsa_index[QK_COUNT][kQsaStack][kQsaVars + 1];
-  bool qsa_models_ok = false;   // model batch fits the preloaded-variable register file
+  std::vector<uint32_t> qsa_off[2];
+  int qsa_index[2][QK_COUNT][kQsaStack][kQsaSel + 1];
   uint32_t qsa_var_row[64];
   DevBuf qsa_args;
+  // host copies of the model batch layout the QSA translation depends on
+  std::vector<uint32_t> var_off_h, var_nl_h;
+  std::vector<mq_func_desc> funcs_h;
+  uint64_t models_gen = 0;      // bumped by every mq_models_upload
   int use_asm = 1;      // MQ_OPT_USE_ASM
   int early_exit = 1;   // MQ_OPT_EARLY_EXIT
   // MQ_OPT_TIME_KERNELS: one HIP event pair bracketing the evaluation kernels of each launch
@@ -104,12 +108,18 @@ struct mq_tapes {
     bool keccak = false;
   };
   // descs layout: [L8 QSA-eligible | L8 other | L16]; the QSA view (qdescs/qprog) holds the
-  // eligible tapes translated to threaded code, in the same order.
+  // eligible tapes translated to threaded code.  The translation depends on the model batch
+  // (variable rows, function table), so it is redone at launch when the models changed: each
+  // eligible tape goes to the P kernel (only preloaded variables) or the G kernel.
   Variant l8_all, l8_rest, l16, l16k, qsa;   // l16k: tapes with interpreted keccak
-  DevBuf qdescs, qprog, qargs;
-  QArgs qargs_host;
-  QArgs qargs_dev_copy;      // what qargs currently holds on the device
-  bool qargs_valid = false;
+  std::vector<CompiledTape> qct;             // compiled programs of the QSA-eligible tapes
+  std::vector<GDesc> qbase;                  // their descriptors (const_base into consts)
+  uint64_t qsa_gen = ~0ull;                  // models_gen of the current translation
+  bool qsa_live = false;                     // the translation succeeded for every tape
+  int q_count[2] = {0, 0}, q_temps[2] = {0, 0};
+  DevBuf qdescs, qprog, qargs[2];
+  QArgs qargs_dev_copy[2];   // what qargs[k] currently holds on the device
+  bool qargs_valid[2] = {false, false};
   // batch-level hoisting: column programs evaluated once per model before the tapes, one
   // launch per (nesting level, kernel variant); GDesc.tape = the model variable written
   struct ColumnLevel {
@@ -154,6 +164,16 @@ int mq_tape_compile_info(const mq_tape_batch* tb, int32_t t, int32_t* supported,
   return MQ_OK;
 }
 
+int mq_tape_program(const mq_tape_batch* tb, int32_t t, uint32_t* words, int32_t cap, int32_t* n_words) {
+  if (!tb || t < 0 || t >= tb->n_tapes || !n_words) return MQ_ERR_ARG;
+  CompileLimits lim;
+  CompiledTape c = compile_tape(tb, t, lim);
+  if (!c.supported) return MQ_ERR_TAPE;
+  *n_words = (int32_t)c.prog.size();
+  if (words && cap >= (int32_t)c.prog.size()) std::memcpy(words, c.prog.data(), c.prog.size() * sizeof(uint32_t));
+  return MQ_OK;
+}
+
 const char* mq_strerror(int code) {
   switch (code) {
     case MQ_OK: return "ok";
@@ -168,28 +188,30 @@ const char* mq_strerror(int code) {
   }
 }
 
-// Read back the byte offset of every handler of the assembly interpreter (kernel mode 2).
+// Read back the byte offset of every handler of the assembly interpreters (kernel mode 2).
 static int qsa_init(mq_ctx* c) {
-  for (int k = 0; k < QK_COUNT; k++)
-    for (int d = 0; d < kQsaStack; d++)
-      for (int v = 0; v <= kQsaVars; v++) c->qsa_index[k][d][v] = -1;
-  for (int h = 0; h < kQsaHandlers; h++) {
-    const QsaHandlerKey& key = kQsaHandlerKeys[h];
-    c->qsa_index[key.kind][key.d < 0 ? 0 : key.d][key.v + 1] = h;
-  }
-  DevBuf table;
-  HIPCHK(table.ensure(sizeof(uint32_t) * kQsaHandlers));
-  HIPCHK(hipMemsetAsync(table.p, 0xFF, sizeof(uint32_t) * kQsaHandlers, c->stream));
-  QArgs qa{};
-  qa.table_out = table.as<uint32_t>();
-  qa.mode = 2;
-  HIPCHK(c->qsa_args.upload(&qa, 1, c->stream));
-  HIPCHK(launch_qsa(c->qsa_args.as<QArgs>(), 1, 1, 0, c->stream));
-  c->qsa_off.resize(kQsaHandlers);
-  HIPCHK(hipMemcpyAsync(c->qsa_off.data(), table.p, sizeof(uint32_t) * kQsaHandlers, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
   bool ok = true;
-  for (int h = 0; h < kQsaHandlers; h++) ok = ok && c->qsa_off[h] != 0xFFFFFFFFu && (c->qsa_off[h] & 3) == 0 && c->qsa_off[h] < (1u << 18);
+  for (int k = 0; k < 2; k++) {
+    const int nh = k == 0 ? kQsaHandlersP : kQsaHandlersG;
+    const QsaHandlerKey* keys = k == 0 ? kQsaHandlerKeysP : kQsaHandlerKeysG;
+    for (int q = 0; q < QK_COUNT; q++)
+      for (int d = 0; d < kQsaStack; d++)
+        for (int v = 0; v <= kQsaSel; v++) c->qsa_index[k][q][d][v] = -1;
+    for (int h = 0; h < nh; h++) c->qsa_index[k][keys[h].kind][keys[h].d < 0 ? 0 : keys[h].d][keys[h].v + 1] = h;
+    DevBuf table;
+    HIPCHK(table.ensure(sizeof(uint32_t) * nh));
+    HIPCHK(hipMemsetAsync(table.p, 0xFF, sizeof(uint32_t) * nh, c->stream));
+    QArgs qa{};
+    qa.table_out = table.as<uint32_t>();
+    qa.mode = 2;
+    HIPCHK(c->qsa_args.upload(&qa, 1, c->stream));
+    HIPCHK(launch_qsa(k, c->qsa_args.as<QArgs>(), 1, 1, 0, c->stream));
+    c->qsa_off[k].resize(nh);
+    HIPCHK(hipMemcpyAsync(c->qsa_off[k].data(), table.p, sizeof(uint32_t) * nh, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (int h = 0; h < nh; h++)
+      ok = ok && c->qsa_off[k][h] != 0xFFFFFFFFu && (c->qsa_off[k][h] & 3) == 0 && c->qsa_off[k][h] < (1u << 18);
+  }
   c->qsa_ready = ok && std::getenv("MQ_DISABLE_QSA") == nullptr;
   return MQ_OK;
 }
@@ -305,17 +327,18 @@ int mq_models_upload(mq_ctx* c, const mq_model_batch* mb) {
       HIPCHK(launch_mask_rows(c->vars.as<uint32_t>(), c->rowmask.as<uint32_t>(), rows, M, c->stream));
     }
   }
-  c->qsa_models_ok = true;
+  // P kernel preload rows: var v < 8, limb l (the zero row where absent; a variable wider
+  // than 256 bits is never preloaded: the translator sends its tapes to the G kernel)
   for (int v = 0; v < 8; v++)
     for (int l = 0; l < 8; l++) {
       uint32_t row = (uint32_t)rows;  // zero row
-      if (v < mb->n_vars) {
-        if (mb->var_width[v] > 256) c->qsa_models_ok = false;
-        if ((uint32_t)l < vnl[v]) row = voff[v] + l;
-      }
+      if (v < mb->n_vars && mb->var_width[v] <= 256 && (uint32_t)l < vnl[v]) row = voff[v] + l;
       c->qsa_var_row[8 * v + l] = row;
     }
-  if ((rows + 1) * M * 4 > (int64_t)0xFFFFFFFFLL * 4) c->qsa_models_ok = false;
+  c->var_off_h.assign(voff.begin(), voff.begin() + mb->n_vars);
+  c->var_nl_h.assign(vnl.begin(), vnl.begin() + mb->n_vars);
+  c->funcs_h.assign(mb->funcs, mb->funcs + F);
+  c->models_gen++;
   HIPCHK(c->var_off.upload(voff.data(), voff.size(), c->stream));
   HIPCHK(c->var_nl.upload(vnl.data(), vnl.size(), c->stream));
   HIPCHK(c->funcs.upload(fd.data(), fd.size(), c->stream));
@@ -339,26 +362,81 @@ int mq_models_upload(mq_ctx* c, const mq_model_batch* mb) {
   return MQ_OK;
 }
 
-// Translate a compiled stack program into QSA threaded code; false if any instruction is
-// outside the assembly interpreter's set (those tapes run on the HIP C++ kernel).
-static bool qsa_translate(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_t>& out) {
+// Translate a compiled stack program into QSA threaded code for kernel k (0 = P, 1 = G).
+// models == false: structural check only (upload time: variable rows and function tables are
+// not known yet, any variable / lookup is assumed expressible).  extra: the tape's derived
+// constants (divisor reciprocals), appended after its own constants in the same order every
+// time.  Returns false if any instruction is outside the interpreter's set (those tapes run on
+// the HIP C++ kernel).
+static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTape& x, std::vector<uint32_t>* out_p,
+                          std::vector<uint32_t>* extra_p) {
+  std::vector<uint32_t> dummy_out, dummy_extra;
+  std::vector<uint32_t>& out = out_p ? *out_p : dummy_out;
+  std::vector<uint32_t>& extra = extra_p ? *extra_p : dummy_extra;
   out.clear();
+  extra.clear();
   if (x.L != 8 || x.depth > kQsaStack) return false;
+  const bool P = k == 0;
   auto word = [&](int kind, int d, int v, uint32_t imm) -> bool {
-    if (d < 0 || d >= kQsaStack || v < -1 || v >= kQsaVars || imm > 0xFFFFu) return false;
-    const int h = c->qsa_index[kind][d][v + 1];
+    if (d < 0 || d >= kQsaStack || v < -1 || v >= kQsaSel || imm > 0xFFFFu) return false;
+    const int h = c->qsa_index[k][kind][d][v + 1];
     if (h < 0) return false;
-    out.push_back((c->qsa_off[h] >> 2) | (imm << 16));
+    out.push_back((c->qsa_off[k][h] >> 2) | (imm << 16));
     return true;
   };
+  // slot d holds a value of width W < 256: clear the bits above W
+  auto mask = [&](int d, uint32_t W) -> bool {
+    if (W >= 256) return true;
+    const int n = (int)(W + 31) / 32;
+    if (W % 32) return word(QK_MASKP, d, n - 1, W % 32);
+    return word(QK_MASKZ, d, n - 1, 0);
+  };
+  auto lshr = [&](int d, uint32_t kbits, bool arith) -> bool {
+    if (kbits == 0) return true;
+    return word(arith ? QK_ASHRI : QK_LSHRI, d, (int)(kbits >> 5), kbits & 31);
+  };
+  auto shl = [&](int d, uint32_t kbits) -> bool {
+    if (kbits == 0) return true;
+    if (kbits & 31) return word(QK_SHLI, d, (int)(kbits >> 5), 32 - (kbits & 31));
+    return word(QK_SHLW, d, (int)(kbits >> 5), 0);
+  };
+  // the constant pushed by the previous instruction (the right operand of a shift / division)
+  auto const_value = [&](uint32_t off, uint32_t (&v)[8]) -> bool {
+    if ((size_t)off + 8 > x.consts.size()) return false;
+    for (int l = 0; l < 8; l++) v[l] = x.consts[off + l];
+    return true;
+  };
+  uint32_t prev_op = G_END, prev_d = 0, prev_imm = 0;
+  size_t prev_out = 0;
   for (size_t pc = 0; pc < x.prog.size(); pc++) {
     const uint32_t w = x.prog[pc];
     const uint32_t op = w & 0xFFu, imm = w >> 12;
     const int d = (int)((w >> 8) & 0xFu);
+    uint32_t imm2 = 0;
+    if (op == G_EXTRACT || op == G_CONCAT || op == G_SEXT || op == G_UF1 || op == G_UF2) {
+      if (++pc >= x.prog.size()) return false;
+      imm2 = x.prog[pc];
+    }
+    const size_t out_before = out.size();
+    const bool after_const = prev_op == G_PUSH_CONST && (int)prev_d == d;
     bool ok;
     switch (op) {
       case G_END: ok = word(QK_END, 0, -1, 0); break;
-      case G_PUSH_VAR: ok = imm < (uint32_t)kQsaVars && word(QK_PUSH_VAR, d, (int)imm, 0); break;
+      case G_PUSH_VAR:
+      case G_PUSH_VAR_B: {
+        const bool b = op == G_PUSH_VAR_B;
+        if (P) {
+          // preloaded variables only (var < 8, at most 256 bits)
+          ok = imm < (uint32_t)kQsaVars && (!models || (imm < c->var_nl_h.size() && c->var_nl_h[imm] <= 8)) &&
+               word(b ? QK_PUSH_VARB : QK_PUSH_VAR, d, b ? (int)imm : (int)imm, 0);
+        } else if (!models) {
+          ok = word(b ? QK_PUSH_MEMB : QK_PUSH_MEM, d, b ? -1 : 7, 0);
+        } else {
+          ok = imm < c->var_off_h.size() && c->var_nl_h[imm] <= 8 && c->var_off_h[imm] <= 0xFFFFu &&
+               word(b ? QK_PUSH_MEMB : QK_PUSH_MEM, d, b ? -1 : (int)c->var_nl_h[imm] - 1, c->var_off_h[imm]);
+        }
+        break;
+      }
       case G_PUSH_CONST: ok = word(QK_PUSH_CONST, d, -1, imm); break;
       case G_PUSH_TMP: ok = word(QK_PUSH_TMP, d, -1, imm); break;
       case G_PUSH_TMP_B: ok = word(QK_PUSH_TMP_BOOL, d, -1, imm); break;
@@ -372,33 +450,140 @@ static bool qsa_translate(const mq_ctx* c, const CompiledTape& x, std::vector<ui
       case G_IFF: ok = word(QK_IFF, d, -1, 0); break;
       case G_IMPLIES: ok = word(QK_IMPLIES, d, -1, 0); break;
       case G_BITE: ok = word(QK_BITE, d, -1, 0); break;
+      case G_BITE_EF: ok = word(QK_BITE_EF, d, -1, 0); break;
       // unsigned predicates / bitwise / ite are exact on canonical values of any width <= 256
-      case G_EQ: ok = word(QK_EQ, d, -1, 0); break;
-      case G_ULT: ok = word(QK_ULT, d, -1, 0); break;
-      case G_ULE: ok = word(QK_ULE, d, -1, 0); break;
-      case G_UGT: ok = word(QK_UGT, d, -1, 0); break;
-      case G_UGE: ok = word(QK_UGE, d, -1, 0); break;
+      case G_EQ: ok = imm >= 1 && word(QK_EQ, d, -1, 0); break;
+      case G_ULT: ok = imm >= 1 && word(QK_ULT, d, -1, 0); break;
+      case G_ULE: ok = imm >= 1 && word(QK_ULE, d, -1, 0); break;
+      case G_UGT: ok = imm >= 1 && word(QK_UGT, d, -1, 0); break;
+      case G_UGE: ok = imm >= 1 && word(QK_UGE, d, -1, 0); break;
       case G_BAND: ok = word(QK_BAND, d, -1, 0); break;
       case G_BOR: ok = word(QK_BOR, d, -1, 0); break;
       case G_BXOR: ok = word(QK_BXOR, d, -1, 0); break;
       case G_ITE: ok = word(QK_ITE, d, -1, 0); break;
       case G_ITE_EF: ok = word(QK_ITE_EF, d, -1, 0); break;
-      case G_BITE_EF: ok = word(QK_BITE_EF, d, -1, 0); break;
-      // signed predicates and wrapping arithmetic: full 256-bit width only (no masking)
-      case G_SLT: ok = imm == 256 && word(QK_SLT, d, -1, 0); break;
-      case G_SLE: ok = imm == 256 && word(QK_SLE, d, -1, 0); break;
-      case G_SGT: ok = imm == 256 && word(QK_SGT, d, -1, 0); break;
-      case G_SGE: ok = imm == 256 && word(QK_SGE, d, -1, 0); break;
-      case G_ADD: ok = imm == 256 && word(QK_ADD, d, -1, 0); break;
-      case G_SUB: ok = imm == 256 && word(QK_SUB, d, -1, 0); break;
-      case G_MUL: ok = imm == 256 && word(QK_MUL, d, -1, 0); break;
-      case G_NEG: ok = imm == 256 && word(QK_NEG, d, -1, 0); break;
-      case G_BNOT: ok = imm == 256 && word(QK_BNOT, d, -1, 0); break;
+      // signed predicates: at 256 bits the handler flips bit 255; below, flip bit W-1 of both
+      // operands (FLIP2) and compare unsigned
+      case G_SLT: case G_SLE: case G_SGT: case G_SGE: {
+        const int su = op == G_SLT ? QK_SLT : op == G_SLE ? QK_SLE : op == G_SGT ? QK_SGT : QK_SGE;
+        const int uu = op == G_SLT ? QK_ULT : op == G_SLE ? QK_ULE : op == G_SGT ? QK_UGT : QK_UGE;
+        if (imm == 256) ok = word(su, d, -1, 0);
+        else ok = imm >= 1 && imm < 256 && word(QK_FLIP2, d, (int)((imm - 1) >> 5), (imm - 1) & 31) && word(uu, d, -1, 0);
+        break;
+      }
+      // wrapping arithmetic: 256-bit handlers, results below 256 bits re-masked
+      case G_ADD: ok = imm <= 256 && word(QK_ADD, d, -1, 0) && mask(d - 1, imm); break;
+      case G_SUB: ok = imm <= 256 && word(QK_SUB, d, -1, 0) && mask(d - 1, imm); break;
+      case G_MUL: ok = imm <= 256 && word(QK_MUL, d, -1, 0) && mask(d - 1, imm); break;
+      case G_NEG: ok = imm <= 256 && word(QK_NEG, d, -1, 0) && mask(d, imm); break;
+      case G_BNOT: ok = imm <= 256 && word(QK_BNOT, d, -1, 0) && mask(d, imm); break;
+      // shifts by a constant amount (the previous instruction pushed it): in place on slot d-1
+      case G_SHL: case G_LSHR: case G_ASHR: {
+        uint32_t cv[8];
+        ok = after_const && d >= 1 && imm >= 1 && imm <= 256 && const_value(prev_imm, cv);
+        if (!ok) break;
+        out.resize(prev_out);  // drop the amount push
+        bool big = false;
+        for (int l = 1; l < 8; l++) big = big || cv[l] != 0;
+        const uint32_t kb = big || cv[0] >= imm ? imm : cv[0];  // >= width: everything shifted out
+        if (op == G_ASHR) {
+          ok = imm == 256 && lshr(d - 1, std::min<uint32_t>(kb, 255), true);
+        } else if (kb >= imm) {
+          ok = word(QK_MASKP, d - 1, 0, 0);  // zero
+        } else if (op == G_LSHR) {
+          ok = lshr(d - 1, kb, false);
+        } else {
+          ok = shl(d - 1, kb) && mask(d - 1, imm);
+        }
+        break;
+      }
+      // division by a constant divisor (the previous instruction pushed it), in place on d-1
+      case G_UDIV: case G_UREM: case G_SDIV: case G_SREM: case G_SMOD: {
+        uint32_t cv[8];
+        ok = after_const && d >= 1 && imm >= 1 && imm <= 256 && const_value(prev_imm, cv);
+        if (!ok) break;
+        const bool sgn = op == G_SDIV || op == G_SREM || op == G_SMOD;
+        bool neg = false;
+        if (sgn) {
+          if (imm != 256) { ok = false; break; }
+          neg = (cv[7] >> 31) != 0;
+          if (neg) {  // |c| = -c
+            uint64_t br = 1;
+            for (int l = 0; l < 8; l++) {
+              const uint64_t t = (uint64_t)(uint32_t)~cv[l] + br;
+              cv[l] = (uint32_t)t;
+              br = t >> 32;
+            }
+          }
+        }
+        bool hi = false;
+        for (int l = 1; l < 8; l++) hi = hi || cv[l] != 0;
+        out.resize(prev_out);  // drop the divisor push
+        if (!sgn && !hi && cv[0] != 0 && (cv[0] & (cv[0] - 1)) == 0) {
+          // unsigned power of two: shift / mask
+          const uint32_t kb = (uint32_t)__builtin_ctz(cv[0]);
+          ok = op == G_UDIV ? lshr(d - 1, kb, false)
+                            : (kb == 0 ? word(QK_MASKP, d - 1, 0, 0) : mask(d - 1, kb));
+          break;
+        }
+        if (hi || cv[0] == 0) { ok = false; break; }
+        const uint32_t cabs = cv[0];
+        const uint32_t sh = (uint32_t)__builtin_clz(cabs);
+        const uint32_t dn = cabs << sh;
+        const uint64_t inv = ~0ull / dn - (1ull << 32);
+        const uint32_t off = (uint32_t)(x.consts.size() + extra.size());
+        extra.push_back(dn);
+        extra.push_back((uint32_t)inv);
+        extra.push_back(sh);
+        extra.push_back(cabs);
+        int kind;
+        switch (op) {
+          case G_UDIV: kind = QK_UDIVC; break;
+          case G_UREM: kind = QK_UREMC; break;
+          case G_SREM: kind = QK_SREMC; break;
+          case G_SMOD: kind = neg ? QK_SMODCN : QK_SMODCP; break;
+          default: kind = neg ? QK_SDIVCN : QK_SDIVCP; break;
+        }
+        ok = word(kind, d - 1, -1, off);
+        break;
+      }
+      case G_EXTRACT:  // imm = lo, imm2 = result width
+        ok = imm < 256 && imm2 >= 1 && imm2 <= 256 && lshr(d, imm, false) && mask(d, imm2);
+        break;
+      case G_CONCAT:  // imm = width of the low operand (slot d), imm2 = result width
+        ok = imm >= 1 && imm < 256 && imm2 <= 256 && shl(d - 1, imm) && word(QK_BOR, d, -1, 0);
+        break;
+      case G_SEXT: {  // imm = source width, imm2 = result width
+        ok = imm >= 1 && imm <= 256 && imm2 <= 256;
+        if (!ok) break;
+        const int p = (int)((imm - 1) >> 5);
+        const uint32_t nb = ((imm - 1) & 31) + 1;
+        if (nb < 32) ok = word(QK_SEXTB, d, p, nb);
+        else if (p < 7) ok = word(QK_SEXTA, d, p, 0);
+        ok = ok && mask(d, imm2);
+        break;
+      }
+      case G_UF1: {  // imm = function id, imm2 = result width (0 = Bool)
+        ok = !P && imm2 <= 256;
+        if (ok && models) {
+          // a function absent from the model batch evaluates to 0 (as in the C++ kernel)
+          ok = imm >= c->funcs_h.size() || (c->funcs_h[imm].arity == 1 && c->funcs_h[imm].arg_width[0] <= 256 &&
+                                            c->funcs_h[imm].result_width <= 256);
+        }
+        if (!ok) break;
+        if (imm2 == 0) ok = word(QK_UF1B, d, -1, imm);
+        else ok = word(QK_UF1, d, -1, imm) && mask(d, imm2);
+        break;
+      }
       default: ok = false;
     }
     if (!ok) return false;
+    prev_op = op;
+    prev_d = (uint32_t)d;
+    prev_imm = imm;
+    prev_out = out_before;
   }
-  return true;
+  return x.consts.size() + extra.size() <= 0x10000u;
 }
 
 int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t* n_unsup_out) {
@@ -420,9 +605,8 @@ int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t*
 #pragma omp parallel for schedule(dynamic, 64)
   for (int t = 0; t < tb->n_tapes; t++) ct[t] = compile_tape(tb, t, lim);
   // descriptor groups: [L8 QSA-eligible | L8 other | L16] (see mq_tapes)
-  std::vector<uint32_t> prog, consts, qprog;
-  std::vector<GDesc> descs, qdescs;
-  std::vector<uint32_t> qwords;
+  std::vector<uint32_t> prog, consts;
+  std::vector<GDesc> descs;
   auto push_desc = [&](int t, const CompiledTape& x) {
     GDesc d{};
     d.prog_off = (uint32_t)prog.size();
@@ -438,12 +622,14 @@ int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t*
     descs.push_back(d);
     return d;
   };
+  // QSA eligibility is structural here (G kernel set, no model information); the derived
+  // constants of an eligible tape (divisor reciprocals) follow its own constants in the pool
   std::vector<char> qsa_ok(tb->n_tapes, 0);
-  std::vector<std::vector<uint32_t>> qtr(tb->n_tapes);
+  std::vector<std::vector<uint32_t>> qextra(tb->n_tapes);
   if (c->qsa_ready)
     for (int t = 0; t < tb->n_tapes; t++)
       if (ct[t].supported && ct[t].L == 8 && ct[t].n_temps <= kQsaMaxTemps)
-        qsa_ok[t] = qsa_translate(c, ct[t], qtr[t]) ? 1 : 0;
+        qsa_ok[t] = qsa_translate(c, 1, false, ct[t], nullptr, &qextra[t]) ? 1 : 0;
   T->qsa.begin = 0;
   for (int pass = 0; pass < 4; pass++) {
     mq_tapes::Variant& v = pass == 0 ? T->qsa : (pass == 1 ? T->l8_rest : (pass == 2 ? T->l16 : T->l16k));
@@ -459,10 +645,9 @@ int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t*
       if (pass == 3 && !x.keccak) continue;
       GDesc d = push_desc(t, x);
       if (pass == 0) {
-        d.prog_off = (uint32_t)qprog.size();
-        d.prog_len = (uint32_t)qtr[t].size();
-        qprog.insert(qprog.end(), qtr[t].begin(), qtr[t].end());
-        qdescs.push_back(d);
+        consts.insert(consts.end(), qextra[t].begin(), qextra[t].end());
+        T->qbase.push_back(d);
+        T->qct.push_back(x);
       }
       v.max_temps = std::max(v.max_temps, x.n_temps);
       v.max_depth = std::max(v.max_depth, x.depth);
@@ -474,9 +659,6 @@ int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t*
   T->l8_all.count = T->qsa.count + T->l8_rest.count;
   T->l8_all.max_temps = std::max(T->qsa.max_temps, T->l8_rest.max_temps);
   T->l8_all.max_depth = std::max(T->qsa.max_depth, T->l8_rest.max_depth);
-  // trailing END words: the dispatch tail prefetches one word past each program's END
-  qprog.push_back(c->qsa_ready ? c->qsa_off[c->qsa_index[QK_END][0][0]] / 4 : 0);
-  qprog.push_back(qprog.back());
   consts.resize(consts.size() + 16, 0);
   prog.push_back(gword(G_END, 0, 0));
   for (int t = 0; t < tb->n_tapes; t++) {
@@ -486,11 +668,9 @@ int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t*
     T->alg_ops[t] = ct[t].alg_ops;
   }
   if (descs.empty()) descs.push_back(GDesc{});
-  if (qdescs.empty()) qdescs.push_back(GDesc{});
   HIPCHK(T->descs.upload(descs.data(), descs.size(), c->stream));
-  HIPCHK(T->qdescs.upload(qdescs.data(), qdescs.size(), c->stream));
-  HIPCHK(T->qprog.upload(qprog.data(), qprog.size(), c->stream));
-  HIPCHK(T->qargs.ensure(sizeof(QArgs)));
+  HIPCHK(T->qargs[0].ensure(sizeof(QArgs)));
+  HIPCHK(T->qargs[1].ensure(sizeof(QArgs)));
   HIPCHK(T->prog.upload(prog.data(), prog.size(), c->stream));
   HIPCHK(T->consts.upload(consts.data(), consts.size(), c->stream));
   HIPCHK(T->unsup_dev.upload(T->unsupported.data(), T->unsupported.size(), c->stream));
@@ -618,11 +798,65 @@ static KArgs make_col_args(mq_ctx* c, mq_tapes* T, const mq_tapes::Variant& v) {
   return a;
 }
 
+// (Re)translate the QSA-eligible tapes for the current model batch (variable rows, function
+// table): the P kernel when every variable a tape reads is preloaded, the G kernel otherwise.
+// If one tape does not translate, the whole group runs on the HIP C++ kernel for this batch.
+static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
+  if (T->qsa_gen == c->models_gen) return MQ_OK;
+  T->qsa_gen = c->models_gen;
+  T->qsa_live = false;
+  std::vector<uint32_t> words[2], tr, extra;
+  std::vector<GDesc> ds[2];
+  int temps[2] = {0, 0};
+  for (size_t i = 0; i < T->qct.size(); i++) {
+    int k = 0;
+    if (!qsa_translate(c, 0, true, T->qct[i], &tr, &extra)) {
+      k = 1;
+      if (!qsa_translate(c, 1, true, T->qct[i], &tr, &extra)) return MQ_OK;
+    }
+    GDesc d = T->qbase[i];
+    d.prog_off = (uint32_t)words[k].size();
+    d.prog_len = (uint32_t)tr.size();
+    words[k].insert(words[k].end(), tr.begin(), tr.end());
+    ds[k].push_back(d);
+    temps[k] = std::max(temps[k], T->qct[i].n_temps);
+  }
+  // [P programs | END END | G programs | END END]: the dispatch tail prefetches one word past
+  // each program's END
+  std::vector<uint32_t> prog;
+  std::vector<GDesc> descs;
+  for (int k = 0; k < 2; k++) {
+    const uint32_t base = (uint32_t)prog.size();
+    for (GDesc d : ds[k]) {
+      d.prog_off += base;
+      descs.push_back(d);
+    }
+    prog.insert(prog.end(), words[k].begin(), words[k].end());
+    const uint32_t endw = c->qsa_off[k][c->qsa_index[k][QK_END][0][0]] / 4;
+    prog.push_back(endw);
+    prog.push_back(endw);
+    T->q_count[k] = (int)ds[k].size();
+    T->q_temps[k] = temps[k];
+  }
+  if (descs.empty()) descs.push_back(GDesc{});
+  HIPCHK(T->qdescs.upload(descs.data(), descs.size(), c->stream));
+  HIPCHK(T->qprog.upload(prog.data(), prog.size(), c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  T->qargs_valid[0] = T->qargs_valid[1] = false;
+  T->qsa_live = true;
+  return MQ_OK;
+}
+
 // Launch every evaluation kernel for a compiled batch: the assembly interpreter for the
 // QSA-eligible tapes (when the model batch fits its register file), the HIP C++ kernels for
 // the rest.  verdicts == nullptr -> first-hit mode into best.
 static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, hipStream_t st) {
-  const bool use_qsa = c->qsa_ready && c->use_asm && c->qsa_models_ok && T->qsa.count > 0;
+  bool use_qsa = c->qsa_ready && c->use_asm && T->qsa.count > 0;
+  if (use_qsa) {
+    const int rc = qsa_prepare(c, T);
+    if (rc) return rc;
+    use_qsa = T->qsa_live;
+  }
   std::vector<mq_tapes::Variant> cpp;
   if (use_qsa) cpp = {T->l8_rest, T->l16, T->l16k};
   else cpp = {T->l8_all, T->l16, T->l16k};
@@ -666,18 +900,15 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       HIPCHK(launch_columns(a, v->L, v->keccak, st));
     }
   }
-  if (use_qsa) {
-    KArgs k = make_args(c, T, T->qsa);
-    // the assembly interpreter's grid is (256-model tiles) x (tape groups): size the groups for
-    // ~8k workgroups with ITS tile count (make_args sizes them for the 64-model C++ tiles)
-    {
-      const int64_t tiles256 = (c->M + 255) / 256;
-      int64_t tpg = (int64_t(T->qsa.count) * tiles256 + 8191) / 8192;
-      k.tapes_per_group = (int)std::max<int64_t>(1, std::min<int64_t>(tpg, T->qsa.count));
-    }
-    QArgs& q = T->qargs_host;
-    q = QArgs{};
-    q.descs = T->qdescs.p;
+  for (int k = 0; use_qsa && k < 2; k++) {
+    const int n = T->q_count[k];
+    if (n <= 0) continue;
+    // grid = (256-model tiles) x (tape groups), groups sized for ~8k workgroups
+    const int64_t tiles256 = (c->M + 255) / 256;
+    int64_t tpg = (int64_t(n) * tiles256 + 8191) / 8192;
+    tpg = std::max<int64_t>(1, std::min<int64_t>(tpg, n));
+    QArgs q{};
+    q.descs = T->qdescs.as<GDesc>() + (k == 0 ? 0 : T->q_count[0]);
     q.prog = T->qprog.p;
     q.consts = T->consts.p;
     q.vars = c->vars.p;
@@ -686,23 +917,28 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     q.verdicts = verdicts;
     q.M = (uint32_t)c->M;
     q.index_base = (uint32_t)c->index_base;
-    q.n_desc = (uint32_t)T->qsa.count;
-    q.tapes_per_group = (uint32_t)k.tapes_per_group;
+    q.n_desc = (uint32_t)n;
+    q.tapes_per_group = (uint32_t)tpg;
     q.early_exit = verdicts ? 0u : (uint32_t)c->early_exit;
     q.mode = verdicts ? 1u : 0u;
-    q.lds_wave_bytes = (uint32_t)T->qsa.max_temps * 2048u;
+    q.lds_wave_bytes = (uint32_t)T->q_temps[k] * 2048u;
     std::memcpy(q.var_row, c->qsa_var_row, sizeof(q.var_row));
+    q.funcs = c->funcs.p;
+    q.entry_ptr = c->entry_ptr.p;
+    q.entry_words = c->entry_words.p;
+    q.else_words = c->else_words.p;
+    q.n_funcs = (uint32_t)c->n_funcs;
     // the argument block only changes with the output buffer / mode / models: re-upload then
-    if (!T->qargs_valid || std::memcmp(&T->qargs_dev_copy, &q, sizeof(QArgs)) != 0) {
-      HIPCHK(hipMemcpyAsync(T->qargs.p, &q, sizeof(QArgs), hipMemcpyHostToDevice, st));
-      HIPCHK(hipStreamSynchronize(st));  // q is host memory that changes on the next call
-      T->qargs_dev_copy = q;
-      T->qargs_valid = true;
+    if (!T->qargs_valid[k] || std::memcmp(&T->qargs_dev_copy[k], &q, sizeof(QArgs)) != 0) {
+      HIPCHK(hipMemcpyAsync(T->qargs[k].p, &q, sizeof(QArgs), hipMemcpyHostToDevice, st));
+      HIPCHK(hipStreamSynchronize(st));  // q is host memory
+      T->qargs_dev_copy[k] = q;
+      T->qargs_valid[k] = true;
     }
-    const unsigned gx = (unsigned)((c->M + 255) / 256);
-    const unsigned gy = (unsigned)((T->qsa.count + k.tapes_per_group - 1) / k.tapes_per_group);
+    const unsigned gx = (unsigned)tiles256;
+    const unsigned gy = (unsigned)((n + tpg - 1) / tpg);
     HIPCHK(start_timer());
-    HIPCHK(launch_qsa(T->qargs.as<QArgs>(), gx, gy, (size_t)q.lds_wave_bytes * 4, st));
+    HIPCHK(launch_qsa(k, T->qargs[k].as<QArgs>(), gx, gy, (size_t)q.lds_wave_bytes * 4, st));
   }
   for (const auto& v : cpp) {
     if (v.count <= 0) continue;
@@ -869,6 +1105,14 @@ int mq_ctx_set_option(mq_ctx* c, int option, int value) {
       return MQ_OK;
     default: return MQ_ERR_ARG;
   }
+}
+
+int mq_tapes_qsa_split(mq_tapes* T, int32_t* n_p, int32_t* n_g, int32_t* live) {
+  if (!T) return MQ_ERR_ARG;
+  if (n_p) *n_p = T->qsa_live ? T->q_count[0] : 0;
+  if (n_g) *n_g = T->qsa_live ? T->q_count[1] : 0;
+  if (live) *live = T->qsa_live ? 1 : 0;
+  return MQ_OK;
 }
 
 int mq_tapes_info(mq_tapes* T, int32_t* n_asm, int32_t* n_generic_l8, int32_t* n_generic_l16) {

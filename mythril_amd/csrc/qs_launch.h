@@ -71,12 +71,21 @@ struct QArgs {
   uint32_t lds_wave_bytes;       // 0x58
   uint32_t pad;                  // 0x5c
   uint32_t var_row[64];          // 0x60: limb row of var v limb l (v < 8), or the zero row
+  const void* funcs;             // 0x160 FuncDev[] (G kernel: UF1 lookups)
+  const void* entry_ptr;         // 0x168
+  const void* entry_words;       // 0x170
+  const void* else_words;        // 0x178
+  uint32_t n_funcs;              // 0x180
+  uint32_t pad2[3];
 };
 static_assert(sizeof(void*) == 8, "64-bit");
 static_assert(__builtin_offsetof(QArgs, M) == 0x40, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, var_row) == 0x60, "QArgs layout");
+static_assert(__builtin_offsetof(QArgs, funcs) == 0x160, "QArgs layout");
+static_assert(__builtin_offsetof(QArgs, n_funcs) == 0x180, "QArgs layout");
 
-hipError_t launch_qsa(const QArgs* d_args, unsigned gx, unsigned gy, size_t lds, hipStream_t st);
+// variant 0 = P (preloaded variables, qsa_kernel), 1 = G (general, qsg_kernel)
+hipError_t launch_qsa(int variant, const QArgs* d_args, unsigned gx, unsigned gy, size_t lds, hipStream_t st);
 hipError_t launch_qs(const KArgs& a, int L, bool keccak, bool verdict, hipStream_t st);
 hipError_t launch_columns(const KArgs& a, int L, bool keccak, hipStream_t st);
 hipError_t launch_init_best(int32_t* best, int n, hipStream_t st);

@@ -1,7 +1,9 @@
-// qsa.hip — the gfx950 threaded-code tape interpreter (generated assembly, gen_qsa.py) wrapped
-// in a HIP kernel so it ships in libmq.so's fat binary and launches like any HIP kernel.
+// qsa.hip — the gfx950 threaded-code tape interpreters (generated assembly, gen_qsa.py) wrapped
+// in HIP kernels so they ship in libmq.so's fat binary and launch like any HIP kernel.
 // One workgroup = 4 waves = 256 candidate models; grid.y = tape groups.  See gen_qsa.py for
-// the register map and the program encoding.
+// the register maps and the program encoding.
+//   qsa_kernel (P): the first 8 model variables preloaded in VGPRs (C2-shaped batches)
+//   qsg_kernel (G): variables pushed from HBM, model-function lookups (EVM-shaped batches)
 #include <hip/hip_runtime.h>
 
 #include "qs_launch.h"
@@ -10,14 +12,22 @@
 namespace mq {
 
 __global__ __launch_bounds__(256) void qsa_kernel(const QArgs* __restrict__ args) {
-  asm volatile(QSA_ASM_TEXT
+  asm volatile(QSA_ASM_TEXT_P
                :
                : "s"(args), "s"(blockIdx.x), "s"(blockIdx.y), "v"(threadIdx.x)
                : QSA_CLOBBERS);
 }
 
-hipError_t launch_qsa(const QArgs* d_args, unsigned gx, unsigned gy, size_t lds, hipStream_t st) {
-  hipLaunchKernelGGL(qsa_kernel, dim3(gx, gy), dim3(256), lds, st, d_args);
+__global__ __launch_bounds__(256) void qsg_kernel(const QArgs* __restrict__ args) {
+  asm volatile(QSA_ASM_TEXT_G
+               :
+               : "s"(args), "s"(blockIdx.x), "s"(blockIdx.y), "v"(threadIdx.x)
+               : QSA_CLOBBERS);
+}
+
+hipError_t launch_qsa(int variant, const QArgs* d_args, unsigned gx, unsigned gy, size_t lds, hipStream_t st) {
+  if (variant == 0) hipLaunchKernelGGL(qsa_kernel, dim3(gx, gy), dim3(256), lds, st, d_args);
+  else hipLaunchKernelGGL(qsg_kernel, dim3(gx, gy), dim3(256), lds, st, d_args);
   return hipGetLastError();
 }
 

@@ -59,6 +59,7 @@ def load_library(path: str = LIB_PATH):
         L.mq_ctx_set_option.argtypes = [P, C.c_int, C.c_int]
         L.mq_kernel_times.argtypes = [P, C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_int32), C.c_int]
         L.mq_tapes_info.argtypes = [P] + [C.POINTER(C.c_int32)] * 3
+        L.mq_tapes_qsa_split.argtypes = [P] + [C.POINTER(C.c_int32)] * 3
         L.mq_eval_verdicts.argtypes = [P, C.POINTER(MqTapeBatch), C.POINTER(C.c_uint8), C.POINTER(C.c_int32)]
         L.mq_eval_tapes_verdicts.argtypes = [P, P, C.POINTER(C.c_uint8), C.POINTER(C.c_int32)]
         L.mq_tapes_set_columns.argtypes = [P, C.POINTER(MqTapeBatch), C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_int32]
@@ -66,6 +67,7 @@ def load_library(path: str = LIB_PATH):
         L.mq_tape_alg_ops.argtypes = [C.POINTER(MqTapeBatch), C.c_int32]
         L.mq_tape_alg_ops.restype = C.c_double
         L.mq_tape_compile_info.argtypes = [C.POINTER(MqTapeBatch), C.c_int32] + [C.POINTER(C.c_int32)] * 5 + [C.c_char_p, C.c_int32]
+        L.mq_tape_program.argtypes = [C.POINTER(MqTapeBatch), C.c_int32, C.POINTER(C.c_uint32), C.c_int32, C.POINTER(C.c_int32)]
         _lib = L
         return L
 
@@ -106,6 +108,17 @@ def compile_info(tb: TapeBatch, t: int) -> CompileInfo:
     return CompileInfo(bool(vals[0].value), vals[1].value, vals[2].value, vals[3].value, vals[4].value, why.value.decode())
 
 
+def tape_program(tb: TapeBatch, t: int) -> np.ndarray:
+    """Host-only: the compiled stack program of tape t (gprog.h words), for inspection/tests."""
+    L = load_library()
+    s, keep = as_tape_batch(tb)
+    n = C.c_int32()
+    _check(L.mq_tape_program(C.byref(s), t, None, 0, C.byref(n)), "tape_program")
+    out = np.zeros(n.value, np.uint32)
+    _check(L.mq_tape_program(C.byref(s), t, out.ctypes.data_as(C.POINTER(C.c_uint32)), n.value, C.byref(n)), "tape_program")
+    return out
+
+
 def tape_alg_ops(tb: TapeBatch, t: int) -> float:
     s, keep = as_tape_batch(tb)
     return float(load_library().mq_tape_alg_ops(C.byref(s), t))
@@ -139,6 +152,13 @@ class CompiledTapes:
         a, b, c = C.c_int32(), C.c_int32(), C.c_int32()
         _check(self.ev.lib.mq_tapes_info(self.handle, C.byref(a), C.byref(b), C.byref(c)), "mq_tapes_info")
         return a.value, b.value, c.value
+
+    def asm_split(self):
+        """After a launch: (tapes on the preloaded-variable assembly kernel, on the general assembly
+        kernel, whether the assembly path ran for the current model batch)."""
+        a, b, c = C.c_int32(), C.c_int32(), C.c_int32()
+        _check(self.ev.lib.mq_tapes_qsa_split(self.handle, C.byref(a), C.byref(b), C.byref(c)), "mq_tapes_qsa_split")
+        return a.value, b.value, bool(c.value)
 
     def free(self) -> None:
         if self.handle:

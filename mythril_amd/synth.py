@@ -277,3 +277,76 @@ def fuzz_workload(seed: int, n_tapes: int, n_models: int, max_width: int = 256, 
     tapes = [fuzz_tape(rng, var_widths, funcs, depth, max_width, ops) for _ in range(n_tapes)]
     models = fuzz_models(rng, var_widths, n_models, funcs)
     return TapeBatch(tapes), models
+
+
+# ---------------------------------------------------------------- constant-operand fuzz (asm parity)
+CONST_OPS = (Op.UDIV, Op.UREM, Op.SDIV, Op.SREM, Op.SMOD, Op.SHL, Op.LSHR, Op.ASHR)
+
+
+def _const_operand(rng: np.random.Generator, op: Op, w: int) -> int:
+    m = (1 << w) - 1
+    r = rng.random()
+    if op in (Op.SHL, Op.LSHR, Op.ASHR):
+        return int(rng.choice([0, 1, 7, 8, 31, 32, 33, 63, 64, 100, 128, 224, 255, w - 1, w, w + 5])) & m if r < 0.9 \
+            else int(rng.integers(0, 1 << 16)) & m
+    if r < 0.25:
+        return (1 << int(rng.integers(0, w))) & m                          # powers of two
+    if r < 0.6:
+        v = int(rng.integers(1, 1 << min(w, 32)))                          # fits 32 bits
+        return v if rng.random() < 0.5 or w < 2 else (-v) & m              # negative for the signed ops
+    if r < 0.7:
+        return int(rng.choice([1, 3, 10, 0xFFFFFFFF, (1 << 31) + 1, m]))  & m
+    return interesting_value(rng, w)                                       # wide (C++ fallback)
+
+
+def const_op_workload(seed: int, n_tapes: int, n_models: int):
+    """Tapes dominated by shifts / divisions by constants, extract / concat / sign extension and
+    array lookups at widths 8..256 over a mix of preloaded (var < 8) and other variables: the
+    assembly interpreters' translated forms (gen_qsa.py), checked against the oracle."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    widths = (8, 32, 64, 160, 256)
+    var_widths = [256, 256, 64, 8, 256, 160, 32, 256] + [int(rng.choice(widths)) for _ in range(8)] + [BOOL, 256]
+    funcs = [FuncSpec(1, 256, (256,)), FuncSpec(1, 32, (160,)), FuncSpec(1, BOOL, (256,))]
+    tapes = []
+    for i in range(n_tapes):
+        t = Tape()
+        lo_vars = i % 3 == 0          # a third of the tapes read only variables 0..7
+        nv = 8 if lo_vars else len(var_widths) - 1
+
+        def var(w):
+            c = [v for v in range(nv) if var_widths[v] == w]
+            return t.var(int(rng.choice(c)), w) if c else t.const(interesting_value(rng, w), w)
+
+        w = int(rng.choice(widths))
+        x = var(w)
+        k = int(rng.integers(1, 4))
+        for _ in range(k):
+            op = CONST_OPS[int(rng.integers(len(CONST_OPS)))]
+            if w != 256 and op in (Op.SDIV, Op.SREM, Op.SMOD, Op.ASHR) and rng.random() < 0.7:
+                op = Op.UREM
+            c = t.const(_const_operand(rng, op, w), w)
+            x = t._bin(op, x, c)
+            if rng.random() < 0.3:
+                x = t.add(x, var(w))
+        r = rng.random()
+        if r < 0.2 and w >= 16:
+            hi = int(rng.integers(7, w))
+            lo = int(rng.integers(0, hi - 6))
+            x = t.extract(hi, lo, x)
+            w = hi - lo + 1
+        elif r < 0.35 and w <= 128:
+            x = t.concat(var(8), x) if rng.random() < 0.5 else t.concat(x, t.const(int(rng.integers(0, 256)), 8))
+            w = w + 8
+        elif r < 0.5 and w <= 160:
+            x = t.sext(256 - w, x)
+            w = 256
+        if not lo_vars and rng.random() < 0.3 and w == 256:
+            f = int(rng.integers(0, 3))
+            app = t.uf(f, funcs[f].result_width, x if f != 1 else t.extract(159, 0, x))
+            root = app if funcs[f].result_width == BOOL else t.ult(app, t.uf(0, 256, var(256)) if f == 0 else var(32))
+        else:
+            y = var(w)
+            cmp = [t.ult, t.ule, t.slt, t.eq][int(rng.integers(4))]
+            root = t.or_(cmp(x, y), t.eq(x, t.const(interesting_value(rng, w), w)))
+        tapes.append(t.finish(root))
+    return TapeBatch(tapes), fuzz_models(rng, var_widths, n_models, funcs)

@@ -386,3 +386,39 @@ def test_c4_hoisted_in_kernel_keccak(evaluator):
     fh = evaluator.first_hit(tb)
     ref, _ = cref.first_hit(plain[0], plain[1])
     assert (ref == exp).all() and (fh == ref).all()
+
+
+# ---------------------------------------------------------------- assembly interpreters: P and G kernels
+@pytest.mark.parametrize("seed", range(4))
+def test_asm_const_ops_and_lookups_match_oracle(evaluator, seed):
+    """Shifts / divisions by constants, extract / concat / sext, masks below 256 bits and array
+    lookups, translated to the P (preloaded variables) and G (general) assembly kernels."""
+    from mythril_amd.synth import const_op_workload
+    tb, mb = const_op_workload(700 + seed, 150, 700)
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    v, fh = evaluator.verdicts(ct)
+    n_p, n_g, live = ct.asm_split()
+    ref = cref.verdicts(tb, mb)
+    mism = np.argwhere(v != ref)
+    assert len(mism) == 0, f"{len(mism)} mismatches (P {n_p}, G {n_g}), first {mism[:5]}"
+    fh_ref, _ = cref.first_hit(tb, mb)
+    assert (evaluator.first_hit(ct) == fh_ref).all()
+    # wide divisors, variable shifts and signed ops below 256 bits stay on the HIP C++ kernel
+    assert live and n_p > 0 and n_g > 0 and n_p + n_g >= 0.4 * tb.n_tapes, (n_p, n_g, live)
+
+
+def test_c3_tapes_run_on_general_asm_kernel(evaluator):
+    from mythril_amd import synth_evm
+    tb, mb, exp, _ = synth_evm.c3_workload(60, 3000, seed=9, hoist=True)
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    fh = evaluator.first_hit(ct)
+    n_p, n_g, live = ct.asm_split()
+    assert live and n_p + n_g >= 0.8 * tb.n_tapes, (n_p, n_g, ct.split())
+    assert (fh == exp).all()
+    evaluator.use_asm(False)
+    try:
+        assert (evaluator.first_hit(ct) == exp).all()
+    finally:
+        evaluator.use_asm(True)
