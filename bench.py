@@ -42,13 +42,15 @@ WORKLOADS = {
            "random 256-bit models per GPU, seed 2, 10% planted", "mq::qsa_kernel (gfx950 threaded-code interpreter)"),
     "c3": (1_000, 1_000_000, 3, "C3 substitute: 10^3 EVM-shaped path conjunctions over 3 txs (calldata bytes/words, "
            "dispatch, SafeMath udiv/urem/smod, shifts, extract/concat/signext, balance table, storage store chains; "
-           "~1060 DAG nodes) x 10^6 models per GPU, seed 3, 10% planted", "qs_first_hit_kernel<8,8> (HIP C++ interpreter)"),
+           "~1060 DAG nodes) x 10^6 models per GPU, seed 3, 10% planted",
+           "mq::qsg_kernel (gfx950 assembly interpreter, variables from HBM) + qs_column_kernel<8> (hoisted columns)"),
     "c4": (200, 1_000_000, 4, "C4: 200 keccak-heavy token-transfer paths over 2 txs (balances[key] = storage at "
            "keccak256(key ++ slot), store chains, keccak UF axioms of keccak_function_manager) x 10^6 "
            "keccak-consistent models per GPU, keccak256_512 evaluated IN-KERNEL (keccak-f[1600]), seed 4, 10% planted",
            "qs_first_hit_kernel<16,6,keccak> (HIP C++ interpreter + keccak-f[1600])"),
     "c5": (256, 1_250_000, 5, "C5: 256 deep EVM-shaped paths over 5 txs (~1900 DAG nodes) x 1.25*10^6 models per GPU "
-           "(10^7 over 8 GPUs), seed 5, 10% planted", "qs_first_hit_kernel<8,8> (HIP C++ interpreter)"),
+           "(10^7 over 8 GPUs), seed 5, 10% planted",
+           "mq::qsg_kernel (gfx950 assembly interpreter, variables from HBM) + qs_column_kernel<8> (hoisted columns)"),
 }
 
 

@@ -48,6 +48,7 @@ D = 6          # stack slots
 NV = 8         # preloaded variables (P)
 L = 8          # limbs (256-bit)
 VBASE, SBASE, TBASE = 8, 72, 120
+UBASE = 128    # G: UF1 work registers v[128:151]
 BBASE = 48
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -83,18 +84,48 @@ def W2(k):
     return f"v[{TBASE + k}:{TBASE + k + 1}]"
 
 
-NEXT = [
-    "s_waitcnt lgkmcnt(0)",
-    "s_and_b32 s18, s16, 0xffff",
-    "s_lshr_b32 s17, s16, 16",
+
+# G: the tape's program is streamed through a 64-word VGPR window (lane i = word i of the
+# window, one coalesced load per window) and read with v_readlane: no scalar-memory round trip
+# per node.  s[14:15] = byte address of the window, s16 = lane of the next word.  The translator
+# places a REFILL word wherever the window runs out (the next window starts right after it) and
+# never splits a PUSH_CONSTW from its inline data words.
+WIN = "v152"
+NEXT_G = [
+    f"v_readlane_b32 s17, {WIN}, s16",
+    "s_add_u32 s16, s16, 1",
+    "s_nop 2",                      # VALU SGPR write -> SALU read
+    "s_and_b32 s18, s17, 0xffff",
+    "s_lshr_b32 s17, s17, 16",
     "s_lshl_b32 s18, s18, 2",
     "s_add_u32 s18, s12, s18",
     "s_addc_u32 s19, s13, 0",
-    "s_load_dword s16, s[14:15], 0x0",
-    "s_add_u32 s14, s14, 4",
-    "s_addc_u32 s15, s15, 0",
     "s_setpc_b64 s[18:19]",
 ]
+
+
+# P: two-word program entries (absolute low 32 bits of the handler address, immediate),
+# prefetched one entry ahead into s[96:97]; s[14:15] = program base, s16 = byte offset of the
+# next entry, s19 = high half of the handler addresses (the host checks they share it).
+NEXT_P = [
+    "s_waitcnt lgkmcnt(0)",
+    "s_mov_b32 s18, s96",
+    "s_mov_b32 s17, s97",
+    "s_load_dwordx2 s[96:97], s[14:15], s16",
+    "s_add_u32 s16, s16, 8",
+    "s_setpc_b64 s[18:19]",
+]
+
+
+def load_window(first):
+    """WIN = the 64 program words at s[14:15] (+ 4*s16 unless first); s16 = 0."""
+    out = []
+    if not first:
+        out += ["s_lshl_b32 s34, s16, 2", "s_add_u32 s14, s14, s34", "s_addc_u32 s15, s15, 0"]
+    out += ["v_mbcnt_lo_u32_b32 v5, -1, 0", "v_mbcnt_hi_u32_b32 v5, -1, v5", "v_lshlrev_b32 v5, 2, v5",
+            f"global_load_dword {WIN}, v5, s[14:15]", "s_mov_b32 s16, 0", "s_waitcnt vmcnt(0)"]
+    return out
+
 
 VMWAIT = "s_waitcnt vmcnt(0)"
 
@@ -114,12 +145,14 @@ def zero_limbs(d, lo):
 
 
 # ---------------------------------------------------------------- handler bodies
-def eq_body(d):
+def eq_body(d, bl=None):
     """8 limb compares into 8 distinct SGPR pairs, then a SALU AND tree (every SALU read is
-    >= 4 instructions after the VALU write)."""
-    a, b = d - 1, d
+    >= 4 instructions after the VALU write).  bl(l): register of the right operand's limb l
+    (default: stack slot d; a preloaded variable in the fused ...V handlers)."""
+    a = d - 1
+    bl = bl or (lambda l: S(d, l))
     regs = ["s[34:35]", "s[36:37]", "s[38:39]", "s[60:61]", "s[64:65]", "s[66:67]", "s[68:69]", "s[70:71]"]
-    out = [f"v_cmp_eq_u32_e64 {regs[l]}, {S(a, l)}, {S(b, l)}" for l in range(L)]
+    out = [f"v_cmp_eq_u32_e64 {regs[l]}, {S(a, l)}, {bl(l)}" for l in range(L)]
     out += ["s_nop 1",
             "s_and_b64 s[34:35], s[34:35], s[36:37]", "s_and_b64 s[38:39], s[38:39], s[60:61]",
             "s_and_b64 s[64:65], s[64:65], s[66:67]", "s_and_b64 s[68:69], s[68:69], s[70:71]",
@@ -129,13 +162,16 @@ def eq_body(d):
 
 
 def lt_chain(x, y, dst):
-    """dst mask = (x < y) unsigned over 8 limbs (slots x, y); borrow chain with hazard nops."""
-    out = [f"v_sub_co_u32_e64 v5, s[34:35], {S(x, 0)}, {S(y, 0)}"]
+    """dst mask = (x < y) unsigned over 8 limbs; x, y are slot numbers or limb -> register
+    functions; borrow chain with hazard nops."""
+    xl = x if callable(x) else (lambda l, _x=x: S(_x, l))
+    yl = y if callable(y) else (lambda l, _y=y: S(_y, l))
+    out = [f"v_sub_co_u32_e64 v5, s[34:35], {xl(0)}, {yl(0)}"]
     cur = "s[34:35]"
     for l in range(1, L):
         nxt = dst if l == L - 1 else ("s[36:37]" if cur == "s[34:35]" else "s[34:35]")
         out.append("s_nop 1")
-        out.append(f"v_subb_co_u32_e64 v5, {nxt}, {S(x, l)}, {S(y, l)}, {cur}")
+        out.append(f"v_subb_co_u32_e64 v5, {nxt}, {xl(l)}, {yl(l)}, {cur}")
         cur = nxt
     return out
 
@@ -152,25 +188,34 @@ def carry_chain(first, rest, n=L):
     return out
 
 
-def mul_body(d):
-    """S[d-1] = S[d-1] * S[d] mod 2^256: product scanning (Comba) columns 0..7, 64-bit column
-    accumulator v[4:5] (v_mad_u64_u32 with carry-out) + overflow word v6; carries are added
-    through three rotating SGPR pairs so every VALU carry read is >= 2 instructions after its
-    write.  Column 0 has no carries; each later column's first carry-add writes the overflow word
-    (no reset move); column 7's low word goes straight to S[d-1][7] after its last product."""
-    a, b = d - 1, d
+def mul_body(d, bl=None):
+    """S[d-1] = S[d-1] * b mod 2^256 (b = slot d, or bl(j) = register of limb j): product
+    scanning (Comba) columns 0..7.  A column's state is a 64-bit accumulator pair (v_mad_u64_u32
+    with carry-out) plus an overflow word; the pairs alternate between v[4:5] and v[6:7] and the
+    overflow of the column in one pair is accumulated directly in the high word of the other, so
+    a column ends with two moves (result word out, high word down).  Carries are added through
+    three rotating SGPR pairs so every VALU carry read is >= 2 instructions after its write; each
+    column's first carry-add resets the overflow word; column 7 keeps only its low word."""
+    a = d - 1
+    bl = bl or (lambda j: S(d, j))
     C = ["s[34:35]", "s[36:37]", "s[38:39]"]
-    out = [f"v_mad_u64_u32 v[4:5], s[60:61], {S(a, 0)}, {S(b, 0)}, 0",
-           f"v_mov_b32 {T(0)}, v4", "v_mov_b32 v4, v5", "v_mov_b32 v5, 0"]
+    PAIRS = (("v[4:5]", "v4", "v5"), ("v[6:7]", "v6", "v7"))
+    out = [f"v_mad_u64_u32 v[4:5], s[60:61], {S(a, 0)}, {bl(0)}, 0",
+           f"v_mov_b32 {T(0)}, v4", "v_mov_b32 v6, v5", "v_mov_b32 v7, 0"]
     for k in range(1, L):
+        pair, lo, hi = PAIRS[k % 2]
+        _, olo, ohi = PAIRS[(k + 1) % 2]   # next column's pair; its high word is our overflow
         prods = [(i, k - i) for i in range(k + 1)]
         if k == L - 1:
             # last column: only the low word matters, no carry tracking
             for i, j in prods:
-                out.append(f"v_mad_u64_u32 v[4:5], s[60:61], {S(a, i)}, {S(b, j)}, v[4:5]")
+                out.append(f"v_mad_u64_u32 {pair}, s[60:61], {S(a, i)}, {bl(j)}, {pair}")
+            out += [f"v_mov_b64 {S2(a, l)}, v[{TBASE + l}:{TBASE + l + 1}]" for l in range(0, 6, 2)]
+            out += [f"v_mov_b32 {S(a, 6)}, {T(6)}", f"v_mov_b32 {S(a, 7)}, {lo}"]
             break
-        mads = [f"v_mad_u64_u32 v[4:5], {C[t % 3]}, {S(a, i)}, {S(b, j)}, v[4:5]" for t, (i, j) in enumerate(prods)]
-        adds = [f"v_addc_co_u32_e64 v6, s[60:61], 0, {'0' if t == 0 else 'v6'}, {C[t % 3]}" for t in range(len(prods))]
+        mads = [f"v_mad_u64_u32 {pair}, {C[t % 3]}, {S(a, i)}, {bl(j)}, {pair}" for t, (i, j) in enumerate(prods)]
+        adds = [f"v_addc_co_u32_e64 {ohi}, s[60:61], 0, {'0' if t == 0 else ohi}, {C[t % 3]}"
+                for t in range(len(prods))]
         seq = []
         n = len(prods)
         # m0 m1 m2 a0 m3 a1 m4 a2 ... then flush
@@ -184,9 +229,7 @@ def mul_body(d):
         else:
             seq += tail
         out += seq
-        out += [f"v_mov_b32 {T(k)}, v4", "v_mov_b32 v4, v5", "v_mov_b32 v5, v6"]
-    out += [f"v_mov_b64 {S2(a, l)}, v[{TBASE + l}:{TBASE + l + 1}]" for l in range(0, 6, 2)]
-    out += [f"v_mov_b32 {S(a, 6)}, {T(6)}", f"v_mov_b32 {S(a, 7)}, v4"]
+        out += [f"v_mov_b32 {T(k)}, {lo}", f"v_mov_b32 {olo}, {hi}"]
     return out
 
 
@@ -336,14 +379,14 @@ def sub_udiv32(pfx):
 
 def sub_uf1(pfx):
     """Arity-1 model function lookup (UF / as-array select, z3 completion: the else value when no
-    entry matches): key W[0..7] (canonical), s98 = function id; result in v[8:15].
+    entry matches): key W[0..7] (canonical), s98 = function id; result in v[128:135].
     FuncDev (qs_launch.h) of the function gives nl_a0 / nl_res / stride and the offsets of its
     entry rows, per-model entry ranges (entry_ptr) and SoA else block.  Per lane the entries are
     scanned in order and the first match wins (mq.h model layout); the wave loops over the
     longest list with finished lanes masked off."""
     P = pfx
     out = [f"{P}_sub_uf1:"]
-    out += [f"v_mov_b64 v[{8 + l}:{9 + l}], 0" for l in range(0, 8, 2)]
+    out += [f"v_mov_b64 v[{UBASE + l}:{UBASE + 1 + l}], 0" for l in range(0, 8, 2)]
     out += ["s_load_dwordx8 s[64:71], s[10:11], 0x160",       # funcs, entry_ptr, entry_words, else_words
             "s_load_dword s99, s[10:11], 0x180",             # n_funcs
             "s_waitcnt lgkmcnt(0)",
@@ -374,7 +417,7 @@ def sub_uf1(pfx):
             "s_mov_b64 s[34:35], s[70:71]"]
     for l in range(L):
         out += [f"s_cmp_le_u32 s37, {l}", f"s_cbranch_scc1 {P}_uf_else_done",
-                f"global_load_dword v{8 + l}, v2, s[34:35]",
+                f"global_load_dword v{UBASE + l}, v2, s[34:35]",
                 "s_add_u32 s34, s34, s74", "s_addc_u32 s35, s35, s75"]
     out += [f"{P}_uf_else_done:",
             "v_lshlrev_b32 v4, 1, v2",                        # m*8
@@ -382,7 +425,7 @@ def sub_uf1(pfx):
             "global_load_dword v6, v4, s[66:67] offset:8",    # end
             "v_mov_b32 v7, s39",
             "s_waitcnt vmcnt(0)",
-            "v_mad_u64_u32 v[16:17], s[34:35], v5, v7, s[68:69]",   # &entry[lo]
+            "v_mad_u64_u32 v[136:137], s[34:35], v5, v7, s[68:69]",   # &entry[lo]
             "s_mov_b64 s[60:61], exec",
             f"{P}_uf_loop:",
             "v_cmp_lt_u32_e64 s[34:35], v5, v6",
@@ -391,29 +434,29 @@ def sub_uf1(pfx):
             f"s_cbranch_execz {P}_uf_done"]
     for l in range(L):
         out += [f"s_cmp_le_u32 s36, {l}", f"s_cbranch_scc1 {P}_uf_kl_done",
-                f"global_load_dword v{20 + l}, v[16:17], off offset:{4 * l}"]
-    out += [f"{P}_uf_kl_done:", "s_waitcnt vmcnt(0)", "v_mov_b32 v28, 0"]
+                f"global_load_dword v{UBASE + 12 + l}, v[136:137], off offset:{4 * l}"]
+    out += [f"{P}_uf_kl_done:", "s_waitcnt vmcnt(0)", "v_mov_b32 v148, 0"]
     for l in range(L):
         out += [f"s_cmp_le_u32 s36, {l}", f"s_cbranch_scc1 {P}_uf_kc_done",
-                f"v_xor_b32 v29, v{20 + l}, {W(l)}", "v_or_b32 v28, v28, v29"]
+                f"v_xor_b32 v149, v{UBASE + 12 + l}, {W(l)}", "v_or_b32 v148, v148, v149"]
     out += [f"{P}_uf_kc_done:",
-            "v_cmp_eq_u32_e64 s[34:35], 0, v28",
-            "v_add_co_u32 v30, vcc, s98, v16",
+            "v_cmp_eq_u32_e64 s[34:35], 0, v148",
+            "v_add_co_u32 v150, vcc, s98, v136",
             "s_nop 1",
-            "v_addc_co_u32 v31, vcc, 0, v17, vcc",
+            "v_addc_co_u32 v151, vcc, 0, v137, vcc",
             "s_nop 3",
             "s_and_saveexec_b64 s[78:79], s[34:35]",
             f"s_cbranch_execz {P}_uf_nomatch"]
     for l in range(L):
         out += [f"s_cmp_le_u32 s37, {l}", f"s_cbranch_scc1 {P}_uf_vl_done",
-                f"global_load_dword v{8 + l}, v[30:31], off offset:{4 * l}"]
+                f"global_load_dword v{UBASE + l}, v[150:151], off offset:{4 * l}"]
     out += [f"{P}_uf_vl_done:", "s_waitcnt vmcnt(0)",
             f"{P}_uf_nomatch:",
             "s_andn2_b64 exec, s[78:79], s[34:35]",           # matched lanes are done
             "v_add_u32 v5, 1, v5",
-            "v_add_co_u32 v16, vcc, v16, v7",
+            "v_add_co_u32 v136, vcc, v136, v7",
             "s_nop 1",
-            "v_addc_co_u32 v17, vcc, 0, v17, vcc",
+            "v_addc_co_u32 v137, vcc, 0, v137, vcc",
             f"s_branch {P}_uf_loop",
             f"{P}_uf_done:",
             "s_mov_b64 exec, s[60:61]",
@@ -430,16 +473,18 @@ def make_handlers(variant, pfx):
 
     def H(key, body, tail=True, reads_stack=True):
         pre = [VMWAIT] if (G and reads_stack) else []
-        hs.append((key, pre + list(body) + (NEXT if tail else [])))
+        hs.append((key, pre + list(body) + ((NEXT_G if G else NEXT_P) if tail else [])))
 
     H(("END",), [f"s_branch {pfx}_tape_end"], tail=False, reads_stack=False)
+    if G:
+        H(("REFILL",), load_window(False), reads_stack=False)
     # ---- leaves
     for d in range(D):
-        if not G:
-            for v in range(NV):
-                H(("PUSH_VAR", d, v), [f"v_mov_b64 {S2(d, l)}, {V2(v, l)}" for l in range(0, L, 2)], reads_stack=False)
-                H(("PUSH_VARB", d, v), [f"v_cmp_ne_u32_e64 {B(d)}, 0, v{VBASE + 8 * v}", "s_nop 3"], reads_stack=False)
-        else:
+        # preloaded variables (P: the batch's first 8; G: the 8 its tapes push most)
+        for v in range(NV):
+            H(("PUSH_VAR", d, v), [f"v_mov_b64 {S2(d, l)}, {V2(v, l)}" for l in range(0, L, 2)], reads_stack=False)
+            H(("PUSH_VARB", d, v), [f"v_cmp_ne_u32_e64 {B(d)}, 0, v{VBASE + 8 * v}", "s_nop 3"], reads_stack=False)
+        if G:
             # variable row imm: loads in flight until the next stack reader's vmcnt wait
             for n in range(1, L + 1):
                 body = ["s_mul_i32 s34, s17, s29", "s_mul_hi_u32 s35, s17, s29", "s_lshl_b64 s[34:35], s[34:35], 2",
@@ -456,6 +501,15 @@ def make_handlers(variant, pfx):
                                  f"v_cmp_ne_u32_e64 {B(d)}, 0, v4", "s_nop 3"], reads_stack=False)
         H(("PUSH_CONST", d), ["s_lshl_b32 s34, s17, 2", "s_load_dwordx8 s[64:71], s[20:21], s34", "s_waitcnt lgkmcnt(0)"]
           + [f"v_mov_b64 {S2(d, l)}, s[{64 + l}:{65 + l}]" for l in range(0, L, 2)], reads_stack=False)
+        if G:
+            # constants inline in the program stream: imm16 (PUSH_CONSTI) or n+1 data words
+            H(("PUSH_CONSTI", d), [f"v_mov_b32 {S(d, 0)}, s17"] + zero_limbs(d, 1), reads_stack=False)
+            for n in range(L):
+                body = []
+                for l in range(n + 1):
+                    body += [f"v_readlane_b32 s{64 + l}, {WIN}, s16", "s_add_u32 s16, s16, 1"]
+                body += ["s_nop 1"] + [f"v_mov_b32 {S(d, l)}, s{64 + l}" for l in range(n + 1)] + zero_limbs(d, n + 1)
+                H(("PUSH_CONSTW", d, n), body, reads_stack=False)
         H(("PUSH_TMP", d), ["s_lshl_b32 s34, s17, 11", "v_add_u32 v5, s34, v1"]
           + [f"ds_read_b64 {S2(d, l)}, v5 offset:{256 * l}" for l in range(0, L, 2)] + ["s_waitcnt lgkmcnt(0)"],
           reads_stack=False)
@@ -541,9 +595,42 @@ def make_handlers(variant, pfx):
     if G:
         for d in range(D):
             H(("UF1", d), copy_to_w(d) + ["s_mov_b32 s98, s17", f"s_call_b64 s[76:77], {pfx}_sub_uf1"]
-              + [f"v_mov_b64 {S2(d, l)}, v[{8 + l}:{9 + l}]" for l in range(0, L, 2)])
+              + [f"v_mov_b64 {S2(d, l)}, v[{UBASE + l}:{UBASE + 1 + l}]" for l in range(0, L, 2)])
             H(("UF1B", d), copy_to_w(d) + ["s_mov_b32 s98, s17", f"s_call_b64 s[76:77], {pfx}_sub_uf1",
-                                            "v_and_b32 v4, 1, v8", f"v_cmp_ne_u32_e64 {B(d)}, 0, v4", "s_nop 3"])
+                                            "v_and_b32 v4, 1, v128", f"v_cmp_ne_u32_e64 {B(d)}, 0, v4", "s_nop 3"])
+    # ---- P: right operand a constant, used straight from SGPRs (one SGPR source per VALU
+    # instruction; ADD/SUB/compares would need a second one for the carry and keep the push)
+    if not G:
+        for d in range(1, D):
+            a = d - 1
+            ld = ["s_lshl_b32 s34, s17, 2", "s_load_dwordx8 s[64:71], s[20:21], s34", "s_waitcnt lgkmcnt(0)"]
+            cl = (lambda l: f"s{64 + l}")
+            for nm, ins in (("BANDC", "v_and_b32"), ("BORC", "v_or_b32"), ("BXORC", "v_xor_b32")):
+                H((nm, d), ld + [f"{ins} {S(a, l)}, {cl(l)}, {S(a, l)}" for l in range(L)])
+            H(("MULC", d), ld + mul_body(d, cl))
+            H(("EQC", d), ld + eq_body(d, cl))
+    # ---- (last: these handlers never branch, so the subroutine calls above stay in s_call range)
+    # ---- binary ops whose right operand is a preloaded variable (the translator fuses
+    # PUSH_VAR v at slot d with the consuming op at d: no stack copy, one dispatch less)
+    if True:
+        for d in range(1, D):
+            a = d - 1
+            for v in range(NV):
+                def vl(l, v=v):
+                    return f"v{VBASE + 8 * v + l}"
+                H(("ADDV", d, v), carry_chain(lambda l: f"v_add_co_u32 {S(a, l)}, vcc, {S(a, l)}, {vl(l)}",
+                                              lambda l: f"v_addc_co_u32 {S(a, l)}, vcc, {S(a, l)}, {vl(l)}, vcc"))
+                H(("SUBV", d, v), carry_chain(lambda l: f"v_sub_co_u32 {S(a, l)}, vcc, {S(a, l)}, {vl(l)}",
+                                              lambda l: f"v_subb_co_u32 {S(a, l)}, vcc, {S(a, l)}, {vl(l)}, vcc"))
+                for nm, ins in (("BANDV", "v_and_b32"), ("BORV", "v_or_b32"), ("BXORV", "v_xor_b32")):
+                    H((nm, d, v), [f"{ins} {S(a, l)}, {S(a, l)}, {vl(l)}" for l in range(L)])
+                H(("MULV", d, v), mul_body(d, vl))
+                H(("EQV", d, v), eq_body(d, vl))
+                xa = (lambda l: S(a, l))
+                H(("ULTV", d, v), lt_chain(xa, vl, B(a)))
+                H(("UGTV", d, v), lt_chain(vl, xa, B(a)))
+                H(("ULEV", d, v), lt_chain(vl, xa, "s[38:39]") + ["s_nop 3", f"s_not_b64 {B(a)}, s[38:39]"])
+                H(("UGEV", d, v), lt_chain(xa, vl, "s[38:39]") + ["s_nop 3", f"s_not_b64 {B(a)}, s[38:39]"])
     subs = sub_abs_cneg(pfx) + sub_udiv32(pfx) + (sub_uf1(pfx) if G else [])
     return hs, subs
 
@@ -577,24 +664,31 @@ def frame(variant, pfx, handlers, subs):
         f"{pfx}_pc:",
         f"s_add_u32 s12, s12, {pfx}_hbase - {pfx}_pc",
         "s_addc_u32 s13, s13, 0",
+        "s_mov_b32 s19, s13",
         # mode 2: dump handler offsets (block 0, lane 0)
         "s_cmp_eq_u32 s31, 2",
         f"s_cbranch_scc0 {pfx}_main",
         "s_or_b32 s34, s96, s97",
         "s_cmp_eq_u32 s34, 0",
-        f"s_cbranch_scc0 {pfx}_end",
+        f"s_cbranch_scc0 {pfx}_exit",
         "v_cmp_eq_u32_e64 s[34:35], 0, v3",
         "s_nop 3",
         "s_and_saveexec_b64 s[36:37], s[34:35]",
         "v_mov_b32 v4, 0",
     ]
     for k in range(len(handlers)):
+        if k % 1000 == 0 and k:
+            P.append(f"v_mov_b32 v4, {4 * k}")   # global offsets are 13-bit signed
         P.append(f"v_mov_b32 v5, {pfx}_h{k} - {pfx}_hbase")
-        P.append(f"global_store_dword v4, v5, s[78:79] offset:{4 * k}")
+        P.append(f"global_store_dword v4, v5, s[78:79] offset:{4 * (k % 1000)}")
+    nh = len(handlers)
+    P += [f"v_mov_b32 v4, {4 * nh}",     # then the absolute handler base (s[12:13])
+          "v_mov_b32 v5, s12", "global_store_dword v4, v5, s[78:79]",
+          "v_mov_b32 v5, s13", "global_store_dword v4, v5, s[78:79] offset:4"]
     P += [
         "s_waitcnt vmcnt(0)",
         "s_mov_b64 exec, s[36:37]",
-        f"s_branch {pfx}_end",
+        f"s_branch {pfx}_exit",
         f"{pfx}_main:",
         # wave / lane / model index
         "v_and_b32 v4, 63, v3",
@@ -608,7 +702,7 @@ def frame(variant, pfx, handlers, subs):
         "s_lshl_b32 s36, s34, 6",
         "s_add_u32 s35, s35, s36",
         "s_cmp_ge_u32 s35, s29",
-        f"s_cbranch_scc1 {pfx}_end",
+        f"s_cbranch_scc1 {pfx}_exit",
         "s_add_u32 s28, s98, s35",            # gfirst
         "v_add_u32 v2, s35, v4",               # m
         "v_cmp_lt_u32_e64 s[62:63], v2, s29",  # valid
@@ -625,7 +719,7 @@ def frame(variant, pfx, handlers, subs):
         "s_add_u32 s25, s24, s83",
         "s_min_u32 s25, s25, s82",
     ]
-    if not G:
+    if True:
         # preload variables: 64 limb rows (row index table at args+0x60; the host points missing
         # limbs / vars at an all-zero row)
         for c in range(4):
@@ -666,10 +760,10 @@ def frame(variant, pfx, handlers, subs):
         "s_lshl_b32 s34, s80, 2",
         "s_add_u32 s14, s46, s34",
         "s_addc_u32 s15, s47, 0",
-        "s_load_dword s16, s[14:15], 0x0",
-        "s_add_u32 s14, s14, 4",
-        "s_addc_u32 s15, s15, 0",
-    ] + NEXT + [
+    ] + (load_window(True) + NEXT_G if G else [
+        "s_load_dwordx2 s[96:97], s[14:15], 0x0",
+        "s_mov_b32 s16, 8",
+    ] + NEXT_P) + [
         f"{pfx}_tape_end:",
         "s_waitcnt lgkmcnt(0)",
         "s_and_b64 s[34:35], s[48:49], s[62:63]",
@@ -726,8 +820,11 @@ def frame(variant, pfx, handlers, subs):
         "global_atomic_add_x2 v6, v[4:5], s[92:93] offset:16",
         "s_waitcnt vmcnt(0)",
         "s_mov_b64 exec, s[60:61]",
-        f"s_branch {pfx}_end",
+        f"s_branch {pfx}_exit",
     ]
+    # the handler area exceeds the 128 KB reach of s_branch: leave through s_setpc
+    P += [f"{pfx}_exit:", "s_getpc_b64 s[34:35]", f"{pfx}_exit_pc:",
+          f"s_add_u32 s34, s34, {pfx}_end - {pfx}_exit_pc", "s_addc_u32 s35, s35, 0", "s_setpc_b64 s[34:35]"]
     P += subs
     P.append(f"{pfx}_hbase:")
     for k, (key, body) in enumerate(handlers):
@@ -741,8 +838,9 @@ VARIANTS = (("p", ".Lqsa", "QSA_ASM_TEXT_P", "P"), ("g", ".Lqsg", "QSA_ASM_TEXT_
 
 
 def main():
-    clob = [f'"v{i}"' for i in range(1, 128)] + [f'"s{i}"' for i in range(10, 100) if i not in (32, 33)]
-    clob += ['"vcc"', '"scc"', '"memory"']
+    sclob = [f'"s{i}"' for i in range(10, 100) if i not in (32, 33)] + ['"vcc"', '"scc"', '"memory"']
+    clob = {"p": [f'"v{i}"' for i in range(1, 128)] + sclob,          # 128 VGPRs: 4 waves / SIMD
+            "g": [f'"v{i}"' for i in range(1, 153)] + sclob}   # + UF1 work, window: 3 waves / SIMD
     gen = {}
     for variant, pfx, macro, suffix in VARIANTS:
         hs, subs = make_handlers(variant, pfx)
@@ -754,7 +852,8 @@ def main():
             for ln in lines:
                 f.write('  "' + ln.replace('"', '\\"') + '\\n" \\\n')
             f.write("  \"\"\n")
-        f.write("#define QSA_CLOBBERS " + ", ".join(clob) + "\n")
+        f.write("#define QSA_CLOBBERS_P " + ", ".join(clob["p"]) + "\n")
+        f.write("#define QSA_CLOBBERS_G " + ", ".join(clob["g"]) + "\n")
     names = sorted({k[0] for hs, *_ in gen.values() for k, _ in hs})
     with open(os.path.join(HERE, "qsa_table.h"), "w") as f:
         f.write("// GENERATED by gen_qsa.py — handler enumerations of the QSA interpreters\n")

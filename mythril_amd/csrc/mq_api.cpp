@@ -78,6 +78,8 @@ struct mq_ctx {
   std::vector<uint32_t> qsa_off[2];
   int qsa_index[2][QK_COUNT][kQsaStack][kQsaSel + 1];
   uint32_t qsa_var_row[64];
+  std::vector<uint8_t> qsa_data_words;
+  uint32_t qsa_hbase_lo[2] = {0, 0};   // low 32 bits of each interpreter's handler base
   DevBuf qsa_args;
   // host copies of the model batch layout the QSA translation depends on
   std::vector<uint32_t> var_off_h, var_nl_h;
@@ -117,6 +119,10 @@ struct mq_tapes {
   uint64_t qsa_gen = ~0ull;                  // models_gen of the current translation
   bool qsa_live = false;                     // the translation succeeded for every tape
   int q_count[2] = {0, 0}, q_temps[2] = {0, 0};
+  // G kernel preload for the current translation: gpre[var] = VGPR slot (or -1) of the (at
+  // most 8) variables the G tapes push most; g_var_row = their limb rows (QArgs.var_row)
+  std::vector<int> gpre;
+  uint32_t g_var_row[64];
   DevBuf qdescs, qprog, qargs[2];
   QArgs qargs_dev_copy[2];   // what qargs[k] currently holds on the device
   bool qargs_valid[2] = {false, false};
@@ -198,20 +204,35 @@ static int qsa_init(mq_ctx* c) {
       for (int d = 0; d < kQsaStack; d++)
         for (int v = 0; v <= kQsaSel; v++) c->qsa_index[k][q][d][v] = -1;
     for (int h = 0; h < nh; h++) c->qsa_index[k][keys[h].kind][keys[h].d < 0 ? 0 : keys[h].d][keys[h].v + 1] = h;
-    DevBuf table;
-    HIPCHK(table.ensure(sizeof(uint32_t) * nh));
-    HIPCHK(hipMemsetAsync(table.p, 0xFF, sizeof(uint32_t) * nh, c->stream));
+    DevBuf table;   // nh handler offsets, then the absolute handler base (lo, hi)
+    HIPCHK(table.ensure(sizeof(uint32_t) * (nh + 2)));
+    HIPCHK(hipMemsetAsync(table.p, 0xFF, sizeof(uint32_t) * (nh + 2), c->stream));
     QArgs qa{};
     qa.table_out = table.as<uint32_t>();
     qa.mode = 2;
     HIPCHK(c->qsa_args.upload(&qa, 1, c->stream));
     HIPCHK(launch_qsa(k, c->qsa_args.as<QArgs>(), 1, 1, 0, c->stream));
-    c->qsa_off[k].resize(nh);
-    HIPCHK(hipMemcpyAsync(c->qsa_off[k].data(), table.p, sizeof(uint32_t) * nh, hipMemcpyDeviceToHost, c->stream));
+    c->qsa_off[k].resize(nh + 2);
+    HIPCHK(hipMemcpyAsync(c->qsa_off[k].data(), table.p, sizeof(uint32_t) * (nh + 2), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    for (int h = 0; h < nh; h++)
+    c->qsa_hbase_lo[k] = c->qsa_off[k][nh];
+    uint32_t max_off = 0;
+    for (int h = 0; h < nh; h++) {
       ok = ok && c->qsa_off[k][h] != 0xFFFFFFFFu && (c->qsa_off[k][h] & 3) == 0 && c->qsa_off[k][h] < (1u << 18);
+      max_off = std::max(max_off, c->qsa_off[k][h]);
+    }
+    // P program entries hold the low 32 bits of absolute handler addresses: they must share
+    // the high half (the kernel keeps it in s19)
+    if (k == 0) ok = ok && (uint64_t)c->qsa_hbase_lo[k] + max_off < (1ull << 32);
+    c->qsa_off[k].resize(nh);
   }
+  // G handler word index -> inline data words that follow it (PUSH_CONSTW)
+  c->qsa_data_words.assign(1 << 16, 0);
+  for (int d = 0; ok && d < kQsaStack; d++)
+    for (int n = 0; n < 8; n++) {
+      const int h = c->qsa_index[1][QK_PUSH_CONSTW][d][n + 1];
+      if (h >= 0) c->qsa_data_words[(c->qsa_off[1][h] >> 2) & 0xFFFFu] = (uint8_t)(n + 1);
+    }
   c->qsa_ready = ok && std::getenv("MQ_DISABLE_QSA") == nullptr;
   return MQ_OK;
 }
@@ -369,7 +390,7 @@ int mq_models_upload(mq_ctx* c, const mq_model_batch* mb) {
 // time.  Returns false if any instruction is outside the interpreter's set (those tapes run on
 // the HIP C++ kernel).
 static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTape& x, std::vector<uint32_t>* out_p,
-                          std::vector<uint32_t>* extra_p) {
+                          std::vector<uint32_t>* extra_p, const std::vector<int>* gpre = nullptr) {
   std::vector<uint32_t> dummy_out, dummy_extra;
   std::vector<uint32_t>& out = out_p ? *out_p : dummy_out;
   std::vector<uint32_t>& extra = extra_p ? *extra_p : dummy_extra;
@@ -377,11 +398,17 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
   extra.clear();
   if (x.L != 8 || x.depth > kQsaStack) return false;
   const bool P = k == 0;
+  const size_t wpi = P ? 2 : 1;   // program words per interpreter instruction
   auto word = [&](int kind, int d, int v, uint32_t imm) -> bool {
     if (d < 0 || d >= kQsaStack || v < -1 || v >= kQsaSel || imm > 0xFFFFu) return false;
     const int h = c->qsa_index[k][kind][d][v + 1];
     if (h < 0) return false;
-    out.push_back((c->qsa_off[k][h] >> 2) | (imm << 16));
+    if (P) {   // two-word entry: absolute handler address (low half), immediate
+      out.push_back(c->qsa_hbase_lo[0] + c->qsa_off[0][h]);
+      out.push_back(imm);
+    } else {
+      out.push_back((c->qsa_off[k][h] >> 2) | (imm << 16));
+    }
     return true;
   };
   // slot d holds a value of width W < 256: clear the bits above W
@@ -408,6 +435,30 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
   };
   uint32_t prev_op = G_END, prev_d = 0, prev_imm = 0;
   size_t prev_out = 0;
+  int prev_pre = -1;   // preload slot of the variable the previous instruction pushed
+  // preload slot of variable v in this kernel, or -1 (P: v itself; G: the batch's choice)
+  auto pre_slot = [&](uint32_t v) -> int {
+    if (P) return v < (uint32_t)kQsaVars ? (int)v : -1;
+    if (!models || !gpre || v >= gpre->size()) return -1;
+    return (*gpre)[v];
+  };
+  // a binary op at slot d whose right operand was just pushed from a preloaded variable runs
+  // as the fused handler kindv(d, slot) (the push word is dropped)
+  // (P) likewise a right operand just pushed from the constants, for the kinds with a kindc
+  // handler (operand read from SGPRs)
+  auto binop = [&](int d, int kind, int kindv, int kindc = -1) -> bool {
+    if (prev_op == G_PUSH_VAR && prev_pre >= 0 && (int)prev_d == d && out.size() == prev_out + wpi &&
+        c->qsa_index[k][kindv][d][prev_pre + 1] >= 0) {
+      out.resize(prev_out);
+      return word(kindv, d, prev_pre, 0);
+    }
+    if (kindc >= 0 && P && prev_op == G_PUSH_CONST && (int)prev_d == d && out.size() == prev_out + wpi &&
+        c->qsa_index[k][kindc][d][0] >= 0) {
+      out.resize(prev_out);
+      return word(kindc, d, -1, prev_imm);
+    }
+    return word(kind, d, -1, 0);
+  };
   for (size_t pc = 0; pc < x.prog.size(); pc++) {
     const uint32_t w = x.prog[pc];
     const uint32_t op = w & 0xFFu, imm = w >> 12;
@@ -419,16 +470,22 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
     }
     const size_t out_before = out.size();
     const bool after_const = prev_op == G_PUSH_CONST && (int)prev_d == d;
+    int pushed_pre = -1;
     bool ok;
     switch (op) {
       case G_END: ok = word(QK_END, 0, -1, 0); break;
       case G_PUSH_VAR:
       case G_PUSH_VAR_B: {
         const bool b = op == G_PUSH_VAR_B;
+        const int ps = pre_slot(imm);
         if (P) {
           // preloaded variables only (var < 8, at most 256 bits)
-          ok = imm < (uint32_t)kQsaVars && (!models || (imm < c->var_nl_h.size() && c->var_nl_h[imm] <= 8)) &&
-               word(b ? QK_PUSH_VARB : QK_PUSH_VAR, d, b ? (int)imm : (int)imm, 0);
+          ok = ps >= 0 && (!models || (imm < c->var_nl_h.size() && c->var_nl_h[imm] <= 8)) &&
+               word(b ? QK_PUSH_VARB : QK_PUSH_VAR, d, ps, 0);
+          pushed_pre = ps;
+        } else if (ps >= 0) {
+          ok = word(b ? QK_PUSH_VARB : QK_PUSH_VAR, d, ps, 0);
+          pushed_pre = ps;
         } else if (!models) {
           ok = word(b ? QK_PUSH_MEMB : QK_PUSH_MEM, d, b ? -1 : 7, 0);
         } else {
@@ -437,7 +494,25 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
         }
         break;
       }
-      case G_PUSH_CONST: ok = word(QK_PUSH_CONST, d, -1, imm); break;
+      case G_PUSH_CONST: {
+        if (P) {
+          ok = word(QK_PUSH_CONST, d, -1, imm);
+          break;
+        }
+        // G: the constant travels inline in the program stream (no scalar load)
+        uint32_t cv[8];
+        ok = const_value(imm, cv);
+        if (!ok) break;
+        int n = 8;
+        while (n > 1 && cv[n - 1] == 0) n--;
+        if (n == 1 && cv[0] <= 0xFFFFu) {
+          ok = word(QK_PUSH_CONSTI, d, -1, cv[0]);
+        } else {
+          ok = word(QK_PUSH_CONSTW, d, n - 1, 0);
+          for (int l = 0; ok && l < n; l++) out.push_back(cv[l]);
+        }
+        break;
+      }
       case G_PUSH_TMP: ok = word(QK_PUSH_TMP, d, -1, imm); break;
       case G_PUSH_TMP_B: ok = word(QK_PUSH_TMP_BOOL, d, -1, imm); break;
       case G_STORE_TMP: ok = d == 0 && word(QK_STORE_TMP, 0, -1, imm); break;
@@ -452,14 +527,14 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
       case G_BITE: ok = word(QK_BITE, d, -1, 0); break;
       case G_BITE_EF: ok = word(QK_BITE_EF, d, -1, 0); break;
       // unsigned predicates / bitwise / ite are exact on canonical values of any width <= 256
-      case G_EQ: ok = imm >= 1 && word(QK_EQ, d, -1, 0); break;
-      case G_ULT: ok = imm >= 1 && word(QK_ULT, d, -1, 0); break;
-      case G_ULE: ok = imm >= 1 && word(QK_ULE, d, -1, 0); break;
-      case G_UGT: ok = imm >= 1 && word(QK_UGT, d, -1, 0); break;
-      case G_UGE: ok = imm >= 1 && word(QK_UGE, d, -1, 0); break;
-      case G_BAND: ok = word(QK_BAND, d, -1, 0); break;
-      case G_BOR: ok = word(QK_BOR, d, -1, 0); break;
-      case G_BXOR: ok = word(QK_BXOR, d, -1, 0); break;
+      case G_EQ: ok = imm >= 1 && binop(d, QK_EQ, QK_EQV, QK_EQC); break;
+      case G_ULT: ok = imm >= 1 && binop(d, QK_ULT, QK_ULTV); break;
+      case G_ULE: ok = imm >= 1 && binop(d, QK_ULE, QK_ULEV); break;
+      case G_UGT: ok = imm >= 1 && binop(d, QK_UGT, QK_UGTV); break;
+      case G_UGE: ok = imm >= 1 && binop(d, QK_UGE, QK_UGEV); break;
+      case G_BAND: ok = binop(d, QK_BAND, QK_BANDV, QK_BANDC); break;
+      case G_BOR: ok = binop(d, QK_BOR, QK_BORV, QK_BORC); break;
+      case G_BXOR: ok = binop(d, QK_BXOR, QK_BXORV, QK_BXORC); break;
       case G_ITE: ok = word(QK_ITE, d, -1, 0); break;
       case G_ITE_EF: ok = word(QK_ITE_EF, d, -1, 0); break;
       // signed predicates: at 256 bits the handler flips bit 255; below, flip bit W-1 of both
@@ -472,9 +547,9 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
         break;
       }
       // wrapping arithmetic: 256-bit handlers, results below 256 bits re-masked
-      case G_ADD: ok = imm <= 256 && word(QK_ADD, d, -1, 0) && mask(d - 1, imm); break;
-      case G_SUB: ok = imm <= 256 && word(QK_SUB, d, -1, 0) && mask(d - 1, imm); break;
-      case G_MUL: ok = imm <= 256 && word(QK_MUL, d, -1, 0) && mask(d - 1, imm); break;
+      case G_ADD: ok = imm <= 256 && binop(d, QK_ADD, QK_ADDV) && mask(d - 1, imm); break;
+      case G_SUB: ok = imm <= 256 && binop(d, QK_SUB, QK_SUBV) && mask(d - 1, imm); break;
+      case G_MUL: ok = imm <= 256 && binop(d, QK_MUL, QK_MULV, QK_MULC) && mask(d - 1, imm); break;
       case G_NEG: ok = imm <= 256 && word(QK_NEG, d, -1, 0) && mask(d, imm); break;
       case G_BNOT: ok = imm <= 256 && word(QK_BNOT, d, -1, 0) && mask(d, imm); break;
       // shifts by a constant amount (the previous instruction pushed it): in place on slot d-1
@@ -582,6 +657,7 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
     prev_d = (uint32_t)d;
     prev_imm = imm;
     prev_out = out_before;
+    prev_pre = op == G_PUSH_VAR ? pushed_pre : -1;
   }
   return x.consts.size() + extra.size() <= 0x10000u;
 }
@@ -798,6 +874,28 @@ static KArgs make_col_args(mq_ctx* c, mq_tapes* T, const mq_tapes::Variant& v) {
   return a;
 }
 
+// G programs stream through a 64-word VGPR window (gen_qsa.py NEXT_G): insert a REFILL word
+// wherever the next handler word and its inline data would not fit in the current window (the
+// refilled window starts right after the REFILL word).
+static void qsa_window_layout(const mq_ctx* c, std::vector<uint32_t>& prog) {
+  const std::vector<uint8_t>& data_words = c->qsa_data_words;
+  const uint32_t refill = c->qsa_off[1][c->qsa_index[1][QK_REFILL][0][0]] >> 2;
+  std::vector<uint32_t> out;
+  out.reserve(prog.size() + prog.size() / 48 + 2);
+  size_t pos = 0;
+  for (size_t i = 0; i < prog.size();) {
+    const size_t g = 1 + (size_t)data_words[prog[i] & 0xFFFFu];
+    if (pos + g > 63) {
+      out.push_back(refill);
+      pos = 0;
+    }
+    for (size_t j = 0; j < g && i + j < prog.size(); j++) out.push_back(prog[i + j]);
+    pos += g;
+    i += g;
+  }
+  prog.swap(out);
+}
+
 // (Re)translate the QSA-eligible tapes for the current model batch (variable rows, function
 // table): the P kernel when every variable a tape reads is preloaded, the G kernel otherwise.
 // If one tape does not translate, the whole group runs on the HIP C++ kernel for this batch.
@@ -808,11 +906,39 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
   std::vector<uint32_t> words[2], tr, extra;
   std::vector<GDesc> ds[2];
   int temps[2] = {0, 0};
+  // pass 1: tapes the P kernel takes; the others go to G, which preloads the (at most 8)
+  // variables of at most 256 bits those tapes push most often
+  std::vector<char> on_p(T->qct.size(), 0);
+  std::vector<int64_t> pushes(c->var_nl_h.size(), 0);
+  for (size_t i = 0; i < T->qct.size(); i++) {
+    on_p[i] = qsa_translate(c, 0, true, T->qct[i], nullptr, nullptr) ? 1 : 0;
+    if (on_p[i]) continue;
+    const auto& pr = T->qct[i].prog;
+    for (size_t pc = 0; pc < pr.size(); pc++) {
+      const uint32_t op = pr[pc] & 0xFFu, imm = pr[pc] >> 12;
+      if ((op == G_PUSH_VAR || op == G_PUSH_VAR_B) && imm < pushes.size() && c->var_nl_h[imm] <= 8) pushes[imm]++;
+      if (op == G_EXTRACT || op == G_CONCAT || op == G_SEXT || op == G_UF1 || op == G_UF2) pc++;
+    }
+  }
+  std::vector<int> order;
+  for (size_t v = 0; v < pushes.size(); v++)
+    if (pushes[v] > 0) order.push_back((int)v);
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return pushes[a] > pushes[b]; });
+  if (order.size() > (size_t)kQsaVars) order.resize(kQsaVars);
+  T->gpre.assign(c->var_nl_h.size(), -1);
+  const uint32_t zero_row = (uint32_t)(c->var_off_h.empty() ? 0 : c->var_off_h.back() + c->var_nl_h.back());
+  for (int j = 0; j < 64; j++) T->g_var_row[j] = zero_row;
+  for (size_t j = 0; j < order.size(); j++) {
+    const int v = order[j];
+    T->gpre[v] = (int)j;
+    for (uint32_t l = 0; l < c->var_nl_h[v]; l++) T->g_var_row[8 * j + l] = c->var_off_h[v] + l;
+  }
   for (size_t i = 0; i < T->qct.size(); i++) {
     int k = 0;
-    if (!qsa_translate(c, 0, true, T->qct[i], &tr, &extra)) {
+    if (!on_p[i] || !qsa_translate(c, 0, true, T->qct[i], &tr, &extra)) {
       k = 1;
-      if (!qsa_translate(c, 1, true, T->qct[i], &tr, &extra)) return MQ_OK;
+      if (!qsa_translate(c, 1, true, T->qct[i], &tr, &extra, &T->gpre)) return MQ_OK;
+      qsa_window_layout(c, tr);
     }
     GDesc d = T->qbase[i];
     d.prog_off = (uint32_t)words[k].size();
@@ -832,9 +958,19 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
       descs.push_back(d);
     }
     prog.insert(prog.end(), words[k].begin(), words[k].end());
-    const uint32_t endw = c->qsa_off[k][c->qsa_index[k][QK_END][0][0]] / 4;
-    prog.push_back(endw);
-    prog.push_back(endw);
+    const uint32_t endo = c->qsa_off[k][c->qsa_index[k][QK_END][0][0]];
+    const uint32_t endw = endo / 4;
+    if (k == 0) {   // P entries are (handler address, imm) pairs
+      for (int r = 0; r < 2; r++) {
+        prog.push_back(c->qsa_hbase_lo[0] + endo);
+        prog.push_back(0);
+      }
+    } else {
+      prog.push_back(endw);
+      prog.push_back(endw);
+    }
+    // G's window loads read up to 63 words past a program's last word
+    if (k == 1) prog.insert(prog.end(), 64, endw);
     T->q_count[k] = (int)ds[k].size();
     T->q_temps[k] = temps[k];
   }
@@ -922,7 +1058,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     q.early_exit = verdicts ? 0u : (uint32_t)c->early_exit;
     q.mode = verdicts ? 1u : 0u;
     q.lds_wave_bytes = (uint32_t)T->q_temps[k] * 2048u;
-    std::memcpy(q.var_row, c->qsa_var_row, sizeof(q.var_row));
+    std::memcpy(q.var_row, k == 0 ? c->qsa_var_row : T->g_var_row, sizeof(q.var_row));
     q.funcs = c->funcs.p;
     q.entry_ptr = c->entry_ptr.p;
     q.entry_words = c->entry_words.p;

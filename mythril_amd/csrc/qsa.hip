@@ -3,7 +3,8 @@
 // One workgroup = 4 waves = 256 candidate models; grid.y = tape groups.  See gen_qsa.py for
 // the register maps and the program encoding.
 //   qsa_kernel (P): the first 8 model variables preloaded in VGPRs (C2-shaped batches)
-//   qsg_kernel (G): variables pushed from HBM, model-function lookups (EVM-shaped batches)
+//   qsg_kernel (G): the 8 variables its tapes push most preloaded, the rest pushed from HBM,
+//                   model-function lookups (EVM-shaped batches)
 #include <hip/hip_runtime.h>
 
 #include "qs_launch.h"
@@ -15,14 +16,14 @@ __global__ __launch_bounds__(256) void qsa_kernel(const QArgs* __restrict__ args
   asm volatile(QSA_ASM_TEXT_P
                :
                : "s"(args), "s"(blockIdx.x), "s"(blockIdx.y), "v"(threadIdx.x)
-               : QSA_CLOBBERS);
+               : QSA_CLOBBERS_P);
 }
 
 __global__ __launch_bounds__(256) void qsg_kernel(const QArgs* __restrict__ args) {
   asm volatile(QSA_ASM_TEXT_G
                :
                : "s"(args), "s"(blockIdx.x), "s"(blockIdx.y), "v"(threadIdx.x)
-               : QSA_CLOBBERS);
+               : QSA_CLOBBERS_G);
 }
 
 hipError_t launch_qsa(int variant, const QArgs* d_args, unsigned gx, unsigned gy, size_t lds, hipStream_t st) {

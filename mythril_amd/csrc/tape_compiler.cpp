@@ -347,7 +347,11 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
       else if (n.nk == 2) {
         int a = nd_of(n.kid[0]), b = nd_of(n.kid[1]);
         int fwd = std::max(a, b + 1), bwd = std::max(b, a + 1);
-        if (n.rev_gop && bwd < fwd) {
+        // tie: put a variable leaf second, where the assembly interpreter fuses its push into
+        // the operation (gen_qsa.py ...V handlers)
+        auto is_var = [&](int c) { return !hoist[c] && B.nodes[c].leaf && B.nodes[c].gop == G_PUSH_VAR; };
+        const bool var_second = bwd == fwd && is_var(n.kid[0]) && !is_var(n.kid[1]);
+        if (n.rev_gop && (bwd < fwd || var_second)) {
           swap[x] = 1;
           need[x] = bwd;
         } else {
