@@ -698,9 +698,18 @@ def frame(variant, pfx, handlers, subs):
         "s_nop 1",
         "v_readfirstlane_b32 s34, v5",
         "s_nop 1",
+    ] + ([
+        # G: the workgroup's 4 waves share one 64-model tile (s96) and take tape groups
+        # 4*s97 + wave, so the model rows they push are fetched once per CU (qsa.hip remaps
+        # the grid so the groups of a tile run together on one XCD and share its L2)
+        "s_lshl_b32 s35, s96, 6",
+        "s_lshl_b32 s97, s97, 2",
+        "s_add_u32 s97, s97, s34",
+    ] if G else [
         "s_lshl_b32 s35, s96, 8",
         "s_lshl_b32 s36, s34, 6",
         "s_add_u32 s35, s35, s36",
+    ]) + [
         "s_cmp_ge_u32 s35, s29",
         f"s_cbranch_scc1 {pfx}_exit",
         "s_add_u32 s28, s98, s35",            # gfirst

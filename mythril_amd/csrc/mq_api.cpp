@@ -983,6 +983,18 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
   return MQ_OK;
 }
 
+// G kernel tape-group size.  Each wave evaluates its group on the 64 models of its workgroup's
+// tile; small groups put many waves on the same tile at once (model rows shared through L1/L2),
+// large ones amortise the per-wave preload of the 8 most pushed variables.  MQ_G_TPG overrides.
+static int64_t g_tapes_per_group(int64_t n, int64_t M) {
+  (void)M;
+  if (const char* e = std::getenv("MQ_G_TPG")) {
+    const long v = std::atol(e);
+    if (v > 0) return v;
+  }
+  return std::min<int64_t>(n, 16);
+}
+
 // Launch every evaluation kernel for a compiled batch: the assembly interpreter for the
 // QSA-eligible tapes (when the model batch fits its register file), the HIP C++ kernels for
 // the rest.  verdicts == nullptr -> first-hit mode into best.
@@ -1039,9 +1051,11 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
   for (int k = 0; use_qsa && k < 2; k++) {
     const int n = T->q_count[k];
     if (n <= 0) continue;
-    // grid = (256-model tiles) x (tape groups), groups sized for ~8k workgroups
+    // P: grid = (256-model tiles) x (tape groups), groups sized for ~8k workgroups.
+    // G: 64-model tiles, 4 tape groups per workgroup (one per wave), XCD-interleaved grid
+    //    (qsa.hip); groups of g_tapes_per_group() tapes.
     const int64_t tiles256 = (c->M + 255) / 256;
-    int64_t tpg = (int64_t(n) * tiles256 + 8191) / 8192;
+    int64_t tpg = k == 0 ? (int64_t(n) * tiles256 + 8191) / 8192 : g_tapes_per_group(n, c->M);
     tpg = std::max<int64_t>(1, std::min<int64_t>(tpg, n));
     QArgs q{};
     q.descs = T->qdescs.as<GDesc>() + (k == 0 ? 0 : T->q_count[0]);
@@ -1071,8 +1085,17 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       T->qargs_dev_copy[k] = q;
       T->qargs_valid[k] = true;
     }
-    const unsigned gx = (unsigned)tiles256;
-    const unsigned gy = (unsigned)((n + tpg - 1) / tpg);
+    unsigned gx = (unsigned)tiles256;
+    unsigned gy = (unsigned)((n + tpg - 1) / tpg);
+    if (k == 1) {
+      const int64_t groups = (n + tpg - 1) / tpg;
+      gx = 8u * (unsigned)((groups + 3) / 4);          // xcd + 8 * (workgroup's group quad)
+      gy = (unsigned)(((c->M + 63) / 64 + 7) / 8);     // tiles of 64 models, 8 per row
+      if (((c->M + 63) / 64 + 7) / 8 > 65535) {
+        g_last_error = "G kernel: more than 33.5M models in one launch (grid.y limit); shard the model axis";
+        return MQ_ERR_ARG;
+      }
+    }
     HIPCHK(start_timer());
     HIPCHK(launch_qsa(k, T->qargs[k].as<QArgs>(), gx, gy, (size_t)q.lds_wave_bytes * 4, st));
   }

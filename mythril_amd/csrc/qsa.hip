@@ -1,6 +1,7 @@
 // qsa.hip — the gfx950 threaded-code tape interpreters (generated assembly, gen_qsa.py) wrapped
 // in HIP kernels so they ship in libmq.so's fat binary and launch like any HIP kernel.
-// One workgroup = 4 waves = 256 candidate models; grid.y = tape groups.  See gen_qsa.py for
+// P: one workgroup = 4 waves = 256 candidate models, grid.y = tape groups.
+// G: one workgroup = 4 waves on the same 64 models, each wave its own tape group.  See gen_qsa.py for
 // the register maps and the program encoding.
 //   qsa_kernel (P): the first 8 model variables preloaded in VGPRs (C2-shaped batches)
 //   qsg_kernel (G): the 8 variables its tapes push most preloaded, the rest pushed from HBM,
@@ -19,10 +20,16 @@ __global__ __launch_bounds__(256) void qsa_kernel(const QArgs* __restrict__ args
                : QSA_CLOBBERS_P);
 }
 
+// G grid: blockIdx.x = xcd + 8 * g, blockIdx.y = t, gridDim.x a multiple of 8.  Workgroups are
+// dispatched round-robin over the 8 XCDs in linear order, so workgroup (t, g) runs on XCD
+// (linear id mod 8) = xcd next to the other groups g of the same 64-model tile 8t + xcd: the
+// tile's model rows are read from HBM once per XCD and then served by that XCD's L2.
 __global__ __launch_bounds__(256) void qsg_kernel(const QArgs* __restrict__ args) {
+  const unsigned tile = blockIdx.y * 8u + (blockIdx.x & 7u);
+  const unsigned grp = blockIdx.x >> 3;
   asm volatile(QSA_ASM_TEXT_G
                :
-               : "s"(args), "s"(blockIdx.x), "s"(blockIdx.y), "v"(threadIdx.x)
+               : "s"(args), "s"(tile), "s"(grp), "v"(threadIdx.x)
                : QSA_CLOBBERS_G);
 }
 
