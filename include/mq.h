@@ -253,6 +253,11 @@ int mq_tapes_info(mq_tapes* tapes, int32_t* n_asm, int32_t* n_generic_l8, int32_
    kernel for the current model batch.  Returns 0 or MQ_ERR_ARG. */
 int mq_tapes_qsa_split(mq_tapes* tapes, int32_t* n_p, int32_t* n_g, int32_t* live);
 
+/* After a launch: hoisted column programs evaluated by the general assembly kernel (qsg_kernel,
+   mode 3) for the current model batch, and whether that path ran (the others, and all of them
+   when it did not, run on the HIP C++ column kernel).  Introspection for tests and the bench. */
+int mq_tapes_column_split(mq_tapes* tapes, int32_t* n_asm, int32_t* live);
+
 /* Static algorithmic cost of a tape; -1 if malformed. */
 double mq_tape_alg_ops(const mq_tape_batch* batch, int32_t t);
 

@@ -636,6 +636,31 @@ def make_handlers(variant, pfx):
 
 
 # ---------------------------------------------------------------- kernel frame
+def store_column(pfx):
+    """G mode 3 (hoisted column programs, mq_api.cpp cq_prepare): write the program's value into
+    the model variable rows of the column, valid lanes only.  Descriptor: s82 = first row of the
+    target variable, s85 = its limbs, s86 = 1 for a Bool root (B(0) stored as 0/1).  A column is
+    not a (tape, model) pair: the pair count the tape end added is taken back."""
+    out = [f"{pfx}_store_column:",
+           "s_sub_u32 s40, s40, s38", "s_subb_u32 s41, s41, 0",
+           VMWAIT,
+           "s_mul_i32 s38, s82, s29", "s_mul_hi_u32 s39, s82, s29", "s_lshl_b64 s[38:39], s[38:39], 2",
+           "s_add_u32 s38, s38, s90", "s_addc_u32 s39, s39, s91",
+           "s_mov_b64 s[60:61], exec", "s_mov_b64 exec, s[62:63]",
+           "s_cmp_eq_u32 s86, 0", f"s_cbranch_scc1 {pfx}_col_value",
+           f"v_cndmask_b32_e64 v5, 0, 1, {B(0)}",
+           "global_store_dword v2, v5, s[38:39]",
+           f"s_branch {pfx}_col_done",
+           f"{pfx}_col_value:"]
+    for l in range(L):
+        out += [f"s_cmp_le_u32 s85, {l}", f"s_cbranch_scc1 {pfx}_col_done",
+                f"global_store_dword v2, {S(0, l)}, s[38:39]"]
+        if l < L - 1:
+            out += ["s_add_u32 s38, s38, s74", "s_addc_u32 s39, s39, s75"]
+    out += [f"{pfx}_col_done:", "s_mov_b64 exec, s[60:61]", f"s_branch {pfx}_next_tape"]
+    return out
+
+
 def frame(variant, pfx, handlers, subs):
     G = variant == "g"
     P = []
@@ -787,6 +812,10 @@ def frame(variant, pfx, handlers, subs):
         "s_mul_hi_u32 s61, s38, s87",
         "s_add_u32 s44, s44, s60",
         "s_addc_u32 s45, s45, s61",
+    ] + ([
+        "s_cmp_eq_u32 s31, 3",
+        f"s_cbranch_scc1 {pfx}_store_column",
+    ] if G else []) + [
         "s_cmp_eq_u32 s31, 1",
         f"s_cbranch_scc1 {pfx}_store_verdict",
         "s_cmp_eq_u64 s[34:35], 0",
@@ -811,6 +840,7 @@ def frame(variant, pfx, handlers, subs):
         "s_mov_b64 exec, s[62:63]",
         "global_store_byte v6, v5, s[38:39]",
         "s_mov_b64 exec, s[60:61]",
+    ] + ([f"s_branch {pfx}_next_tape"] + store_column(pfx) if G else []) + [
         f"{pfx}_next_tape:",
         "s_add_u32 s24, s24, 1",
         f"s_branch {pfx}_tape_loop",

@@ -56,6 +56,7 @@ struct DevBuf {
 
 // the assembly interpreter keeps temps in LDS (2 KB per temp per wave, 4 waves per workgroup)
 static constexpr int kQsaMaxTemps = 16;
+static constexpr int64_t kColAsmMinNodes = 32;   // hoisted columns on qsg_kernel from this size
 
 struct mq_ctx {
   int device = 0;
@@ -128,12 +129,25 @@ struct mq_tapes {
   bool qargs_valid[2] = {false, false};
   // batch-level hoisting: column programs evaluated once per model before the tapes, one
   // launch per (nesting level, kernel variant); GDesc.tape = the model variable written
+  // v8 begins with the v8q columns the G assembly interpreter can take (structurally); when
+  // their translation for the current model batch succeeds (cq_live) they run on qsg_kernel in
+  // mode 3 and the HIP C++ column kernel takes the rest of v8
   struct ColumnLevel {
     Variant v8, v16, v16k;
+    int v8q = 0;
+    int cq_begin = 0;   // first of the level's columns in cq_ct / cqdescs
   };
   std::vector<ColumnLevel> clevels;
   std::vector<int32_t> col_var, col_width;
   DevBuf cdescs, cprog, cconsts;
+  std::vector<CompiledTape> cq_ct;   // the G-eligible columns, level by level
+  std::vector<int32_t> cq_var;
+  std::vector<uint8_t> cq_bool;
+  uint64_t cq_gen = ~0ull;
+  bool cq_live = false;
+  int cq_temps = 0;
+  DevBuf cqdescs, cqprog, cqconsts, cqargs;
+  std::vector<QArgs> cqargs_host;   // what cqargs holds on the device, per level
 };
 
 static thread_local std::string g_last_error;
@@ -786,17 +800,36 @@ int mq_tapes_set_columns(mq_tapes* T, const mq_tape_batch* progs, const int32_t*
   }
   std::vector<uint32_t> prog, consts;
   std::vector<GDesc> descs;
+  // G assembly eligibility is structural here, as for tapes (mq_tapes_upload).  Short column
+  // programs stay on the HIP C++ column kernel: per program, qsg_kernel pays a descriptor load
+  // and a dependent program-window load, which a few-node column does not amortise
+  // (profiles/r01p_*: C3's 5.7-node columns took 45 ms on qsg_kernel vs 24 ms on the C++ kernel).
+  // MQ_G_COL_MIN_NODES overrides the threshold.
+  int64_t min_nodes = kColAsmMinNodes;
+  if (const char* e = std::getenv("MQ_G_COL_MIN_NODES")) min_nodes = std::atol(e);
+  std::vector<char> gq(n_columns, 0);
+  if (c->qsa_ready)
+    for (int k = 0; k < n_columns; k++)
+      gq[k] = ct[k].L == 8 && !ct[k].keccak && ct[k].n_temps <= kQsaMaxTemps && (int64_t)ct[k].n_nodes >= min_nodes &&
+              qsa_translate(c, 1, false, ct[k], nullptr, nullptr);
+  T->cq_ct.clear();
+  T->cq_var.clear();
+  T->cq_bool.clear();
+  T->cq_gen = ~0ull;
+  T->cq_live = false;
   T->clevels.resize((size_t)max_level + 1);
   for (int lv = 0; lv <= max_level; lv++) {
-    for (int pass = 0; pass < 3; pass++) {
-      mq_tapes::Variant& v = pass == 0 ? T->clevels[lv].v8 : (pass == 1 ? T->clevels[lv].v16 : T->clevels[lv].v16k);
-      v.L = pass == 0 ? 8 : 16;
+    T->clevels[lv].cq_begin = (int)T->cq_ct.size();
+    for (int pass = -1; pass < 3; pass++) {
+      mq_tapes::Variant& v = pass <= 0 ? T->clevels[lv].v8 : (pass == 1 ? T->clevels[lv].v16 : T->clevels[lv].v16k);
+      v.L = pass <= 0 ? 8 : 16;
       v.keccak = pass == 2;
-      v.begin = (int)descs.size();
+      if (pass != 0) v.begin = (int)descs.size();
       for (int k = 0; k < n_columns; k++) {
         const CompiledTape& x = ct[k];
         if (level[k] != lv) continue;
-        if (pass == 0 && !(x.L == 8 && !x.keccak)) continue;
+        if (pass == -1 && !gq[k]) continue;
+        if (pass == 0 && !(x.L == 8 && !x.keccak && !gq[k])) continue;
         if (pass == 1 && !(x.L == 16 && !x.keccak)) continue;
         if (pass == 2 && !x.keccak) continue;
         GDesc d{};
@@ -813,8 +846,14 @@ int mq_tapes_set_columns(mq_tapes* T, const mq_tape_batch* progs, const int32_t*
         descs.push_back(d);
         v.max_temps = std::max(v.max_temps, x.n_temps);
         v.max_depth = std::max(v.max_depth, x.depth);
+        if (pass == -1) {
+          T->cq_ct.push_back(x);
+          T->cq_var.push_back(var_index[k]);
+          T->cq_bool.push_back(T->col_width[k] == 0 ? 1 : 0);
+        }
       }
-      v.count = (int)descs.size() - v.begin;
+      if (pass == -1) T->clevels[lv].v8q = (int)descs.size() - v.begin;
+      if (pass != -1) v.count = (int)descs.size() - v.begin;
     }
   }
   consts.resize(consts.size() + 16, 0);
@@ -983,6 +1022,58 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
   return MQ_OK;
 }
 
+// Translate the G-eligible column programs for the current model batch (variable rows): one
+// program segment and descriptor list, levels contiguous.  GDesc for mode 3: tape = first row
+// of the target variable, n_temps = its limbs, depth = Bool root (gen_qsa.py store_column).
+// If one column does not translate, all columns run on the HIP C++ column kernel.
+static int cq_prepare(mq_ctx* c, mq_tapes* T) {
+  if (T->cq_gen == c->models_gen) return MQ_OK;
+  T->cq_gen = c->models_gen;
+  T->cq_live = false;
+  if (T->cq_ct.empty()) return MQ_OK;
+  std::vector<uint32_t> prog, consts, tr, extra;
+  std::vector<GDesc> descs;
+  int temps = 0;
+  for (size_t i = 0; i < T->cq_ct.size(); i++) {
+    const CompiledTape& x = T->cq_ct[i];
+    if (!qsa_translate(c, 1, true, x, &tr, &extra)) return MQ_OK;
+    qsa_window_layout(c, tr);
+    const int v = T->cq_var[i];
+    GDesc d{};
+    d.prog_off = (uint32_t)prog.size();
+    d.prog_len = (uint32_t)tr.size();
+    d.tape = c->var_off_h[v];
+    d.const_base = (uint32_t)consts.size();
+    d.n_nodes = x.n_nodes;
+    d.n_temps = c->var_nl_h[v];
+    d.depth = T->cq_bool[i];
+    d.alg_ops = (uint32_t)std::min(x.alg_ops, 4.0e9);
+    prog.insert(prog.end(), tr.begin(), tr.end());
+    consts.insert(consts.end(), x.consts.begin(), x.consts.end());
+    consts.insert(consts.end(), extra.begin(), extra.end());
+    descs.push_back(d);
+    temps = std::max(temps, x.n_temps);
+  }
+  const uint32_t endw = c->qsa_off[1][c->qsa_index[1][QK_END][0][0]] / 4;
+  prog.insert(prog.end(), 66, endw);   // the window loads read up to 63 words past the last END
+  consts.resize(consts.size() + 16, 0);
+  HIPCHK(T->cqdescs.upload(descs.data(), descs.size(), c->stream));
+  HIPCHK(T->cqprog.upload(prog.data(), prog.size(), c->stream));
+  HIPCHK(T->cqconsts.upload(consts.data(), consts.size(), c->stream));
+  HIPCHK(T->cqargs.ensure(sizeof(QArgs) * T->clevels.size()));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  T->cqargs_host.assign(T->clevels.size(), QArgs{});
+  T->cq_temps = temps;
+  T->cq_live = true;
+  return MQ_OK;
+}
+
+static mq_tapes::Variant cut_front(mq_tapes::Variant v, int n) {
+  v.begin += n;
+  v.count -= n;
+  return v;
+}
+
 // G kernel tape-group size.  Each wave evaluates its group on the 64 models of its workgroup's
 // tile; small groups put many waves on the same tile at once (model rows shared through L1/L2),
 // large ones amortise the per-wave preload of the 8 most pushed variables.  MQ_G_TPG overrides.
@@ -1035,8 +1126,60 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       return MQ_ERR_ARG;
     }
   }
-  for (const auto& lv : T->clevels) {
-    for (const mq_tapes::Variant* v : {&lv.v8, &lv.v16, &lv.v16k}) {
+  bool use_cq = c->qsa_ready && c->use_asm && !T->cq_ct.empty();
+  if (use_cq) {
+    const int rc = cq_prepare(c, T);
+    if (rc) return rc;
+    use_cq = T->cq_live;
+  } else {
+    T->cq_live = false;   // (re-translated when the assembly path is enabled again)
+    T->cq_gen = ~0ull;
+  }
+  const uint32_t zero_row = (uint32_t)(c->var_off_h.empty() ? 0 : c->var_off_h.back() + c->var_nl_h.back());
+  for (size_t li = 0; li < T->clevels.size(); li++) {
+    const auto& lv = T->clevels[li];
+    const mq_tapes::Variant v8 = use_cq ? cut_front(lv.v8, lv.v8q) : lv.v8;
+    if (use_cq && lv.v8q > 0) {
+      // the level's G columns on qsg_kernel, mode 3 (no preloaded variables)
+      const int n = lv.v8q;
+      const int64_t tpg = std::max<int64_t>(1, std::min<int64_t>(g_tapes_per_group(n, c->M), n));
+      QArgs q{};
+      q.descs = T->cqdescs.as<GDesc>() + lv.cq_begin;
+      q.prog = T->cqprog.p;
+      q.consts = T->cqconsts.p;
+      q.vars = c->vars.p;
+      q.best = best;
+      q.counters = c->counters.as<unsigned long long>();
+      q.verdicts = nullptr;
+      q.M = (uint32_t)c->M;
+      q.index_base = (uint32_t)c->index_base;
+      q.n_desc = (uint32_t)n;
+      q.tapes_per_group = (uint32_t)tpg;
+      q.early_exit = 0;
+      q.mode = 3;
+      q.lds_wave_bytes = (uint32_t)T->cq_temps * 2048u;
+      for (int j = 0; j < 64; j++) q.var_row[j] = zero_row;
+      q.funcs = c->funcs.p;
+      q.entry_ptr = c->entry_ptr.p;
+      q.entry_words = c->entry_words.p;
+      q.else_words = c->else_words.p;
+      q.n_funcs = (uint32_t)c->n_funcs;
+      QArgs* dq = T->cqargs.as<QArgs>() + li;
+      if (std::memcmp(&T->cqargs_host[li], &q, sizeof(QArgs)) != 0) {
+        HIPCHK(hipMemcpyAsync(dq, &q, sizeof(QArgs), hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));  // q is host memory
+        T->cqargs_host[li] = q;
+      }
+      const int64_t groups = (n + tpg - 1) / tpg;
+      const int64_t rows = ((c->M + 63) / 64 + 7) / 8;
+      if (rows > 65535) {
+        g_last_error = "G kernel: more than 33.5M models in one launch (grid.y limit); shard the model axis";
+        return MQ_ERR_ARG;
+      }
+      HIPCHK(start_timer());
+      HIPCHK(launch_qsa(1, dq, 8u * (unsigned)((groups + 3) / 4), (unsigned)rows, (size_t)q.lds_wave_bytes * 4, st));
+    }
+    for (const mq_tapes::Variant* v : {&v8, &lv.v16, &lv.v16k}) {
       if (v->count <= 0) continue;
       KArgs a = make_col_args(c, T, *v);
       const size_t scratch_bytes = (size_t)a.grid * (size_t)a.tmp_words_per_wave * 4;
@@ -1271,6 +1414,13 @@ int mq_tapes_qsa_split(mq_tapes* T, int32_t* n_p, int32_t* n_g, int32_t* live) {
   if (n_p) *n_p = T->qsa_live ? T->q_count[0] : 0;
   if (n_g) *n_g = T->qsa_live ? T->q_count[1] : 0;
   if (live) *live = T->qsa_live ? 1 : 0;
+  return MQ_OK;
+}
+
+int mq_tapes_column_split(mq_tapes* T, int32_t* n_asm, int32_t* live) {
+  if (!T) return MQ_ERR_ARG;
+  if (n_asm) *n_asm = T->cq_live ? (int32_t)T->cq_ct.size() : 0;
+  if (live) *live = T->cq_live ? 1 : 0;
   return MQ_OK;
 }
 

@@ -60,6 +60,7 @@ def load_library(path: str = LIB_PATH):
         L.mq_kernel_times.argtypes = [P, C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_int32), C.c_int]
         L.mq_tapes_info.argtypes = [P] + [C.POINTER(C.c_int32)] * 3
         L.mq_tapes_qsa_split.argtypes = [P] + [C.POINTER(C.c_int32)] * 3
+        L.mq_tapes_column_split.argtypes = [P] + [C.POINTER(C.c_int32)] * 2
         L.mq_eval_verdicts.argtypes = [P, C.POINTER(MqTapeBatch), C.POINTER(C.c_uint8), C.POINTER(C.c_int32)]
         L.mq_eval_tapes_verdicts.argtypes = [P, P, C.POINTER(C.c_uint8), C.POINTER(C.c_int32)]
         L.mq_tapes_set_columns.argtypes = [P, C.POINTER(MqTapeBatch), C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_int32]
@@ -159,6 +160,12 @@ class CompiledTapes:
         a, b, c = C.c_int32(), C.c_int32(), C.c_int32()
         _check(self.ev.lib.mq_tapes_qsa_split(self.handle, C.byref(a), C.byref(b), C.byref(c)), "mq_tapes_qsa_split")
         return a.value, b.value, bool(c.value)
+
+    def column_asm_split(self):
+        """After a launch: (hoisted columns on the general assembly kernel, whether that path ran)."""
+        a, b = C.c_int32(), C.c_int32()
+        _check(self.ev.lib.mq_tapes_column_split(self.handle, C.byref(a), C.byref(b)), "mq_tapes_column_split")
+        return a.value, bool(b.value)
 
     def free(self) -> None:
         if self.handle:

@@ -341,8 +341,13 @@ def test_c5_deep_tapes_match_oracle(evaluator):
 
 
 # ---------------------------------------------------------------- batch-level hoisting (column programs)
-def test_c3_hoisted_columns_match_unhoisted_oracle(evaluator):
+@pytest.mark.parametrize("col_min_nodes", ["0", None])
+def test_c3_hoisted_columns_match_unhoisted_oracle(evaluator, monkeypatch, col_min_nodes):
+    """col_min_nodes "0": every column on the G assembly kernel (mode 3); None: the default split
+    (short columns on the HIP C++ column kernel)."""
     from mythril_amd.synth_evm import c3_workload
+    if col_min_nodes is not None:
+        monkeypatch.setenv("MQ_G_COL_MIN_NODES", col_min_nodes)
     plain = c3_workload(60, 3000, seed=3, planted_frac=0.3)
     tb, mb, exp, _ = c3_workload(60, 3000, seed=3, planted_frac=0.3, hoist=True)
     assert tb.columns.n > 0
@@ -352,11 +357,23 @@ def test_c3_hoisted_columns_match_unhoisted_oracle(evaluator):
     fh = evaluator.first_hit(ct)
     ref, _ = cref.first_hit(plain[0], plain[1])
     assert (ref == exp).all() and (fh == ref).all(), np.flatnonzero(fh != ref)[:10]
+    n_cols_asm, cols_live = ct.column_asm_split()
+    if col_min_nodes == "0":
+        assert cols_live and n_cols_asm >= 0.5 * tb.columns.n, (n_cols_asm, tb.columns.n)
+    vref = cref.verdicts(plain[0], plain[1])
     v, _ = evaluator.verdicts(ct)
-    assert (v == cref.verdicts(plain[0], plain[1])).all()
+    assert (v == vref).all()
+    # the same columns on the HIP C++ column kernel
+    evaluator.use_asm(False)
+    try:
+        v2, _ = evaluator.verdicts(ct)
+        assert ct.column_asm_split() == (0, False) and (v2 == vref).all()
+    finally:
+        evaluator.use_asm(True)
 
 
-def test_hoisting_nested_levels_on_gpu(evaluator):
+def test_hoisting_nested_levels_on_gpu(evaluator, monkeypatch):
+    monkeypatch.setenv("MQ_G_COL_MIN_NODES", "0")
     from mythril_amd import smt as S
     from mythril_amd.lower import lower_batch, serialize_models
     from mythril_amd.smt_model import Model
@@ -372,9 +389,11 @@ def test_hoisting_nested_levels_on_gpu(evaluator):
     assert tb.columns.n >= 2 and tb.columns.level.max() >= 1
     tb2, syms2, _ = lower_batch(roots)
     evaluator.upload_models(serialize_models(models, syms))
-    v, fh = evaluator.verdicts(tb)
+    ct = evaluator.compile(tb)
+    v, fh = evaluator.verdicts(ct)
     ref = cref.verdicts(tb2, serialize_models(models, syms2))
     assert (v == ref).all()
+    assert ct.column_asm_split()[1]
 
 
 def test_c4_hoisted_in_kernel_keccak(evaluator):
