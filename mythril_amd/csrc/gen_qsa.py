@@ -13,15 +13,17 @@ Two variants are generated from the same handler code (one asm statement each, l
 
   P ("preload", qsa_kernel):  the wave's 64 models' first 8 variables are preloaded into VGPRs
      once per workgroup; PUSH_VAR is a register copy.  C2-shaped batches.
-  G ("general", qsg_kernel):  no preload; variables are pushed from the model rows in HBM
-     (PUSH_MEM: the loads are issued by the push and waited for by the first consumer), and
-     v[8:71] are the work registers of the table-lookup subroutine (UF1).  EVM-shaped batches.
+  G ("general", qsg_kernel):  the 4 variables the batch pushes most preloaded, the others
+     pushed from the model rows in HBM (PUSH_MEM: the loads are issued by the push and waited
+     for by the first consumer); table-lookup subroutine (UF1); 128 VGPRs so 4 waves per SIMD
+     hide the push latency.  EVM-shaped batches and hoisted column programs (mode 3).
 
 Register map (both):
   VGPR  v1       LDS temp address (wave base + lane*8)
         v2       model byte offset m*4 (clamped)          v3 sign mask of signed division
         v[4:7]   scratch / MUL accumulator / division step
-        v[8:71]  P: preloaded variables V[v][l] = v(8+8v+l);  G: UF1 work registers
+        v[8:71]  P: preloaded variables V[v][l] = v(8+8v+l), v < 8
+                 G: v[8:39] preloaded variables (v < 4), v[40:63] UF1 work, v64 program window
         v[72:119] operand stack S[d][l] = v(72+8d+l), d < 6 (256-bit values, 8 x u32 limbs)
         v[120:127] MUL column results / division + lookup operand
   SGPR  s[48:59] Bool stack B[d] = s[48+2d : 49+2d] as 64-lane masks (Bool ops are SALU)
@@ -42,13 +44,15 @@ Outputs: qsa_gen.inc (the two asm texts as C string literals + clobber list) and
 from __future__ import annotations
 
 import os
+import re
 import sys
 
 D = 6          # stack slots
 NV = 8         # preloaded variables (P)
+NVG = 4        # preloaded variables (G): v[8:39], so the kernel fits 128 VGPRs (4 waves / SIMD)
 L = 8          # limbs (256-bit)
 VBASE, SBASE, TBASE = 8, 72, 120
-UBASE = 128    # G: UF1 work registers v[128:151]
+UBASE = 40     # G: UF1 work registers v[40:63]
 BBASE = 48
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -90,7 +94,7 @@ def W2(k):
 # per node.  s[14:15] = byte address of the window, s16 = lane of the next word.  The translator
 # places a REFILL word wherever the window runs out (the next window starts right after it) and
 # never splits a PUSH_CONSTW from its inline data words.
-WIN = "v152"
+WIN = "v64"
 NEXT_G = [
     f"v_readlane_b32 s17, {WIN}, s16",
     "s_add_u32 s16, s16, 1",
@@ -379,7 +383,7 @@ def sub_udiv32(pfx):
 
 def sub_uf1(pfx):
     """Arity-1 model function lookup (UF / as-array select, z3 completion: the else value when no
-    entry matches): key W[0..7] (canonical), s98 = function id; result in v[128:135].
+    entry matches): key W[0..7] (canonical), s98 = function id; result in v[UBASE:UBASE+7].
     FuncDev (qs_launch.h) of the function gives nl_a0 / nl_res / stride and the offsets of its
     entry rows, per-model entry ranges (entry_ptr) and SoA else block.  Per lane the entries are
     scanned in order and the first match wins (mq.h model layout); the wave loops over the
@@ -462,7 +466,15 @@ def sub_uf1(pfx):
             "s_mov_b64 exec, s[60:61]",
             f"{P}_uf_ret:",
             "s_setpc_b64 s[76:77]"]
-    return out
+    # the lookup's pointer / match registers were written as v128..v151: move them to UBASE + k
+    def remap(line):
+        line = re.sub(r"v\[(\d+):(\d+)\]", lambda m: f"v[{fix(int(m.group(1)))}:{fix(int(m.group(2)))}]", line)
+        return re.sub(r"\bv(\d+)\b", lambda m: f"v{fix(int(m.group(1)))}", line)
+    return [remap(x) for x in out]
+
+
+def fix(r):
+    return UBASE + r - 128 if 128 <= r < 152 else r
 
 
 # ---------------------------------------------------------------- handler table
@@ -481,7 +493,7 @@ def make_handlers(variant, pfx):
     # ---- leaves
     for d in range(D):
         # preloaded variables (P: the batch's first 8; G: the 8 its tapes push most)
-        for v in range(NV):
+        for v in range(NVG if G else NV):
             H(("PUSH_VAR", d, v), [f"v_mov_b64 {S2(d, l)}, {V2(v, l)}" for l in range(0, L, 2)], reads_stack=False)
             H(("PUSH_VARB", d, v), [f"v_cmp_ne_u32_e64 {B(d)}, 0, v{VBASE + 8 * v}", "s_nop 3"], reads_stack=False)
         if G:
@@ -597,7 +609,7 @@ def make_handlers(variant, pfx):
             H(("UF1", d), copy_to_w(d) + ["s_mov_b32 s98, s17", f"s_call_b64 s[76:77], {pfx}_sub_uf1"]
               + [f"v_mov_b64 {S2(d, l)}, v[{UBASE + l}:{UBASE + 1 + l}]" for l in range(0, L, 2)])
             H(("UF1B", d), copy_to_w(d) + ["s_mov_b32 s98, s17", f"s_call_b64 s[76:77], {pfx}_sub_uf1",
-                                            "v_and_b32 v4, 1, v128", f"v_cmp_ne_u32_e64 {B(d)}, 0, v4", "s_nop 3"])
+                                            f"v_and_b32 v4, 1, v{UBASE}", f"v_cmp_ne_u32_e64 {B(d)}, 0, v4", "s_nop 3"])
     # ---- P: right operand a constant, used straight from SGPRs (one SGPR source per VALU
     # instruction; ADD/SUB/compares would need a second one for the carry and keep the push)
     if not G:
@@ -615,7 +627,7 @@ def make_handlers(variant, pfx):
     if True:
         for d in range(1, D):
             a = d - 1
-            for v in range(NV):
+            for v in range(NVG if G else NV):
                 def vl(l, v=v):
                     return f"v{VBASE + 8 * v + l}"
                 H(("ADDV", d, v), carry_chain(lambda l: f"v_add_co_u32 {S(a, l)}, vcc, {S(a, l)}, {vl(l)}",
@@ -756,7 +768,7 @@ def frame(variant, pfx, handlers, subs):
     if True:
         # preload variables: 64 limb rows (row index table at args+0x60; the host points missing
         # limbs / vars at an all-zero row)
-        for c in range(4):
+        for c in range(NVG * L // 16 if G else NV * L // 16):
             P += [f"s_load_dwordx16 s[64:79], s[10:11], {0x60 + 64 * c:#x}", "s_waitcnt lgkmcnt(0)"]
             for j in range(16):
                 idx = 16 * c + j
@@ -879,7 +891,7 @@ VARIANTS = (("p", ".Lqsa", "QSA_ASM_TEXT_P", "P"), ("g", ".Lqsg", "QSA_ASM_TEXT_
 def main():
     sclob = [f'"s{i}"' for i in range(10, 100) if i not in (32, 33)] + ['"vcc"', '"scc"', '"memory"']
     clob = {"p": [f'"v{i}"' for i in range(1, 128)] + sclob,          # 128 VGPRs: 4 waves / SIMD
-            "g": [f'"v{i}"' for i in range(1, 153)] + sclob}   # + UF1 work, window: 3 waves / SIMD
+            "g": [f'"v{i}"' for i in range(1, 128)] + sclob}  # 4 preloaded vars, UF1 work, window: 4 waves / SIMD
     gen = {}
     for variant, pfx, macro, suffix in VARIANTS:
         hs, subs = make_handlers(variant, pfx)
@@ -897,7 +909,7 @@ def main():
     with open(os.path.join(HERE, "qsa_table.h"), "w") as f:
         f.write("// GENERATED by gen_qsa.py — handler enumerations of the QSA interpreters\n")
         f.write("#ifndef MQ_QSA_TABLE_H\n#define MQ_QSA_TABLE_H\nnamespace mq {\n")
-        f.write(f"constexpr int kQsaStack = {D};\nconstexpr int kQsaVars = {NV};\nconstexpr int kQsaSel = {L};\n")
+        f.write(f"constexpr int kQsaStack = {D};\nconstexpr int kQsaVars = {NV};\nconstexpr int kQsaVarsG = {NVG};\nconstexpr int kQsaSel = {L};\n")
         f.write("enum QsaKind {\n" + "".join(f"  QK_{n},\n" for n in names) + "  QK_COUNT\n};\n")
         f.write("struct QsaHandlerKey { int kind, d, v; };\n")
         for variant, (hs, lines, macro, suffix) in gen.items():

@@ -963,7 +963,7 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
   for (size_t v = 0; v < pushes.size(); v++)
     if (pushes[v] > 0) order.push_back((int)v);
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return pushes[a] > pushes[b]; });
-  if (order.size() > (size_t)kQsaVars) order.resize(kQsaVars);
+  if (order.size() > (size_t)kQsaVarsG) order.resize(kQsaVarsG);
   T->gpre.assign(c->var_nl_h.size(), -1);
   const uint32_t zero_row = (uint32_t)(c->var_off_h.empty() ? 0 : c->var_off_h.back() + c->var_nl_h.back());
   for (int j = 0; j < 64; j++) T->g_var_row[j] = zero_row;
