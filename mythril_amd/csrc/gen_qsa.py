@@ -195,29 +195,37 @@ def carry_chain(first, rest, n=L):
 def mul_body(d, bl=None):
     """S[d-1] = S[d-1] * b mod 2^256 (b = slot d, or bl(j) = register of limb j): product
     scanning (Comba) columns 0..7.  A column's state is a 64-bit accumulator pair (v_mad_u64_u32
-    with carry-out) plus an overflow word; the pairs alternate between v[4:5] and v[6:7] and the
-    overflow of the column in one pair is accumulated directly in the high word of the other, so
-    a column ends with two moves (result word out, high word down).  Carries are added through
-    three rotating SGPR pairs so every VALU carry read is >= 2 instructions after its write; each
-    column's first carry-add resets the overflow word; column 7 keeps only its low word."""
+    with carry-out) plus an overflow word accumulated directly in the high word of the NEXT
+    column's pair.  Even columns k accumulate in (T(k), T(k+1)), so their result word is already
+    in place and only the high word moves down into v4; odd columns accumulate in v[4:5] and move
+    result and high word out (T(k), T(k+1)): 16 moves per multiply instead of 20.  Carries are
+    added through three rotating SGPR pairs so every VALU carry read is >= 2 instructions after
+    its write; each column's first carry-add resets the overflow word; column 7 keeps only its
+    low word."""
     a = d - 1
     bl = bl or (lambda j: S(d, j))
     C = ["s[34:35]", "s[36:37]", "s[38:39]"]
-    PAIRS = (("v[4:5]", "v4", "v5"), ("v[6:7]", "v6", "v7"))
-    out = [f"v_mad_u64_u32 v[4:5], s[60:61], {S(a, 0)}, {bl(0)}, 0",
-           f"v_mov_b32 {T(0)}, v4", "v_mov_b32 v6, v5", "v_mov_b32 v7, 0"]
+
+    def pair(k):   # (pair, lo, hi) of column k's accumulator
+        if k % 2 == 0:
+            return f"v[{TBASE + k}:{TBASE + k + 1}]", T(k), T(k + 1)
+        return "v[4:5]", "v4", "v5"
+
+    p0, lo0, hi0 = pair(0)
+    out = [f"v_mad_u64_u32 {p0}, s[60:61], {S(a, 0)}, {bl(0)}, 0",
+           f"v_mov_b32 v4, {hi0}", "v_mov_b32 v5, 0"]
     for k in range(1, L):
-        pair, lo, hi = PAIRS[k % 2]
-        _, olo, ohi = PAIRS[(k + 1) % 2]   # next column's pair; its high word is our overflow
+        pr, lo, hi = pair(k)
         prods = [(i, k - i) for i in range(k + 1)]
         if k == L - 1:
             # last column: only the low word matters, no carry tracking
             for i, j in prods:
-                out.append(f"v_mad_u64_u32 {pair}, s[60:61], {S(a, i)}, {bl(j)}, {pair}")
+                out.append(f"v_mad_u64_u32 {pr}, s[60:61], {S(a, i)}, {bl(j)}, {pr}")
             out += [f"v_mov_b64 {S2(a, l)}, v[{TBASE + l}:{TBASE + l + 1}]" for l in range(0, 6, 2)]
             out += [f"v_mov_b32 {S(a, 6)}, {T(6)}", f"v_mov_b32 {S(a, 7)}, {lo}"]
             break
-        mads = [f"v_mad_u64_u32 {pair}, {C[t % 3]}, {S(a, i)}, {bl(j)}, {pair}" for t, (i, j) in enumerate(prods)]
+        _, _, ohi = pair(k + 1)            # next column's pair; its high word is our overflow
+        mads = [f"v_mad_u64_u32 {pr}, {C[t % 3]}, {S(a, i)}, {bl(j)}, {pr}" for t, (i, j) in enumerate(prods)]
         adds = [f"v_addc_co_u32_e64 {ohi}, s[60:61], 0, {'0' if t == 0 else ohi}, {C[t % 3]}"
                 for t in range(len(prods))]
         seq = []
@@ -233,7 +241,10 @@ def mul_body(d, bl=None):
         else:
             seq += tail
         out += seq
-        out += [f"v_mov_b32 {T(k)}, {lo}", f"v_mov_b32 {olo}, {hi}"]
+        if k % 2 == 0:
+            out += [f"v_mov_b32 v4, {hi}"]                           # result already in T(k)
+        else:
+            out += [f"v_mov_b32 {T(k)}, v4", f"v_mov_b32 {T(k + 1)}, v5"]
     return out
 
 
