@@ -49,7 +49,8 @@ import sys
 
 D = 6          # stack slots
 NV = 8         # preloaded variables (P)
-NVG = 4        # preloaded variables (G): v[8:39], so the kernel fits 128 VGPRs (4 waves / SIMD)
+NVG = 4        # preloaded variables (G); 0 selects the compact G layout (set_layout): 96 VGPRs,
+               # 5 waves / SIMD.  4 = v[8:39] preloaded in a 128-VGPR kernel (4 waves / SIMD)
 L = 8          # limbs (256-bit)
 VBASE, SBASE, TBASE = 8, 72, 120
 UBASE = 40     # G: UF1 work registers v[40:63]
@@ -95,7 +96,7 @@ def W2(k):
 # places a REFILL word wherever the window runs out (the next window starts right after it) and
 # never splits a PUSH_CONSTW from its inline data words.
 WIN = "v64"
-NEXT_G = [
+NEXT_G_TEMPLATE = [
     f"v_readlane_b32 s17, {WIN}, s16",
     "s_add_u32 s16, s16, 1",
     "s_nop 2",                      # VALU SGPR write -> SALU read
@@ -106,6 +107,7 @@ NEXT_G = [
     "s_addc_u32 s19, s13, 0",
     "s_setpc_b64 s[18:19]",
 ]
+NEXT_G = list(NEXT_G_TEMPLATE)
 
 
 # P: two-word program entries (absolute low 32 bits of the handler address, immediate),
@@ -899,12 +901,28 @@ def frame(variant, pfx, handlers, subs):
 VARIANTS = (("p", ".Lqsa", "QSA_ASM_TEXT_P", "P"), ("g", ".Lqsg", "QSA_ASM_TEXT_G", "G"))
 
 
+def set_layout(variant):
+    """Register map of the variant being generated (the body functions read these globals).
+    P and G with preloads: the map in the module docstring.  Compact G (NVG = 0): UF1 work
+    v[8:31], program window v32, stack v[40:87], T/W v[88:95] -> 96 VGPRs."""
+    global SBASE, TBASE, UBASE, WIN, NEXT_G
+    if variant == "g" and NVG == 0:
+        SBASE, TBASE, UBASE, WIN = 40, 88, 8, "v32"
+    else:
+        SBASE, TBASE, UBASE, WIN = 72, 120, 40, "v64"
+    NEXT_G = [ln.replace("v64", WIN) if ln.startswith("v_readlane") else ln for ln in NEXT_G_TEMPLATE]
+
+
+def vgprs(variant):
+    return 96 if (variant == "g" and NVG == 0) else 128
+
+
 def main():
     sclob = [f'"s{i}"' for i in range(10, 100) if i not in (32, 33)] + ['"vcc"', '"scc"', '"memory"']
-    clob = {"p": [f'"v{i}"' for i in range(1, 128)] + sclob,          # 128 VGPRs: 4 waves / SIMD
-            "g": [f'"v{i}"' for i in range(1, 128)] + sclob}  # 4 preloaded vars, UF1 work, window: 4 waves / SIMD
+    clob = {v: [f'"v{i}"' for i in range(1, vgprs(v))] + sclob for v in ("p", "g")}
     gen = {}
     for variant, pfx, macro, suffix in VARIANTS:
+        set_layout(variant)
         hs, subs = make_handlers(variant, pfx)
         gen[variant] = (hs, frame(variant, pfx, hs, subs), macro, suffix)
     with open(os.path.join(HERE, "qsa_gen.inc"), "w") as f:
