@@ -634,6 +634,18 @@ def make_handlers(variant, pfx):
                 H((nm, d), ld + [f"{ins} {S(a, l)}, {cl(l)}, {S(a, l)}" for l in range(L)])
             H(("MULC", d), ld + mul_body(d, cl))
             H(("EQC", d), ld + eq_body(d, cl))
+            # carry chains and compares read VCC / a carry SGPR besides their operands: the
+            # constant goes to T first (one dispatch and no stack copy instead of PUSH_CONST)
+            tl = [f"v_mov_b64 v[{TBASE + l}:{TBASE + l + 1}], s[{64 + l}:{65 + l}]" for l in range(0, L, 2)]
+            H(("ADDC", d), ld + tl + carry_chain(lambda l: f"v_add_co_u32 {S(a, l)}, vcc, {S(a, l)}, {T(l)}",
+                                                 lambda l: f"v_addc_co_u32 {S(a, l)}, vcc, {S(a, l)}, {T(l)}, vcc"))
+            H(("SUBC", d), ld + tl + carry_chain(lambda l: f"v_sub_co_u32 {S(a, l)}, vcc, {S(a, l)}, {T(l)}",
+                                                 lambda l: f"v_subb_co_u32 {S(a, l)}, vcc, {S(a, l)}, {T(l)}, vcc"))
+            xa = (lambda l: S(a, l))
+            H(("ULTC", d), ld + tl + lt_chain(xa, T, B(a)))
+            H(("UGTC", d), ld + tl + lt_chain(T, xa, B(a)))
+            H(("ULEC", d), ld + tl + lt_chain(T, xa, "s[38:39]") + ["s_nop 3", f"s_not_b64 {B(a)}, s[38:39]"])
+            H(("UGEC", d), ld + tl + lt_chain(xa, T, "s[38:39]") + ["s_nop 3", f"s_not_b64 {B(a)}, s[38:39]"])
     # ---- (last: these handlers never branch, so the subroutine calls above stay in s_call range)
     # ---- binary ops whose right operand is a preloaded variable (the translator fuses
     # PUSH_VAR v at slot d with the consuming op at d: no stack copy, one dispatch less)

@@ -542,10 +542,10 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
       case G_BITE_EF: ok = word(QK_BITE_EF, d, -1, 0); break;
       // unsigned predicates / bitwise / ite are exact on canonical values of any width <= 256
       case G_EQ: ok = imm >= 1 && binop(d, QK_EQ, QK_EQV, QK_EQC); break;
-      case G_ULT: ok = imm >= 1 && binop(d, QK_ULT, QK_ULTV); break;
-      case G_ULE: ok = imm >= 1 && binop(d, QK_ULE, QK_ULEV); break;
-      case G_UGT: ok = imm >= 1 && binop(d, QK_UGT, QK_UGTV); break;
-      case G_UGE: ok = imm >= 1 && binop(d, QK_UGE, QK_UGEV); break;
+      case G_ULT: ok = imm >= 1 && binop(d, QK_ULT, QK_ULTV, QK_ULTC); break;
+      case G_ULE: ok = imm >= 1 && binop(d, QK_ULE, QK_ULEV, QK_ULEC); break;
+      case G_UGT: ok = imm >= 1 && binop(d, QK_UGT, QK_UGTV, QK_UGTC); break;
+      case G_UGE: ok = imm >= 1 && binop(d, QK_UGE, QK_UGEV, QK_UGEC); break;
       case G_BAND: ok = binop(d, QK_BAND, QK_BANDV, QK_BANDC); break;
       case G_BOR: ok = binop(d, QK_BOR, QK_BORV, QK_BORC); break;
       case G_BXOR: ok = binop(d, QK_BXOR, QK_BXORV, QK_BXORC); break;
@@ -561,8 +561,8 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
         break;
       }
       // wrapping arithmetic: 256-bit handlers, results below 256 bits re-masked
-      case G_ADD: ok = imm <= 256 && binop(d, QK_ADD, QK_ADDV) && mask(d - 1, imm); break;
-      case G_SUB: ok = imm <= 256 && binop(d, QK_SUB, QK_SUBV) && mask(d - 1, imm); break;
+      case G_ADD: ok = imm <= 256 && binop(d, QK_ADD, QK_ADDV, QK_ADDC) && mask(d - 1, imm); break;
+      case G_SUB: ok = imm <= 256 && binop(d, QK_SUB, QK_SUBV, QK_SUBC) && mask(d - 1, imm); break;
       case G_MUL: ok = imm <= 256 && binop(d, QK_MUL, QK_MULV, QK_MULC) && mask(d - 1, imm); break;
       case G_NEG: ok = imm <= 256 && word(QK_NEG, d, -1, 0) && mask(d, imm); break;
       case G_BNOT: ok = imm <= 256 && word(QK_BNOT, d, -1, 0) && mask(d, imm); break;
