@@ -50,6 +50,9 @@ typedef enum mq_status {
  * width: result width in bits; 0 means Bool sort.  Array-sorted nodes (STORE, CONST_ARRAY,
  * ARRAY_VAR) carry the range width.
  * Semantics: SMT-LIB 2.6 FixedSizeBitVectors + z3 model completion.
+ * Widths up to 2048 bits (keccak256_<n> inputs of up to 256 bytes: Concat of memory bytes,
+ * mythril/laser/ethereum/instructions.py:1043-1052); MUL / *DIV / *REM / SMOD and the *MUL_NO*
+ * predicates up to 512 bits.  Anything wider makes the tape MQ_UNSUPPORTED (fail closed).
  * Vocabulary: mythril/laser/smt/{bitvec,bitvec_helper,bool,array,function}.py.
  */
 typedef enum mq_op {
@@ -179,13 +182,21 @@ typedef struct mq_stats {
 typedef struct mq_ctx mq_ctx;
 typedef struct mq_tapes mq_tapes;
 
-/* Create a context on device dev_ids[0] (one context per GPU; multi-GPU runs one process per
-   GPU and min-reduces first_hit over RCCL in the host layer).  n_dev must be 1. */
+/* Create a context over n_dev devices dev_ids[0..n_dev) (dev_ids may be NULL for n_dev = 1:
+   device 0).  Mythril is one process (mythril/mythril/mythril_analyzer.py:136-185), so one
+   context drives every GPU of the node: mq_models_upload splits the candidate
+   axis into contiguous shards in global candidate order (device g holds [g*M/n, (g+1)*M/n)),
+   tapes are compiled once and replicated, and the per-tape first hits are combined by an
+   in-library RCCL ncclAllReduce(ncclMin) over xGMI (communicators from ncclCommInitAll), so the
+   global MRU-first order of support_utils.py:62 survives the merge.  With
+   n_dev = 1 the RCCL path is off unless MQ_OPT_USE_RCCL is set.  The alternative of one process
+   per GPU (torch.distributed, mythril_amd/dist.py) uses n_dev = 1 contexts. */
 int mq_ctx_create(int n_dev, const int* dev_ids, mq_ctx** out);
 void mq_ctx_destroy(mq_ctx* ctx);
 const char* mq_strerror(int code);
 
-/* Replace the candidate set (ModelCache contents, support_utils.py:56-58 / model.py:125). */
+/* Replace the candidate set (ModelCache contents, support_utils.py:56-58 / model.py:125).
+   n_models may be 0 (an empty model-axis shard: every tape reports MQ_NO_HIT). */
 int mq_models_upload(mq_ctx* ctx, const mq_model_batch* models);
 
 /* Compile + upload a tape batch once (the lowering of simplify(And(*constraints)).raw,
@@ -219,7 +230,8 @@ int mq_finalize_first_hit(mq_ctx* ctx, mq_tapes* tapes, int32_t* d_first_hit, vo
    (SURVEY §8(d)).  Synchronizes the context stream. */
 int mq_counters(mq_ctx* ctx, double* out3, int reset);
 
-/* Full verdict matrix for parity dumps: bit (t*M + m) of bits_out = tape t true on model m.
+/* Full verdict matrix for parity dumps: bit (t*M + m) of bits_out = tape t true on model m
+   (M = all models of the last mq_models_upload, every device's shard in place).
    bits_out has ceil(n_tapes*M/8) bytes.  Unsupported tapes yield all-zero rows and are
    reported through first_hit_out (may be NULL). */
 int mq_eval_verdicts(mq_ctx* ctx, const mq_tape_batch* batch, uint8_t* bits_out, int32_t* first_hit_out);
@@ -235,17 +247,27 @@ int mq_keccak256(mq_ctx* ctx, const uint8_t* data, const int64_t* offsets, int32
    parity cross-check).  MQ_OPT_EARLY_EXIT (default 1): waves skip a tape once a lower first
    hit is published.  MQ_OPT_ASM_READY (query): returns 1 if the assembly interpreter loaded.
    MQ_OPT_TIME_KERNELS (default 0): bracket the evaluation kernels of every launch with a HIP
-   event pair on the launch stream (read back with mq_kernel_times; setting it clears them). */
-enum mq_option { MQ_OPT_USE_ASM = 1, MQ_OPT_EARLY_EXIT = 2, MQ_OPT_ASM_READY = 3, MQ_OPT_TIME_KERNELS = 4 };
+   event pair on the launch stream (read back with mq_kernel_times; setting it clears them).
+   MQ_OPT_USE_RCCL (default 1 when n_dev > 1, else 0): combine first hits with the RCCL MIN
+   all-reduce; 1 on a single-device context runs that path with one rank (0 is refused when
+   n_dev > 1).  MQ_OPT_RCCL_ACTIVE (query): 1 if the context reduces over RCCL. */
+enum mq_option {
+  MQ_OPT_USE_ASM = 1,
+  MQ_OPT_EARLY_EXIT = 2,
+  MQ_OPT_ASM_READY = 3,
+  MQ_OPT_TIME_KERNELS = 4,
+  MQ_OPT_USE_RCCL = 5,
+  MQ_OPT_RCCL_ACTIVE = 6
+};
 int mq_ctx_set_option(mq_ctx* ctx, int option, int value);
 
 /* Device durations (ms) of the evaluation kernels of each launch since the last reset, in
-   launch order (MQ_OPT_TIME_KERNELS on).  Waits for those launches.  *n_out = number recorded
+   launch order (MQ_OPT_TIME_KERNELS on; several devices: the slowest device per launch).  Waits for those launches.  *n_out = number recorded
    (may exceed max_out; only max_out are written).  reset != 0 forgets them. */
 int mq_kernel_times(mq_ctx* ctx, float* out_ms, int32_t max_out, int32_t* n_out, int reset);
 
 /* How a compiled batch is split: tapes on the assembly interpreter, on the generic 256-bit
-   and on the 512-bit HIP C++ kernels (any pointer may be NULL). */
+   and on the wider (512 / 1024 / 2048-bit) HIP C++ kernels (any pointer may be NULL). */
 int mq_tapes_info(mq_tapes* tapes, int32_t* n_asm, int32_t* n_generic_l8, int32_t* n_generic_l16);
 
 /* After a launch: how the assembly-eligible tapes were split between the preloaded-variable
@@ -262,7 +284,7 @@ int mq_tapes_column_split(mq_tapes* tapes, int32_t* n_asm, int32_t* live);
 double mq_tape_alg_ops(const mq_tape_batch* batch, int32_t t);
 
 /* Host-only compile report for tape t (no device needed): *supported (0/1), limbs per value L
-   (8 or 16), register-stack depth, LDS temp slots, program words; reason (if unsupported) is
+   (8, 16, 32 or 64), register-stack depth, LDS temp slots, program words; reason (if unsupported) is
    copied into why[why_len].  Returns 0 or MQ_ERR_ARG. */
 int mq_tape_compile_info(const mq_tape_batch* batch, int32_t t, int32_t* supported, int32_t* limbs,
                          int32_t* depth, int32_t* n_temps, int32_t* prog_words, char* why, int32_t why_len);

@@ -22,6 +22,10 @@ HEADERS = ["gprog.h", "bvops.h", "qs_launch.h", "tape_compiler.h", "qsa_table.h"
 ARCH = os.environ.get("MQ_OFFLOAD_ARCH", "gfx950")
 
 
+def _rocm() -> str:
+    return os.environ.get("ROCM_PATH", "/opt/rocm")
+
+
 def _hipcc() -> str:
     for c in (os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc"), shutil.which("hipcc") or ""):
         if c and os.path.exists(c):
@@ -67,7 +71,9 @@ def build(force: bool = False, verbose: bool = False) -> str:
             if res.returncode:
                 raise RuntimeError(f"compile failed: {' '.join(cmd)}")
     if force or jobs or not os.path.exists(OUT):
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT, *objs]
+        # librccl: the in-library MIN all-reduce of a multi-device context (mq_ctx_create n_dev > 1)
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT, *objs,
+               f"-L{_rocm()}/lib", "-lrccl", f"-Wl,-rpath,{_rocm()}/lib"]
         res = subprocess.run(cmd, capture_output=True, text=True)
         if res.returncode:
             sys.stderr.write(res.stderr)

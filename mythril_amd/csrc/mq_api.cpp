@@ -4,6 +4,7 @@
 // (ModelCache contents, mythril/support/support_utils.py:56-58), compiles boundary tapes into
 // GPU stack programs (tape_compiler.cpp) and launches the gfx950 kernels (qs_kernels.hip).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -56,6 +57,19 @@ struct DevBuf {
 
 // the assembly interpreter keeps temps in LDS (2 KB per temp per wave, 4 waves per workgroup)
 static constexpr int kQsaMaxTemps = 16;
+
+// HIP C++ interpreter variants (qs_kernels.hip launch_qs): limbs per stack slot and whether the
+// variant carries the interpreted-keccak handler.  Kind 0 (L = 8) is where 256-bit tapes the
+// assembly interpreters cannot take run; 32 / 64 limbs hold the > 512-bit values of keccak
+// inputs longer than 64 bytes (Concat / Extract / EQ / ITE / UF keys) and always carry keccak.
+static constexpr int kGen = 5;
+static constexpr int kGenL[kGen] = {8, 16, 16, 32, 64};
+static constexpr bool kGenK[kGen] = {false, false, true, true, true};
+static int gen_kind(const CompiledTape& x) {
+  if (x.L == 8) return 0;
+  if (x.L == 16) return x.keccak ? 2 : 1;
+  return x.L == 32 ? 3 : 4;
+}
 static constexpr int64_t kColAsmMinNodes = 32;   // hoisted columns on qsg_kernel from this size
 
 struct mq_ctx {
@@ -92,6 +106,14 @@ struct mq_ctx {
   int time_kernels = 0;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> kev;
   size_t kev_used = 0;
+  // Several devices from one process (mq_ctx_create(n_dev > 1)): this context is
+  // the lead (dev_ids[0]); peers[i] is a single-device context on dev_ids[i + 1].  The candidate
+  // axis is split contiguously over [lead, peers...] (shard_lo[g] = first local model of device
+  // g); per-tape first hits are combined by an in-library RCCL MIN all-reduce (comms, lead first).
+  std::vector<mq_ctx*> peers;
+  std::vector<ncclComm_t> comms;
+  std::vector<int64_t> shard_lo;
+  int64_t M_total = 0;
 };
 
 struct mq_tapes {
@@ -110,11 +132,12 @@ struct mq_tapes {
     int max_depth = 1;
     bool keccak = false;
   };
-  // descs layout: [L8 QSA-eligible | L8 other | L16]; the QSA view (qdescs/qprog) holds the
-  // eligible tapes translated to threaded code.  The translation depends on the model batch
-  // (variable rows, function table), so it is redone at launch when the models changed: each
-  // eligible tape goes to the P kernel (only preloaded variables) or the G kernel.
-  Variant l8_all, l8_rest, l16, l16k, qsa;   // l16k: tapes with interpreted keccak
+  // descs layout: [L8 QSA-eligible | gen[0] (L8 other) | gen[1..] (wider kinds)]; the QSA view
+  // (qdescs/qprog) holds the eligible tapes translated to threaded code.  The translation depends
+  // on the model batch (variable rows, function table), so it is redone at launch when the models
+  // changed: each eligible tape goes to the P kernel (only preloaded variables) or the G kernel.
+  Variant l8_all, qsa;
+  Variant gen[kGen];                         // HIP C++ interpreter kinds (kGenL / kGenK)
   std::vector<CompiledTape> qct;             // compiled programs of the QSA-eligible tapes
   std::vector<GDesc> qbase;                  // their descriptors (const_base into consts)
   uint64_t qsa_gen = ~0ull;                  // models_gen of the current translation
@@ -133,7 +156,7 @@ struct mq_tapes {
   // their translation for the current model batch succeeds (cq_live) they run on qsg_kernel in
   // mode 3 and the HIP C++ column kernel takes the rest of v8
   struct ColumnLevel {
-    Variant v8, v16, v16k;
+    Variant v[kGen];    // v[0]: L = 8 (its first v8q columns are the G-eligible ones)
     int v8q = 0;
     int cq_begin = 0;   // first of the level's columns in cq_ct / cqdescs
   };
@@ -148,6 +171,11 @@ struct mq_tapes {
   int cq_temps = 0;
   DevBuf cqdescs, cqprog, cqconsts, cqargs;
   std::vector<QArgs> cqargs_host;   // what cqargs holds on the device, per level
+  // multi-device context: the same batch compiled on each peer device (ctx->peers order)
+  std::vector<mq_tapes*> peers;
+  ~mq_tapes() {
+    for (mq_tapes* p : peers) delete p;
+  }
 };
 
 static thread_local std::string g_last_error;
@@ -251,12 +279,10 @@ static int qsa_init(mq_ctx* c) {
   return MQ_OK;
 }
 
-int mq_ctx_create(int n_dev, const int* dev_ids, mq_ctx** out) {
-  if (!out || n_dev != 1) return MQ_ERR_ARG;
+static int create_one(int dev, mq_ctx** out) {
   *out = nullptr;
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return MQ_ERR_NODEV;
-  int dev = dev_ids ? dev_ids[0] : 0;
   if (dev < 0 || dev >= count) return MQ_ERR_NODEV;
   hipDeviceProp_t prop;
   HIPCHK(hipGetDeviceProperties(&prop, dev));
@@ -269,11 +295,11 @@ int mq_ctx_create(int n_dev, const int* dev_ids, mq_ctx** out) {
   c->device = dev;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
-    delete c;
+    mq_ctx_destroy(c);
     return MQ_ERR_HIP;
   }
   if (c->counters.ensure(4 * sizeof(unsigned long long)) != hipSuccess) {
-    delete c;
+    mq_ctx_destroy(c);
     return MQ_ERR_NOMEM;
   }
   int rc = qsa_init(c);
@@ -285,8 +311,65 @@ int mq_ctx_create(int n_dev, const int* dev_ids, mq_ctx** out) {
   return MQ_OK;
 }
 
+static int rccl_fail(ncclResult_t r, const char* what) {
+  g_last_error = std::string(what) + ": " + ncclGetErrorString(r);
+  return MQ_ERR_HIP;
+}
+
+// One RCCL communicator per device of the context (lead first), single process: ncclCommInitAll.
+static int rccl_init(mq_ctx* c) {
+  if (!c->comms.empty()) return MQ_OK;
+  std::vector<int> devs{c->device};
+  for (mq_ctx* p : c->peers) devs.push_back(p->device);
+  std::vector<ncclComm_t> comms(devs.size());
+  ncclResult_t r = ncclCommInitAll(comms.data(), (int)devs.size(), devs.data());
+  if (r != ncclSuccess) return rccl_fail(r, "ncclCommInitAll");
+  c->comms = comms;
+  return MQ_OK;
+}
+
+// [lead, peers...]
+static std::vector<mq_ctx*> devices_of(mq_ctx* c) {
+  std::vector<mq_ctx*> v{c};
+  v.insert(v.end(), c->peers.begin(), c->peers.end());
+  return v;
+}
+
+int mq_ctx_create(int n_dev, const int* dev_ids, mq_ctx** out) {
+  if (!out || n_dev < 1 || (n_dev > 1 && !dev_ids)) return MQ_ERR_ARG;
+  *out = nullptr;
+  for (int i = 0; i < n_dev; i++)
+    for (int j = 0; j < i; j++)
+      if (dev_ids[i] == dev_ids[j]) return MQ_ERR_ARG;   // one context per device
+  mq_ctx* lead = nullptr;
+  int rc = create_one(dev_ids ? dev_ids[0] : 0, &lead);
+  if (rc) return rc;
+  for (int i = 1; i < n_dev; i++) {
+    mq_ctx* p = nullptr;
+    rc = create_one(dev_ids[i], &p);
+    if (rc) {
+      mq_ctx_destroy(lead);
+      return rc;
+    }
+    lead->peers.push_back(p);
+  }
+  if (n_dev > 1) {
+    rc = rccl_init(lead);
+    if (rc) {
+      mq_ctx_destroy(lead);
+      return rc;
+    }
+  }
+  *out = lead;
+  return MQ_OK;
+}
+
 void mq_ctx_destroy(mq_ctx* c) {
   if (!c) return;
+  for (ncclComm_t cm : c->comms) (void)ncclCommDestroy(cm);
+  c->comms.clear();
+  for (mq_ctx* p : c->peers) mq_ctx_destroy(p);
+  c->peers.clear();
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -299,8 +382,9 @@ void mq_ctx_destroy(mq_ctx* c) {
   delete c;
 }
 
-int mq_models_upload(mq_ctx* c, const mq_model_batch* mb) {
-  if (!c || !mb || mb->n_models <= 0 || mb->n_vars < 0 || mb->n_funcs < 0) return MQ_ERR_ARG;
+// Upload a model batch to ONE device (n_models may be 0: an empty shard evaluates to "no hit").
+static int upload_one(mq_ctx* c, const mq_model_batch* mb) {
+  if (!c || !mb || mb->n_models < 0 || mb->n_vars < 0 || mb->n_funcs < 0) return MQ_ERR_ARG;
   if (mb->n_models > 0x7FFFFFFF || mb->index_base + mb->n_models > 0x7FFFFFFE) return MQ_ERR_ARG;
   HIPCHK(hipSetDevice(c->device));
   const int64_t M = mb->n_models;
@@ -394,6 +478,74 @@ int mq_models_upload(mq_ctx* c, const mq_model_batch* mb) {
   c->n_funcs = F;
   c->var_width.assign(mb->var_width, mb->var_width + mb->n_vars);
   c->have_models = true;
+  return MQ_OK;
+}
+
+// Models [lo, hi) of mb as a batch of their own (global index base + lo).  Variable rows and the
+// entries of every function are packed into `keep`; else values are a view into mb.
+struct ShardBuffers {
+  std::vector<uint32_t> var_words, entry_words;
+  std::vector<int64_t> entry_ptr, entry_base, else_base;
+};
+static mq_model_batch shard_view(const mq_model_batch* mb, int64_t lo, int64_t hi, ShardBuffers& keep) {
+  const int64_t M = mb->n_models, Ms = hi - lo;
+  mq_model_batch s = *mb;
+  s.n_models = Ms;
+  s.index_base = mb->index_base + lo;
+  int64_t rows = 0;
+  for (int v = 0; v < mb->n_vars; v++) rows += nl_of(mb->var_width[v]);
+  keep.var_words.resize((size_t)std::max<int64_t>(rows * Ms, 1));
+  for (int64_t r = 0; r < rows; r++)
+    std::memcpy(keep.var_words.data() + r * Ms, mb->var_words + r * M + lo, sizeof(uint32_t) * (size_t)Ms);
+  s.var_words = keep.var_words.data();
+  const int F = mb->n_funcs;
+  keep.entry_ptr.assign((size_t)F * (Ms + 1) + 1, 0);
+  keep.entry_base.assign((size_t)F + 1, 0);
+  keep.else_base.assign((size_t)F + 1, 0);
+  keep.entry_words.clear();
+  for (int f = 0; f < F; f++) {
+    const mq_func_desc& d = mb->funcs[f];
+    int64_t stride = nl_of(d.result_width);
+    for (int i = 0; i < d.arity && i < 2; i++) stride += nl_of(d.arg_width[i]);
+    const int64_t* ptr = mb->entry_ptr + (int64_t)f * (M + 1);
+    const int64_t a = ptr[lo], b = ptr[hi];
+    keep.entry_base[f] = (int64_t)keep.entry_words.size();
+    const uint32_t* src = mb->entry_words + mb->entry_base[f] + a * stride;
+    keep.entry_words.insert(keep.entry_words.end(), src, src + (b - a) * stride);
+    for (int64_t m = 0; m <= Ms; m++) keep.entry_ptr[(size_t)f * (Ms + 1) + m] = ptr[lo + m] - a;
+    keep.else_base[f] = mb->else_base[f] + lo * nl_of(d.result_width);
+  }
+  if (keep.entry_words.empty()) keep.entry_words.push_back(0);
+  s.entry_ptr = keep.entry_ptr.data();
+  s.entry_base = keep.entry_base.data();
+  s.entry_words = keep.entry_words.data();
+  s.n_entry_words = (int64_t)keep.entry_words.size();
+  s.else_base = keep.else_base.data();
+  return s;
+}
+
+int mq_models_upload(mq_ctx* c, const mq_model_batch* mb) {
+  if (!c || !mb || mb->n_models < 0) return MQ_ERR_ARG;
+  if (c->peers.empty()) {
+    c->shard_lo.assign(1, 0);
+    c->M_total = mb->n_models;
+    return upload_one(c, mb);
+  }
+  // contiguous model-axis shards in global candidate order; a device whose range
+  // is empty (fewer models than devices) holds zero models and reports no hit
+  const std::vector<mq_ctx*> devs = devices_of(c);
+  const int64_t G = (int64_t)devs.size(), M = mb->n_models;
+  std::vector<int64_t> lo(G);
+  for (int64_t g = 0; g < G; g++) {
+    lo[g] = M * g / G;
+    const int64_t hi = M * (g + 1) / G;
+    ShardBuffers keep;
+    const mq_model_batch sb = shard_view(mb, lo[g], hi, keep);
+    const int rc = upload_one(devs[g], &sb);
+    if (rc) return rc;
+  }
+  c->shard_lo = lo;
+  c->M_total = M;
   return MQ_OK;
 }
 
@@ -676,25 +828,17 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
   return x.consts.size() + extra.size() <= 0x10000u;
 }
 
-int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t* n_unsup_out) {
-  if (!c || !tb || !out || tb->n_tapes < 0 || (tb->n_tapes > 0 && (!tb->tape_offsets || !tb->nodes))) return MQ_ERR_ARG;
+// Upload a compiled batch to ONE device.
+static int tapes_upload_one(mq_ctx* c, int32_t n_tapes, const std::vector<CompiledTape>& ct, mq_tapes** out) {
   *out = nullptr;
   HIPCHK(hipSetDevice(c->device));
   auto T = std::make_unique<mq_tapes>();
   T->ctx = c;
-  T->n_tapes = tb->n_tapes;
-  T->unsupported.assign(std::max(tb->n_tapes, 1), 0);
-  T->n_nodes.assign(tb->n_tapes, 0);
-  T->alg_ops.assign(tb->n_tapes, 0);
-  CompileLimits lim;
-  std::vector<CompiledTape> ct(tb->n_tapes);
-  for (int t = 0; t < tb->n_tapes; t++) {
-    if (tb->tape_offsets[t + 1] < tb->tape_offsets[t]) return MQ_ERR_ARG;
-  }
-  // compile (independent per tape)
-#pragma omp parallel for schedule(dynamic, 64)
-  for (int t = 0; t < tb->n_tapes; t++) ct[t] = compile_tape(tb, t, lim);
-  // descriptor groups: [L8 QSA-eligible | L8 other | L16] (see mq_tapes)
+  T->n_tapes = n_tapes;
+  T->unsupported.assign(std::max(n_tapes, 1), 0);
+  T->n_nodes.assign(n_tapes, 0);
+  T->alg_ops.assign(n_tapes, 0);
+  // descriptor groups: [L8 QSA-eligible | gen[0] | gen[1..]] (see mq_tapes)
   std::vector<uint32_t> prog, consts;
   std::vector<GDesc> descs;
   auto push_desc = [&](int t, const CompiledTape& x) {
@@ -714,27 +858,23 @@ int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t*
   };
   // QSA eligibility is structural here (G kernel set, no model information); the derived
   // constants of an eligible tape (divisor reciprocals) follow its own constants in the pool
-  std::vector<char> qsa_ok(tb->n_tapes, 0);
-  std::vector<std::vector<uint32_t>> qextra(tb->n_tapes);
+  std::vector<char> qsa_ok(n_tapes, 0);
+  std::vector<std::vector<uint32_t>> qextra(n_tapes);
   if (c->qsa_ready)
-    for (int t = 0; t < tb->n_tapes; t++)
+    for (int t = 0; t < n_tapes; t++)
       if (ct[t].supported && ct[t].L == 8 && ct[t].n_temps <= kQsaMaxTemps)
         qsa_ok[t] = qsa_translate(c, 1, false, ct[t], nullptr, &qextra[t]) ? 1 : 0;
-  T->qsa.begin = 0;
-  for (int pass = 0; pass < 4; pass++) {
-    mq_tapes::Variant& v = pass == 0 ? T->qsa : (pass == 1 ? T->l8_rest : (pass == 2 ? T->l16 : T->l16k));
-    v.L = pass >= 2 ? 16 : 8;
-    v.keccak = pass == 3;
+  for (int pass = -1; pass < kGen; pass++) {
+    mq_tapes::Variant& v = pass < 0 ? T->qsa : T->gen[pass];
+    v.L = pass < 0 ? 8 : kGenL[pass];
+    v.keccak = pass < 0 ? false : kGenK[pass];
     v.begin = (int)descs.size();
-    for (int t = 0; t < tb->n_tapes; t++) {
+    for (int t = 0; t < n_tapes; t++) {
       const CompiledTape& x = ct[t];
       if (!x.supported) continue;
-      if (pass == 0 && !(x.L == 8 && qsa_ok[t])) continue;
-      if (pass == 1 && !(x.L == 8 && !qsa_ok[t])) continue;
-      if (pass == 2 && !(x.L == 16 && !x.keccak)) continue;
-      if (pass == 3 && !x.keccak) continue;
+      if (pass < 0 ? !(x.L == 8 && qsa_ok[t]) : (gen_kind(x) != pass || (pass == 0 && qsa_ok[t]))) continue;
       GDesc d = push_desc(t, x);
-      if (pass == 0) {
+      if (pass < 0) {
         consts.insert(consts.end(), qextra[t].begin(), qextra[t].end());
         T->qbase.push_back(d);
         T->qct.push_back(x);
@@ -746,12 +886,12 @@ int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t*
   }
   T->l8_all.L = 8;
   T->l8_all.begin = 0;
-  T->l8_all.count = T->qsa.count + T->l8_rest.count;
-  T->l8_all.max_temps = std::max(T->qsa.max_temps, T->l8_rest.max_temps);
-  T->l8_all.max_depth = std::max(T->qsa.max_depth, T->l8_rest.max_depth);
+  T->l8_all.count = T->qsa.count + T->gen[0].count;
+  T->l8_all.max_temps = std::max(T->qsa.max_temps, T->gen[0].max_temps);
+  T->l8_all.max_depth = std::max(T->qsa.max_depth, T->gen[0].max_depth);
   consts.resize(consts.size() + 16, 0);
   prog.push_back(gword(G_END, 0, 0));
-  for (int t = 0; t < tb->n_tapes; t++) {
+  for (int t = 0; t < n_tapes; t++) {
     T->unsupported[t] = ct[t].supported ? 0 : 1;
     T->n_unsupported += ct[t].supported ? 0 : 1;
     T->n_nodes[t] = ct[t].n_nodes;
@@ -765,17 +905,40 @@ int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t*
   HIPCHK(T->consts.upload(consts.data(), consts.size(), c->stream));
   HIPCHK(T->unsup_dev.upload(T->unsupported.data(), T->unsupported.size(), c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
-  if (n_unsup_out) *n_unsup_out = T->n_unsupported;
   *out = T.release();
+  return MQ_OK;
+}
+
+int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t* n_unsup_out) {
+  if (!c || !tb || !out || tb->n_tapes < 0 || (tb->n_tapes > 0 && (!tb->tape_offsets || !tb->nodes))) return MQ_ERR_ARG;
+  *out = nullptr;
+  for (int t = 0; t < tb->n_tapes; t++) {
+    if (tb->tape_offsets[t + 1] < tb->tape_offsets[t]) return MQ_ERR_ARG;
+  }
+  // compile once (independent per tape), upload to every device of the context
+  CompileLimits lim;
+  std::vector<CompiledTape> ct(tb->n_tapes);
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int t = 0; t < tb->n_tapes; t++) ct[t] = compile_tape(tb, t, lim);
+  mq_tapes* T = nullptr;
+  int rc = tapes_upload_one(c, tb->n_tapes, ct, &T);
+  if (rc) return rc;
+  std::unique_ptr<mq_tapes> guard(T);
+  for (mq_ctx* p : c->peers) {
+    mq_tapes* pt = nullptr;
+    rc = tapes_upload_one(p, tb->n_tapes, ct, &pt);
+    if (rc) return rc;
+    T->peers.push_back(pt);
+  }
+  if (n_unsup_out) *n_unsup_out = T->n_unsupported;
+  *out = guard.release();
   return MQ_OK;
 }
 
 void mq_tapes_free(mq_tapes* t) { delete t; }
 
-int mq_tapes_set_columns(mq_tapes* T, const mq_tape_batch* progs, const int32_t* var_index, const int32_t* level,
-                         int32_t n_columns) {
-  if (!T || n_columns < 0 || (n_columns > 0 && (!progs || !var_index || !level || progs->n_tapes != n_columns)))
-    return MQ_ERR_ARG;
+static int set_columns_one(mq_tapes* T, const mq_tape_batch* progs, const int32_t* var_index, const int32_t* level,
+                           int32_t n_columns) {
   mq_ctx* c = T->ctx;
   HIPCHK(hipSetDevice(c->device));
   T->clevels.clear();
@@ -820,18 +983,17 @@ int mq_tapes_set_columns(mq_tapes* T, const mq_tape_batch* progs, const int32_t*
   T->clevels.resize((size_t)max_level + 1);
   for (int lv = 0; lv <= max_level; lv++) {
     T->clevels[lv].cq_begin = (int)T->cq_ct.size();
-    for (int pass = -1; pass < 3; pass++) {
-      mq_tapes::Variant& v = pass <= 0 ? T->clevels[lv].v8 : (pass == 1 ? T->clevels[lv].v16 : T->clevels[lv].v16k);
-      v.L = pass <= 0 ? 8 : 16;
-      v.keccak = pass == 2;
+    // pass -1: the G-eligible L = 8 columns (front of v[0]); pass g: kind g (qs_column_kernel)
+    for (int pass = -1; pass < kGen; pass++) {
+      mq_tapes::Variant& v = T->clevels[lv].v[pass < 0 ? 0 : pass];
+      v.L = pass < 0 ? 8 : kGenL[pass];
+      v.keccak = pass < 0 ? false : kGenK[pass];
       if (pass != 0) v.begin = (int)descs.size();
       for (int k = 0; k < n_columns; k++) {
         const CompiledTape& x = ct[k];
         if (level[k] != lv) continue;
         if (pass == -1 && !gq[k]) continue;
-        if (pass == 0 && !(x.L == 8 && !x.keccak && !gq[k])) continue;
-        if (pass == 1 && !(x.L == 16 && !x.keccak)) continue;
-        if (pass == 2 && !x.keccak) continue;
+        if (pass >= 0 && (gen_kind(x) != pass || (pass == 0 && gq[k]))) continue;
         GDesc d{};
         d.prog_off = (uint32_t)prog.size();
         d.prog_len = (uint32_t)x.prog.size();
@@ -863,6 +1025,15 @@ int mq_tapes_set_columns(mq_tapes* T, const mq_tape_batch* progs, const int32_t*
   HIPCHK(T->cconsts.upload(consts.data(), consts.size(), c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return MQ_OK;
+}
+
+int mq_tapes_set_columns(mq_tapes* T, const mq_tape_batch* progs, const int32_t* var_index, const int32_t* level,
+                         int32_t n_columns) {
+  if (!T || n_columns < 0 || (n_columns > 0 && (!progs || !var_index || !level || progs->n_tapes != n_columns)))
+    return MQ_ERR_ARG;
+  int rc = set_columns_one(T, progs, var_index, level, n_columns);
+  for (size_t i = 0; rc == MQ_OK && i < T->peers.size(); i++) rc = set_columns_one(T->peers[i], progs, var_index, level, n_columns);
+  return rc;
 }
 
 // Workgroups (one wave each) of the persistent HIP C++ kernels: 16 per CU on 256 CUs; each
@@ -898,7 +1069,9 @@ static KArgs make_args(mq_ctx* c, mq_tapes* T, const mq_tapes::Variant& v) {
   const int64_t groups = (int64_t(v.count) + tpg - 1) / tpg;
   a.tiles = tiles;
   a.n_items = tiles * groups;
-  a.grid = (int)std::min<int64_t>(a.n_items, kPersistentGroups);
+  // the 1024/2048-bit kinds: 64-128 KB of LDS stack per wave, so fewer resident waves; a smaller
+  // persistent grid also bounds their temp scratch (grid x temps x 8-16 KB)
+  a.grid = (int)std::min<int64_t>(a.n_items, v.L >= 32 ? kPersistentGroups / 4 : kPersistentGroups);
   a.scratch = nullptr;
   a.stack_slots = std::max(1, v.max_depth);
   return a;
@@ -1096,9 +1269,8 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     if (rc) return rc;
     use_qsa = T->qsa_live;
   }
-  std::vector<mq_tapes::Variant> cpp;
-  if (use_qsa) cpp = {T->l8_rest, T->l16, T->l16k};
-  else cpp = {T->l8_all, T->l16, T->l16k};
+  std::vector<mq_tapes::Variant> cpp(T->gen, T->gen + kGen);
+  if (!use_qsa) cpp[0] = T->l8_all;
   hipEvent_t kend = nullptr;
   if (c->time_kernels) {
     if (c->kev_used == c->kev.size()) {
@@ -1118,6 +1290,13 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     started = true;
     return hipEventRecord(c->kev[c->kev_used - 1].first, st);
   };
+  if (c->M == 0) {   // an empty model shard: every tape keeps "no hit" (the caller's init)
+    if (kend) {
+      HIPCHK(start_timer());
+      HIPCHK(hipEventRecord(kend, st));
+    }
+    return MQ_OK;
+  }
   // hoisted columns first (they write model variable rows the tapes read)
   for (size_t i = 0; i < T->col_var.size(); i++) {
     const int v = T->col_var[i];
@@ -1138,7 +1317,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
   const uint32_t zero_row = (uint32_t)(c->var_off_h.empty() ? 0 : c->var_off_h.back() + c->var_nl_h.back());
   for (size_t li = 0; li < T->clevels.size(); li++) {
     const auto& lv = T->clevels[li];
-    const mq_tapes::Variant v8 = use_cq ? cut_front(lv.v8, lv.v8q) : lv.v8;
+    const mq_tapes::Variant v8 = use_cq ? cut_front(lv.v[0], lv.v8q) : lv.v[0];
     if (use_cq && lv.v8q > 0) {
       // the level's G columns on qsg_kernel, mode 3 (no preloaded variables)
       const int n = lv.v8q;
@@ -1179,7 +1358,8 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       HIPCHK(start_timer());
       HIPCHK(launch_qsa(1, dq, 8u * (unsigned)((groups + 3) / 4), (unsigned)rows, (size_t)q.lds_wave_bytes * 4, st));
     }
-    for (const mq_tapes::Variant* v : {&v8, &lv.v16, &lv.v16k}) {
+    for (int g = 0; g < kGen; g++) {
+      const mq_tapes::Variant* v = g == 0 ? &v8 : &lv.v[g];
       if (v->count <= 0) continue;
       KArgs a = make_col_args(c, T, *v);
       const size_t scratch_bytes = (size_t)a.grid * (size_t)a.tmp_words_per_wave * 4;
@@ -1263,30 +1443,74 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
   return MQ_OK;
 }
 
-int mq_kernel_times(mq_ctx* c, float* out_ms, int32_t max_out, int32_t* n_out, int reset) {
-  if (!c || (max_out > 0 && !out_ms)) return MQ_ERR_ARG;
+static int kernel_times_one(mq_ctx* c, std::vector<float>& ms_out, int reset) {
   HIPCHK(hipSetDevice(c->device));
-  int32_t n = 0;
+  ms_out.clear();
   for (size_t i = 0; i < c->kev_used; i++) {
     HIPCHK(hipEventSynchronize(c->kev[i].second));
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, c->kev[i].first, c->kev[i].second));
-    if (n < max_out) out_ms[n] = ms;
-    n++;
+    ms_out.push_back(ms);
   }
-  if (n_out) *n_out = n;
   if (reset) c->kev_used = 0;
   return MQ_OK;
+}
+
+int mq_kernel_times(mq_ctx* c, float* out_ms, int32_t max_out, int32_t* n_out, int reset) {
+  if (!c || (max_out > 0 && !out_ms)) return MQ_ERR_ARG;
+  // several devices: launch i took as long as its slowest device
+  std::vector<float> all, one;
+  for (mq_ctx* d : devices_of(c)) {
+    const int rc = kernel_times_one(d, one, reset);
+    if (rc) return rc;
+    if (all.size() < one.size()) all.resize(one.size(), 0.f);
+    for (size_t i = 0; i < one.size(); i++) all[i] = std::max(all[i], one[i]);
+  }
+  HIPCHK(hipSetDevice(c->device));
+  const int32_t n = (int32_t)all.size();
+  for (int32_t i = 0; i < n && i < max_out; i++) out_ms[i] = all[i];
+  if (n_out) *n_out = n;
+  return MQ_OK;
+}
+
+static int launch_one(mq_ctx* c, mq_tapes* T, int32_t* d_best, hipStream_t st) {
+  if (!c->have_models) return MQ_ERR_NO_MODELS;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(launch_init_best(d_best, T->n_tapes, st));
+  return launch_all(c, T, d_best, nullptr, st);
 }
 
 int mq_launch_first_hit(mq_ctx* c, mq_tapes* T, int32_t* d_best, void* stream) {
   if (!c || !T || !d_best) return MQ_ERR_ARG;
   if (!c->have_models) return MQ_ERR_NO_MODELS;
-  if (T->ctx != c) return MQ_ERR_STATE;
-  HIPCHK(hipSetDevice(c->device));
+  if (T->ctx != c || T->peers.size() != c->peers.size()) return MQ_ERR_STATE;
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-  HIPCHK(launch_init_best(d_best, T->n_tapes, st));
-  return launch_all(c, T, d_best, nullptr, st);
+  int rc = launch_one(c, T, d_best, st);
+  if (rc || c->comms.empty()) return rc;
+  // every device evaluates its contiguous shard of candidates (global indices), then ONE RCCL
+  // MIN all-reduce of int32[N] (4N bytes over xGMI) leaves the global first hit in d_best
+  std::vector<mq_ctx*> devs = devices_of(c);
+  std::vector<int32_t*> bufs{d_best};
+  std::vector<hipStream_t> streams{st};
+  for (size_t i = 0; i < c->peers.size(); i++) {
+    mq_ctx* p = c->peers[i];
+    HIPCHK(hipSetDevice(p->device));
+    HIPCHK(p->best_tmp.ensure(sizeof(int32_t) * std::max(T->n_tapes, 1)));
+    rc = launch_one(p, T->peers[i], p->best_tmp.as<int32_t>(), p->stream);
+    if (rc) return rc;
+    bufs.push_back(p->best_tmp.as<int32_t>());
+    streams.push_back(p->stream);
+  }
+  if (T->n_tapes > 0) {
+    ncclResult_t r = ncclGroupStart();
+    for (size_t g = 0; r == ncclSuccess && g < devs.size(); g++)
+      r = ncclAllReduce(bufs[g], bufs[g], (size_t)T->n_tapes, ncclInt32, ncclMin, c->comms[g], streams[g]);
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess) return rccl_fail(r, "ncclAllReduce(ncclMin)");
+    if (r2 != ncclSuccess) return rccl_fail(r2, "ncclGroupEnd");
+  }
+  HIPCHK(hipSetDevice(c->device));
+  return MQ_OK;
 }
 
 int mq_finalize_first_hit(mq_ctx* c, mq_tapes* T, int32_t* d_best, void* stream) {
@@ -1299,12 +1523,16 @@ int mq_finalize_first_hit(mq_ctx* c, mq_tapes* T, int32_t* d_best, void* stream)
 
 int mq_counters(mq_ctx* c, double* out3, int reset) {
   if (!c || !out3) return MQ_ERR_ARG;
+  for (int i = 0; i < 3; i++) out3[i] = 0;
+  for (mq_ctx* d : devices_of(c)) {
+    HIPCHK(hipSetDevice(d->device));
+    HIPCHK(hipDeviceSynchronize());
+    unsigned long long cnt[3] = {0, 0, 0};
+    HIPCHK(hipMemcpy(cnt, d->counters.p, sizeof(cnt), hipMemcpyDeviceToHost));
+    for (int i = 0; i < 3; i++) out3[i] += (double)cnt[i];
+    if (reset) HIPCHK(hipMemset(d->counters.p, 0, 4 * sizeof(unsigned long long)));
+  }
   HIPCHK(hipSetDevice(c->device));
-  HIPCHK(hipDeviceSynchronize());
-  unsigned long long cnt[3] = {0, 0, 0};
-  HIPCHK(hipMemcpy(cnt, c->counters.p, sizeof(cnt), hipMemcpyDeviceToHost));
-  for (int i = 0; i < 3; i++) out3[i] = (double)cnt[i];
-  if (reset) HIPCHK(hipMemset(c->counters.p, 0, 4 * sizeof(unsigned long long)));
   return MQ_OK;
 }
 
@@ -1316,25 +1544,38 @@ int mq_eval_tapes_first_hit(mq_ctx* c, mq_tapes* T, int32_t* out, mq_stats* stat
     if (stats) std::memset(stats, 0, sizeof(*stats));
     return MQ_OK;
   }
+  const std::vector<mq_ctx*> devs = devices_of(c);
+  for (mq_ctx* d : devs) {
+    HIPCHK(hipSetDevice(d->device));
+    HIPCHK(hipMemsetAsync(d->counters.p, 0, 4 * sizeof(unsigned long long), d->stream));
+  }
+  HIPCHK(hipSetDevice(c->device));
   HIPCHK(c->best_tmp.ensure(sizeof(int32_t) * T->n_tapes));
-  HIPCHK(hipMemsetAsync(c->counters.p, 0, 4 * sizeof(unsigned long long), c->stream));
   HIPCHK(hipEventRecord(c->ev0, c->stream));
   int rc = mq_launch_first_hit(c, T, c->best_tmp.as<int32_t>(), c->stream);
   if (rc) return rc;
   HIPCHK(hipEventRecord(c->ev1, c->stream));
   rc = mq_finalize_first_hit(c, T, c->best_tmp.as<int32_t>(), c->stream);
   if (rc) return rc;
-  unsigned long long cnt[3] = {0, 0, 0};
   HIPCHK(hipMemcpyAsync(out, c->best_tmp.p, sizeof(int32_t) * T->n_tapes, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync(cnt, c->counters.p, sizeof(cnt), hipMemcpyDeviceToHost, c->stream));
+  unsigned long long total[3] = {0, 0, 0};
+  for (mq_ctx* d : devs) {
+    HIPCHK(hipSetDevice(d->device));
+    unsigned long long cnt[3] = {0, 0, 0};
+    HIPCHK(hipMemcpyAsync(cnt, d->counters.p, sizeof(cnt), hipMemcpyDeviceToHost, d->stream));
+    HIPCHK(hipStreamSynchronize(d->stream));
+    for (int i = 0; i < 3; i++) total[i] += cnt[i];
+  }
+  HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
   if (stats) {
     float ms = 0;
+    // lead stream: from before the first launch to after the RCCL reduce (all devices)
     HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     stats->kernel_ms = ms;
-    stats->pairs_evaluated = (int64_t)cnt[0];
-    stats->node_evals = (double)cnt[1];
-    stats->alg_ops = (double)cnt[2];  // exact: per evaluated (tape, model) pair, the tape's cost
+    stats->pairs_evaluated = (int64_t)total[0];
+    stats->node_evals = (double)total[1];
+    stats->alg_ops = (double)total[2];  // exact: per evaluated (tape, model) pair, the tape's cost
     int hits = 0;
     for (int t = 0; t < T->n_tapes; t++) hits += out[t] >= 0;
     stats->n_hits = hits;
@@ -1362,41 +1603,66 @@ int mq_eval_verdicts(mq_ctx* c, const mq_tape_batch* tb, uint8_t* bits, int32_t*
   return mq_eval_tapes_verdicts(c, T, bits, first_hit_out);
 }
 
-int mq_eval_tapes_verdicts(mq_ctx* c, mq_tapes* T, uint8_t* bits, int32_t* first_hit_out) {
-  if (!c || !T || !bits) return MQ_ERR_ARG;
+// verdict bytes [tape][local model] of ONE device
+static int verdict_bytes_one(mq_ctx* c, mq_tapes* T, std::vector<uint8_t>& host) {
   if (!c->have_models) return MQ_ERR_NO_MODELS;
-  if (T->ctx != c) return MQ_ERR_STATE;
   HIPCHK(hipSetDevice(c->device));
-  int rc;
   const size_t nbytes = (size_t)T->n_tapes * (size_t)c->M;
   HIPCHK(c->verdict_buf.ensure(std::max<size_t>(nbytes, 1)));
   HIPCHK(hipMemsetAsync(c->verdict_buf.p, 0, std::max<size_t>(nbytes, 1), c->stream));
-  rc = launch_all(c, T, nullptr, c->verdict_buf.as<uint8_t>(), c->stream);
+  const int rc = launch_all(c, T, nullptr, c->verdict_buf.as<uint8_t>(), c->stream);
   if (rc) return rc;
-  std::vector<uint8_t> host(nbytes);
+  host.assign(nbytes, 0);
   if (nbytes) HIPCHK(hipMemcpyAsync(host.data(), c->verdict_buf.p, nbytes, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
-  std::memset(bits, 0, (nbytes + 7) / 8);
-  for (size_t i = 0; i < nbytes; i++)
-    if (host[i]) bits[i >> 3] |= (uint8_t)(1u << (i & 7));
-  if (first_hit_out) {
+  return MQ_OK;
+}
+
+int mq_eval_tapes_verdicts(mq_ctx* c, mq_tapes* T, uint8_t* bits, int32_t* first_hit_out) {
+  if (!c || !T || !bits) return MQ_ERR_ARG;
+  if (!c->have_models) return MQ_ERR_NO_MODELS;
+  if (T->ctx != c || T->peers.size() != c->peers.size()) return MQ_ERR_STATE;
+  const std::vector<mq_ctx*> devs = devices_of(c);
+  const int64_t M = c->peers.empty() ? c->M : c->M_total;
+  std::memset(bits, 0, ((size_t)T->n_tapes * (size_t)M + 7) / 8);
+  std::vector<int32_t> fh(T->n_tapes, -1);
+  std::vector<uint8_t> host;
+  // devices in global candidate order: the first set bit met per tape is its global first hit
+  for (size_t g = 0; g < devs.size(); g++) {
+    mq_tapes* tg = g == 0 ? T : T->peers[g - 1];
+    const int rc = verdict_bytes_one(devs[g], tg, host);
+    if (rc) return rc;
+    const int64_t Mg = devs[g]->M, lo = g < c->shard_lo.size() ? c->shard_lo[g] : 0;
     for (int t = 0; t < T->n_tapes; t++) {
-      int32_t h = -1;
-      if (T->unsupported[t]) h = -2;
-      else
-        for (int64_t m = 0; m < c->M; m++)
-          if (host[(size_t)t * c->M + m]) {
-            h = (int32_t)(c->index_base + m);
-            break;
-          }
-      first_hit_out[t] = h;
+      const uint8_t* row = host.data() + (size_t)t * Mg;
+      for (int64_t m = 0; m < Mg; m++) {
+        if (!row[m]) continue;
+        const size_t i = (size_t)t * M + lo + m;
+        bits[i >> 3] |= (uint8_t)(1u << (i & 7));
+        if (fh[t] < 0) fh[t] = (int32_t)(devs[g]->index_base + m);
+      }
     }
   }
+  HIPCHK(hipSetDevice(c->device));
+  if (first_hit_out)
+    for (int t = 0; t < T->n_tapes; t++) first_hit_out[t] = T->unsupported[t] ? -2 : fh[t];
   return MQ_OK;
 }
 
 int mq_ctx_set_option(mq_ctx* c, int option, int value) {
   if (!c) return MQ_ERR_ARG;
+  if (option == MQ_OPT_USE_RCCL) {
+    if (value) return rccl_init(c);
+    if (!c->peers.empty()) return MQ_ERR_ARG;   // several devices always reduce over RCCL
+    for (ncclComm_t cm : c->comms) (void)ncclCommDestroy(cm);
+    c->comms.clear();
+    return MQ_OK;
+  }
+  if (option == MQ_OPT_RCCL_ACTIVE) return c->comms.empty() ? 0 : 1;
+  for (mq_ctx* p : c->peers) {
+    const int rc = mq_ctx_set_option(p, option, value);
+    if (rc < 0) return rc;
+  }
   switch (option) {
     case MQ_OPT_USE_ASM: c->use_asm = value ? 1 : 0; return MQ_OK;
     case MQ_OPT_EARLY_EXIT: c->early_exit = value ? 1 : 0; return MQ_OK;
@@ -1427,8 +1693,10 @@ int mq_tapes_column_split(mq_tapes* T, int32_t* n_asm, int32_t* live) {
 int mq_tapes_info(mq_tapes* T, int32_t* n_asm, int32_t* n_generic_l8, int32_t* n_generic_l16) {
   if (!T) return MQ_ERR_ARG;
   if (n_asm) *n_asm = T->qsa.count;
-  if (n_generic_l8) *n_generic_l8 = T->l8_rest.count;
-  if (n_generic_l16) *n_generic_l16 = T->l16.count + T->l16k.count;
+  if (n_generic_l8) *n_generic_l8 = T->gen[0].count;
+  int wide = 0;
+  for (int g = 1; g < kGen; g++) wide += T->gen[g].count;
+  if (n_generic_l16) *n_generic_l16 = wide;
   return MQ_OK;
 }
 

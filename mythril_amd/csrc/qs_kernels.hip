@@ -86,11 +86,20 @@ MQ_DEV Ctx make_ctx(const KArgs& a, int64_t m, uint32_t* tmp, uint4* stk, int la
 MQ_DEV uint32_t nl_of_w(uint32_t W) { return W == 0 ? 1u : (W + 31u) >> 5; }
 
 // ---------------------------------------------------------------- LDS stack access
+// Multiplication, division and the multiplication-overflow predicates work on at most
+// kArithLimbs limbs (512 bits): the tape compiler rejects them wider, so on the 1024/2048-bit
+// stacks (L = 32, 64: wide Concat / Extract / EQ / ITE / UF keys / keccak inputs) they read
+// and write only the low limbs of a slot and keep the register footprint of L = 16.
+constexpr int kArithLimbs = 16;
 template <int L>
-MQ_DEV void sld(const Ctx& cx, int d, uint32_t (&x)[L], uint32_t nl = L) {
+constexpr int arith_limbs() { return L > kArithLimbs ? kArithLimbs : L; }
+
+// the low A limbs of slot d (A <= L, a multiple of 4); limb groups at or above nl read as zero
+template <int L, int A>
+MQ_DEV void sld_a(const Ctx& cx, int d, uint32_t (&x)[A], uint32_t nl = A) {
   const uint4* p = cx.stk + (d * (L / 4)) * 64;
 #pragma unroll
-  for (int g = 0; g < L / 4; g++) {
+  for (int g = 0; g < A / 4; g++) {
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
     if (g == 0 || (uint32_t)(4 * g) < nl) v = p[g * 64];
     x[4 * g] = v.x;
@@ -99,11 +108,22 @@ MQ_DEV void sld(const Ctx& cx, int d, uint32_t (&x)[L], uint32_t nl = L) {
     x[4 * g + 3] = v.w;
   }
 }
-template <int L>
-MQ_DEV void sst(const Ctx& cx, int d, const uint32_t (&x)[L]) {
+// write A limbs into slot d and zero its limbs above them (slots stay canonical)
+template <int L, int A>
+MQ_DEV void sst_a(const Ctx& cx, int d, const uint32_t (&x)[A]) {
   uint4* p = cx.stk + (d * (L / 4)) * 64;
 #pragma unroll
-  for (int g = 0; g < L / 4; g++) p[g * 64] = make_uint4(x[4 * g], x[4 * g + 1], x[4 * g + 2], x[4 * g + 3]);
+  for (int g = 0; g < A / 4; g++) p[g * 64] = make_uint4(x[4 * g], x[4 * g + 1], x[4 * g + 2], x[4 * g + 3]);
+#pragma unroll
+  for (int g = A / 4; g < L / 4; g++) p[g * 64] = make_uint4(0u, 0u, 0u, 0u);
+}
+template <int L>
+MQ_DEV void sld(const Ctx& cx, int d, uint32_t (&x)[L], uint32_t nl = L) {
+  sld_a<L, L>(cx, d, x, nl);
+}
+template <int L>
+MQ_DEV void sst(const Ctx& cx, int d, const uint32_t (&x)[L]) {
+  sst_a<L, L>(cx, d, x);
 }
 template <int L>
 MQ_DEV uint32_t sld0(const Ctx& cx, int d) {
@@ -241,12 +261,13 @@ MQ_DEV void h_mul(const Ctx& cx, int d, uint32_t W) {
     sst0<L>(cx, d - 1, (sld0<L>(cx, d - 1) * sld0<L>(cx, d)) & mask32(W));
     return;
   }
-  uint32_t x[L], y[L], r[L];
-  sld<L>(cx, d - 1, x);
-  sld<L>(cx, d, y);
-  mul_lo_n<L>(r, x, y);
-  mask_w<L>(r, W);
-  sst<L>(cx, d - 1, r);
+  constexpr int A = arith_limbs<L>();
+  uint32_t x[A], y[A], r[A];
+  sld_a<L, A>(cx, d - 1, x);
+  sld_a<L, A>(cx, d, y);
+  mul_lo_n<A>(r, x, y);
+  mask_w<A>(r, W);
+  sst_a<L, A>(cx, d - 1, r);
 }
 
 template <int L>
@@ -407,12 +428,13 @@ MQ_DEV void udivrem_fast(uint32_t (&q)[L], uint32_t (&r)[L], const uint32_t (&a)
   }
 }
 
-template <int L>
+template <int Ls>
 MQ_DEV void h_div(const Ctx& cx, int d, uint32_t op, uint32_t W) {
+  constexpr int L = arith_limbs<Ls>();   // (the tape compiler keeps divisions <= 512 bits)
   uint32_t x[L], y[L], Q[L], R[L];
   const uint32_t nl = nl_of_w(W);
-  sld<L>(cx, d - 1, x, nl);
-  sld<L>(cx, d, y, nl);
+  sld_a<Ls, L>(cx, d - 1, x, nl);
+  sld_a<Ls, L>(cx, d, y, nl);
   if (op == G_UDIV || op == G_UREM) {
     udivrem_fast<L>(Q, R, x, y);
     if (op == G_UDIV) {
@@ -420,7 +442,7 @@ MQ_DEV void h_div(const Ctx& cx, int d, uint32_t op, uint32_t W) {
       for (int i = 0; i < L; i++) R[i] = Q[i];
     }
     mask_w<L>(R, W);
-    sst<L>(cx, d - 1, R);
+    sst_a<Ls, L>(cx, d - 1, R);
     return;
   }
   sext_full<L>(x, W);
@@ -454,7 +476,7 @@ MQ_DEV void h_div(const Ctx& cx, int d, uint32_t op, uint32_t W) {
     }
   }
   mask_w<L>(R, W);
-  sst<L>(cx, d - 1, R);
+  sst_a<Ls, L>(cx, d - 1, R);
 }
 
 // ---------------------------------------------------------------- shifts by a stack value
@@ -485,11 +507,12 @@ MQ_DEV void h_shift(const Ctx& cx, int d, uint32_t op, uint32_t W) {
 }
 
 // ---------------------------------------------------------------- overflow predicates
-template <int L>
+template <int Ls>
 MQ_DEV void h_mul_ovfl(const Ctx& cx, int d, uint32_t op, uint32_t W) {
+  constexpr int L = arith_limbs<Ls>();   // (operands <= 512 bits, tape compiler)
   uint32_t X[L], Y[L];
-  sld<L>(cx, d - 1, X);
-  sld<L>(cx, d, Y);
+  sld_a<Ls, L>(cx, d - 1, X);
+  sld_a<Ls, L>(cx, d, Y);
   uint32_t LO[L], HI[L];
   bool res;
   if (op == G_UMUL_NOOVFL) {
@@ -520,7 +543,7 @@ MQ_DEV void h_mul_ovfl(const Ctx& cx, int d, uint32_t op, uint32_t W) {
     if (op == G_SMUL_NOOVFL) res = (neg || pz) ? true : (!gt && !eq);
     else res = (!neg || pz) ? true : !gt;
   }
-  sstb<L>(cx, d - 1, res);
+  sstb<Ls>(cx, d - 1, res);
 }
 
 // ---------------------------------------------------------------- model functions
@@ -589,8 +612,9 @@ MQ_DEV void h_uf(const Ctx& cx, int d, uint32_t op, uint32_t f, uint32_t W) {
 
 // ---------------------------------------------------------------- interpreted keccak256
 // keccak256 (Ethereum padding) of the big-endian bytes of S[d] (imm = width in bits, a multiple
-// of 8, <= 512 -> one 136-byte block); the digest read big-endian replaces S[d] (256 bits).
-// kfm.py:56-69 semantics; only bit-exact with UF table lookup on keccak-consistent models.
+// of 8, at most 32L bits: one 136-byte block up to 1080 bits, two up to 2048); the digest read
+// big-endian replaces S[d] (256 bits).  kfm.py:56-69 semantics; only bit-exact with UF table
+// lookup on keccak-consistent models.
 __constant__ uint64_t kKeccakRC[24] = {
     0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808Aull, 0x8000000080008000ull,
     0x000000000000808Bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
@@ -629,22 +653,39 @@ MQ_DEV void h_keccak(const Ctx& cx, int d, uint32_t W) {
   uint32_t X[L];
   sld<L>(cx, d, X);
   const uint32_t nbytes = W >> 3;
-  // full-width byte reversal, then shift the message to byte 0: message byte p = LE byte p
+  // full-width byte reversal, then shift the message to byte 0: message byte p = LE byte p of R
+  // (bytes >= nbytes are zero)
   uint32_t R[L];
 #pragma unroll
   for (int k = 0; k < L; k++) R[k] = __builtin_bswap32(X[L - 1 - k]);
   shr_uni<L>(R, 8u * (4u * L - nbytes));
-  // padding: 0x01 right after the message (bytes >= nbytes are zero after the shift)
-#pragma unroll
-  for (int k = 0; k < L; k++)
-    if ((uint32_t)k == (nbytes >> 2)) R[k] |= 1u << (8u * (nbytes & 3u));
+  // absorb: block b holds message bytes [136 b, 136 b + 136) = R words 34 b .. 34 b + 33; the
+  // final block carries the 0x01 pad byte at message position nbytes and 0x80 in its last byte
+  constexpr int kMaxBlocks = (4 * L) / 136 + 1;
+  const uint32_t nblocks = nbytes / 136u + 1u;   // uniform
   uint64_t A[25];
 #pragma unroll
-  for (int w = 0; w < 25; w++) A[w] = (2 * w + 1 < L) ? ((uint64_t)R[2 * w] | ((uint64_t)R[2 * w + 1] << 32)) : 0ull;
-  // nbytes == 4L (a 512-bit argument): the 0x01 pad byte is byte 64, outside R
-  if (nbytes >= 4u * L) A[nbytes >> 3] |= 1ull << (8u * (nbytes & 7u));
-  A[16] |= 0x8000000000000000ull;
-  keccak_f1600(A);
+  for (int w = 0; w < 25; w++) A[w] = 0ull;
+#pragma unroll
+  for (int b = 0; b < kMaxBlocks; b++) {
+    if ((uint32_t)b >= nblocks) break;
+#pragma unroll
+    for (int w = 0; w < 17; w++) {
+      const int i0 = 34 * b + 2 * w;
+      uint64_t lane = 0ull;
+      if (i0 < L) lane = R[i0];
+      if (i0 + 1 < L) lane |= (uint64_t)R[i0 + 1] << 32;
+      A[w] ^= lane;
+    }
+    if ((uint32_t)b == nblocks - 1u) {
+      const uint32_t pp = nbytes - 136u * (uint32_t)b;   // pad position inside the final block
+#pragma unroll
+      for (int w = 0; w < 17; w++)
+        if ((uint32_t)w == (pp >> 3)) A[w] ^= 1ull << (8u * (pp & 7u));
+      A[16] ^= 0x8000000000000000ull;
+    }
+    keccak_f1600(A);
+  }
 #pragma unroll
   for (int i = 0; i < L; i++) {
     uint32_t v = 0;
@@ -850,18 +891,30 @@ __global__ __launch_bounds__(64) void qs_column_kernel(KArgs args) {
   }
 }
 
+// The 1024/2048-bit stacks may need more than 64 KB of dynamic LDS (up to 8 x 16 KB per wave).
+template <class F>
+static hipError_t allow_lds(F* kernel, size_t lds) {
+  if (lds <= 65536) return hipSuccess;
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+}
+
 template <int L, bool K>
 static hipError_t launch_column_variant(const KArgs& a, hipStream_t st) {
   if (a.n_desc <= 0 || a.grid <= 0) return hipSuccess;
   const size_t lds = (size_t)a.stack_slots * L * 64 * 4;
+  hipError_t e = allow_lds(qs_column_kernel<L, K>, lds);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL((qs_column_kernel<L, K>), dim3((unsigned)a.grid), dim3(64), lds, st, a);
   return hipGetLastError();
 }
 
+// kernel variants: (8, plain), (16, plain), (16, keccak), (32, keccak), (64, keccak); the wide
+// stacks always carry the keccak handler (their registers are dominated by the wide operands)
 hipError_t launch_columns(const KArgs& a, int L, bool keccak, hipStream_t st) {
-  if (keccak) return L == 16 ? launch_column_variant<16, true>(a, st) : hipErrorInvalidValue;
-  if (L == 8) return launch_column_variant<8, false>(a, st);
-  if (L == 16) return launch_column_variant<16, false>(a, st);
+  if (L == 8 && !keccak) return launch_column_variant<8, false>(a, st);
+  if (L == 16) return keccak ? launch_column_variant<16, true>(a, st) : launch_column_variant<16, false>(a, st);
+  if (L == 32) return launch_column_variant<32, true>(a, st);
+  if (L == 64) return launch_column_variant<64, true>(a, st);
   return hipErrorInvalidValue;
 }
 
@@ -895,15 +948,18 @@ template <int L, bool K>
 static hipError_t launch_variant(const KArgs& a, bool verdict, hipStream_t st) {
   if (a.n_desc <= 0 || a.grid <= 0) return hipSuccess;
   const size_t lds = (size_t)a.stack_slots * L * 64 * 4;
+  hipError_t e = verdict ? allow_lds(qs_verdict_kernel<L, K>, lds) : allow_lds(qs_first_hit_kernel<L, K>, lds);
+  if (e != hipSuccess) return e;
   if (verdict) hipLaunchKernelGGL((qs_verdict_kernel<L, K>), dim3((unsigned)a.grid), dim3(64), lds, st, a);
   else hipLaunchKernelGGL((qs_first_hit_kernel<L, K>), dim3((unsigned)a.grid), dim3(64), lds, st, a);
   return hipGetLastError();
 }
 
 hipError_t launch_qs(const KArgs& a, int L, bool keccak, bool verdict, hipStream_t st) {
-  if (keccak) return L == 16 ? launch_variant<16, true>(a, verdict, st) : hipErrorInvalidValue;
-  if (L == 8) return launch_variant<8, false>(a, verdict, st);
-  if (L == 16) return launch_variant<16, false>(a, verdict, st);
+  if (L == 8 && !keccak) return launch_variant<8, false>(a, verdict, st);
+  if (L == 16) return keccak ? launch_variant<16, true>(a, verdict, st) : launch_variant<16, false>(a, verdict, st);
+  if (L == 32) return launch_variant<32, true>(a, verdict, st);
+  if (L == 64) return launch_variant<64, true>(a, verdict, st);
   return hipErrorInvalidValue;
 }
 

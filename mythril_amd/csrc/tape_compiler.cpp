@@ -12,6 +12,7 @@
 #include "tape_compiler.h"
 
 #include <algorithm>
+#include <cmath>
 #include <functional>
 #include <map>
 #include <tuple>
@@ -144,17 +145,27 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
         throw Fail{"predicate operand width mismatch"};
       if (n.op == MQ_OP_KECCAK) {
         const int aw = nd[n.a].width;
-        if (aw == 0 || aw % 8 || aw > 512 || n.width != 256) throw Fail{"keccak argument must be 8..512 bits, bytes"};
+        if (aw == 0 || aw % 8 || aw > kMaxWidth || n.width != 256) throw Fail{"keccak argument must be 8..2048 bits, bytes"};
         out.keccak = true;
       }
+      // multiplication, division and the multiplication-overflow predicates run on at most 16
+      // limbs (qs_kernels.hip kArithLimbs); Mythril only builds them at 256 / 257 bits
+      if ((n.op == MQ_OP_MUL || n.op == MQ_OP_UDIV || n.op == MQ_OP_UREM || n.op == MQ_OP_SDIV ||
+           n.op == MQ_OP_SREM || n.op == MQ_OP_SMOD) && n.width > 512)
+        throw Fail{"multiplication / division wider than 512 bits"};
+      if ((n.op == MQ_OP_UMUL_NOOVFL || n.op == MQ_OP_SMUL_NOOVFL || n.op == MQ_OP_SMUL_NOUDFL) && nd[n.a].width > 512)
+        throw Fail{"overflow predicate wider than 512 bits"};
     }
     if (kind[nn - 1] != K_BOOL && !(lim.value_root && kind[nn - 1] == K_BV)) throw Fail{"root is not Bool"};
+    // limbs per stack slot: the widest value of the tape (interpreted keccak runs on L >= 16)
     if (maxw <= 256 && !out.keccak) out.L = 8;
     else if (maxw <= 512) out.L = 16;
-    else throw Fail{"width > 512"};
+    else if (maxw <= 1024) out.L = 32;
+    else if (maxw <= kMaxWidth) out.L = 64;
+    else throw Fail{"width > 2048"};
     const int L = out.L;
-    const int max_depth = L == 8 ? lim.max_depth_l8 : lim.max_depth_l16;
-    const int max_temps = L == 8 ? lim.max_temps_l8 : lim.max_temps_l16;
+    const int max_depth = L == 8 ? lim.max_depth_l8 : L == 16 ? lim.max_depth_l16 : L == 32 ? lim.max_depth_l32 : lim.max_depth_l64;
+    const int max_temps = L == 8 ? lim.max_temps_l8 : L == 16 ? lim.max_temps_l16 : L == 32 ? lim.max_temps_l32 : lim.max_temps_l64;
 
     // ---------------------------------------------------------------- 2. internal DAG
     Builder B;
@@ -533,7 +544,8 @@ double tape_alg_ops(const mq_tape_batch* batch, int32_t t) {
         break;
       }
       case MQ_OP_KECCAK:
-        ops += 8000.0 * ((La * 4 + 1 + 135) / 136);
+        // keccak-f[1600] permutations: one per started 136-byte block (padding included)
+        ops += kKeccakOpsPerBlock * std::floor((La * 4 + 1 + 135) / 136);
         break;
       default:
         return -1;

@@ -9,11 +9,17 @@
 
 namespace mq {
 
+constexpr int kMaxWidth = 2048;   // widest value a tape may hold (64 limbs)
+
+// keccak-f[1600] cost per absorbed 136-byte block in 32-bit VALU ops; the
+// per-block instruction mix is counted in profiles/ 
+constexpr double kKeccakOpsPerBlock = 8000.0;
+
 struct CompiledTape {
   bool supported = false;
   std::string why;               // reason when unsupported
-  int L = 0;                     // limbs per value (8 or 16)
-  bool keccak = false;           // uses interpreted keccak (G_KECCAK): runs on the L=16 keccak kernel
+  int L = 0;                     // limbs per value (8, 16, 32 or 64)
+  bool keccak = false;           // uses interpreted keccak (G_KECCAK): runs on an L >= 16 keccak kernel
   int depth = 0;                 // max stack slots used
   int n_temps = 0;               // LDS temp slots
   std::vector<uint32_t> prog;    // instruction words, terminated by G_END
@@ -23,10 +29,18 @@ struct CompiledTape {
 };
 
 struct CompileLimits {
+  // LDS operand stack per wave: depth x L x 256 B (L = 8: 2 KB, 16: 4 KB, 32: 8 KB, 64: 16 KB
+  // per slot; gfx950 has 160 KB of LDS per CU, so a 2048-bit tape of depth 8 runs one wave per CU)
   int max_depth_l8 = 8;
   int max_depth_l16 = 6;
-  int max_temps_l8 = 64;      // temps live in a per-wave global scratch slot (64 x 2 KB)
-  int max_temps_l16 = 32;     // (32 x 4 KB)
+  int max_depth_l32 = 10;
+  int max_depth_l64 = 8;
+  // temps live in a per-wave HBM scratch slot (L x 256 B each): 64 x 2 KB, 32 x 4 KB, 32 x 8 KB,
+  // 32 x 16 KB (the wide kinds run on a 4x smaller persistent grid, mq_api.cpp make_args)
+  int max_temps_l8 = 64;
+  int max_temps_l16 = 32;
+  int max_temps_l32 = 32;
+  int max_temps_l64 = 32;
   int remat_max_nodes = 3;    // shared sub-terms up to this many cheap nodes are re-evaluated
   bool value_root = false;    // column program: any BV/Bool root, its value is the result
 };

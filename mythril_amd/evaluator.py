@@ -149,7 +149,7 @@ class CompiledTapes:
             self.n_columns = cols.n
 
     def split(self):
-        """(tapes on the assembly interpreter, generic 256-bit, generic 512-bit)."""
+        """(tapes on the assembly interpreter, generic 256-bit, wider generic kernels (512..2048-bit))."""
         a, b, c = C.c_int32(), C.c_int32(), C.c_int32()
         _check(self.ev.lib.mq_tapes_info(self.handle, C.byref(a), C.byref(b), C.byref(c)), "mq_tapes_info")
         return a.value, b.value, c.value
@@ -180,19 +180,32 @@ class CompiledTapes:
 
 
 class Evaluator:
-    """One evaluator context per GPU (one process per GPU for multi-GPU runs)."""
+    """An evaluator context (``mq_ctx``).  ``devices=[d0, d1, ...]`` drives several GPUs from this
+    one process (Mythril is single-process): the candidate axis is sharded over them
+    inside ``mq_models_upload`` and first hits are MIN-reduced over RCCL inside the library.
+    ``use_rccl=True`` on one device runs that RCCL path with a single rank.  The alternative, one
+    process per GPU under torch.distributed, uses single-device contexts (:mod:`mythril_amd.dist`)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, devices: Optional[Sequence[int]] = None, use_rccl: bool = False):
         self.lib = load_library()
+        ids = [int(d) for d in devices] if devices is not None else [int(device)]
         ctx = C.c_void_p()
-        dev = C.c_int(device)
-        _check(self.lib.mq_ctx_create(1, C.byref(dev), C.byref(ctx)), "mq_ctx_create")
+        arr = (C.c_int * len(ids))(*ids)
+        _check(self.lib.mq_ctx_create(len(ids), arr, C.byref(ctx)), "mq_ctx_create")
         self.ctx = ctx
-        self.device = device
+        self.devices = ids
+        self.device = ids[0]
         self.n_models = 0
         self.index_base = 0
+        if use_rccl and len(ids) == 1:
+            self.set_option(self.OPT_USE_RCCL, 1)
 
     OPT_USE_ASM, OPT_EARLY_EXIT, OPT_ASM_READY, OPT_TIME_KERNELS = 1, 2, 3, 4
+    OPT_USE_RCCL, OPT_RCCL_ACTIVE = 5, 6
+
+    @property
+    def rccl_active(self) -> bool:
+        return self.set_option(self.OPT_RCCL_ACTIVE, 0) == 1
 
     def set_option(self, option: int, value: int) -> int:
         rc = self.lib.mq_ctx_set_option(self.ctx, option, value)

@@ -34,12 +34,14 @@ class KeccakFunctionManager:
 
     def __init__(self, hasher: Optional[Callable[[bytes], bytes]] = None):
         self.hasher = hasher
+        self._index_counter = TOTAL_PARTS - 34534   # kfm.py:41, set once per manager
         self.reset()
 
     def reset(self) -> None:
+        """kfm.py:48-54: forgets functions, intervals and inputs but keeps ``_index_counter``, so
+        the interval of a size first seen after a reset differs from a fresh manager's."""
         self.store_function: Dict[int, Tuple[S.Function, S.Function]] = {}
         self.interval_hook_for_size: Dict[int, int] = {}
-        self._index_counter = TOTAL_PARTS - 34534
         self.hash_result_store: Dict[int, List[S.Term]] = {}
         self.concrete_hashes: Dict[S.Term, S.Term] = {}
         self.symbolic_inputs: Dict[int, List[S.Term]] = {}

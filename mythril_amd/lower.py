@@ -247,7 +247,7 @@ def shared_subterms(roots: Sequence[S.Term], min_nodes: int = 8, min_tapes: int 
             size[id(t)] = s
         return s
 
-    eligible = {i for i, c in count.items() if c >= min_tapes and terms[i].width <= 512}
+    eligible = {i for i, c in count.items() if c >= min_tapes and terms[i].width <= 2048}
     chosen: Dict[int, S.Term] = {}
     for r in roots:   # top-down: the first eligible term on every path is maximal for that root
         stack = list(r.args)

@@ -185,17 +185,35 @@ _UNSUPPORTED = object()
 class ModelCache:
     """support_utils.py:56-70 with the GPU verdict engine behind ``check_quick_sat``."""
 
+    MEMO_SIZE = 2 ** 10   # @lru_cache(maxsize=2**10) on check_quick_sat (support_utils.py:60)
+
     def __init__(self, engine: Optional[VerdictEngine] = None):
         self.model_cache = LRUCache(size=100)
         self.engine = engine or VerdictEngine()
         # expr -> {model: verdict} for conjunctions evaluated ahead of their check_quick_sat call
         self._rows: Dict[object, object] = {}
         self._pending: "OrderedDict[object, None]" = OrderedDict()
+        # the memo of check_quick_sat: functools.lru_cache semantics (a hit moves to MRU, the LRU
+        # entry is evicted past MEMO_SIZE, exceptions are not cached), kept as a dict so prefetch
+        # can tell which conjunctions will never reach the evaluator again
+        self._memo: "OrderedDict[object, object]" = OrderedDict()
         self.stats = {"queries": 0, "hits": 0, "unsupported": 0}
 
-    # support_utils.py:60-67
-    @lru_cache(maxsize=2 ** 10)
     def check_quick_sat(self, constraints):
+        """support_utils.py:60-67, memoized per ``(self, constraints)`` like the reference's
+        ``@lru_cache(maxsize=2**10)``: a memoized ``False`` or model is returned again without
+        re-evaluation and without an LRU bump."""
+        memo = self._memo
+        if constraints in memo:
+            memo.move_to_end(constraints)
+            return memo[constraints]
+        result = self._check_quick_sat(constraints)
+        memo[constraints] = result
+        if len(memo) > self.MEMO_SIZE:
+            memo.popitem(last=False)
+        return result
+
+    def _check_quick_sat(self, constraints):
         self.stats["queries"] += 1
         order = list(reversed(self.model_cache.lru_cache.keys()))
         row = self._verdicts(constraints, order)
@@ -223,8 +241,9 @@ class ModelCache:
 
     # -------------------------------------------------------------- batching
     def prefetch(self, exprs: Iterable) -> None:
-        """Evaluate pending conjunctions against the current cache in one launch (a10)."""
-        exprs = [e for e in dict.fromkeys(exprs) if e not in self._rows]
+        """Evaluate pending conjunctions against the current cache in one launch (a10).
+        Conjunctions the memo already answers never reach the evaluator again: they are skipped."""
+        exprs = [e for e in dict.fromkeys(exprs) if e not in self._rows and e not in self._memo]
         order = list(reversed(self.model_cache.lru_cache.keys()))
         for e in exprs:
             self._rows[e] = {}
@@ -232,10 +251,20 @@ class ModelCache:
         if exprs and order:
             self._fill(exprs, order)
 
+    def discard(self, exprs: Iterable) -> None:
+        """Forget prefetched rows of conjunctions whose check_quick_sat never ran (their answer
+        came from get_model's own memo): they must not ride along in later launches."""
+        for e in exprs:
+            self._rows.pop(e, None)
+            self._pending.pop(e, None)
+
     def check_quick_sat_batch(self, exprs: Sequence) -> list:
         """``[check_quick_sat(e) for e in exprs]`` with one GPU launch for the whole batch."""
         self.prefetch(exprs)
-        return [self.check_quick_sat(e) for e in exprs]
+        try:
+            return [self.check_quick_sat(e) for e in exprs]
+        finally:
+            self.discard(exprs)
 
     def _fill(self, exprs: List, models: List) -> None:
         rows = self.engine.rows(exprs, models)
@@ -343,6 +372,8 @@ def get_model(constraints, minimize=(), maximize=(), solver_timeout=None):
 
     if len(maximize) + len(minimize) == 0:
         ret_model = model_cache.check_quick_sat(simplify(S.And(*constraints)))
+        # the reference's cached models are mythril ``Model`` wrappers (smt/model.py:6-18), which
+        # define neither __len__ nor __bool__: any model is truthy, exactly like ours
         if ret_model:
             counters["quick_sat_answers"] += 1
             return ret_model
@@ -351,7 +382,9 @@ def get_model(constraints, minimize=(), maximize=(), solver_timeout=None):
     try:
         res = pool.apply_async(solver_worker, args=(constraints, minimize, maximize, solver_timeout))
         try:
-            status, factory = res.get(None if math.isinf(solver_timeout) else solver_timeout / 1000.0)
+            # model.py:110 hands the millisecond timeout to AsyncResult.get(), which reads it as
+            # seconds: the pool wait never pre-empts the solver's own timeout.  Kept as is.
+            status, factory = res.get(None if math.isinf(solver_timeout) else solver_timeout)
         except _PoolTimeout:
             status, factory = "unknown", None
         except Exception:
@@ -442,7 +475,12 @@ def is_possible_batch(states: Sequence[Constraints], solver_timeout=None) -> Lis
     for all quick-sat queries.  Answers are identical to the sequential loop (see module doc)."""
     exprs = [e for e in (quick_sat_expr(c) for c in states) if e is not None]
     model_cache.prefetch(exprs)
-    return [c.is_possible(solver_timeout=solver_timeout) for c in states]
+    try:
+        return [c.is_possible(solver_timeout=solver_timeout) for c in states]
+    finally:
+        # a state whose get_model call was answered by get_model's own memo never reached
+        # check_quick_sat: drop its prefetched row so it does not ride along in later launches
+        model_cache.discard(exprs)
 
 
 def enable_dump(directory: Optional[str]) -> None:

@@ -106,6 +106,10 @@ def c2_workload(n_tapes: int = 10_000, n_models: int = 100_000, seed: int = 2,
 _BV_BIN = [Op.ADD, Op.SUB, Op.MUL, Op.UDIV, Op.UREM, Op.SDIV, Op.SREM, Op.SMOD,
            Op.BAND, Op.BOR, Op.BXOR, Op.SHL, Op.LSHR, Op.ASHR]
 _PRED = [Op.EQ, Op.ULT, Op.ULE, Op.SLT, Op.SLE, Op.UMUL_NOOVFL, Op.SMUL_NOOVFL, Op.SMUL_NOUDFL]
+# multiplication / division / the multiplication-overflow predicates stop at 512 bits (mq.h)
+_MULDIV = frozenset({Op.MUL, Op.UDIV, Op.UREM, Op.SDIV, Op.SREM, Op.SMOD,
+                     Op.UMUL_NOOVFL, Op.SMUL_NOOVFL, Op.SMUL_NOUDFL})
+FUZZ_WIDTHS = (1, 8, 32, 64, 160, 256, 512, 544, 768, 1088, 2048)
 
 
 def interesting_value(rng: np.random.Generator, w: int) -> int:
@@ -170,6 +174,8 @@ class _Fuzz:
             op = _BV_BIN[int(rng.integers(len(_BV_BIN)))]
             if not self.allowed(op):
                 return self.bv_leaf(w)
+            if w > 512 and op in _MULDIV:
+                op = Op.BXOR
             a = self.bv(w, depth - 1)
             if op in (Op.SHL, Op.LSHR, Op.ASHR) and rng.random() < 0.6:
                 b = t.const(int(rng.integers(0, w + 3)) & ((1 << w) - 1), w)
@@ -223,7 +229,9 @@ class _Fuzz:
             op = _PRED[int(rng.integers(len(_PRED)))]
             if not self.allowed(op):
                 op = Op.EQ
-            w = int(rng.choice(self.widths or [w for w in (1, 8, 32, 64, 160, 256, 512) if w <= self.maxw]))
+            w = int(rng.choice(self.widths or [w for w in FUZZ_WIDTHS if w <= self.maxw]))
+            if w > 512 and op in _MULDIV:
+                op = Op.EQ
             a = self.bv(w, depth - 1)
             b = self.bv(w, depth - 1) if rng.random() < 0.7 else a
             if op == Op.EQ and rng.random() < 0.3:
@@ -267,13 +275,15 @@ def fuzz_workload(seed: int, n_tapes: int, n_models: int, max_width: int = 256, 
         var_widths = [256] * 8
         tapes = [fuzz_tape(rng, var_widths, (), depth, 256, ASM_OPS, widths=[256]) for _ in range(n_tapes)]
         return TapeBatch(tapes), fuzz_models(rng, var_widths, n_models)
-    widths = [w for w in (1, 8, 32, 64, 160, 256, 512) if w <= max_width]
+    widths = [w for w in FUZZ_WIDTHS if w <= max_width]
     var_widths = [int(rng.choice(widths)) for _ in range(10)] + [256, 256, BOOL, 8]
     funcs: List[FuncSpec] = []
     if with_funcs:
         funcs = [FuncSpec(1, 256, (256,)), FuncSpec(1, 8, (256,)), FuncSpec(2, 256, (256, 256))]
         if max_width >= 512:
             funcs.append(FuncSpec(1, 256, (512,)))
+        if max_width >= 1088:   # keccak256_1088 and its inverse (a 1088-bit result)
+            funcs += [FuncSpec(1, 256, (1088,)), FuncSpec(1, 1088, (256,))]
     tapes = [fuzz_tape(rng, var_widths, funcs, depth, max_width, ops) for _ in range(n_tapes)]
     models = fuzz_models(rng, var_widths, n_models, funcs)
     return TapeBatch(tapes), models

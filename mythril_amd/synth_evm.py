@@ -538,3 +538,106 @@ def c4_workload(n_tapes: int = 200, n_models: int = 1_000_000, seed: int = 4, pl
     tb, syms, ok = lower_batch(roots, syms, hoist=hoist)
     assert ok.all()
     return tb, models.batch(syms), expected, syms
+
+
+# ====================================================================== C4-wide: keccak of > 64 bytes
+WIDE_SIZES = (544, 768, 1088)   # keccak256(msg.data) of a 2-argument call, abi.encode of 3 words, 136 B
+
+
+def c4_wide_workload(n_tapes: int = 48, n_models: int = 2048, seed: int = 44, sizes: Sequence[int] = WIDE_SIZES,
+                     planted_frac: float = 0.3, hasher=None, hoist: bool = False):
+    """Keccak inputs LONGER than 64 bytes, the shape of ``WalletLibrary.sol:134``
+    (``keccak256(msg.data)`` on ``changeOwner(address,address)``: 68 bytes = 544 bits) and of
+    ``abi.encode`` of three words (768 bits), plus a 136-byte (one full keccak block) input.
+
+    Mythril hashes ``Concat`` of memory bytes (instructions.py:1017-1052) through the UF
+    ``keccak256_<n>``; the manager's axioms (keccak_function_manager.py:116-179) for EVERY input of
+    the run ride on every query: ``inv(f(x)) == x`` at n bits, interval + ``urem 64`` on f(x), or a
+    match with a concretely hashed input.  Candidate models are z3-shaped: ``keccak256_<n>`` maps the
+    model's own input to a multiple of 64 inside the size's interval (what a solver picks) and each
+    concrete input to its true digest; ``keccak256_<n>-1`` inverts both.  Paths: actor caller,
+    selector dispatch, ``pending[h]`` storage reads keyed by the hash, interval comparisons on h
+    and a selector re-read through the inverse (``Extract`` of a > 512-bit UF result).
+    Returns ``(tapes, models, expected first hits, records)`` (``records`` = the Model objects)."""
+    from .function_managers import KeccakFunctionManager
+    from .lower import serialize_models
+    from .smt_model import Model
+
+    if hasher is None:
+        from .evaluator import default_evaluator
+        hasher = lambda b: default_evaluator().keccak256([b])[0]   # noqa: E731
+    rng = np.random.Generator(np.random.PCG64(seed))
+    km = KeccakFunctionManager(hasher=hasher)
+    for n in sizes:                      # intervals in a fixed order (first use order in Mythril)
+        km.interval(n)
+    nmax = max(sizes) // 8
+    tx = _Tx(1)
+    data = {n: S.Concat(*[tx.byte(i) for i in range(n // 8)]) for n in sizes}
+    # one concretely hashed input per size (constant keys: find_concrete_keccak, kfm.py:56-69)
+    conc = {n: int.from_bytes(rng.bytes(n // 8), "big") for n in sizes}
+    conc_h = {n: km.create_keccak(S.BitVecVal(conc[n], n)).value for n in sizes}
+    hashes = {n: km.create_keccak(data[n]) for n in sizes}
+    axioms = km.create_conditions()
+    f = {n: km.get_function(n) for n in sizes}
+
+    # candidate models
+    records = []
+    wit = []
+    for m in range(n_models):
+        who = int(rng.integers(0, 10))
+        sender = ACTORS[who // 3] if who < 9 else int.from_bytes(rng.bytes(20), "big")
+        cds = int(rng.integers(4, nmax + 24))
+        cd = [int(x) for x in rng.integers(0, 256, nmax + 24)]
+        funcs = {"1_calldata": ({(i,): cd[i] for i in range(len(cd))}, 0)}
+        vals = {}
+        for n in sizes:
+            x = 0
+            for i in range(n // 8):
+                x = (x << 8) | (cd[i] if i < cds else 0)
+            lo, hi = km.interval(n)
+            v = (lo + 63) // 64 * 64 + 64 * int(rng.integers(0, 1 << 40))
+            assert v < hi
+            fwd, inv = f[n]
+            funcs[fwd.name] = ({(x,): v, (conc[n],): conc_h[n]}, 0)
+            funcs[inv.name] = ({(v,): x, (conc_h[n],): conc[n]}, 0)
+            vals[n] = (x, v)
+        records.append(Model({"sender_1": sender, "1_calldatasize": cds}, funcs))
+        wit.append({"sender": sender, "cds": cds, "cd": cd, "vals": vals})
+
+    def path(w, planted_: bool) -> S.Term:
+        cs = [S.Or(*[tx.sender == a for a in ACTORS]),
+              _holds(S.ULT(tx.cds, S.BitVecVal(4, 256)), w["cds"] < 4)]
+        sel = _word_val(w["cd"], w["cds"], 0) >> 224
+        cs.append(S.Extract(255, 224, tx.word(0)) == sel)
+        pending = S.K(256, 256, 0)
+        for n in sizes:
+            pending = S.Store(pending, S.BitVecVal(conc_h[n], 256), 1)
+        for n in sizes:
+            if rng.random() < 0.25:
+                continue
+            h = hashes[n]
+            x, v = w["vals"][n]
+            cs.append(_holds(S.Select(pending, h) == 0, v not in conc_h.values()))
+            t = int.from_bytes(rng.bytes(32), "big") | (1 << 255)
+            cs.append(_holds(S.ULT(h, S.BitVecVal(t, 256)), v < t))
+            # the selector read back through the inverse: a > 512-bit UF result, Extract'ed
+            cs.append(S.Extract(n - 1, n - 32, f[n][1](h)) == (x >> (n - 32)))
+        return S.And(*cs, axioms)
+
+    roots, expected = [], np.full(n_tapes, -1, np.int32)
+    planted = rng.random(n_tapes) < planted_frac
+    for t in range(n_tapes):
+        if planted[t]:
+            while True:
+                p = int(rng.integers(n_models))
+                if wit[p]["sender"] in ACTORS and wit[p]["cds"] >= 4:
+                    break
+            roots.append(path(wit[p], True))
+            expected[t] = p   # the first hit can be lower: fixed below against the oracle
+        else:
+            g = {"sender": ACTORS[0], "cds": 200, "cd": [int(x) for x in rng.integers(0, 256, nmax + 24)],
+                 "vals": {n: (0, 0) for n in sizes}}
+            roots.append(path(g, False))
+    tb, syms, ok = lower_batch(roots, SymbolTable(), hoist=hoist)
+    assert ok.all()
+    return tb, serialize_models(records, syms), expected, records

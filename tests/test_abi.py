@@ -69,14 +69,34 @@ def test_compile_fuzz_tapes_mostly_supported():
         assert all(i.limbs == (8 if mw == 256 else i.limbs) for i in sup)
 
 
+def test_compile_supports_values_up_to_2048_bits():
+    """Keccak inputs longer than 64 bytes (WalletLibrary.sol:134 keccak256(msg.data): 544 bits;
+    abi.encode of 3 words: 768; one full block: 1088) compile onto the 1024 / 2048-bit stacks."""
+    for w, L in ((544, 32), (768, 32), (1024, 32), (1088, 64), (2048, 64)):
+        t = Tape()
+        x = t.var(0, w)
+        root = t.and_(t.eq(x, t.const(3, w)), t.ult(t.keccak(x), t.const(5, 256)))
+        ci = evaluator.compile_info(TapeBatch([t.finish(root)]), 0)
+        assert ci.supported and ci.limbs == L, (w, ci)
+    t = Tape()   # a > 512-bit UF result (keccak256_<n>-1) extracted back to a selector
+    inv = t.uf(1, 1088, t.var(0, 256))
+    ci = evaluator.compile_info(TapeBatch([t.finish(t.eq(t.extract(1087, 1056, inv), t.const(7, 32)))]), 0)
+    assert ci.supported and ci.limbs == 64
+
+
 def test_compile_rejects_what_it_cannot_do():
     t = Tape()
-    x = t.var(0, 1024)
-    tb = TapeBatch([t.finish(t.eq(x, t.const(3, 1024)))])
+    x = t.var(0, 2056)
+    tb = TapeBatch([t.finish(t.eq(x, t.const(3, 2056)))])
+    ci = evaluator.compile_info(tb, 0)
+    assert not ci.supported and "2048" in ci.why
+    t = Tape()
+    a = t.var(0, 1024)        # multiplication / division stop at 512 bits
+    tb = TapeBatch([t.finish(t.eq(t.mul(a, a), t.const(3, 1024)))])
     ci = evaluator.compile_info(tb, 0)
     assert not ci.supported and "512" in ci.why
     t = Tape()
-    k = t.keccak(t.var(0, 520))   # one keccak block holds at most 64 argument bytes here
+    k = t.keccak(t.var(0, 2056))
     tb = TapeBatch([t.finish(t.eq(k, t.const(3, 256)))])
     assert not evaluator.compile_info(tb, 0).supported
 

@@ -258,3 +258,46 @@ def test_exponent_manager():
     table[(256, 33)] = 256
     assert eval_under(cond, Model({"e": 33}, {"Power": (dict(table), 0)}))
     assert not eval_under(cond, Model({"e": 33}, {"Power": ({(256, 33): 256}, 0)}))  # axioms missing
+
+
+def test_prefetch_skips_memoized_and_leaves_nothing_pending(cache):
+    """a conjunction already answered by the check_quick_sat memo must not stay in
+    the pending set (it would ride along in every later launch)."""
+    m = Model({"x": 4})
+    cache.put(m, 1)
+    e1 = S.And(x == 4)
+    assert cache.check_quick_sat(e1) is m
+    cache.prefetch([e1])
+    assert e1 not in cache._pending and e1 not in cache._rows
+    e2 = S.ULT(x, S.BitVecVal(9, 256))
+    cache.prefetch([e2])            # prefetched but never asked (answered elsewhere)
+    cache.discard([e2])
+    assert not cache._pending and not cache._rows
+
+
+def test_is_possible_batch_discards_rows_answered_by_get_model_memo(fresh):
+    sp.set_solver_backend(ScriptedSolver(lambda cs: Model({"x": 2})))
+    c = sp.Constraints([x == 2])
+    assert c.is_possible()                        # solver call, model cached, get_model memoized
+    assert sp.is_possible_batch([c, c]) == [True, True]
+    assert not sp.model_cache._pending and not sp.model_cache._rows
+
+
+def test_check_quick_sat_memo_is_bounded_lru(cache):
+    cache.put(Model({"x": 1}), 1)
+    cache.MEMO_SIZE = 4
+    exprs = [S.And(x == v) for v in range(6)]
+    for e in exprs:
+        cache.check_quick_sat(e)
+    assert list(cache._memo) == exprs[2:]
+    cache.check_quick_sat(exprs[2])              # a memo hit moves to MRU
+    assert list(cache._memo)[-1] is exprs[2]
+
+
+def test_keccak_manager_reset_keeps_index_counter():
+    """kfm.py:48-54: reset() does not rewind _index_counter."""
+    km = KeccakFunctionManager(hasher=keccak_ref.keccak256)
+    lo0, _ = km.interval(512)
+    km.reset()
+    lo1, _ = km.interval(512)
+    assert lo1 != lo0
