@@ -199,6 +199,14 @@ const char* mq_strerror(int code);
    n_models may be 0 (an empty model-axis shard: every tape reports MQ_NO_HIT). */
 int mq_models_upload(mq_ctx* ctx, const mq_model_batch* models);
 
+/* Host-only (no device needed): candidates [lo, hi) of `models` as a batch of their own, with
+   index_base + lo — exactly the shard device g of a multi-device context holds (contiguous in
+   global candidate order); also what a one-process-per-GPU caller uploads per rank.
+   Variable rows and function entries are packed into a buffer owned by *handle (else values
+   point into `models`, which must outlive *out); release it with mq_models_shard_free. */
+int mq_models_shard(const mq_model_batch* models, int64_t lo, int64_t hi, mq_model_batch* out, void** handle);
+void mq_models_shard_free(void* handle);
+
 /* Compile + upload a tape batch once (the lowering of simplify(And(*constraints)).raw,
    model.py:101); reusable across evaluations.  n_unsupported_out may be NULL. */
 int mq_tapes_upload(mq_ctx* ctx, const mq_tape_batch* batch, mq_tapes** out, int32_t* n_unsupported_out);

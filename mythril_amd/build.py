@@ -49,12 +49,25 @@ def _stale(obj: str, src: str) -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
+def _generated_current() -> bool:
+    """qsa_gen.inc / qsa_table.h (generated, not tracked) carry the sha256 of gen_qsa.py."""
+    import hashlib
+    with open(os.path.join(CSRC, "gen_qsa.py"), "rb") as f:
+        stamp = hashlib.sha256(f.read()).hexdigest()[:16]
+    for name in ("qsa_gen.inc", "qsa_table.h"):
+        path = os.path.join(CSRC, name)
+        if not os.path.exists(path):
+            return False
+        with open(path) as f:
+            if f"(source {stamp})" not in f.readline():
+                return False
+    return True
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     hipcc = _hipcc()
-    gen = os.path.join(CSRC, "gen_qsa.py")
-    inc = os.path.join(CSRC, "qsa_gen.inc")
-    if force or not os.path.exists(inc) or os.path.getmtime(inc) < os.path.getmtime(gen):
-        subprocess.check_call([sys.executable, gen])
+    if force or not _generated_current():
+        subprocess.check_call([sys.executable, os.path.join(CSRC, "gen_qsa.py")])
     os.makedirs(OBJDIR, exist_ok=True)
     jobs = []
     objs = []

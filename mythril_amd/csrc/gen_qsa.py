@@ -929,7 +929,16 @@ def vgprs(variant):
     return 96 if (variant == "g" and NVG == 0) else 128
 
 
+def source_stamp() -> str:
+    """sha256 of this generator: written into both outputs, compared by build.py (regenerate on
+    any change of the generator, independent of file times)."""
+    import hashlib
+    with open(os.path.abspath(__file__), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def main():
+    stamp = source_stamp()
     sclob = [f'"s{i}"' for i in range(10, 100) if i not in (32, 33)] + ['"vcc"', '"scc"', '"memory"']
     clob = {v: [f'"v{i}"' for i in range(1, vgprs(v))] + sclob for v in ("p", "g")}
     gen = {}
@@ -938,7 +947,7 @@ def main():
         hs, subs = make_handlers(variant, pfx)
         gen[variant] = (hs, frame(variant, pfx, hs, subs), macro, suffix)
     with open(os.path.join(HERE, "qsa_gen.inc"), "w") as f:
-        f.write("// GENERATED by gen_qsa.py — do not edit\n")
+        f.write(f"// GENERATED by gen_qsa.py (source {stamp}) — do not edit\n")
         for variant, (hs, lines, macro, suffix) in gen.items():
             f.write(f"#define {macro} \\\n")
             for ln in lines:
@@ -948,7 +957,7 @@ def main():
         f.write("#define QSA_CLOBBERS_G " + ", ".join(clob["g"]) + "\n")
     names = sorted({k[0] for hs, *_ in gen.values() for k, _ in hs})
     with open(os.path.join(HERE, "qsa_table.h"), "w") as f:
-        f.write("// GENERATED by gen_qsa.py — handler enumerations of the QSA interpreters\n")
+        f.write(f"// GENERATED by gen_qsa.py (source {stamp}) — handler enumerations of the QSA interpreters\n")
         f.write("#ifndef MQ_QSA_TABLE_H\n#define MQ_QSA_TABLE_H\nnamespace mq {\n")
         f.write(f"constexpr int kQsaStack = {D};\nconstexpr int kQsaVars = {NV};\nconstexpr int kQsaVarsG = {NVG};\nconstexpr int kQsaSel = {L};\n")
         f.write("enum QsaKind {\n" + "".join(f"  QK_{n},\n" for n in names) + "  QK_COUNT\n};\n")

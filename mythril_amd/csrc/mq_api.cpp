@@ -524,6 +524,17 @@ static mq_model_batch shard_view(const mq_model_batch* mb, int64_t lo, int64_t h
   return s;
 }
 
+int mq_models_shard(const mq_model_batch* mb, int64_t lo, int64_t hi, mq_model_batch* out, void** handle) {
+  if (!mb || !out || !handle || lo < 0 || hi < lo || hi > mb->n_models || mb->n_funcs < 0 || mb->n_vars < 0)
+    return MQ_ERR_ARG;
+  auto* keep = new ShardBuffers();
+  *out = shard_view(mb, lo, hi, *keep);
+  *handle = keep;
+  return MQ_OK;
+}
+
+void mq_models_shard_free(void* handle) { delete static_cast<ShardBuffers*>(handle); }
+
 int mq_models_upload(mq_ctx* c, const mq_model_batch* mb) {
   if (!c || !mb || mb->n_models < 0) return MQ_ERR_ARG;
   if (c->peers.empty()) {

@@ -69,6 +69,9 @@ def load_library(path: str = LIB_PATH):
         L.mq_tape_alg_ops.restype = C.c_double
         L.mq_tape_compile_info.argtypes = [C.POINTER(MqTapeBatch), C.c_int32] + [C.POINTER(C.c_int32)] * 5 + [C.c_char_p, C.c_int32]
         L.mq_tape_program.argtypes = [C.POINTER(MqTapeBatch), C.c_int32, C.POINTER(C.c_uint32), C.c_int32, C.POINTER(C.c_int32)]
+        L.mq_models_shard.argtypes = [C.POINTER(MqModelBatch), C.c_int64, C.c_int64, C.POINTER(MqModelBatch), C.POINTER(P)]
+        L.mq_models_shard_free.argtypes = [P]
+        L.mq_models_shard_free.restype = None
         _lib = L
         return L
 
@@ -118,6 +121,33 @@ def tape_program(tb: TapeBatch, t: int) -> np.ndarray:
     out = np.zeros(n.value, np.uint32)
     _check(L.mq_tape_program(C.byref(s), t, out.ctypes.data_as(C.POINTER(C.c_uint32)), n.value, C.byref(n)), "tape_program")
     return out
+
+
+def shard_models(mb: ModelBatch, lo: int, hi: int) -> ModelBatch:
+    """Host-only: candidates [lo, hi) as their own batch (``mq_models_shard``) — the contiguous
+    shard a device of a multi-device context, or one rank of the per-process path, holds."""
+    L = load_library()
+    s, keep = as_model_batch(mb)
+    out = MqModelBatch()
+    h = C.c_void_p()
+    _check(L.mq_models_shard(C.byref(s), int(lo), int(hi), C.byref(out), C.byref(h)), "mq_models_shard")
+    try:
+        ms, F = hi - lo, len(mb.funcs)
+        rows = int(mb.var_word_offsets()[-1])
+
+        def arr(ptr, n, dtype):
+            return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dtype, copy=True) if n else np.zeros(0, dtype)
+
+        words = arr(out.var_words, rows * ms, np.uint32).reshape(rows, ms)
+        if not F:
+            return ModelBatch(mb.var_widths, words, index_base=out.index_base)
+        eptr = arr(out.entry_ptr, F * (ms + 1), np.int64).reshape(F, ms + 1)
+        ebase = arr(out.entry_base, F, np.int64)
+        ew = arr(out.entry_words, int(out.n_entry_words), np.uint32)
+        elb = arr(out.else_base, F, np.int64)
+        return ModelBatch(mb.var_widths, words, mb.funcs, eptr, ew, ebase, mb.else_words, elb, out.index_base)
+    finally:
+        L.mq_models_shard_free(h)
 
 
 def tape_alg_ops(tb: TapeBatch, t: int) -> float:

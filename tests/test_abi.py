@@ -125,3 +125,25 @@ def test_alg_ops_cost_table():
     root = t.and_(t.eq(t.add(x, y), t.mul(x, y)), t.ult(x, y))
     tb = TapeBatch([t.finish(root)])
     assert evaluator.tape_alg_ops(tb, 0) == 8 + 72 + 8 + 8 + 1
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 7])
+def test_models_shard_matches_python_shard_and_covers_the_batch(world):
+    """mq_models_shard (what mq_models_upload gives each device of a multi-device context) equals
+    ModelBatch.shard, and the shards' cref first hits MIN-merge to the unsharded first hits
+    (the RCCL ncclMin of the library, restated on the host; support_utils.py:62 order)."""
+    import cref
+    from mythril_amd import dist
+    tb, mb = fuzz_workload(31, 25, 50, max_width=512)
+    ref, _ = cref.first_hit(tb, mb)
+    parts = []
+    for r in range(world):
+        lo, hi = dist.shard_bounds(mb.n_models, r, world)
+        a, b = evaluator.shard_models(mb, lo, hi), mb.shard(lo, hi)
+        assert a.index_base == b.index_base == lo and a.n_models == hi - lo
+        assert (a.var_words == b.var_words).all()
+        for m in range(hi - lo):
+            for f in range(len(mb.funcs)):
+                assert a.func_table(f, m) == b.func_table(f, m) == mb.func_table(f, lo + m)
+        parts.append(dist.encode_local(cref.first_hit(tb, a)[0]))
+    assert (dist.decode_global(np.minimum.reduce(parts)) == ref).all()
