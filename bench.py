@@ -97,31 +97,62 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(tb, mb, target_s: float):
-    """Oracle C restatement (oracle/cref.c, OpenMP) timed on a bounded sample of the SAME
-    workload: the first n tapes x all models of the shard, n sized to ~target_s."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import cref  # oracle: checker / CPU baseline only
-    cores = min(16, os.cpu_count() or 1)
-    n = max(8, min(tb.n_tapes, 32))
+def host_cores():
+    """CPU counts of this host: ``nproc`` (os.cpu_count), the CPUs this process may run on
+    (sched_getaffinity) and the cgroup CPU quota; the OpenMP leg uses every core this job can
+    actually use = min(affinity, quota)."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = nproc
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, period = open(path).read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(period)))
+        except (OSError, ValueError):
+            pass
+    usable = min(aff, quota) if quota else aff
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota": quota, "usable": usable}
+
+
+def _timed_first_hit(cref, tb, mb, target_s: float, threads: int):
+    """The first n tapes x all models, n grown until the oracle runs ~target_s."""
+    n = max(4, min(tb.n_tapes, 16))
     while True:
         sub = tb.subset(range(n))
         t0 = time.perf_counter()
-        fh, pairs = cref.first_hit(sub, mb, nthreads=cores)
+        fh, pairs = cref.first_hit(sub, mb, nthreads=threads)
         dt = time.perf_counter() - t0
         if dt >= target_s * 0.5 or n >= tb.n_tapes:
             break
         n = min(tb.n_tapes, int(n * max(2.0, target_s / max(dt, 1e-3))))
-    node_evals = 0.0
     sizes = sub.sizes()
-    # pairs per tape are not returned individually; approximate with the full-M pass for
-    # unsatisfied tapes and first_hit+1 models for satisfied ones (exact for cref's early exit)
+    # node-evals the oracle performed: the full M for tapes without a hit, first hit + 1 otherwise
+    # (cref stops a tape at its first satisfying model, support_utils.py:62-66)
+    node_evals = 0.0
     for t in range(sub.n_tapes):
         evals = mb.n_models if fh[t] < 0 else (fh[t] - mb.index_base + 1)
         node_evals += float(evals) * float(sizes[t])
-    return {"value": node_evals / dt, "unit": "node-evals/s", "cores": cores, "kind": "port",
-            "sample": f"first {n} of {tb.n_tapes} tapes x {mb.n_models} models of the same workload, oracle/cref.c "
-                      f"(OpenMP {cores} threads), {dt:.1f} s", "seconds": dt}
+    return node_evals / dt, n, dt
+
+
+def cpu_baseline(tb, mb, target_s: float):
+    """Oracle C restatement (oracle/cref.c) timed on bounded samples of the SAME workload, once on
+    every usable host core (OpenMP over tapes) and once single-core (BASELINE.md CPU plan)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cref  # oracle: checker / CPU baseline only
+    hc = host_cores()
+    cores = hc["usable"]
+    v_all, n_all, dt_all = _timed_first_hit(cref, tb, mb, target_s * 2 / 3, cores)
+    v_one, n_one, dt_one = _timed_first_hit(cref, tb, mb, target_s / 3, 1)
+    return {"value": v_all, "unit": "node-evals/s", "cores": cores, "kind": "port",
+            "sample": f"first {n_all} of {tb.n_tapes} tapes x {mb.n_models} models of the same workload, "
+                      f"oracle/cref.c OpenMP over {cores} threads, {dt_all:.1f} s; single core: first {n_one} tapes, "
+                      f"{dt_one:.1f} s",
+            "single_core_value": v_one, "host": hc, "seconds": dt_all + dt_one}
 
 
 def pmc_traffic(workload_key: str):
@@ -286,7 +317,7 @@ def main():
                 cb = cpu_baseline(ptb, pmb, args.cpu_seconds)
             else:
                 cb = cpu_baseline(tb, mb, args.cpu_seconds)
-            out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
+            out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample", "single_core_value", "host")}
             out["gpu_over_cpu"] = out["value"] / cb["value"]
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -131,6 +131,23 @@ typedef struct mq_tape_batch {
   int64_t n_const_words;
 } mq_tape_batch;
 
+/* A stream of queries over ONE hash-consed DAG (the z3 AST table of a run: paths forked from a
+ * common parent share their constraints, and the keccak axioms ride on every query,
+ * constraints.py:127-128).  nodes[0..n_nodes) is postfix (operands precede users) and grows
+ * append-only on the caller's side; tape t is the AND of the conjunct roots
+ * roots[root_offsets[t] .. root_offsets[t+1]) (none: true), i.e. And(*constraints) of
+ * model.py:101 without re-lowering shared conjuncts.  The evaluator extracts each tape's
+ * reachable nodes itself. */
+typedef struct mq_dag_batch {
+  int64_t n_nodes;
+  const mq_node* nodes;
+  const uint32_t* const_words;
+  int64_t n_const_words;
+  int32_t n_tapes;
+  const int64_t* root_offsets;   /* [n_tapes+1] */
+  const uint32_t* roots;
+} mq_dag_batch;
+
 /* ------------------------------------------------------------------ candidate models
  * One batch = M candidate models in global candidate order (0 = MRU), the z3 ModelRef
  * contents serialized WITHOUT completion (support_utils.py:63 deep-copies because eval with
@@ -211,6 +228,15 @@ void mq_models_shard_free(void* handle);
    model.py:101); reusable across evaluations.  n_unsupported_out may be NULL. */
 int mq_tapes_upload(mq_ctx* ctx, const mq_tape_batch* batch, mq_tapes** out, int32_t* n_unsupported_out);
 void mq_tapes_free(mq_tapes* tapes);
+
+/* Same for a DAG batch (the drop-in query stream; see mq_dag_batch). */
+int mq_tapes_upload_dag(mq_ctx* ctx, const mq_dag_batch* dag, mq_tapes** out, int32_t* n_unsupported_out);
+
+/* Host-only: tape t of a DAG batch as a self-contained postfix block (reachable nodes in DAG
+   order, references renumbered, AND chain over the roots last; CONST nodes index the DAG's
+   const pool) into nodes_out[cap]; *n_out = its length (nothing copied when cap is too small).
+   For parity dumps / the oracle.  Returns 0, MQ_ERR_ARG or MQ_ERR_TAPE. */
+int mq_dag_expand(const mq_dag_batch* dag, int32_t t, mq_node* nodes_out, int64_t cap, int64_t* n_out);
 
 /* Batch-level hoisting: sub-terms shared by several tapes of the batch depend only on the model,
    so the lowering can replace them by derived model variables.  Column program k (a tape whose

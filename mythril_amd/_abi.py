@@ -61,6 +61,18 @@ class MqStats(C.Structure):
     ]
 
 
+class MqDagBatch(C.Structure):
+    _fields_ = [
+        ("n_nodes", C.c_int64),
+        ("nodes", C.c_void_p),
+        ("const_words", C.POINTER(C.c_uint32)),
+        ("n_const_words", C.c_int64),
+        ("n_tapes", C.c_int32),
+        ("root_offsets", C.POINTER(C.c_int64)),
+        ("roots", C.POINTER(C.c_uint32)),
+    ]
+
+
 def _ptr(arr: np.ndarray, ctype):
     return arr.ctypes.data_as(C.POINTER(ctype))
 
@@ -91,3 +103,15 @@ def as_model_batch(mb: ModelBatch):
         len(mb.funcs), funcs.ctypes.data, _ptr(eptr, C.c_int64), _ptr(ebase, C.c_int64),
         _ptr(ew, C.c_uint32), ew.size, _ptr(elb, C.c_int64), _ptr(elw, C.c_uint32), elw.size)
     return s, (vw, words, funcs, eptr, ebase, ew, elb, elw)
+
+
+def as_dag_batch(db):
+    nodes = np.ascontiguousarray(db.nodes)
+    consts = np.ascontiguousarray(db.consts, dtype=np.uint32)
+    offs = np.ascontiguousarray(db.root_offsets, dtype=np.int64)
+    roots = np.ascontiguousarray(db.roots, dtype=np.uint32)
+    if roots.size == 0:
+        roots = np.zeros(1, np.uint32)
+    s = MqDagBatch(len(nodes), nodes.ctypes.data if len(nodes) else None, _ptr(consts, C.c_uint32), consts.size,
+                   db.n_tapes, _ptr(offs, C.c_int64), _ptr(roots, C.c_uint32))
+    return s, (nodes, consts, offs, roots)

@@ -920,6 +920,24 @@ static int tapes_upload_one(mq_ctx* c, int32_t n_tapes, const std::vector<Compil
   return MQ_OK;
 }
 
+// Upload compiled tapes to every device of the context (lead + peers).
+static int tapes_upload_all(mq_ctx* c, int32_t n_tapes, const std::vector<CompiledTape>& ct, mq_tapes** out,
+                            int32_t* n_unsup_out) {
+  mq_tapes* T = nullptr;
+  int rc = tapes_upload_one(c, n_tapes, ct, &T);
+  if (rc) return rc;
+  std::unique_ptr<mq_tapes> guard(T);
+  for (mq_ctx* p : c->peers) {
+    mq_tapes* pt = nullptr;
+    rc = tapes_upload_one(p, n_tapes, ct, &pt);
+    if (rc) return rc;
+    T->peers.push_back(pt);
+  }
+  if (n_unsup_out) *n_unsup_out = T->n_unsupported;
+  *out = guard.release();
+  return MQ_OK;
+}
+
 int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t* n_unsup_out) {
   if (!c || !tb || !out || tb->n_tapes < 0 || (tb->n_tapes > 0 && (!tb->tape_offsets || !tb->nodes))) return MQ_ERR_ARG;
   *out = nullptr;
@@ -931,18 +949,152 @@ int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t*
   std::vector<CompiledTape> ct(tb->n_tapes);
 #pragma omp parallel for schedule(dynamic, 64)
   for (int t = 0; t < tb->n_tapes; t++) ct[t] = compile_tape(tb, t, lim);
-  mq_tapes* T = nullptr;
-  int rc = tapes_upload_one(c, tb->n_tapes, ct, &T);
-  if (rc) return rc;
-  std::unique_ptr<mq_tapes> guard(T);
-  for (mq_ctx* p : c->peers) {
-    mq_tapes* pt = nullptr;
-    rc = tapes_upload_one(p, tb->n_tapes, ct, &pt);
-    if (rc) return rc;
-    T->peers.push_back(pt);
+  return tapes_upload_all(c, tb->n_tapes, ct, out, n_unsup_out);
+}
+
+// ---------------------------------------------------------------- DAG batches (the query stream)
+// Node fields that reference other nodes (include/mq.h operand conventions).
+static int node_refs(const mq_node& n, uint32_t r[3]) {
+  switch (n.op) {
+    case MQ_OP_CONST: case MQ_OP_VAR: case MQ_OP_TRUE: case MQ_OP_FALSE: case MQ_OP_ARRAY_VAR:
+      return 0;
+    case MQ_OP_NOT: case MQ_OP_NEG: case MQ_OP_BNOT: case MQ_OP_EXTRACT: case MQ_OP_ZEXT: case MQ_OP_SEXT:
+    case MQ_OP_CONST_ARRAY: case MQ_OP_KECCAK:
+      r[0] = n.a;
+      return 1;
+    case MQ_OP_BITE: case MQ_OP_ITE: case MQ_OP_STORE:
+      r[0] = n.a; r[1] = n.b; r[2] = n.c;
+      return 3;
+    case MQ_OP_UF:
+      r[0] = n.b;
+      if (n.c == MQ_NONE) return 1;
+      r[1] = n.c;
+      return 2;
+    default:
+      r[0] = n.a; r[1] = n.b;
+      return 2;
   }
-  if (n_unsup_out) *n_unsup_out = T->n_unsupported;
-  *out = guard.release();
+}
+
+// Tape t of a DAG batch as a self-contained postfix block: the nodes reachable from its conjunct
+// roots in ascending DAG order (the DAG is postfix, so that order is topological), references
+// renumbered, then an AND chain over the roots.  CONST nodes keep indexing the shared pool.
+// mark: per-thread scratch of dag->n_nodes entries, stamp unique per call.
+static bool expand_dag_tape(const mq_dag_batch* dag, int32_t t, std::vector<int32_t>& mark, int32_t stamp,
+                            std::vector<mq_node>& out) {
+  out.clear();
+  const int64_t r0 = dag->root_offsets[t], r1 = dag->root_offsets[t + 1];
+  std::vector<uint32_t> reach, st;
+  for (int64_t i = r0; i < r1; i++) {
+    const uint32_t r = dag->roots[i];
+    if ((int64_t)r >= dag->n_nodes) return false;
+    if (mark[r] != stamp) {
+      mark[r] = stamp;
+      st.push_back(r);
+    }
+  }
+  while (!st.empty()) {
+    const uint32_t x = st.back();
+    st.pop_back();
+    reach.push_back(x);
+    uint32_t kids[3];
+    const int nk = node_refs(dag->nodes[x], kids);
+    for (int k = 0; k < nk; k++) {
+      const uint32_t c = kids[k];
+      if (c >= x) return false;   // not postfix
+      if (mark[c] != stamp) {
+        mark[c] = stamp;
+        st.push_back(c);
+      }
+    }
+  }
+  std::sort(reach.begin(), reach.end());
+  // renumber: mark[x] = -(local index) - 2 for reached nodes (distinct from any stamp >= 1)
+  for (size_t i = 0; i < reach.size(); i++) mark[reach[i]] = -(int32_t)i - 2;
+  out.reserve(reach.size() + (size_t)std::max<int64_t>(r1 - r0, 1));
+  for (uint32_t x : reach) {
+    mq_node n = dag->nodes[x];
+    uint32_t* f[3] = {&n.a, &n.b, &n.c};
+    switch (n.op) {   // rewrite exactly the reference fields
+      case MQ_OP_CONST: case MQ_OP_VAR: case MQ_OP_TRUE: case MQ_OP_FALSE: case MQ_OP_ARRAY_VAR:
+        break;
+      case MQ_OP_NOT: case MQ_OP_NEG: case MQ_OP_BNOT: case MQ_OP_EXTRACT: case MQ_OP_ZEXT: case MQ_OP_SEXT:
+      case MQ_OP_CONST_ARRAY: case MQ_OP_KECCAK:
+        n.a = (uint32_t)(-mark[n.a] - 2);
+        break;
+      case MQ_OP_BITE: case MQ_OP_ITE: case MQ_OP_STORE:
+        for (int k = 0; k < 3; k++) *f[k] = (uint32_t)(-mark[*f[k]] - 2);
+        break;
+      case MQ_OP_UF:
+        n.b = (uint32_t)(-mark[n.b] - 2);
+        if (n.c != MQ_NONE) n.c = (uint32_t)(-mark[n.c] - 2);
+        break;
+      default:
+        n.a = (uint32_t)(-mark[n.a] - 2);
+        n.b = (uint32_t)(-mark[n.b] - 2);
+    }
+    out.push_back(n);
+  }
+  if (r1 == r0) {   // And() of nothing: true
+    out.push_back(mq_node{MQ_OP_TRUE, 0, 0, 0, 0});
+  } else {
+    uint32_t acc = (uint32_t)(-mark[dag->roots[r0]] - 2);
+    for (int64_t i = r0 + 1; i < r1; i++) {
+      out.push_back(mq_node{MQ_OP_AND, 0, acc, (uint32_t)(-mark[dag->roots[i]] - 2), 0});
+      acc = (uint32_t)out.size() - 1;
+    }
+    // the root must be the last node: a single-conjunct tape whose root is not last gets an
+    // AND with itself (idempotent)
+    if (r1 - r0 == 1 && acc != (uint32_t)out.size() - 1) out.push_back(mq_node{MQ_OP_AND, 0, acc, acc, 0});
+  }
+  for (uint32_t x : reach) mark[x] = stamp;   // back to "seen in this call"
+  return true;
+}
+
+static bool dag_ok(const mq_dag_batch* d) {
+  return d && d->n_tapes >= 0 && d->n_nodes >= 0 && (d->n_tapes == 0 || (d->root_offsets && d->roots)) &&
+         (d->n_nodes == 0 || d->nodes) && d->n_nodes < 0x7FFFFFFF;
+}
+
+// Compile every tape of a DAG batch (parallel over tapes).
+static std::vector<CompiledTape> compile_dag(const mq_dag_batch* dag, const CompileLimits& lim) {
+  std::vector<CompiledTape> ct(dag->n_tapes);
+#pragma omp parallel
+  {
+    std::vector<int32_t> mark((size_t)std::max<int64_t>(dag->n_nodes, 1), 0);
+    std::vector<mq_node> block;
+    int32_t stamp = 0;
+#pragma omp for schedule(dynamic, 16)
+    for (int t = 0; t < dag->n_tapes; t++) {
+      if (!expand_dag_tape(dag, t, mark, ++stamp, block)) {
+        ct[t].why = "malformed DAG (operand does not precede its user)";
+        continue;
+      }
+      const int64_t offs[2] = {0, (int64_t)block.size()};
+      mq_tape_batch one{1, offs, block.data(), dag->const_words, dag->n_const_words};
+      ct[t] = compile_tape(&one, 0, lim);
+    }
+  }
+  return ct;
+}
+
+int mq_tapes_upload_dag(mq_ctx* c, const mq_dag_batch* dag, mq_tapes** out, int32_t* n_unsup_out) {
+  if (!c || !out || !dag_ok(dag)) return MQ_ERR_ARG;
+  *out = nullptr;
+  for (int t = 0; t < dag->n_tapes; t++)
+    if (dag->root_offsets[t + 1] < dag->root_offsets[t]) return MQ_ERR_ARG;
+  CompileLimits lim;
+  const std::vector<CompiledTape> ct = compile_dag(dag, lim);
+  return tapes_upload_all(c, dag->n_tapes, ct, out, n_unsup_out);
+}
+
+int mq_dag_expand(const mq_dag_batch* dag, int32_t t, mq_node* nodes_out, int64_t cap, int64_t* n_out) {
+  if (!dag_ok(dag) || t < 0 || t >= dag->n_tapes || !n_out) return MQ_ERR_ARG;
+  std::vector<int32_t> mark((size_t)std::max<int64_t>(dag->n_nodes, 1), 0);
+  std::vector<mq_node> block;
+  if (!expand_dag_tape(dag, t, mark, 1, block)) return MQ_ERR_TAPE;
+  *n_out = (int64_t)block.size();
+  if (nodes_out && cap >= (int64_t)block.size()) std::memcpy(nodes_out, block.data(), block.size() * sizeof(mq_node));
   return MQ_OK;
 }
 

@@ -15,7 +15,7 @@ from typing import List, Optional, Sequence
 
 import numpy as np
 
-from ._abi import MqModelBatch, MqStats, MqTapeBatch, as_model_batch, as_tape_batch
+from ._abi import MqDagBatch, MqModelBatch, MqNode, MqStats, MqTapeBatch, as_dag_batch, as_model_batch, as_tape_batch
 from .models import ModelBatch
 from .tape import TapeBatch
 
@@ -69,6 +69,8 @@ def load_library(path: str = LIB_PATH):
         L.mq_tape_alg_ops.restype = C.c_double
         L.mq_tape_compile_info.argtypes = [C.POINTER(MqTapeBatch), C.c_int32] + [C.POINTER(C.c_int32)] * 5 + [C.c_char_p, C.c_int32]
         L.mq_tape_program.argtypes = [C.POINTER(MqTapeBatch), C.c_int32, C.POINTER(C.c_uint32), C.c_int32, C.POINTER(C.c_int32)]
+        L.mq_tapes_upload_dag.argtypes = [P, C.POINTER(MqDagBatch), C.POINTER(P), C.POINTER(C.c_int32)]
+        L.mq_dag_expand.argtypes = [C.POINTER(MqDagBatch), C.c_int32, P, C.c_int64, C.POINTER(C.c_int64)]
         L.mq_models_shard.argtypes = [C.POINTER(MqModelBatch), C.c_int64, C.c_int64, C.POINTER(MqModelBatch), C.POINTER(P)]
         L.mq_models_shard_free.argtypes = [P]
         L.mq_models_shard_free.restype = None
@@ -150,6 +152,23 @@ def shard_models(mb: ModelBatch, lo: int, hi: int) -> ModelBatch:
         L.mq_models_shard_free(h)
 
 
+def dag_expand(db) -> TapeBatch:
+    """Host-only: every tape of a DagBatch as a self-contained postfix block (``mq_dag_expand``)."""
+    from .tape import NODE_DTYPE
+    L = load_library()
+    s, keep = as_dag_batch(db)
+    chunks, offs = [], [0]
+    n = C.c_int64()
+    for t in range(db.n_tapes):
+        _check(L.mq_dag_expand(C.byref(s), t, None, 0, C.byref(n)), "mq_dag_expand")
+        out = np.zeros(n.value, NODE_DTYPE)
+        _check(L.mq_dag_expand(C.byref(s), t, out.ctypes.data, n.value, C.byref(n)), "mq_dag_expand")
+        chunks.append(out)
+        offs.append(offs[-1] + n.value)
+    nodes = np.concatenate(chunks) if chunks else np.zeros(0, NODE_DTYPE)
+    return TapeBatch.from_arrays(nodes, np.asarray(offs, np.int64), db.consts)
+
+
 def tape_alg_ops(tb: TapeBatch, t: int) -> float:
     s, keep = as_tape_batch(tb)
     return float(load_library().mq_tape_alg_ops(C.byref(s), t))
@@ -161,11 +180,14 @@ class CompiledTapes:
     def __init__(self, ev: "Evaluator", tb: TapeBatch):
         self.ev = ev
         self.n_tapes = tb.n_tapes
-        self.node_counts = tb.sizes()
-        s, keep = as_tape_batch(tb)
         h = C.c_void_p()
         nu = C.c_int32()
-        _check(ev.lib.mq_tapes_upload(ev.ctx, C.byref(s), C.byref(h), C.byref(nu)), "mq_tapes_upload")
+        if hasattr(tb, "root_offsets"):   # a DagBatch (the drop-in query stream)
+            s, keep = as_dag_batch(tb)
+            _check(ev.lib.mq_tapes_upload_dag(ev.ctx, C.byref(s), C.byref(h), C.byref(nu)), "mq_tapes_upload_dag")
+        else:
+            s, keep = as_tape_batch(tb)
+            _check(ev.lib.mq_tapes_upload(ev.ctx, C.byref(s), C.byref(h), C.byref(nu)), "mq_tapes_upload")
         self.handle = h
         self.n_unsupported = nu.value
         cols = getattr(tb, "columns", None)

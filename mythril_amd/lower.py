@@ -24,7 +24,8 @@ from . import smt as S
 from .exceptions import LoweringError
 from .models import FuncSpec, ModelBatch
 from .smt_model import Model
-from .tape import BOOL, NONE, ColumnSet, Tape, TapeBatch, limbs, to_words
+from .smt_model import as_record
+from .tape import BOOL, NODE_DTYPE, NONE, ColumnSet, Op, Tape, TapeBatch, limbs, to_words
 
 MAX_WIDTH = 0xFFFF
 
@@ -100,7 +101,17 @@ def lower_term(root: S.Term, syms: SymbolTable, hoisted: Optional[Dict[int, int]
     hoisted = hoisted or {}
     tp = Tape()
     node: Dict[int, int] = {}
+    for t in _walk_cut(root, hoisted):
+        if id(t) in hoisted and t is not root:
+            node[id(t)] = tp.var(hoisted[id(t)], _w(t))
+            continue
+        node[id(t)] = _lower_one(t, [node[id(x)] for x in t.args], tp, syms, node)
+    return tp.finish(node[id(root)], value_root=value_root)
 
+
+def _lower_one(t: S.Term, a: List[int], tp: Tape, syms: SymbolTable, node: Dict[int, int]) -> int:
+    """The tape node of term ``t`` whose arguments are already the tape nodes ``a`` (a symbolic
+    array is -1 until its first table use materialises it, cached in ``node``)."""
     def arr_node(arr: S.Term, r: int) -> int:
         if r >= 0:
             return r
@@ -108,97 +119,87 @@ def lower_term(root: S.Term, syms: SymbolTable, hoisted: Optional[Dict[int, int]
         node[id(arr)] = r
         return r
 
-    for t in _walk_cut(root, hoisted):
-        k = t.kind
-        if id(t) in hoisted and t is not root:
-            node[id(t)] = tp.var(hoisted[id(t)], _w(t))
-            continue
-        a = [node[id(x)] for x in t.args]
-        if k == S.SYM:
-            r = tp.var(syms.var(t.params[0], _w(t)), _w(t))
-        elif k == S.VAL:
-            r = tp.const(t.params[0], _w(t))
-        elif k == S.TRUE:
-            r = tp.true()
-        elif k == S.FALSE:
-            r = tp.false()
-        elif k == S.NOT:
-            r = tp.not_(a[0])
-        elif k == S.AND:
-            r = tp.and_(*a)
-        elif k == S.OR:
-            r = tp.or_(*a)
-        elif k == S.XOR:
-            r = tp.xor(a[0], a[1])
-        elif k == S.IMPLIES:
-            r = tp.implies(a[0], a[1])
-        elif k == S.IFF:
-            r = tp.iff(a[0], a[1])
-        elif k == S.BITE:
-            r = tp.bite(a[0], a[1], a[2])
-        elif k == S.EQ:
-            if t.args[0].sort == "array":
-                raise LoweringError("array equality")
-            r = tp.eq(a[0], a[1])
-        elif k == S.BVULT:
-            r = tp.ult(a[0], a[1])
-        elif k == S.BVULE:
-            r = tp.ule(a[0], a[1])
-        elif k == S.BVSLT:
-            r = tp.slt(a[0], a[1])
-        elif k == S.BVSLE:
-            r = tp.sle(a[0], a[1])
-        elif k == S.UMUL_NOOVFL:
-            r = tp.umul_noovfl(a[0], a[1])
-        elif k == S.SMUL_NOOVFL:
-            r = tp.smul_noovfl(a[0], a[1])
-        elif k == S.SMUL_NOUDFL:
-            r = tp.smul_noudfl(a[0], a[1])
-        elif k in _BIN:
-            r = getattr(tp, _BIN[k])(a[0], a[1])
-        elif k == S.NEG:
-            r = tp.neg(a[0])
-        elif k == S.BNOT:
-            r = tp.bnot(a[0])
-        elif k == S.EXTRACT:
-            r = tp.extract(t.params[0], t.params[1], a[0])
-        elif k == S.CONCAT:
-            _w(t)
-            r = tp.concat(a[0], a[1])
-        elif k == S.ZEXT:
-            r = tp.zext(t.params[0], a[0])
-        elif k == S.SEXT:
-            r = tp.sext(t.params[0], a[0])
-        elif k == S.ITE:
-            r = tp.ite(a[0], a[1], a[2])
-        elif k == S.ARRAY_SYM:
-            r = -1  # materialised at its first table use (a symbol only read at constant indices
-            #         never enters the model's function tables)
-        elif k == S.CONST_ARRAY:
-            r = tp.const_array(a[0])
-        elif k == S.STORE:
-            r = tp.store(arr_node(t.args[0], a[0]), a[1], a[2])
-        elif k == S.SELECT:
-            arr, idx = t.args
-            if syms.derive and arr.kind == S.ARRAY_SYM and idx.kind == S.VAL:
-                r = tp.var(syms.derived_var(arr.params[0], (idx.params[0],), _w(t)), _w(t))
-            else:
-                r = tp.select(arr_node(arr, a[0]), a[1])
-        elif k == S.KECCAK:
-            r = tp.keccak(a[0])
-        elif k == S.APP and syms.interpret_keccak and _is_keccak_uf(t.params[0]):
-            r = tp.keccak(a[0])
-        elif k == S.APP:
-            name, dom = t.params
-            fid = syms.func(name, dom, t.width)
-            if syms.derive and all(x.kind == S.VAL for x in t.args):
-                r = tp.var(syms.derived_var(name, tuple(x.params[0] for x in t.args), _w(t)), _w(t))
-            else:
-                r = tp.uf(fid, t.width, *a)
-        else:
-            raise LoweringError(f"term kind {k!r} not in the tape vocabulary")
-        node[id(t)] = r
-    return tp.finish(node[id(root)], value_root=value_root)
+    k = t.kind
+    if k == S.SYM:
+        return tp.var(syms.var(t.params[0], _w(t)), _w(t))
+    if k == S.VAL:
+        return tp.const(t.params[0], _w(t))
+    if k == S.TRUE:
+        return tp.true()
+    if k == S.FALSE:
+        return tp.false()
+    if k == S.NOT:
+        return tp.not_(a[0])
+    if k == S.AND:
+        return tp.and_(*a)
+    if k == S.OR:
+        return tp.or_(*a)
+    if k == S.XOR:
+        return tp.xor(a[0], a[1])
+    if k == S.IMPLIES:
+        return tp.implies(a[0], a[1])
+    if k == S.IFF:
+        return tp.iff(a[0], a[1])
+    if k == S.BITE:
+        return tp.bite(a[0], a[1], a[2])
+    if k == S.EQ:
+        if t.args[0].sort == "array":
+            raise LoweringError("array equality")
+        return tp.eq(a[0], a[1])
+    if k == S.BVULT:
+        return tp.ult(a[0], a[1])
+    if k == S.BVULE:
+        return tp.ule(a[0], a[1])
+    if k == S.BVSLT:
+        return tp.slt(a[0], a[1])
+    if k == S.BVSLE:
+        return tp.sle(a[0], a[1])
+    if k == S.UMUL_NOOVFL:
+        return tp.umul_noovfl(a[0], a[1])
+    if k == S.SMUL_NOOVFL:
+        return tp.smul_noovfl(a[0], a[1])
+    if k == S.SMUL_NOUDFL:
+        return tp.smul_noudfl(a[0], a[1])
+    if k in _BIN:
+        return getattr(tp, _BIN[k])(a[0], a[1])
+    if k == S.NEG:
+        return tp.neg(a[0])
+    if k == S.BNOT:
+        return tp.bnot(a[0])
+    if k == S.EXTRACT:
+        return tp.extract(t.params[0], t.params[1], a[0])
+    if k == S.CONCAT:
+        _w(t)
+        return tp.concat(a[0], a[1])
+    if k == S.ZEXT:
+        return tp.zext(t.params[0], a[0])
+    if k == S.SEXT:
+        return tp.sext(t.params[0], a[0])
+    if k == S.ITE:
+        return tp.ite(a[0], a[1], a[2])
+    if k == S.ARRAY_SYM:
+        return -1  # materialised at its first table use (a symbol only read at constant indices
+        #            never enters the model's function tables)
+    if k == S.CONST_ARRAY:
+        return tp.const_array(a[0])
+    if k == S.STORE:
+        return tp.store(arr_node(t.args[0], a[0]), a[1], a[2])
+    if k == S.SELECT:
+        arr, idx = t.args
+        if syms.derive and arr.kind == S.ARRAY_SYM and idx.kind == S.VAL:
+            return tp.var(syms.derived_var(arr.params[0], (idx.params[0],), _w(t)), _w(t))
+        return tp.select(arr_node(arr, a[0]), a[1])
+    if k == S.KECCAK:
+        return tp.keccak(a[0])
+    if k == S.APP and syms.interpret_keccak and _is_keccak_uf(t.params[0]):
+        return tp.keccak(a[0])
+    if k == S.APP:
+        name, dom = t.params
+        fid = syms.func(name, dom, t.width)
+        if syms.derive and all(x.kind == S.VAL for x in t.args):
+            return tp.var(syms.derived_var(name, tuple(x.params[0] for x in t.args), _w(t)), _w(t))
+        return tp.uf(fid, t.width, *a)
+    raise LoweringError(f"term kind {k!r} not in the tape vocabulary")
 
 
 def _walk_cut(root: S.Term, cut: Dict[int, int]) -> List[S.Term]:
@@ -364,3 +365,220 @@ def serialize_models(models: Sequence[Model], syms: SymbolTable, index_base: int
     fb = ModelBatch.from_python(widths or [], fmodels, syms.func_specs, index_base)
     return ModelBatch(widths, words, syms.func_specs, fb.entry_ptr, fb.entry_words, fb.entry_base,
                       fb.else_words, fb.else_base, index_base)
+
+
+# ---------------------------------------------------------------------------- the drop-in path
+class DagBatch:
+    """A query batch over the persistent DAG (``mq_dag_batch``, include/mq.h): the DAG's nodes and
+    const pool (shared by all tapes) and, per tape, the node ids of its conjunct roots."""
+
+    def __init__(self, nodes: np.ndarray, consts: np.ndarray, root_offsets: np.ndarray, roots: np.ndarray):
+        self.nodes = nodes
+        self.consts = consts if consts.size else np.zeros(1, np.uint32)
+        self.root_offsets = np.ascontiguousarray(root_offsets, np.int64)
+        self.roots = np.ascontiguousarray(roots, np.uint32)
+        self.n_tapes = len(self.root_offsets) - 1
+        self.columns = None
+
+    def to_tapes(self) -> TapeBatch:
+        """The equivalent self-contained TapeBatch (``mq_dag_expand``; oracle / parity dumps)."""
+        from .evaluator import dag_expand
+        return dag_expand(self)
+
+
+class IncrementalLowering:
+    """Lowering + model serialization for a STREAM of quick-sat queries (the drop-in path).
+
+    ``get_model`` hands ``check_quick_sat`` the conjunction ``And(*constraints)`` of a path
+    (model.py:92-101).  Paths forked from a common parent share their constraints, and the keccak
+    axioms of the run ride on every query (constraints.py:127-128).  So every term is lowered ONCE
+    into a persistent hash-consed DAG — the counterpart of z3's AST table — and a query is just
+    the list of its conjuncts' DAG nodes (``mq_dag_batch``); the evaluator extracts each tape's
+    reachable sub-DAG itself.  Likewise each candidate model's variable values and function
+    tables are serialized once (per variable / function) and gathered per batch.
+
+    Terms are held alive while they are in the DAG (the id memo must stay valid); past
+    ``MAX_NODES`` the DAG starts over (the symbol table, hence the model rows, persist)."""
+
+    MAX_NODES = 1 << 22
+
+    def __init__(self) -> None:
+        self.syms = SymbolTable()
+        self._reset_dag()
+        self._models: Dict[int, Tuple[object, List[np.ndarray], Dict[int, Tuple[np.ndarray, np.ndarray]]]] = {}
+
+    def _reset_dag(self) -> None:
+        self.tape = Tape()
+        self._node: Dict[int, int] = {}       # id(term) -> DAG node
+        self._keep: Dict[int, S.Term] = {}    # keeps those terms (and their ids) alive
+        self._bad: Dict[int, S.Term] = {}     # terms that failed to lower
+        self._np_nodes = np.zeros(1024, NODE_DTYPE)
+        self._np_n = 0
+        self._np_consts = np.zeros(1024, np.uint32)
+        self._np_c = 0
+
+    # ------------------------------------------------------------ DAG
+    def _lower(self, root: S.Term) -> int:
+        """DAG node of a Bool conjunct (lowering only the terms not seen before)."""
+        hit = self._node.get(id(root))
+        if hit is not None:
+            return hit
+        if id(root) in self._bad:
+            raise LoweringError("conjunct not in the tape vocabulary")
+        node, tp, syms = self._node, self.tape, self.syms
+        order: List[S.Term] = []
+        seen = set()
+        stack = [(root, False)]
+        while stack:
+            t, done = stack.pop()
+            if done:
+                order.append(t)
+                continue
+            if id(t) in seen or id(t) in node:
+                continue
+            seen.add(id(t))
+            stack.append((t, True))
+            for a in reversed(t.args):
+                if id(a) not in seen and id(a) not in node:
+                    stack.append((a, False))
+        try:
+            for t in order:
+                node[id(t)] = _lower_one(t, [node.get(id(x), -1) for x in t.args], tp, syms, node)
+                self._keep[id(t)] = t
+        except (LoweringError, TypeError) as e:
+            self._bad[id(root)] = root
+            raise LoweringError(str(e))
+        return node[id(root)]
+
+    def _sync(self) -> Tuple[np.ndarray, np.ndarray]:
+        """The DAG's nodes / consts as numpy (append-only mirror of the Python node table)."""
+        n, nc = len(self.tape.nodes), len(self.tape.consts)
+        if n > self._np_nodes.size:
+            grow = np.zeros(max(n, 2 * self._np_nodes.size), NODE_DTYPE)
+            grow[:self._np_n] = self._np_nodes[:self._np_n]
+            self._np_nodes = grow
+        if n > self._np_n:
+            tail = np.array(self.tape.nodes[self._np_n:n], dtype=np.uint64).reshape(-1, 5)
+            blk = self._np_nodes[self._np_n:n]
+            for j, fld in enumerate(("op", "width", "a", "b", "c")):
+                blk[fld] = tail[:, j]
+            self._np_n = n
+        if nc > self._np_consts.size:
+            grow = np.zeros(max(nc, 2 * self._np_consts.size), np.uint32)
+            grow[:self._np_c] = self._np_consts[:self._np_c]
+            self._np_consts = grow
+        if nc > self._np_c:
+            self._np_consts[self._np_c:nc] = np.asarray(self.tape.consts[self._np_c:nc], np.uint32)
+            self._np_c = nc
+        return self._np_nodes[:n], self._np_consts[:max(nc, 1)]
+
+    def lower(self, roots: Sequence[S.Term]):
+        """``(DagBatch, supported mask)``.  A query whose conjuncts do not all lower is flagged
+        unsupported (its tape is a FALSE placeholder: the caller routes it to z3)."""
+        if len(self.tape.nodes) > self.MAX_NODES:
+            self._reset_dag()
+        offs, flat = [0], []
+        ok = np.ones(len(roots), bool)
+        false_node = None
+        for i, r in enumerate(roots):
+            if r.sort != "bool":
+                raise LoweringError("quick-sat root must be Bool")
+            conj = r.args if r.kind == S.AND else (r,)
+            try:
+                ids = [self._lower(c) for c in conj]
+            except LoweringError:
+                ok[i] = False
+                if false_node is None:
+                    false_node = self.tape.false()
+                ids = [false_node]
+            flat.extend(ids)
+            offs.append(len(flat))
+        nodes, consts = self._sync()
+        return DagBatch(nodes, consts, np.asarray(offs, np.int64), np.asarray(flat, np.uint32)), ok
+
+    # ------------------------------------------------------------ models
+    def _var_words(self, rec: Model, v: int) -> np.ndarray:
+        name, w = self._var_names[v]
+        if v in self.syms.derived:
+            fname, fargs = self.syms.derived[v]
+            interp = rec.functions.get(fname)
+            val = 0 if interp is None else interp[0].get(fargs, interp[1])
+        else:
+            val = rec.assignment.get(name)
+        val = 0 if val is None else int(val) & ((1 << max(w, 1)) - 1)
+        return np.asarray(to_words(val, w), np.uint32)
+
+    def _func_table(self, rec: Model, f: int) -> Tuple[np.ndarray, np.ndarray]:
+        spec, name = self.syms.func_specs[f], self.syms.func_names[f]
+        interp = rec.functions.get(name)
+        nres = limbs(spec.result_width)
+        if interp is None:
+            return np.zeros((0, spec.stride), np.uint32), np.zeros(nres, np.uint32)
+        table, els = interp
+        rows = []
+        for args, val in table.items():
+            if not isinstance(args, tuple):
+                args = (args,)
+            w = []
+            for aw, av in zip(spec.arg_widths, args):
+                w.extend(to_words(int(av), aw))
+            w.extend(to_words(int(val), spec.result_width))
+            rows.append(w)
+        ent = np.asarray(rows, np.uint32).reshape(-1, spec.stride)
+        return ent, np.asarray(to_words(int(els), spec.result_width), np.uint32)
+
+    def serialize(self, models: Sequence, index_base: int = 0) -> ModelBatch:
+        """All variables / functions of the symbol table for ``models`` in global candidate
+        order, WITHOUT completion (absent: 0 / no entries, else 0).  A model's rows are computed
+        once per variable and function and reused by every later batch."""
+        syms = self.syms
+        nv = len(syms.var_widths)
+        if getattr(self, "_names_n", -1) != nv:
+            self._var_names = {i: k for k, i in syms.vars.items()}
+            self._names_n = nv
+        M = len(models)
+        cols, fcache = [], []
+        for mod in models:
+            ent = self._models.get(id(mod))
+            if ent is None or ent[0] is not mod:
+                ent = (mod, [], {})
+                self._models[id(mod)] = ent
+            vl = ent[1]
+            if len(vl) < nv:
+                rec = as_record(mod)
+                vl.extend(self._var_words(rec, v) for v in range(len(vl), nv))
+            cols.append(np.concatenate(vl) if nv else np.zeros(0, np.uint32))
+            fcache.append((mod, ent[2]))
+        rows = sum(limbs(w) for w in syms.var_widths)
+        words = np.stack(cols, axis=1) if M else np.zeros((rows, 0), np.uint32)
+        if len(self._models) > 4 * M + 256:   # forget models that left the candidate set
+            live = {id(m) for m in models}
+            for k in [k for k in self._models if k not in live]:
+                del self._models[k]
+        F = len(syms.func_specs)
+        if not F:
+            return ModelBatch(syms.var_widths, words, index_base=index_base)
+        eptr = np.zeros((F, M + 1), np.int64)
+        ebase = np.zeros(F, np.int64)
+        elb = np.zeros(F, np.int64)
+        ew_chunks, el_chunks = [], []
+        wpos = epos = 0
+        for f in range(F):
+            tabs = []
+            for mod, fc in fcache:
+                t = fc.get(f)
+                if t is None:
+                    t = fc[f] = self._func_table(as_record(mod), f)
+                tabs.append(t)
+            counts = np.fromiter((len(t[0]) for t in tabs), np.int64, M)
+            eptr[f, 1:] = np.cumsum(counts)
+            ebase[f] = wpos
+            ew = np.concatenate([t[0].reshape(-1) for t in tabs]) if M else np.zeros(0, np.uint32)
+            ew_chunks.append(ew)
+            wpos += ew.size
+            elb[f] = epos
+            el = np.concatenate([t[1] for t in tabs]) if M else np.zeros(0, np.uint32)
+            el_chunks.append(el)
+            epos += el.size
+        return ModelBatch(syms.var_widths, words, list(syms.func_specs), eptr, np.concatenate(ew_chunks), ebase,
+                          np.concatenate(el_chunks), elb, index_base)

@@ -126,14 +126,25 @@ class VerdictEngine:
 
     ``rows(exprs, models)`` -> one ``bool[len(models)]`` verdict row per expression (``None`` =
     unsupported: fail closed).  Works on z3-free terms (:mod:`mythril_amd.smt`) and, on a z3 host,
-    on z3 ``BoolRef`` (lowered by :mod:`mythril_amd.lower_z3`)."""
+    on z3 ``BoolRef`` (lowered by :mod:`mythril_amd.lower_z3`).
 
+    ``timing`` accumulates host seconds per stage of every call (lower, serialize, upload,
+    compile, evaluate = launch + readback) — the drop-in leg of bench.py reports it."""
+
+    # batch-level hoisting pays off when the device work dominates: many conjunctions x many
+    # candidates (generated candidates); at the LRU's <= 100 models the host stages dominate and
+    # the incremental lowering (cached conjunct fragments and model rows) is used instead
     hoist_min_batch = 8
+    hoist_min_models = 1024
+    STAGES = ("lower", "serialize", "upload", "compile", "evaluate")
 
     def __init__(self, evaluator=None):
+        from .lower import IncrementalLowering
         self._ev = evaluator
         self.launches = 0
         self.pairs = 0
+        self.timing = dict.fromkeys(self.STAGES, 0.0)
+        self.incremental = IncrementalLowering()
 
     @property
     def evaluator(self):
@@ -142,34 +153,63 @@ class VerdictEngine:
             self._ev = default_evaluator()
         return self._ev
 
+    def _lower(self, exprs, models, hoist: bool):
+        clock = time.perf_counter
+        t0 = clock()
+        if all(isinstance(e, S.Term) for e in exprs) and not hoist:
+            inc = self.incremental
+            tb, ok = inc.lower(exprs)
+            t1 = clock()
+            mb = inc.serialize(models)
+        elif all(isinstance(e, S.Term) for e in exprs):
+            from .lower import lower_batch, serialize_models
+            # states forked from a common parent share constraint prefixes: hoist what a batch
+            # shares into once-per-model columns (lower.py lower_batch)
+            records = [as_record(m) for m in models]
+            tb, syms, ok = lower_batch(exprs, hoist=hoist)
+            t1 = clock()
+            mb = serialize_models(records, syms)
+        else:
+            from .lower_z3 import lower_batch_z3
+            tb, mb, ok = lower_batch_z3(exprs, models)
+            t1 = clock()
+        self.timing["lower"] += t1 - t0
+        self.timing["serialize"] += clock() - t1
+        return tb, mb, ok
+
+    def _evaluate(self, tb, mb):
+        clock = time.perf_counter
+        ev = self.evaluator
+        t0 = clock()
+        ev.upload_models(mb)
+        t1 = clock()
+        ct = ev.compile(tb)
+        t2 = clock()
+        try:
+            v, fh = ev.verdicts(ct)
+        finally:
+            ct.free()
+        self.timing["upload"] += t1 - t0
+        self.timing["compile"] += t2 - t1
+        self.timing["evaluate"] += clock() - t2
+        return v, fh
+
     def rows(self, exprs: Sequence, models: Sequence) -> List[Optional[np.ndarray]]:
         if not exprs:
             return []
         if not models:
             return [np.zeros(0, bool) for _ in exprs]
-        if all(isinstance(e, S.Term) for e in exprs):
-            from .lower import lower_batch, serialize_models
-            # states forked from a common parent share constraint prefixes: hoist what a batch
-            # shares into once-per-model columns (lower.py lower_batch)
-            records = [as_record(m) for m in models]
-            tb, syms, ok = lower_batch(exprs, hoist=len(exprs) >= self.hoist_min_batch)
-            mb = serialize_models(records, syms)
-        else:
-            from .lower_z3 import lower_batch_z3
-            tb, mb, ok = lower_batch_z3(exprs, models)
-        ev = self.evaluator
-        ev.upload_models(mb)
+        hoist = len(exprs) >= self.hoist_min_batch and len(models) >= self.hoist_min_models
+        tb, mb, ok = self._lower(exprs, models, hoist)
         try:
-            v, fh = ev.verdicts(tb)
+            v, fh = self._evaluate(tb, mb)
         except Exception:
             if getattr(tb, "columns", None) is None:
                 raise
             # a column program the compiler rejects (mq_tapes_set_columns -> MQ_ERR_TAPE):
             # evaluate the batch without hoisting instead
-            tb, syms, ok = lower_batch(exprs)
-            mb = serialize_models(records, syms)
-            ev.upload_models(mb)
-            v, fh = ev.verdicts(tb)
+            tb, mb, ok = self._lower(exprs, models, False)
+            v, fh = self._evaluate(tb, mb)
         self.launches += 1
         self.pairs += tb.n_tapes * mb.n_models
         out: List[Optional[np.ndarray]] = []

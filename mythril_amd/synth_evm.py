@@ -641,3 +641,43 @@ def c4_wide_workload(n_tapes: int = 48, n_models: int = 2048, seed: int = 44, si
     tb, syms, ok = lower_batch(roots, SymbolTable(), hoist=hoist)
     assert ok.all()
     return tb, serialize_models(records, syms), expected, records
+
+
+# ====================================================================== the drop-in shape
+def evm_model_record(wit: Dict, n_tx: int):
+    """A candidate model as the z3 solver would return it for an EVM path (the LRU keys of
+    ModelCache, support_utils.py:58): senders, call values, calldata sizes, the calldata arrays'
+    as-array interpretations and the balance table (smt_model.Model, no completion)."""
+    from .smt_model import Model
+    asg, funcs = {}, {}
+    for k in range(n_tx):
+        asg[f"sender_{k + 1}"] = wit["sender"][k]
+        asg[f"call_value{k + 1}"] = wit["value"][k]
+        asg[f"{k + 1}_calldatasize"] = wit["cds"][k]
+        funcs[f"{k + 1}_calldata"] = ({(i,): b for i, b in enumerate(wit["bytes"][k])}, 0)
+    bal, els = wit["balance"]
+    funcs["balance"] = ({(a,): v for a, v in bal.items()}, els)
+    return Model(asg, funcs)
+
+
+def dropin_workload(n_queries: int, n_models: int, seed: int = 7, n_tx: int = 3, planted_frac: float = 0.3,
+                    checks_per_tx: Tuple[int, int] = (3, 6)):
+    """Quick-sat at the reference's own shape: ``n_models`` <= 100 cached
+    models (the LRU, MRU first) and ``n_queries`` EVM-shaped path conjunctions, a fraction of them
+    satisfied by one of the cached models.  Returns ``(exprs, records, planted index or -1)``."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    models = EvmModels(seed, n_models, n_tx)
+    ghost = EvmModels(seed + 1_000_003, max(1, n_queries), n_tx, 0, 0)
+    records = [evm_model_record(models.witness(m), n_tx) for m in range(n_models)]
+    exprs, planted = [], []
+    for q in range(n_queries):
+        if rng.random() < planted_frac:
+            p = int(rng.integers(n_models))
+            wit = models.witness(p)
+            if all(x in ACTORS for x in wit["sender"]):
+                exprs.append(evm_path(rng, wit, n_tx, checks_per_tx))
+                planted.append(p)
+                continue
+        exprs.append(evm_path(rng, ghost.witness(q), n_tx, checks_per_tx))
+        planted.append(-1)
+    return exprs, records, planted

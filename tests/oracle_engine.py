@@ -10,26 +10,27 @@ import numpy as np
 
 import cref
 import pyoracle
+import term_eval
 from mythril_amd.lower import lower_batch, lower_term, serialize_models, SymbolTable
+from mythril_amd.support import VerdictEngine
 from mythril_amd.tape import TapeBatch
 
 
-class OracleEngine:
-    """Same contract as ``mythril_amd.support.VerdictEngine.rows`` — evaluated by oracle/cref.c."""
+class OracleEngine(VerdictEngine):
+    """The product ``VerdictEngine`` — batching, incremental DAG lowering, model serialization —
+    with only the device evaluation swapped for oracle/cref.c, so the host-side quick-sat logic
+    runs on CPU exactly as in the product (tests only)."""
+
+    hoist_min_models = 1 << 30   # the oracle evaluates unhoisted tapes
 
     def __init__(self):
-        self.launches = 0
-        self.pairs = 0
+        super().__init__(evaluator=None)
 
-    def rows(self, exprs, models):
-        if not models:
-            return [np.zeros(0, bool) for _ in exprs]
-        tb, syms, ok = lower_batch(exprs)
-        mb = serialize_models(models, syms)
-        v = cref.verdicts(tb, mb)
-        self.launches += 1
-        self.pairs += tb.n_tapes * mb.n_models
-        return [v[i].copy() if ok[i] else None for i in range(len(exprs))]
+    def _evaluate(self, tb, mb):
+        if hasattr(tb, "root_offsets"):   # DagBatch -> self-contained tapes
+            tb = tb.to_tapes()
+        fh, _ = cref.first_hit(tb, mb)
+        return cref.verdicts(tb, mb), fh
 
 
 def eval_under(expr, model) -> bool:
@@ -41,7 +42,8 @@ def eval_under(expr, model) -> bool:
 
 
 class ReferenceLoopCache:
-    """support_utils.py:34-67 verbatim in behaviour: LRU of 100, MRU-first loop, bump on hit,
+    """Checked per model by tests/term_eval.py (direct term evaluation, independent of the
+    product lowering).  support_utils.py:34-67 verbatim in behaviour: LRU of 100, MRU-first loop, bump on hit,
     per-expression memo (functools.lru_cache(2**10) semantics for these small tests: unbounded)."""
 
     def __init__(self):
@@ -66,7 +68,7 @@ class ReferenceLoopCache:
             return self.memo[expr]
         res = False
         for model in reversed(list(self.lru.keys())):
-            if eval_under(expr, model):
+            if term_eval.is_true(expr, model):
                 self.put(model, self.get(model) + 1)
                 res = model
                 break

@@ -150,3 +150,46 @@ def test_hoisting_levels_nest():
     mb = apply_columns(tb, serialize_models(models, syms))
     tb2, syms2, _ = lower_batch(roots)
     assert (cref.verdicts(tb, mb) == cref.verdicts(tb2, serialize_models(models, syms2))).all()
+
+
+def test_product_lowering_agrees_with_direct_term_evaluation():
+    """Both product lowerings (batch lower_batch + serialize_models, and the drop-in
+    IncrementalLowering DAG + mq_dag_expand) evaluated by the tape oracle agree with a direct
+    evaluation of the terms (tests/term_eval.py), which shares no code with the lowering."""
+    import cref
+    import term_eval
+    from mythril_amd.lower import IncrementalLowering, lower_batch, serialize_models
+    from mythril_amd.synth_evm import dropin_workload
+    exprs, recs, planted = dropin_workload(40, 30, seed=3)
+    direct = np.array([[term_eval.is_true(e, m) for m in recs] for e in exprs])
+    tb, syms, ok = lower_batch(exprs)
+    assert ok.all()
+    assert (cref.verdicts(tb, serialize_models(recs, syms)) == direct).all()
+    inc = IncrementalLowering()
+    for _ in range(2):      # the second pass runs entirely from the caches
+        db, ok = inc.lower(exprs)
+        assert ok.all()
+        assert (cref.verdicts(db.to_tapes(), inc.serialize(recs)) == direct).all()
+    assert all(direct[q, p] for q, p in enumerate(planted) if p >= 0)
+
+
+def test_incremental_lowering_shares_the_dag_across_queries():
+    from mythril_amd.lower import IncrementalLowering
+    from mythril_amd.synth_evm import dropin_workload
+    exprs, recs, _ = dropin_workload(64, 10, seed=4)
+    inc = IncrementalLowering()
+    db, ok = inc.lower(exprs)
+    per_query = db.to_tapes().sizes().sum()
+    assert len(db.nodes) < per_query / 4      # calldata bytes / words / dispatch shared
+    n = len(db.nodes)
+    db2, _ = inc.lower(exprs[:10])
+    assert len(db2.nodes) == n                # nothing new to lower
+
+
+def test_c4_wide_planted_hits_hold_in_the_oracle():
+    import cref
+    import keccak_ref
+    from mythril_amd.synth_evm import c4_wide_workload
+    tb, mb, exp, recs = c4_wide_workload(8, 40, seed=46, hasher=keccak_ref.keccak256)
+    v = cref.verdicts(tb, mb)
+    assert (v[exp >= 0, exp[exp >= 0]]).all()
