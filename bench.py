@@ -94,6 +94,7 @@ def parse():
                         "the host and lets a 1-GPU box rehearse N>1 with --device 0")
     p.add_argument("--device", type=int, default=None, help="override LOCAL_RANK -> device mapping (rehearsal)")
     p.add_argument("--no-hoist", action="store_true", help="c3/c4/c5: lower without batch-level hoisting")
+    p.add_argument("--no-dropin", action="store_true", help="skip the drop-in leg (ModelCache at N<=256, M<=100)")
     return p.parse_args()
 
 
@@ -153,6 +154,65 @@ def cpu_baseline(tb, mb, target_s: float):
                       f"oracle/cref.c OpenMP over {cores} threads, {dt_all:.1f} s; single core: first {n_one} tapes, "
                       f"{dt_one:.1f} s",
             "single_core_value": v_one, "host": hc, "seconds": dt_all + dt_one}
+
+
+def dropin_leg(ev, grid=((1, 16), (1, 100), (32, 16), (32, 100), (256, 16), (256, 100)), seed: int = 7):
+    """The drop-in path at the reference's own shape: ``ModelCache.
+    check_quick_sat_batch`` end to end over N EVM-shaped path conjunctions x M <= 100 cached
+    models, through the product VerdictEngine (DAG lowering, model serialization, upload, compile,
+    launch, readback) — NOT part of the headline metric.  Each cell first warms the run-level
+    caches with one batch of queries, then times a fresh batch from the same contract shape
+    (what a LASER run looks like after its first transaction).  The CPU column is the oracle
+    (cref, one thread) evaluating the same lowered tapes x models: the evaluation stage only."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cref  # oracle: CPU comparison only
+    from mythril_amd import support as sp
+    from mythril_amd.synth_evm import dropin_workload
+    out = []
+    for n, m in grid:
+        eng = sp.VerdictEngine(ev)
+        warm, recs, _ = dropin_workload(n, m, seed=seed)
+        cache = sp.ModelCache(eng)
+        for r in reversed(recs):
+            cache.put(r, 1)
+        cache.check_quick_sat_batch(warm)
+        exprs, _, planted = dropin_workload(n, m, seed=seed + 1)
+        # same candidate set (models of seed) so planted hits of seed + 1 are not expected here;
+        # answers are checked against the oracle below
+        cache = sp.ModelCache(eng)
+        for r in reversed(recs):
+            cache.put(r, 1)
+        before = dict(eng.timing)
+        ev.time_kernels(True)
+        t0 = time.perf_counter()
+        answers = cache.check_quick_sat_batch(exprs)
+        wall = time.perf_counter() - t0
+        kt = ev.kernel_times(reset=True)
+        ev.time_kernels(False)
+        stages = {k: (eng.timing[k] - before[k]) * 1e3 for k in eng.timing}
+        # the oracle on the same lowered tapes x models (candidate index = position in recs,
+        # MRU first), then the reference loop replayed on its verdicts: first hit in the current
+        # order, bump to MRU (support_utils.py:62-66)
+        db, ok = eng.incremental.lower(exprs)
+        tb = db.to_tapes()
+        mb = eng.incremental.serialize(recs)
+        t1 = time.perf_counter()
+        fh, _ = cref.first_hit(tb, mb, nthreads=1)
+        cpu_eval = time.perf_counter() - t1
+        v = cref.verdicts(tb, mb)
+        order, ref = list(range(m)), []
+        for q in range(n):
+            hit = next((i for i in order if v[q, i]), None)
+            if hit is not None:
+                order.remove(hit)
+                order.insert(0, hit)
+            ref.append(False if hit is None else recs[hit])
+        same = all((a is False and b is False) or a is b for a, b in zip(answers, ref))
+        out.append({"n_queries": n, "n_models": m, "avg_tape_nodes": float(tb.sizes().mean()),
+                    "ms_per_batch": wall * 1e3, "ms_per_query": wall * 1e3 / n, "stage_ms": stages,
+                    "kernel_ms": float(sum(kt)), "hits": int(sum(a is not False for a in answers)),
+                    "cpu_oracle_eval_ms_1thread": cpu_eval * 1e3, "answers_match_reference_loop": bool(same)})
+    return out
 
 
 def pmc_traffic(workload_key: str):
@@ -319,6 +379,8 @@ def main():
                 cb = cpu_baseline(tb, mb, args.cpu_seconds)
             out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample", "single_core_value", "host")}
             out["gpu_over_cpu"] = out["value"] / cb["value"]
+        if world == 1 and not args.no_dropin:
+            out["dropin"] = dropin_leg(ev)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -94,6 +94,10 @@ class Args(metaclass=Singleton):
         self.pruning_factor = None
         self.solver_log = None
         self.parallel_solving = False
+        # build extension (not a reference flag): on a quick-sat miss, a verdict-only caller
+        # (Constraints.is_possible) also tries generated candidates (mythril_amd.candidates)
+        self.quick_sat_candidates = False
+        self.quick_sat_candidate_budget = 100_000
 
 
 args = Args()
@@ -194,6 +198,42 @@ class VerdictEngine:
         self.timing["evaluate"] += clock() - t2
         return v, fh
 
+    def candidate_first_hits(self, exprs: Sequence, models: Sequence, generator):
+        """First hits of ``exprs`` over the LRU ``models`` followed by generated candidates (one
+        launch): ``(int32[N] global indices / -1 / -2, CandidateSet)``.  z3-free terms only."""
+        clock = time.perf_counter
+        t0 = clock()
+        inc = self.incremental
+        db, ok = inc.lower(exprs)
+        t1 = clock()
+        cs = generator.generate(db, inc.syms, inc.serialize(models), models)
+        t2 = clock()
+        fh, t3, t4 = self._first_hit(db, cs.batch)
+        self.timing["lower"] += t1 - t0
+        self.timing["serialize"] += t2 - t1
+        self.timing["upload"] += t3 - t2
+        self.timing["compile"] += t4 - t3
+        self.timing["evaluate"] += clock() - t4
+        self.launches += 1
+        self.pairs += len(exprs) * cs.batch.n_models
+        fh = np.where(ok, fh, -2)
+        return fh, cs
+
+    def _first_hit(self, tb, mb):
+        """Upload + compile + first-hit launch; returns (first hits, time after upload, time
+        after compile)."""
+        clock = time.perf_counter
+        ev = self.evaluator
+        ev.upload_models(mb)
+        t3 = clock()
+        ct = ev.compile(tb)
+        t4 = clock()
+        try:
+            fh = ev.first_hit(ct)
+        finally:
+            ct.free()
+        return fh, t3, t4
+
     def rows(self, exprs: Sequence, models: Sequence) -> List[Optional[np.ndarray]]:
         if not exprs:
             return []
@@ -237,6 +277,7 @@ class ModelCache:
         # entry is evicted past MEMO_SIZE, exceptions are not cached), kept as a dict so prefetch
         # can tell which conjunctions will never reach the evaluator again
         self._memo: "OrderedDict[object, object]" = OrderedDict()
+        self._cand: Dict[object, object] = {}   # prefetched generated-candidate answers
         self.stats = {"queries": 0, "hits": 0, "unsupported": 0}
 
     def check_quick_sat(self, constraints):
@@ -290,6 +331,45 @@ class ModelCache:
             self._pending[e] = None
         if exprs and order:
             self._fill(exprs, order)
+
+    # -------------------------------------------------------------- generated candidates
+    def candidates(self, exprs: Sequence) -> list:
+        """Verdict-only extension (``Args.quick_sat_candidates``): for conjunctions quick-sat did
+        not answer, search the LRU models followed by up to ``quick_sat_candidate_budget``
+        generated candidates in ONE launch.  Returns per expression a satisfying model (an LRU
+        model, or a generated candidate materialized as a Model: never inserted into the cache)
+        or False.  Only for callers that use the verdict, never the model's contents."""
+        from .candidates import CandidateGenerator
+        exprs = list(exprs)
+        out = [False] * len(exprs)
+        todo = [i for i, e in enumerate(exprs) if isinstance(e, S.Term)]
+        if not todo:
+            return out
+        order = list(reversed(self.model_cache.lru_cache.keys()))
+        gen = CandidateGenerator(args.quick_sat_candidate_budget, seed=len(self.stats) + self.stats["queries"])
+        fh, cs = self.engine.candidate_first_hits([exprs[i] for i in todo], order, gen)
+        for i, h in zip(todo, fh):
+            if h < 0:
+                continue
+            out[i] = order[h] if h < cs.n_lru else cs.materialize(int(h))
+            self.stats["candidate_hits"] = self.stats.get("candidate_hits", 0) + 1
+        return out
+
+    def prefetch_candidates(self, exprs: Iterable) -> None:
+        """Batch form: the candidates search of every conjunction the prefetched LRU rows already
+        show as a miss, in one launch; consumed by :meth:`candidate_for`."""
+        miss = []
+        for e in dict.fromkeys(exprs):
+            d = self._rows.get(e)
+            if isinstance(d, dict) and d and not any(d.values()) and e not in self._cand:
+                miss.append(e)
+        for e, r in zip(miss, self.candidates(miss)):
+            self._cand[e] = r
+
+    def candidate_for(self, expr):
+        if expr in self._cand:
+            return self._cand.pop(expr)
+        return self.candidates([expr])[0]
 
     def discard(self, exprs: Iterable) -> None:
         """Forget prefetched rows of conjunctions whose check_quick_sat never ran (their answer
@@ -375,7 +455,7 @@ def _default_backend() -> SolverBackend:
 
 model_cache = ModelCache()
 solver_backend: SolverBackend = None  # type: ignore[assignment]
-counters = {"get_model_calls": 0, "quick_sat_answers": 0, "solver_calls": 0}
+counters = {"get_model_calls": 0, "quick_sat_answers": 0, "candidate_answers": 0, "solver_calls": 0}
 
 
 def set_solver_backend(backend: Optional[SolverBackend]) -> None:
@@ -396,8 +476,10 @@ def simplify(expr):
 
 
 @lru_cache(maxsize=2 ** 23)
-def get_model(constraints, minimize=(), maximize=(), solver_timeout=None):
-    """model.py:68-130."""
+def get_model(constraints, minimize=(), maximize=(), solver_timeout=None, verdict_only=False):
+    """model.py:68-130.  ``verdict_only`` (build extension, default off): the caller only uses
+    whether a model exists (``Constraints.is_possible``); with ``Args.quick_sat_candidates`` a
+    quick-sat miss then also tries generated candidates before the solver."""
     counters["get_model_calls"] += 1
     solver_timeout = solver_timeout or args.solver_timeout
     solver_timeout = min(solver_timeout, time_handler.time_remaining())
@@ -417,6 +499,11 @@ def get_model(constraints, minimize=(), maximize=(), solver_timeout=None):
         if ret_model:
             counters["quick_sat_answers"] += 1
             return ret_model
+        if verdict_only and args.quick_sat_candidates:
+            cand = model_cache.candidate_for(simplify(S.And(*constraints)))
+            if cand is not False:
+                counters["candidate_answers"] += 1
+                return cand
     counters["solver_calls"] += 1
     pool = ThreadPool(1)
     try:
@@ -451,7 +538,10 @@ class Constraints(list):
     def is_possible(self, solver_timeout=None) -> bool:
         """constraints.py:28-43: a timeout under the default timeout prunes the state."""
         try:
-            get_model(self, solver_timeout=solver_timeout)
+            if args.quick_sat_candidates:
+                get_model(self, solver_timeout=solver_timeout, verdict_only=True)
+            else:
+                get_model(self, solver_timeout=solver_timeout)
         except SolverTimeOutException:
             return solver_timeout is not None
         except UnsatError:
@@ -515,12 +605,16 @@ def is_possible_batch(states: Sequence[Constraints], solver_timeout=None) -> Lis
     for all quick-sat queries.  Answers are identical to the sequential loop (see module doc)."""
     exprs = [e for e in (quick_sat_expr(c) for c in states) if e is not None]
     model_cache.prefetch(exprs)
+    if args.quick_sat_candidates:
+        model_cache.prefetch_candidates(exprs)
     try:
         return [c.is_possible(solver_timeout=solver_timeout) for c in states]
     finally:
         # a state whose get_model call was answered by get_model's own memo never reached
         # check_quick_sat: drop its prefetched row so it does not ride along in later launches
         model_cache.discard(exprs)
+        for e in exprs:
+            model_cache._cand.pop(e, None)
 
 
 def enable_dump(directory: Optional[str]) -> None:

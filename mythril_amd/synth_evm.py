@@ -681,3 +681,45 @@ def dropin_workload(n_queries: int, n_models: int, seed: int = 7, n_tx: int = 3,
         exprs.append(evm_path(rng, ghost.witness(q), n_tx, checks_per_tx))
         planted.append(-1)
     return exprs, records, planted
+
+
+def fork_workload(n_queries: int, n_models: int, seed: int = 8, n_tx: int = 3,
+                  checks_per_tx: Tuple[int, int] = (3, 6)):
+    """Fork-pruning queries (svm.py:351-358): each query is a path that a cached model satisfies
+    plus ONE new branch condition on the last transaction's calldata — the successor of a JUMPI —
+    which that model falsifies.  These are the misses a candidate generator can answer without
+    z3.  Returns ``(exprs, records, parent index)`` (records = the cached models, MRU first)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    models = EvmModels(seed, n_models, n_tx)
+    records, wits = [], []
+    for m in range(n_models):
+        w = models.witness(m)
+        w["sender"] = [ACTORS[int(rng.integers(3))] if s not in ACTORS else s for s in w["sender"]]
+        wits.append(w)
+        records.append(evm_model_record(w, n_tx))
+    exprs, parents = [], []
+    tx = _Tx(n_tx)
+    for q in range(n_queries):
+        p = int(rng.integers(n_models))
+        wit = wits[p]
+        path = evm_path(rng, dict(wit), n_tx, checks_per_tx)
+        B, cds = wit["bytes"][n_tx - 1], wit["cds"][n_tx - 1]
+        kind = int(rng.integers(4))
+        if kind == 0:      # require(arg == c): the parent's argument differs
+            c = int.from_bytes(rng.bytes(4), "big")
+            cond = S.Extract(31, 0, tx.word(36)) == c
+        elif kind == 1:    # if (arg < c) with the parent on the other side
+            W = _word_val(B, cds, 36)
+            c = int(rng.integers(1, 1 << 16))
+            cond = S.ULT(tx.word(36), S.BitVecVal(c, 256)) if W >= c else S.Not(S.ULT(tx.word(36), S.BitVecVal(c, 256)))
+        elif kind == 2:    # a flag byte of the first argument
+            c = int(rng.integers(0, 256))
+            cond = S.Extract(7, 0, tx.word(4)) == c
+            if (_word_val(B, cds, 4) & 0xFF) == c:
+                cond = S.Not(cond)
+        else:              # calldata size branch
+            c = int(rng.integers(4, 100))
+            cond = S.ULT(tx.cds, S.BitVecVal(c, 256)) if cds >= c else S.Not(S.ULT(tx.cds, S.BitVecVal(c, 256)))
+        exprs.append(S.And(*(path.args + (cond,))))
+        parents.append(p)
+    return exprs, records, parents

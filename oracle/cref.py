@@ -65,6 +65,13 @@ def verdicts(tb: TapeBatch, mb: ModelBatch, nthreads: int = 0) -> np.ndarray:
     return np.unpackbits(bits, bitorder="little")[:nbits].reshape(tb.n_tapes, mb.n_models).astype(bool)
 
 
+def eval_tape(tb: TapeBatch, t: int, mb: ModelBatch, m: int) -> int:
+    """Verdict of tape t on local model m (1 / 0, -2 unsupported)."""
+    ts, k1 = as_tape_batch(tb)
+    ms, k2 = as_model_batch(mb)
+    return int(lib().cref_eval_tape(C.byref(ts), t, C.byref(ms), m))
+
+
 def eval_node(tb: TapeBatch, t: int, mb: ModelBatch, m: int, node: int) -> int:
     ts, keep_t = as_tape_batch(tb)
     ms, keep_m = as_model_batch(mb)

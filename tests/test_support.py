@@ -301,3 +301,43 @@ def test_keccak_manager_reset_keeps_index_counter():
     km.reset()
     lo1, _ = km.interval(512)
     assert lo1 != lo0
+
+
+def test_generated_candidates_answer_fork_verdicts(fresh):
+    """Args.quick_sat_candidates: forks the LRU misses (fork_workload: a cached path + one new
+    branch condition) are answered by generated candidates without the solver; every answer is
+    a model that satisfies the query under direct term evaluation, and is NOT inserted into the
+    LRU (the cache contents stay the solver's)."""
+    import term_eval
+    from mythril_amd.synth_evm import fork_workload
+    exprs, recs, parents = fork_workload(24, 40, seed=9)
+    solver = ScriptedSolver(lambda cs: "unknown")
+    sp.set_solver_backend(solver)
+    for m in reversed(recs):
+        sp.model_cache.put(m, 1)
+    before = list(sp.model_cache.model_cache.lru_cache)
+    sp.args.quick_sat_candidates, budget = True, sp.args.quick_sat_candidate_budget
+    sp.args.quick_sat_candidate_budget = 6000
+    try:
+        states = [sp.Constraints(list(e.args)) for e in exprs]
+        got = sp.is_possible_batch(states)
+    finally:
+        sp.args.quick_sat_candidates, sp.args.quick_sat_candidate_budget = False, budget
+    assert sp.counters["candidate_answers"] == sum(got) > 0
+    assert solver.calls == len(states) - sum(got)
+    assert list(sp.model_cache.model_cache.lru_cache) == before
+    # each answered state: the candidate model found for it satisfies the full query
+    cs_answers = [sp.model_cache.candidates([e])[0] for e, ok in zip(exprs, got) if ok]
+    assert all(a is not False for a in cs_answers)
+    for e, a in zip([e for e, ok in zip(exprs, got) if ok], cs_answers):
+        assert term_eval.is_true(e, a)
+
+
+def test_candidates_off_by_default(fresh):
+    from mythril_amd.synth_evm import fork_workload
+    exprs, recs, _ = fork_workload(4, 10, seed=10)
+    sp.set_solver_backend(ScriptedSolver(lambda cs: "unknown"))
+    for m in reversed(recs):
+        sp.model_cache.put(m, 1)
+    assert sp.is_possible_batch([sp.Constraints(list(e.args)) for e in exprs]) == [False] * 4
+    assert sp.counters["candidate_answers"] == 0

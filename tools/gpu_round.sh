@@ -16,16 +16,16 @@ fi
 if has bench; then
   timeout -k 10 400 python -u bench.py > "$OUT/bench_c2.json" 2> "$OUT/bench_c2.err" || exit 12
   for c in c3 c4 c5; do
-    timeout -k 10 400 python -u bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || exit 13
+    timeout -k 10 400 python -u bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-dropin > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || exit 13
   done
 fi
 cd /tmp
 if has trace; then
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run -- python3 "$R/bench.py" --no-cpu-baseline > "$OUT/kt_bench.json" 2> "$OUT/kt_bench.err" || exit 16
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt_c3" -o run -- python3 "$R/bench.py" --config c3 --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/kt_c3_bench.json" 2> "$OUT/kt_c3_bench.err" || exit 17
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run -- python3 "$R/bench.py" --no-cpu-baseline --no-dropin > "$OUT/kt_bench.json" 2> "$OUT/kt_bench.err" || exit 16
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt_c3" -o run -- python3 "$R/bench.py" --config c3 --steps 2 --warmup 1 --no-cpu-baseline --no-dropin > "$OUT/kt_c3_bench.json" 2> "$OUT/kt_c3_bench.err" || exit 17
 fi
 if has pmc; then
-  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/pmc_fetch.json" 2>&1 || exit 18
-  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/pmc_write.json" 2>&1 || exit 19
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-dropin > "$OUT/pmc_fetch.json" 2>&1 || exit 18
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-dropin > "$OUT/pmc_write.json" 2>&1 || exit 19
 fi
 echo "done $TAG"
