@@ -176,9 +176,7 @@ def dropin_leg(ev, grid=((1, 16), (1, 100), (32, 16), (32, 100), (256, 16), (256
         for r in reversed(recs):
             cache.put(r, 1)
         cache.check_quick_sat_batch(warm)
-        exprs, _, planted = dropin_workload(n, m, seed=seed + 1)
-        # same candidate set (models of seed) so planted hits of seed + 1 are not expected here;
-        # answers are checked against the oracle below
+        exprs, _, planted = dropin_workload(n, m, seed=seed, query_seed=1)   # new paths, same models
         cache = sp.ModelCache(eng)
         for r in reversed(recs):
             cache.put(r, 1)

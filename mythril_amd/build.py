@@ -86,7 +86,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if force or jobs or not os.path.exists(OUT):
         # librccl: the in-library MIN all-reduce of a multi-device context (mq_ctx_create n_dev > 1)
         cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT, *objs,
-               f"-L{_rocm()}/lib", "-lrccl", f"-Wl,-rpath,{_rocm()}/lib"]
+               f"-L{_rocm()}/lib", "-lrccl", f"-Wl,-rpath,{_rocm()}/lib", "-lpthread"]
         res = subprocess.run(cmd, capture_output=True, text=True)
         if res.returncode:
             sys.stderr.write(res.stderr)

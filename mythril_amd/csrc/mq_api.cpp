@@ -7,7 +7,9 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <thread>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -179,6 +181,39 @@ struct mq_tapes {
 };
 
 static thread_local std::string g_last_error;
+
+// Host-side parallel loop over independent items (tape compilation): std::threads pulling
+// chunks off a shared counter.  Threads: MQ_HOST_THREADS, else OMP_NUM_THREADS, else the
+// hardware concurrency, at most 64.  (No OpenMP runtime: the library shares its process with
+// torch's own.)
+template <class F>
+static void parallel_for(int64_t n, int64_t chunk, F&& fn) {
+  static const int kThreads = [] {
+    for (const char* v : {"MQ_HOST_THREADS", "OMP_NUM_THREADS"})
+      if (const char* e = std::getenv(v)) {
+        const int t = std::atoi(e);
+        if (t > 0) return std::min(t, 64);
+      }
+    return (int)std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
+  }();
+  const int T = (int)std::min<int64_t>(kThreads, (n + chunk - 1) / std::max<int64_t>(chunk, 1));
+  if (T <= 1) {
+    fn(0, 0, n);
+    return;
+  }
+  std::atomic<int64_t> next{0};
+  auto work = [&](int tid) {
+    for (;;) {
+      const int64_t b = next.fetch_add(chunk);
+      if (b >= n) break;
+      fn(tid, b, std::min(n, b + chunk));
+    }
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < T; t++) pool.emplace_back(work, t);
+  work(0);
+  for (auto& th : pool) th.join();
+}
 
 static int hip_fail(hipError_t e, const char* what) {
   g_last_error = std::string(what) + ": " + hipGetErrorString(e);
@@ -947,8 +982,9 @@ int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t*
   // compile once (independent per tape), upload to every device of the context
   CompileLimits lim;
   std::vector<CompiledTape> ct(tb->n_tapes);
-#pragma omp parallel for schedule(dynamic, 64)
-  for (int t = 0; t < tb->n_tapes; t++) ct[t] = compile_tape(tb, t, lim);
+  parallel_for(tb->n_tapes, 16, [&](int, int64_t b, int64_t e) {
+    for (int64_t t = b; t < e; t++) ct[t] = compile_tape(tb, (int32_t)t, lim);
+  });
   return tapes_upload_all(c, tb->n_tapes, ct, out, n_unsup_out);
 }
 
@@ -1059,22 +1095,25 @@ static bool dag_ok(const mq_dag_batch* d) {
 // Compile every tape of a DAG batch (parallel over tapes).
 static std::vector<CompiledTape> compile_dag(const mq_dag_batch* dag, const CompileLimits& lim) {
   std::vector<CompiledTape> ct(dag->n_tapes);
-#pragma omp parallel
-  {
-    std::vector<int32_t> mark((size_t)std::max<int64_t>(dag->n_nodes, 1), 0);
+  struct Scratch {
+    std::vector<int32_t> mark;
     std::vector<mq_node> block;
     int32_t stamp = 0;
-#pragma omp for schedule(dynamic, 16)
-    for (int t = 0; t < dag->n_tapes; t++) {
-      if (!expand_dag_tape(dag, t, mark, ++stamp, block)) {
+  };
+  std::vector<Scratch> scratch(64);
+  parallel_for(dag->n_tapes, 4, [&](int tid, int64_t b, int64_t e) {
+    Scratch& sc = scratch[tid];
+    if (sc.mark.empty()) sc.mark.assign((size_t)std::max<int64_t>(dag->n_nodes, 1), 0);
+    for (int64_t t = b; t < e; t++) {
+      if (!expand_dag_tape(dag, (int32_t)t, sc.mark, ++sc.stamp, sc.block)) {
         ct[t].why = "malformed DAG (operand does not precede its user)";
         continue;
       }
-      const int64_t offs[2] = {0, (int64_t)block.size()};
-      mq_tape_batch one{1, offs, block.data(), dag->const_words, dag->n_const_words};
+      const int64_t offs[2] = {0, (int64_t)sc.block.size()};
+      mq_tape_batch one{1, offs, sc.block.data(), dag->const_words, dag->n_const_words};
       ct[t] = compile_tape(&one, 0, lim);
     }
-  }
+  });
   return ct;
 }
 
@@ -1111,8 +1150,9 @@ static int set_columns_one(mq_tapes* T, const mq_tape_batch* progs, const int32_
   CompileLimits lim;
   lim.value_root = true;
   std::vector<CompiledTape> ct(n_columns);
-#pragma omp parallel for schedule(dynamic, 16)
-  for (int k = 0; k < n_columns; k++) ct[k] = compile_tape(progs, k, lim);
+  parallel_for(n_columns, 16, [&](int, int64_t b, int64_t e) {
+    for (int64_t k = b; k < e; k++) ct[k] = compile_tape(progs, (int32_t)k, lim);
+  });
   int max_level = 0;
   for (int k = 0; k < n_columns; k++) {
     if (!ct[k].supported) {

@@ -400,7 +400,7 @@ class IncrementalLowering:
     Terms are held alive while they are in the DAG (the id memo must stay valid); past
     ``MAX_NODES`` the DAG starts over (the symbol table, hence the model rows, persist)."""
 
-    MAX_NODES = 1 << 22
+    MAX_NODES = 1 << 20
 
     def __init__(self) -> None:
         self.syms = SymbolTable()

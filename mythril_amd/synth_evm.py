@@ -661,11 +661,12 @@ def evm_model_record(wit: Dict, n_tx: int):
 
 
 def dropin_workload(n_queries: int, n_models: int, seed: int = 7, n_tx: int = 3, planted_frac: float = 0.3,
-                    checks_per_tx: Tuple[int, int] = (3, 6)):
+                    checks_per_tx: Tuple[int, int] = (3, 6), query_seed: int = None):
     """Quick-sat at the reference's own shape: ``n_models`` <= 100 cached
     models (the LRU, MRU first) and ``n_queries`` EVM-shaped path conjunctions, a fraction of them
-    satisfied by one of the cached models.  Returns ``(exprs, records, planted index or -1)``."""
-    rng = np.random.Generator(np.random.PCG64(seed))
+    satisfied by one of the cached models.  ``query_seed`` draws another query set over the same
+    models (default: ``seed``).  Returns ``(exprs, records, planted index or -1)``."""
+    rng = np.random.Generator(np.random.PCG64(seed if query_seed is None else (seed, query_seed)))
     models = EvmModels(seed, n_models, n_tx)
     ghost = EvmModels(seed + 1_000_003, max(1, n_queries), n_tx, 0, 0)
     records = [evm_model_record(models.witness(m), n_tx) for m in range(n_models)]
