@@ -213,6 +213,33 @@ def dropin_leg(ev, grid=((1, 16), (1, 100), (32, 16), (32, 100), (256, 16), (256
     return out
 
 
+def keccak_leg(ev, sizes=(1, 64, 4096, 262144), msg_bytes: int = 64):
+    """Concrete keccak service (mythril_amd.keccak_service): GPU mq_keccak256 per-call latency by
+    batch size vs the per-call CPU keccak the reference uses (eth_hash from Python, here the
+    oracle's C keccak called from Python per message: oracle/cref.c, one core)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cref  # oracle: CPU comparison only
+    rng = np.random.default_rng(5)
+    out = []
+    for n in sizes:
+        msgs = rng.integers(0, 256, (n, msg_bytes), dtype=np.uint8)
+        ev.keccak256_array(msgs[:1])
+        reps = max(1, min(50, 20000 // n))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dg = ev.keccak256_array(msgs)
+        gpu = (time.perf_counter() - t0) / reps
+        k = min(n, 20000)
+        t0 = time.perf_counter()
+        ref = [cref.keccak256(bytes(m)) for m in msgs[:k]]
+        cpu = (time.perf_counter() - t0) / k * n
+        ok = all(bytes(dg[i]) == ref[i] for i in range(min(k, 256)))
+        out.append({"messages": n, "bytes_each": msg_bytes, "gpu_ms_per_call": gpu * 1e3,
+                    "gpu_us_per_hash": gpu / n * 1e6, "cpu_us_per_hash_1core": cpu / n * 1e6,
+                    "gpu_over_cpu": cpu / gpu, "digests_match": bool(ok)})
+    return out
+
+
 def pmc_traffic(workload_key: str):
     """HBM bytes per launch of the evaluation kernel from the committed rocprofv3 PMC summary of
     this exact workload (profiles/, FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; see
@@ -379,6 +406,7 @@ def main():
             out["gpu_over_cpu"] = out["value"] / cb["value"]
         if world == 1 and not args.no_dropin:
             out["dropin"] = dropin_leg(ev)
+            out["keccak_service"] = keccak_leg(ev)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -62,3 +62,17 @@ def test_enable_dump_on_the_global_cache(tmp_path):
         assert sp.model_cache.recorder is None
     finally:
         sp.reset_caches()
+
+
+def test_records_mark_the_reference_answer_not_recorded_without_z3(tmp_path):
+    """Without z3 (z3-free terms) the reference loop's answer is not recorded (-3) and replay
+    falls back to the evaluator's own answer; on a z3 host ref_answer holds z3's first hit."""
+    from mythril_amd.corpus import NOT_RECORDED
+    cache = sp.ModelCache(OracleEngine())
+    cache.recorder = Recorder(str(tmp_path))
+    cache.put(Model({"x": 1}), 1)
+    cache.check_quick_sat(S.And(x == 1))
+    (path,) = records(str(tmp_path))
+    with np.load(path, allow_pickle=False) as z:
+        assert int(z["ref_answer"]) == NOT_RECORDED and int(z["answer"]) == 0
+    assert load_record(path, reference=True)[2] == 0
