@@ -95,6 +95,7 @@ def parse():
     p.add_argument("--device", type=int, default=None, help="override LOCAL_RANK -> device mapping (rehearsal)")
     p.add_argument("--no-hoist", action="store_true", help="c3/c4/c5: lower without batch-level hoisting")
     p.add_argument("--no-dropin", action="store_true", help="skip the drop-in leg (ModelCache at N<=256, M<=100)")
+    p.add_argument("--no-early-exit", action="store_true", help="diagnostic: evaluate every (tape, model) pair")
     return p.parse_args()
 
 
@@ -292,6 +293,8 @@ def main():
     t_gen = time.perf_counter() - t_gen
 
     ev = Evaluator(local)
+    if args.no_early_exit:
+        ev.set_option(Evaluator.OPT_EARLY_EXIT, 0)
     ev.upload_models(mb)
     ct = ev.compile(tb)
     if ct.n_unsupported:

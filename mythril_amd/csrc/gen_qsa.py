@@ -56,6 +56,12 @@ VBASE, SBASE, TBASE = 8, 72, 120
 UBASE = 40     # G: UF1 work registers v[40:63]
 BBASE = 48
 
+STG = "v65"    # G: LDS address of the staged model rows of this lane (stage base + 4 * lane)
+# G early exit: a 64-desc window of the wave's tapes, lane i <-> desc s25 - 1 - 64w - i (w = the
+# window of the current tape counted from the wave's LAST desc); EEA = byte offset of best[tape]
+# of that desc, EEV = best[] as gathered while the previous tape ran (None: scalar check)
+EEA, EEV = "v67", "v66"
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
@@ -133,7 +139,9 @@ def load_window(first):
     return out
 
 
-VMWAIT = "s_waitcnt vmcnt(0)"
+# G: a handler that reads the stack first waits for the pushes in flight — global loads (PUSH_MEM)
+# and LDS reads of staged model rows (PUSH_MEMS)
+VMWAIT = "s_waitcnt vmcnt(0) lgkmcnt(0)"
 
 
 def zero_limbs(d, lo):
@@ -524,6 +532,15 @@ def make_handlers(variant, pfx):
                                  "s_add_u32 s34, s34, s90", "s_addc_u32 s35, s35, s91",
                                  "global_load_dword v4, v2, s[34:35]", "s_waitcnt vmcnt(0)",
                                  f"v_cmp_ne_u32_e64 {B(d)}, 0, v4", "s_nop 3"], reads_stack=False)
+            # staged rows (imm = LDS slot of the variable's first limb row, the tile's 64 words of
+            # a row at STAGE + 256 * slot; v65 = STAGE + 4 * lane): LDS reads instead of global
+            # loads, waited for by the next stack reader
+            for n in range(1, L + 1):
+                H(("PUSH_MEMS", d, n - 1), ["s_lshl_b32 s34, s17, 8", f"v_add_u32 v5, s34, {STG}"]
+                  + [f"ds_read_b32 {S(d, l)}, v5 offset:{256 * l}" for l in range(n)] + zero_limbs(d, n),
+                  reads_stack=False)
+            H(("PUSH_MEMSB", d), ["s_lshl_b32 s34, s17, 8", f"v_add_u32 v5, s34, {STG}", "ds_read_b32 v4, v5",
+                                  "s_waitcnt lgkmcnt(0)", f"v_cmp_ne_u32_e64 {B(d)}, 0, v4", "s_nop 3"], reads_stack=False)
         H(("PUSH_CONST", d), ["s_lshl_b32 s34, s17, 2", "s_load_dwordx8 s[64:71], s[20:21], s34", "s_waitcnt lgkmcnt(0)"]
           + [f"v_mov_b64 {S2(d, l)}, s[{64 + l}:{65 + l}]" for l in range(0, L, 2)], reads_stack=False)
         if G:
@@ -698,6 +715,64 @@ def store_column(pfx):
     return out
 
 
+def stage_rows(pfx):
+    """G: copy the model rows the batch's tapes push most (QArgs stage_rows[0..n_stage), a
+    multiple of 8, padded with the zero row) for this workgroup's 64-model tile into LDS at
+    stage_base + 256 * slot, 8 rows per wave per round (8 loads in flight), then s_barrier: the
+    4 waves of the workgroup share the tile, so each row is fetched once per workgroup and every
+    PUSH_MEMS of its tapes is an LDS read."""
+    out = ["s_load_dwordx2 s[64:65], s[10:11], 0x184",     # n_stage, stage_base
+           "s_load_dwordx2 s[66:67], s[10:11], 0x190",     # stage_rows
+           "v_and_b32 v4, 63, v3",
+           "v_lshlrev_b32 v4, 2, v4",
+           "v_lshrrev_b32 v5, 6, v3",
+           "s_nop 1",
+           "v_readfirstlane_b32 s60, v5",                  # wave
+           "s_waitcnt lgkmcnt(0)",
+           f"v_add_u32 {STG}, s65, v4",
+           "s_lshl_b32 s61, s60, 3",                        # first row of this wave's rounds
+           f"{pfx}_stage_loop:",
+           "s_cmp_ge_u32 s61, s64",
+           f"s_cbranch_scc1 {pfx}_stage_done",
+           "s_lshl_b32 s70, s61, 2",
+           "s_load_dwordx8 s[80:87], s[66:67], s70",
+           "s_waitcnt lgkmcnt(0)"]
+    for j in range(8):
+        out += [f"s_mul_i32 s68, s{80 + j}, s29", f"s_mul_hi_u32 s69, s{80 + j}, s29", "s_lshl_b64 s[68:69], s[68:69], 2",
+                "s_add_u32 s68, s68, s90", "s_addc_u32 s69, s69, s91",
+                f"global_load_dword {T(j)}, v2, s[68:69]"]
+    out += ["s_lshl_b32 s70, s61, 8", f"v_add_u32 v5, s70, {STG}", "s_waitcnt vmcnt(0)"]
+    out += [f"ds_write_b32 v5, {T(j)} offset:{256 * j}" for j in range(8)]
+    out += ["s_add_u32 s61, s61, 32", f"s_branch {pfx}_stage_loop",
+            f"{pfx}_stage_done:",
+            "s_waitcnt lgkmcnt(0)",
+            "s_barrier"]
+    return out
+
+
+def ee_window():
+    """G: load the early-exit window of the tape with s34 = s25 - 1 - s24 (tapes of the wave
+    after it): EEA[i] = 4 * descs[s25 - 1 - 64 * (s34 / 64) - i].tape (clamped at desc 0),
+    EEV[i] = best[] there, for all 64 lanes whatever exec holds.  Clobbers s35, s[60:61]; waits
+    for both loads."""
+    return ["s_mov_b64 s[60:61], exec",
+            "s_mov_b64 exec, -1",
+            "s_andn2_b32 s35, s34, 63",
+            "s_sub_u32 s35, s25, s35",
+            "s_sub_u32 s35, s35, 1",
+            f"v_mbcnt_lo_u32_b32 {EEA}, -1, 0",
+            f"v_mbcnt_hi_u32_b32 {EEA}, -1, {EEA}",
+            f"v_sub_u32 {EEA}, s35, {EEA}",
+            f"v_max_i32 {EEA}, 0, {EEA}",
+            f"v_lshlrev_b32 {EEA}, 5, {EEA}",
+            f"global_load_dword {EEA}, {EEA}, s[22:23] offset:8",
+            "s_waitcnt vmcnt(0)",
+            f"v_lshlrev_b32 {EEA}, 2, {EEA}",
+            f"global_load_dword {EEV}, {EEA}, s[26:27] sc1",
+            "s_waitcnt vmcnt(0)",
+            "s_mov_b64 exec, s[60:61]"]
+
+
 def frame(variant, pfx, handlers, subs):
     G = variant == "g"
     P = []
@@ -803,6 +878,18 @@ def frame(variant, pfx, handlers, subs):
                       f"global_load_dword v{VBASE + 8 * v + l}, v2, s[34:35]"]
         P += ["s_waitcnt vmcnt(0)"]
     P += ["s_lshl_b32 s74, s29, 2", "s_lshr_b32 s75, s29, 30"]   # M*4 (after the preload's s[64:79] use)
+    if G:
+        P += stage_rows(pfx)
+    ee = G and EEV is not None
+    if ee:
+        P += ["s_cmp_lg_u32 s31, 0",
+              f"s_cbranch_scc1 {pfx}_ee_init_done",
+              "s_cmp_eq_u32 s30, 0",
+              f"s_cbranch_scc1 {pfx}_ee_init_done",
+              "s_cmp_ge_u32 s24, s25",
+              f"s_cbranch_scc1 {pfx}_ee_init_done",
+              "s_sub_u32 s34, s25, s24",
+              "s_sub_u32 s34, s34, 1"] + ee_window() + [f"{pfx}_ee_init_done:"]
     # tape loop
     P += [
         f"{pfx}_tape_loop:",
@@ -820,10 +907,34 @@ def frame(variant, pfx, handlers, subs):
         f"s_cbranch_scc1 {pfx}_run",
         "s_cmp_eq_u32 s30, 0",
         f"s_cbranch_scc1 {pfx}_run",
+    ] + ([
+        # best[tape] from the window gathered while the previous tape ran (a stale value only
+        # costs a tape that a fresher one would have skipped); a new window every 64 tapes
+        "s_sub_u32 s34, s25, s24",
+        "s_sub_u32 s34, s34, 1",
+        "s_and_b32 s35, s34, 63",
+        "s_cmp_lg_u32 s35, 63",
+        f"s_cbranch_scc1 {pfx}_ee_have",
+    ] + ee_window() + [
+        f"{pfx}_ee_have:",
+        "s_waitcnt vmcnt(0)",
+        "s_and_b32 s35, s34, 63",
+        f"v_readlane_b32 s36, {EEV}, s35",
+        "s_nop 3",                      # VALU SGPR write -> SALU read
+        "s_cmp_ge_i32 s28, s36",
+        f"s_cbranch_scc1 {pfx}_next_tape",
+        # refresh the window for the next tape, waited for at its check (the run's first
+        # vmcnt wait usually covers it)
+        "s_mov_b64 s[60:61], exec",
+        "s_mov_b64 exec, -1",
+        f"global_load_dword {EEV}, {EEA}, s[26:27] sc1",
+        "s_mov_b64 exec, s[60:61]",
+    ] if ee else [
         "s_load_dword s34, s[72:73], 0x0 glc",
         "s_waitcnt lgkmcnt(0)",
         "s_cmp_ge_i32 s28, s34",
         f"s_cbranch_scc1 {pfx}_next_tape",
+    ]) + [
         f"{pfx}_run:",
         "s_lshl_b32 s34, s83, 2",
         "s_add_u32 s20, s88, s34",
@@ -882,9 +993,14 @@ def frame(variant, pfx, handlers, subs):
         "s_add_u32 s24, s24, 1",
         f"s_branch {pfx}_tape_loop",
         f"{pfx}_tapes_done:",
+        # the wave's counters go to slot (tile ^ group) mod 256 of the slotted counter array
+        # (qs_launch.h kCounterSlots): 10^6 waves adding into one cache line serialise in L2
+        "s_xor_b32 s34, s96, s97",
+        "s_and_b32 s34, s34, 255",
+        "s_lshl_b32 s34, s34, 7",
         "s_mov_b64 s[60:61], exec",
         "s_mov_b64 exec, 1",
-        "v_mov_b32 v6, 0",
+        "v_mov_b32 v6, s34",
         "v_mov_b32 v4, s40",
         "v_mov_b32 v5, s41",
         "global_atomic_add_x2 v6, v[4:5], s[92:93]",
@@ -917,11 +1033,13 @@ def set_layout(variant):
     """Register map of the variant being generated (the body functions read these globals).
     P and G with preloads: the map in the module docstring.  Compact G (NVG = 0): UF1 work
     v[8:31], program window v32, stack v[40:87], T/W v[88:95] -> 96 VGPRs."""
-    global SBASE, TBASE, UBASE, WIN, NEXT_G
+    global SBASE, TBASE, UBASE, WIN, NEXT_G, EEA, EEV
     if variant == "g" and NVG == 0:
         SBASE, TBASE, UBASE, WIN = 40, 88, 8, "v32"
+        EEA = EEV = None
     else:
         SBASE, TBASE, UBASE, WIN = 72, 120, 40, "v64"
+        EEA, EEV = "v67", "v66"
     NEXT_G = [ln.replace("v64", WIN) if ln.startswith("v_readlane") else ln for ln in NEXT_G_TEMPLATE]
 
 

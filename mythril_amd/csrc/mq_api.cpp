@@ -149,6 +149,11 @@ struct mq_tapes {
   // most 8) variables the G tapes push most; g_var_row = their limb rows (QArgs.var_row)
   std::vector<int> gpre;
   uint32_t g_var_row[64];
+  // G rows staged in LDS per workgroup: gstage[var] = LDS slot of its first limb row (or -1),
+  // stage_rows = global row of every slot (padded to a multiple of 8 with the zero row)
+  std::vector<int> gstage;
+  std::vector<uint32_t> stage_rows;
+  DevBuf stage_dev;
   DevBuf qdescs, qprog, qargs[2];
   QArgs qargs_dev_copy[2];   // what qargs[k] currently holds on the device
   bool qargs_valid[2] = {false, false};
@@ -173,6 +178,9 @@ struct mq_tapes {
   int cq_temps = 0;
   DevBuf cqdescs, cqprog, cqconsts, cqargs;
   std::vector<QArgs> cqargs_host;   // what cqargs holds on the device, per level
+  std::vector<int> cq_stage;         // staged rows of the G column programs (as gstage)
+  std::vector<uint32_t> cq_stage_rows;
+  DevBuf cq_stage_dev;
   // multi-device context: the same batch compiled on each peer device (ctx->peers order)
   std::vector<mq_tapes*> peers;
   ~mq_tapes() {
@@ -181,6 +189,15 @@ struct mq_tapes {
 };
 
 static thread_local std::string g_last_error;
+
+static constexpr size_t kCounterBytes = sizeof(unsigned long long) * kCounterSlots * kCounterStride;
+
+// the three work counters, summed over the slots (qs_launch.h)
+static void sum_counter_slots(const std::vector<unsigned long long>& raw, unsigned long long out[3]) {
+  out[0] = out[1] = out[2] = 0;
+  for (int s = 0; s < kCounterSlots; s++)
+    for (int i = 0; i < 3; i++) out[i] += raw[(size_t)s * kCounterStride + i];
+}
 
 // Host-side parallel loop over independent items (tape compilation): std::threads pulling
 // chunks off a shared counter.  Threads: MQ_HOST_THREADS, else OMP_NUM_THREADS, else the
@@ -333,7 +350,7 @@ static int create_one(int dev, mq_ctx** out) {
     mq_ctx_destroy(c);
     return MQ_ERR_HIP;
   }
-  if (c->counters.ensure(4 * sizeof(unsigned long long)) != hipSuccess) {
+  if (c->counters.ensure(kCounterBytes) != hipSuccess) {
     mq_ctx_destroy(c);
     return MQ_ERR_NOMEM;
   }
@@ -602,7 +619,8 @@ int mq_models_upload(mq_ctx* c, const mq_model_batch* mb) {
 // time.  Returns false if any instruction is outside the interpreter's set (those tapes run on
 // the HIP C++ kernel).
 static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTape& x, std::vector<uint32_t>* out_p,
-                          std::vector<uint32_t>* extra_p, const std::vector<int>* gpre = nullptr) {
+                          std::vector<uint32_t>* extra_p, const std::vector<int>* gpre = nullptr,
+                          const std::vector<int>* gstage = nullptr) {
   std::vector<uint32_t> dummy_out, dummy_extra;
   std::vector<uint32_t>& out = out_p ? *out_p : dummy_out;
   std::vector<uint32_t>& extra = extra_p ? *extra_p : dummy_extra;
@@ -700,6 +718,9 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
           pushed_pre = ps;
         } else if (!models) {
           ok = word(b ? QK_PUSH_MEMB : QK_PUSH_MEM, d, b ? -1 : 7, 0);
+        } else if (gstage && imm < gstage->size() && (*gstage)[imm] >= 0 && c->var_nl_h[imm] <= 8) {
+          // a row staged in LDS by the workgroup (gen_qsa.py stage_rows)
+          ok = word(b ? QK_PUSH_MEMSB : QK_PUSH_MEMS, d, b ? -1 : (int)c->var_nl_h[imm] - 1, (uint32_t)(*gstage)[imm]);
         } else {
           ok = imm < c->var_off_h.size() && c->var_nl_h[imm] <= 8 && c->var_off_h[imm] <= 0xFFFFu &&
                word(b ? QK_PUSH_MEMB : QK_PUSH_MEM, d, b ? -1 : (int)c->var_nl_h[imm] - 1, c->var_off_h[imm]);
@@ -1311,6 +1332,47 @@ static void qsa_window_layout(const mq_ctx* c, std::vector<uint32_t>& prog) {
   prog.swap(out);
 }
 
+// Push counts of the variables (<= 256 bits) a set of compiled programs reads.
+static std::vector<int64_t> count_pushes(const mq_ctx* c, const std::vector<CompiledTape>& cts,
+                                         const std::vector<char>* skip = nullptr) {
+  std::vector<int64_t> pushes(c->var_nl_h.size(), 0);
+  for (size_t i = 0; i < cts.size(); i++) {
+    if (skip && (*skip)[i]) continue;
+    const auto& pr = cts[i].prog;
+    for (size_t pc = 0; pc < pr.size(); pc++) {
+      const uint32_t op = pr[pc] & 0xFFu, imm = pr[pc] >> 12;
+      if ((op == G_PUSH_VAR || op == G_PUSH_VAR_B) && imm < pushes.size() && c->var_nl_h[imm] <= 8) pushes[imm]++;
+      if (op == G_EXTRACT || op == G_CONCAT || op == G_SEXT || op == G_UF1 || op == G_UF2) pc++;
+    }
+  }
+  return pushes;
+}
+
+// G kernel LDS staging plan: the most pushed variables (not preloaded) whose rows fit the
+// workgroup's staging budget get consecutive LDS slots (gen_qsa.py stage_rows); their pushes
+// become LDS reads.  Budget: MQ_G_STAGE_KB (default 32) KB per workgroup minus the temps of
+// its 4 waves.  stage_rows is padded to a multiple of 8 with the zero row.
+static void plan_stage(const mq_ctx* c, const std::vector<int64_t>& pushes, const std::vector<int>* gpre, int temps,
+                       std::vector<int>& gstage, std::vector<uint32_t>& rows) {
+  int64_t kb = 32;
+  if (const char* e = std::getenv("MQ_G_STAGE_KB")) kb = std::atol(e);
+  const int64_t budget = (kb * 1024 - 4 * (int64_t)temps * 2048) / 256;
+  gstage.assign(c->var_nl_h.size(), -1);
+  rows.clear();
+  std::vector<int> order;
+  for (size_t v = 0; v < pushes.size(); v++)
+    if (pushes[v] > 0 && !(gpre && v < gpre->size() && (*gpre)[v] >= 0)) order.push_back((int)v);
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return pushes[a] > pushes[b]; });
+  for (int v : order) {
+    const int64_t nl = c->var_nl_h[v];
+    if ((int64_t)rows.size() + nl > budget) continue;
+    gstage[v] = (int)rows.size();
+    for (int64_t l = 0; l < nl; l++) rows.push_back(c->var_off_h[v] + (uint32_t)l);
+  }
+  const uint32_t zero_row = (uint32_t)(c->var_off_h.empty() ? 0 : c->var_off_h.back() + c->var_nl_h.back());
+  while (rows.size() % 8) rows.push_back(zero_row);
+}
+
 // (Re)translate the QSA-eligible tapes for the current model batch (variable rows, function
 // table): the P kernel when every variable a tape reads is preloaded, the G kernel otherwise.
 // If one tape does not translate, the whole group runs on the HIP C++ kernel for this batch.
@@ -1348,11 +1410,15 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
     T->gpre[v] = (int)j;
     for (uint32_t l = 0; l < c->var_nl_h[v]; l++) T->g_var_row[8 * j + l] = c->var_off_h[v] + l;
   }
+  int g_temps = 0;
+  for (size_t i = 0; i < T->qct.size(); i++)
+    if (!on_p[i]) g_temps = std::max(g_temps, T->qct[i].n_temps);
+  plan_stage(c, pushes, &T->gpre, g_temps, T->gstage, T->stage_rows);
   for (size_t i = 0; i < T->qct.size(); i++) {
     int k = 0;
     if (!on_p[i] || !qsa_translate(c, 0, true, T->qct[i], &tr, &extra)) {
       k = 1;
-      if (!qsa_translate(c, 1, true, T->qct[i], &tr, &extra, &T->gpre)) return MQ_OK;
+      if (!qsa_translate(c, 1, true, T->qct[i], &tr, &extra, &T->gpre, &T->gstage)) return MQ_OK;
       qsa_window_layout(c, tr);
     }
     GDesc d = T->qbase[i];
@@ -1392,6 +1458,8 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
   if (descs.empty()) descs.push_back(GDesc{});
   HIPCHK(T->qdescs.upload(descs.data(), descs.size(), c->stream));
   HIPCHK(T->qprog.upload(prog.data(), prog.size(), c->stream));
+  if (T->stage_rows.empty()) HIPCHK(T->stage_dev.ensure(sizeof(uint32_t)));
+  else HIPCHK(T->stage_dev.upload(T->stage_rows.data(), T->stage_rows.size(), c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   T->qargs_valid[0] = T->qargs_valid[1] = false;
   T->qsa_live = true;
@@ -1410,9 +1478,12 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
   std::vector<uint32_t> prog, consts, tr, extra;
   std::vector<GDesc> descs;
   int temps = 0;
+  for (const CompiledTape& x : T->cq_ct) temps = std::max(temps, x.n_temps);
+  plan_stage(c, count_pushes(c, T->cq_ct), nullptr, temps, T->cq_stage, T->cq_stage_rows);
+  temps = 0;
   for (size_t i = 0; i < T->cq_ct.size(); i++) {
     const CompiledTape& x = T->cq_ct[i];
-    if (!qsa_translate(c, 1, true, x, &tr, &extra)) return MQ_OK;
+    if (!qsa_translate(c, 1, true, x, &tr, &extra, nullptr, &T->cq_stage)) return MQ_OK;
     qsa_window_layout(c, tr);
     const int v = T->cq_var[i];
     GDesc d{};
@@ -1437,6 +1508,8 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
   HIPCHK(T->cqprog.upload(prog.data(), prog.size(), c->stream));
   HIPCHK(T->cqconsts.upload(consts.data(), consts.size(), c->stream));
   HIPCHK(T->cqargs.ensure(sizeof(QArgs) * T->clevels.size()));
+  if (T->cq_stage_rows.empty()) HIPCHK(T->cq_stage_dev.ensure(sizeof(uint32_t)));
+  else HIPCHK(T->cq_stage_dev.upload(T->cq_stage_rows.data(), T->cq_stage_rows.size(), c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   T->cqargs_host.assign(T->clevels.size(), QArgs{});
   T->cq_temps = temps;
@@ -1540,6 +1613,9 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       q.early_exit = 0;
       q.mode = 3;
       q.lds_wave_bytes = (uint32_t)T->cq_temps * 2048u;
+      q.n_stage = (uint32_t)T->cq_stage_rows.size();
+      q.stage_base = 4u * q.lds_wave_bytes;
+      q.stage_rows = T->cq_stage_dev.as<uint32_t>();
       for (int j = 0; j < 64; j++) q.var_row[j] = zero_row;
       q.funcs = c->funcs.p;
       q.entry_ptr = c->entry_ptr.p;
@@ -1559,7 +1635,8 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
         return MQ_ERR_ARG;
       }
       HIPCHK(start_timer());
-      HIPCHK(launch_qsa(1, dq, 8u * (unsigned)((groups + 3) / 4), (unsigned)rows, (size_t)q.lds_wave_bytes * 4, st));
+      HIPCHK(launch_qsa(1, dq, 8u * (unsigned)((groups + 3) / 4), (unsigned)rows,
+                        (size_t)q.lds_wave_bytes * 4 + (size_t)q.n_stage * 256, st));
     }
     for (int g = 0; g < kGen; g++) {
       const mq_tapes::Variant* v = g == 0 ? &v8 : &lv.v[g];
@@ -1598,6 +1675,11 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     q.early_exit = verdicts ? 0u : (uint32_t)c->early_exit;
     q.mode = verdicts ? 1u : 0u;
     q.lds_wave_bytes = (uint32_t)T->q_temps[k] * 2048u;
+    if (k == 1) {
+      q.n_stage = (uint32_t)T->stage_rows.size();
+      q.stage_base = 4u * q.lds_wave_bytes;
+      q.stage_rows = T->stage_dev.as<uint32_t>();
+    }
     std::memcpy(q.var_row, k == 0 ? c->qsa_var_row : T->g_var_row, sizeof(q.var_row));
     q.funcs = c->funcs.p;
     q.entry_ptr = c->entry_ptr.p;
@@ -1623,7 +1705,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       }
     }
     HIPCHK(start_timer());
-    HIPCHK(launch_qsa(k, T->qargs[k].as<QArgs>(), gx, gy, (size_t)q.lds_wave_bytes * 4, st));
+    HIPCHK(launch_qsa(k, T->qargs[k].as<QArgs>(), gx, gy, (size_t)q.lds_wave_bytes * 4 + (size_t)q.n_stage * 256, st));
   }
   for (const auto& v : cpp) {
     if (v.count <= 0) continue;
@@ -1730,10 +1812,12 @@ int mq_counters(mq_ctx* c, double* out3, int reset) {
   for (mq_ctx* d : devices_of(c)) {
     HIPCHK(hipSetDevice(d->device));
     HIPCHK(hipDeviceSynchronize());
-    unsigned long long cnt[3] = {0, 0, 0};
-    HIPCHK(hipMemcpy(cnt, d->counters.p, sizeof(cnt), hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> raw(kCounterBytes / sizeof(unsigned long long));
+    HIPCHK(hipMemcpy(raw.data(), d->counters.p, kCounterBytes, hipMemcpyDeviceToHost));
+    unsigned long long cnt[3];
+    sum_counter_slots(raw, cnt);
     for (int i = 0; i < 3; i++) out3[i] += (double)cnt[i];
-    if (reset) HIPCHK(hipMemset(d->counters.p, 0, 4 * sizeof(unsigned long long)));
+    if (reset) HIPCHK(hipMemset(d->counters.p, 0, kCounterBytes));
   }
   HIPCHK(hipSetDevice(c->device));
   return MQ_OK;
@@ -1750,7 +1834,7 @@ int mq_eval_tapes_first_hit(mq_ctx* c, mq_tapes* T, int32_t* out, mq_stats* stat
   const std::vector<mq_ctx*> devs = devices_of(c);
   for (mq_ctx* d : devs) {
     HIPCHK(hipSetDevice(d->device));
-    HIPCHK(hipMemsetAsync(d->counters.p, 0, 4 * sizeof(unsigned long long), d->stream));
+    HIPCHK(hipMemsetAsync(d->counters.p, 0, kCounterBytes, d->stream));
   }
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(c->best_tmp.ensure(sizeof(int32_t) * T->n_tapes));
@@ -1764,9 +1848,11 @@ int mq_eval_tapes_first_hit(mq_ctx* c, mq_tapes* T, int32_t* out, mq_stats* stat
   unsigned long long total[3] = {0, 0, 0};
   for (mq_ctx* d : devs) {
     HIPCHK(hipSetDevice(d->device));
-    unsigned long long cnt[3] = {0, 0, 0};
-    HIPCHK(hipMemcpyAsync(cnt, d->counters.p, sizeof(cnt), hipMemcpyDeviceToHost, d->stream));
+    std::vector<unsigned long long> raw(kCounterBytes / sizeof(unsigned long long));
+    HIPCHK(hipMemcpyAsync(raw.data(), d->counters.p, kCounterBytes, hipMemcpyDeviceToHost, d->stream));
     HIPCHK(hipStreamSynchronize(d->stream));
+    unsigned long long cnt[3];
+    sum_counter_slots(raw, cnt);
     for (int i = 0; i < 3; i++) total[i] += cnt[i];
   }
   HIPCHK(hipSetDevice(c->device));

@@ -819,9 +819,10 @@ __global__ __launch_bounds__(64) void qs_first_hit_kernel(KArgs args) {
     }
   }
   if (lane == 0 && args.counters) {
-    atomicAdd(&args.counters[0], (unsigned long long)pairs);
-    atomicAdd(&args.counters[1], (unsigned long long)nodes);
-    atomicAdd(&args.counters[2], (unsigned long long)ops);
+    unsigned long long* cnt = args.counters + (blockIdx.x % kCounterSlots) * kCounterStride;
+    atomicAdd(&cnt[0], (unsigned long long)pairs);
+    atomicAdd(&cnt[1], (unsigned long long)nodes);
+    atomicAdd(&cnt[2], (unsigned long long)ops);
   }
 }
 
@@ -886,8 +887,9 @@ __global__ __launch_bounds__(64) void qs_column_kernel(KArgs args) {
     }
   }
   if (lane == 0 && args.counters) {
-    atomicAdd(&args.counters[1], (unsigned long long)nodes);
-    atomicAdd(&args.counters[2], (unsigned long long)ops);
+    unsigned long long* cnt = args.counters + (blockIdx.x % kCounterSlots) * kCounterStride;
+    atomicAdd(&cnt[1], (unsigned long long)nodes);
+    atomicAdd(&cnt[2], (unsigned long long)ops);
   }
 }
 

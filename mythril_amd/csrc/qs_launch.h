@@ -7,6 +7,12 @@
 
 namespace mq {
 
+// Work counters (pairs evaluated, node-evals, algorithmic ops): kCounterSlots slots of
+// kCounterStride u64 (128 B apart), a wave adds into slot (workgroup id mod kCounterSlots) so a
+// launch of 10^6 waves does not serialise on one cache line; the host sums the slots.
+constexpr int kCounterSlots = 256;
+constexpr int kCounterStride = 16;
+
 // device view of one model function (UF or as-array interpretation)
 struct FuncDev {
   uint32_t arity;
@@ -41,7 +47,7 @@ struct KArgs {
   // outputs
   int32_t* best;                 // first-hit accumulator (global index, INT32_MAX = none)
   uint8_t* verdicts;             // verdict mode: [tape][M] bytes
-  unsigned long long* counters;  // [0] pairs evaluated, [1] node-evals, [2] algorithmic ops
+  unsigned long long* counters;  // [slot][0] pairs evaluated, [1] node-evals, [2] algorithmic ops
   int tmp_words_per_wave;        // temp words per wave (slot, limb, lane)
   int early_exit;
   uint32_t* scratch;             // per-wave temp slots in HBM: [gridDim.x][tmp_words_per_wave]
@@ -76,13 +82,18 @@ struct QArgs {
   const void* entry_words;       // 0x170
   const void* else_words;        // 0x178
   uint32_t n_funcs;              // 0x180
-  uint32_t pad2[3];
+  uint32_t n_stage;              // 0x184 G: model rows staged in LDS per workgroup (multiple of 8)
+  uint32_t stage_base;           // 0x188 G: LDS byte offset of the staged rows
+  uint32_t pad2;                 // 0x18c
+  const uint32_t* stage_rows;    // 0x190 G: global row of each staged slot
 };
 static_assert(sizeof(void*) == 8, "64-bit");
 static_assert(__builtin_offsetof(QArgs, M) == 0x40, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, var_row) == 0x60, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, funcs) == 0x160, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, n_funcs) == 0x180, "QArgs layout");
+static_assert(__builtin_offsetof(QArgs, n_stage) == 0x184, "QArgs layout");
+static_assert(__builtin_offsetof(QArgs, stage_rows) == 0x190, "QArgs layout");
 
 // variant 0 = P (preloaded variables, qsa_kernel), 1 = G (general, qsg_kernel)
 hipError_t launch_qsa(int variant, const QArgs* d_args, unsigned gx, unsigned gy, size_t lds, hipStream_t st);

@@ -34,6 +34,11 @@ __global__ __launch_bounds__(256) void qsg_kernel(const QArgs* __restrict__ args
 }
 
 hipError_t launch_qsa(int variant, const QArgs* d_args, unsigned gx, unsigned gy, size_t lds, hipStream_t st) {
+  if (lds > 65536) {   // temps + staged model rows beyond 64 KB (gfx950: 160 KB of LDS per CU)
+    const void* f = variant == 0 ? reinterpret_cast<const void*>(qsa_kernel) : reinterpret_cast<const void*>(qsg_kernel);
+    const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
   if (variant == 0) hipLaunchKernelGGL(qsa_kernel, dim3(gx, gy), dim3(256), lds, st, d_args);
   else hipLaunchKernelGGL(qsg_kernel, dim3(gx, gy), dim3(256), lds, st, d_args);
   return hipGetLastError();

@@ -441,3 +441,20 @@ def test_c3_tapes_run_on_general_asm_kernel(evaluator):
         assert (evaluator.first_hit(ct) == exp).all()
     finally:
         evaluator.use_asm(True)
+
+
+@pytest.mark.parametrize("stage_kb", ["0", "4", "32", "96"])
+def test_g_kernel_lds_staged_rows_match_oracle(evaluator, monkeypatch, stage_kb):
+    """G kernel with 0 / a few / many model rows staged in LDS per workgroup (MQ_G_STAGE_KB;
+    96 KB exceeds the 64 KB default dynamic LDS): identical first hits to the oracle."""
+    from mythril_amd.synth_evm import c3_workload
+    monkeypatch.setenv("MQ_G_STAGE_KB", stage_kb)
+    tb, mb, exp, _ = c3_workload(24, 3000, seed=13, planted_frac=0.5)
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    fh = evaluator.first_hit(ct)
+    assert ct.asm_split()[1] > 0          # the G kernel ran
+    ref, _ = cref.first_hit(tb, mb)
+    assert (ref == exp).all() and (fh == ref).all()
+    v, _ = evaluator.verdicts(ct)
+    assert (v == cref.verdicts(tb, mb)).all()
