@@ -314,6 +314,18 @@ int mq_tapes_qsa_split(mq_tapes* tapes, int32_t* n_p, int32_t* n_g, int32_t* liv
    when it did not, run on the HIP C++ column kernel).  Introspection for tests and the bench. */
 int mq_tapes_column_split(mq_tapes* tapes, int32_t* n_asm, int32_t* live);
 
+/* After a launch: handler-kind histogram of the current assembly translation (which = 0: P
+   tapes, 1: G tapes, 2: G column programs) into hist_out[cap]; each tape's program runs once per
+   (tape, model) pair, so these are the dispatches per pair summed over tapes.  pairs_out
+   (cap x cap, may be NULL): (kind, next kind) counts over the G tapes (which = 1, else zeros).
+   *n_kinds_out = number of kinds.  Diagnostic (superinstruction planning).  Returns 0 or
+   MQ_ERR_ARG. */
+int mq_tapes_qsa_histogram(mq_tapes* tapes, int32_t which, int64_t* hist_out, int32_t cap, int64_t* pairs_out,
+                           int32_t* n_kinds_out);
+
+/* Name of handler kind `kind` of the assembly interpreters (NULL when out of range). */
+const char* mq_qsa_kind_name(int32_t kind);
+
 /* Static algorithmic cost of a tape; -1 if malformed. */
 double mq_tape_alg_ops(const mq_tape_batch* batch, int32_t t);
 

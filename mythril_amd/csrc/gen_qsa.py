@@ -101,19 +101,23 @@ def W2(k):
 # per node.  s[14:15] = byte address of the window, s16 = lane of the next word.  The translator
 # places a REFILL word wherever the window runs out (the next window starts right after it) and
 # never splits a PUSH_CONSTW from its inline data words.
-WIN = "v64"
-NEXT_G_TEMPLATE = [
-    f"v_readlane_b32 s17, {WIN}, s16",
-    "s_add_u32 s16, s16, 1",
-    "s_nop 2",                      # VALU SGPR write -> SALU read
-    "s_and_b32 s18, s17, 0xffff",
-    "s_lshr_b32 s17, s17, 16",
-    "s_lshl_b32 s18, s18, 2",
-    "s_add_u32 s18, s12, s18",
-    "s_addc_u32 s19, s13, 0",
-    "s_setpc_b64 s[18:19]",
-]
-NEXT_G = list(NEXT_G_TEMPLATE)
+# The window is decoded once per load (load_window), in VALU: WINA = low 32 bits of each word's
+# handler address (s12 + 4 * (word & 0xffff); the host checks the handler area does not cross a
+# 4 GB boundary, so s19 = s13 throughout), WINI = its immediate (word >> 16).  A dispatch is then
+# two lane reads, one SALU add and the jump: the scalar unit, shared by the CU's four SIMDs, was
+# the binding issue port at six SALU per dispatch.
+WIN, WINA, WINI = "v64", "v68", "v69"
+
+
+def next_g():
+    return [f"v_readlane_b32 s18, {WINA}, s16",
+            f"v_readlane_b32 s17, {WINI}, s16",
+            "s_add_u32 s16, s16, 1",
+            "s_nop 1",                      # VALU SGPR write -> SALU read (s_setpc)
+            "s_setpc_b64 s[18:19]"]
+
+
+NEXT_G = next_g()
 
 
 # P: two-word program entries (absolute low 32 bits of the handler address, immediate),
@@ -135,7 +139,11 @@ def load_window(first):
     if not first:
         out += ["s_lshl_b32 s34, s16, 2", "s_add_u32 s14, s14, s34", "s_addc_u32 s15, s15, 0"]
     out += ["v_mbcnt_lo_u32_b32 v5, -1, 0", "v_mbcnt_hi_u32_b32 v5, -1, v5", "v_lshlrev_b32 v5, 2, v5",
-            f"global_load_dword {WIN}, v5, s[14:15]", "s_mov_b32 s16, 0", "s_waitcnt vmcnt(0)"]
+            f"global_load_dword {WIN}, v5, s[14:15]", "s_mov_b32 s16, 0", "s_waitcnt vmcnt(0)",
+            f"v_and_b32 v5, 0xffff, {WIN}",
+            f"v_lshl_add_u32 {WINA}, v5, 2, s12",
+            f"v_lshrrev_b32 {WINI}, 16, {WIN}",
+            "s_nop 1"]                      # VALU VGPR write -> v_readlane of it
     return out
 
 
@@ -499,14 +507,26 @@ def fix(r):
 
 
 # ---------------------------------------------------------------- handler table
+# Bool producers with fused AND / OR forms (make_handlers); ACC_UNARY leave their result at their
+# own slot d, the others (binary) at d - 1
+ACC_UNARY = ("PUSH_VARB", "PUSH_MEMB", "PUSH_MEMSB", "PUSH_PKB", "PUSH_TMP_BOOL", "NOT")
+ACC_KINDS = ACC_UNARY + ("AND", "OR", "EQ", "EQV", "EQC") + tuple(
+    p + c + sfx for p in "US" for c in ("LT", "GT", "LE", "GE") for sfx in ("", "V", "C") if not (p == "S" and sfx))
+# a compare followed by NOT becomes the complementary compare (translator peephole)
+NOT_OF = {"LT": "GE", "GE": "LT", "GT": "LE", "LE": "GT"}
+
+
 def make_handlers(variant, pfx):
     """(key, body lines) for the variant; key = (kind, d, v)."""
     G = variant == "g"
     hs = []
+    acc = []   # (key, body without the dispatch tail) of the Bool producers that get _A/_O forms
 
     def H(key, body, tail=True, reads_stack=True):
         pre = [VMWAIT] if (G and reads_stack) else []
         hs.append((key, pre + list(body) + ((NEXT_G if G else NEXT_P) if tail else [])))
+        if key[0] in ACC_KINDS and tail:
+            acc.append((key, pre + list(body)))
 
     H(("END",), [f"s_branch {pfx}_tape_end"], tail=False, reads_stack=False)
     if G:
@@ -541,6 +561,10 @@ def make_handlers(variant, pfx):
                   reads_stack=False)
             H(("PUSH_MEMSB", d), ["s_lshl_b32 s34, s17, 8", f"v_add_u32 v5, s34, {STG}", "ds_read_b32 v4, v5",
                                   "s_waitcnt lgkmcnt(0)", f"v_cmp_ne_u32_e64 {B(d)}, 0, v4", "s_nop 3"], reads_stack=False)
+            # Bool variable imm as the tile's packed lane mask (QArgs bool_masks; s[96:97] = this
+            # tile's masks): one scalar load straight into the Bool stack
+            H(("PUSH_PKB", d), ["s_lshl_b32 s34, s17, 3", f"s_load_dwordx2 {B(d)}, s[96:97], s34", "s_waitcnt lgkmcnt(0)"],
+              reads_stack=False)
         H(("PUSH_CONST", d), ["s_lshl_b32 s34, s17, 2", "s_load_dwordx8 s[64:71], s[20:21], s34", "s_waitcnt lgkmcnt(0)"]
           + [f"v_mov_b64 {S2(d, l)}, s[{64 + l}:{65 + l}]" for l in range(0, L, 2)], reads_stack=False)
         if G:
@@ -685,6 +709,20 @@ def make_handlers(variant, pfx):
                 H(("UGTV", d, v), lt_chain(vl, xa, B(a)))
                 H(("ULEV", d, v), lt_chain(vl, xa, "s[38:39]") + ["s_nop 3", f"s_not_b64 {B(a)}, s[38:39]"])
                 H(("UGEV", d, v), lt_chain(xa, vl, "s[38:39]") + ["s_nop 3", f"s_not_b64 {B(a)}, s[38:39]"])
+    # ---- Bool producers fused with the AND / OR that consumes their result (kind_A / kind_O):
+    # the translator rewrites "X; AND" into "X_A" when X leaves its result at the AND's right
+    # slot, one dispatch instead of two (AND / OR are ~30 % of the dispatches of EVM-shaped tapes)
+    for key, body in acc:
+        kind, d = key[0], key[1]
+        r = d if kind in ACC_UNARY else d - 1
+        if r < 1:
+            continue
+        for suf, ins, ins_n in (("_A", "s_and_b64", "s_andn2_b64"), ("_O", "s_or_b64", "s_orn2_b64")):
+            if kind == "NOT":   # the consumer takes the complement directly
+                fused = [f"{ins_n} {B(r - 1)}, {B(r - 1)}, {B(r)}"]
+            else:
+                fused = list(body) + (["s_nop 3"] if body[-1].startswith("v_") else []) + [f"{ins} {B(r - 1)}, {B(r - 1)}, {B(r)}"]
+            hs.append(((kind + suf,) + tuple(key[1:]), fused + (NEXT_G if G else NEXT_P)))
     subs = sub_abs_cneg(pfx) + sub_udiv32(pfx) + (sub_uf1(pfx) if G else [])
     return hs, subs
 
@@ -864,7 +902,17 @@ def frame(variant, pfx, handlers, subs):
         "s_mul_i32 s24, s97, s83",
         "s_add_u32 s25, s24, s83",
         "s_min_u32 s25, s25, s82",
-    ]
+    ] + ([
+        # G: s[96:97] = this tile's packed Bool masks, bool_masks + 8 * tile * n_bool_masks
+        "s_load_dwordx2 s[64:65], s[10:11], 0x198",
+        "s_load_dword s66, s[10:11], 0x1a0",
+        "s_waitcnt lgkmcnt(0)",
+        "s_mul_i32 s68, s96, s66",
+        "s_mul_hi_u32 s69, s96, s66",
+        "s_lshl_b64 s[68:69], s[68:69], 3",
+        "s_add_u32 s96, s64, s68",
+        "s_addc_u32 s97, s65, s69",
+    ] if G else [])
     if True:
         # preload variables: 64 limb rows (row index table at args+0x60; the host points missing
         # limbs / vars at an all-zero row)
@@ -993,9 +1041,10 @@ def frame(variant, pfx, handlers, subs):
         "s_add_u32 s24, s24, 1",
         f"s_branch {pfx}_tape_loop",
         f"{pfx}_tapes_done:",
-        # the wave's counters go to slot (tile ^ group) mod 256 of the slotted counter array
+        # the wave's counters go to slot (tile ^ last tape) mod 256 of the slotted counter array
         # (qs_launch.h kCounterSlots): 10^6 waves adding into one cache line serialise in L2
-        "s_xor_b32 s34, s96, s97",
+        "s_lshr_b32 s34, s28, 6",
+        "s_xor_b32 s34, s34, s25",
         "s_and_b32 s34, s34, 255",
         "s_lshl_b32 s34, s34, 7",
         "s_mov_b64 s[60:61], exec",
@@ -1031,16 +1080,19 @@ VARIANTS = (("p", ".Lqsa", "QSA_ASM_TEXT_P", "P"), ("g", ".Lqsg", "QSA_ASM_TEXT_
 
 def set_layout(variant):
     """Register map of the variant being generated (the body functions read these globals).
-    P and G with preloads: the map in the module docstring.  Compact G (NVG = 0): UF1 work
-    v[8:31], program window v32, stack v[40:87], T/W v[88:95] -> 96 VGPRs."""
-    global SBASE, TBASE, UBASE, WIN, NEXT_G, EEA, EEV
+    P and G with preloads: the map in the module docstring (G adds the early-exit window v66/v67
+    and the decoded program window v68/v69).  Compact G (NVG = 0): UF1 work v[8:31], program
+    window v[32:34], staging address v35, stack v[40:87], T/W v[88:95] -> 96 VGPRs."""
+    global SBASE, TBASE, UBASE, WIN, WINA, WINI, STG, NEXT_G, EEA, EEV
     if variant == "g" and NVG == 0:
-        SBASE, TBASE, UBASE, WIN = 40, 88, 8, "v32"
+        SBASE, TBASE, UBASE = 40, 88, 8
+        WIN, WINA, WINI, STG = "v32", "v33", "v34", "v35"
         EEA = EEV = None
     else:
-        SBASE, TBASE, UBASE, WIN = 72, 120, 40, "v64"
+        SBASE, TBASE, UBASE = 72, 120, 40
+        WIN, WINA, WINI, STG = "v64", "v68", "v69", "v65"
         EEA, EEV = "v67", "v66"
-    NEXT_G = [ln.replace("v64", WIN) if ln.startswith("v_readlane") else ln for ln in NEXT_G_TEMPLATE]
+    NEXT_G = next_g()
 
 
 def vgprs(variant):
@@ -1079,6 +1131,21 @@ def main():
         f.write("#ifndef MQ_QSA_TABLE_H\n#define MQ_QSA_TABLE_H\nnamespace mq {\n")
         f.write(f"constexpr int kQsaStack = {D};\nconstexpr int kQsaVars = {NV};\nconstexpr int kQsaVarsG = {NVG};\nconstexpr int kQsaSel = {L};\n")
         f.write("enum QsaKind {\n" + "".join(f"  QK_{n},\n" for n in names) + "  QK_COUNT\n};\n")
+        f.write("static const char* const kQsaKindNames[] = {" + ", ".join(f'"{n}"' for n in names) + "};\n")
+        idx = {n: i for i, n in enumerate(names)}
+
+        def table(name, fn):
+            f.write(f"static const short {name}[] = {{" + ", ".join(str(fn(n)) for n in names) + "};\n")
+        # fused AND / OR form of a kind (-1: none); where its Bool result lands (0: slot d,
+        # 1: slot d - 1, -1: not a fusable producer); the complementary compare (-1: none)
+        table("kQsaKindAndForm", lambda n: idx.get(n + "_A", -1))
+        table("kQsaKindOrForm", lambda n: idx.get(n + "_O", -1))
+        table("kQsaKindBoolRes", lambda n: (0 if n in ACC_UNARY else 1) if n in ACC_KINDS else -1)
+
+        def inv(n):
+            m = re.fullmatch(r"([US])(LT|GT|LE|GE)([VC]?)", n)
+            return idx.get(m.group(1) + NOT_OF[m.group(2)] + m.group(3), -1) if m else -1
+        table("kQsaKindNot", inv)
         f.write("struct QsaHandlerKey { int kind, d, v; };\n")
         for variant, (hs, lines, macro, suffix) in gen.items():
             f.write(f"constexpr int kQsaHandlers{suffix} = {len(hs)};\n")

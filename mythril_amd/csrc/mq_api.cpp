@@ -72,7 +72,7 @@ static int gen_kind(const CompiledTape& x) {
   if (x.L == 16) return x.keccak ? 2 : 1;
   return x.L == 32 ? 3 : 4;
 }
-static constexpr int64_t kColAsmMinNodes = 32;   // hoisted columns on qsg_kernel from this size
+static constexpr int64_t kColAsmMinNodes = 1;    // hoisted columns on qsg_kernel from this size
 
 struct mq_ctx {
   int device = 0;
@@ -88,6 +88,11 @@ struct mq_ctx {
   DevBuf best_tmp;  // scratch first-hit buffer for the synchronous API
   DevBuf scratch;   // per-wave temp slots of the HIP C++ interpreter (persistent grid)
   DevBuf rowmask;   // per-row masks applied to uploaded variable words
+  // Bool variables as packed lane masks [tile][n_bmask] (G kernel PUSH_PKB): bmask_of_var[v] =
+  // mask index of Bool variable v (-1: none); bmask_rows[j] = its variable row
+  std::vector<int32_t> bmask_of_var;
+  int32_t n_bmask = 0;
+  DevBuf bmasks, bmask_rows;
   DevBuf verdict_buf;
   // assembly interpreters (qsa.hip): handler byte offsets read back at context creation;
   // k = 0 the P kernel (preloaded variables), k = 1 the G kernel (general)
@@ -97,6 +102,7 @@ struct mq_ctx {
   uint32_t qsa_var_row[64];
   std::vector<uint8_t> qsa_data_words;
   uint32_t qsa_hbase_lo[2] = {0, 0};   // low 32 bits of each interpreter's handler base
+  std::vector<int16_t> qsa_kind_of[2];  // handler byte offset / 4 -> QsaKind (histograms)
   DevBuf qsa_args;
   // host copies of the model batch layout the QSA translation depends on
   std::vector<uint32_t> var_off_h, var_nl_h;
@@ -154,6 +160,9 @@ struct mq_tapes {
   std::vector<int> gstage;
   std::vector<uint32_t> stage_rows;
   DevBuf stage_dev;
+  // handler-kind histograms of the current translation (mq_tapes_qsa_histogram): [0] P tapes,
+  // [1] G tapes, [2] G column programs; qpairs = (kind, next kind) counts over the G tapes
+  std::vector<int64_t> qhist[3], qpairs;
   DevBuf qdescs, qprog, qargs[2];
   QArgs qargs_dev_copy[2];   // what qargs[k] currently holds on the device
   bool qargs_valid[2] = {false, false};
@@ -168,7 +177,11 @@ struct mq_tapes {
     int cq_begin = 0;   // first of the level's columns in cq_ct / cqdescs
   };
   std::vector<ColumnLevel> clevels;
-  std::vector<int32_t> col_var, col_width;
+  std::vector<int32_t> col_var, col_width, col_level;
+  // per column level: mask indices of its Bool columns, repacked after the level ran
+  std::vector<std::vector<int32_t>> lvl_bmask_h;
+  std::vector<DevBuf> lvl_bmask;
+  uint64_t bmask_gen = ~0ull;
   DevBuf cdescs, cprog, cconsts;
   std::vector<CompiledTape> cq_ct;   // the G-eligible columns, level by level
   std::vector<int32_t> cq_var;
@@ -310,14 +323,17 @@ static int qsa_init(mq_ctx* c) {
     HIPCHK(hipMemcpyAsync(c->qsa_off[k].data(), table.p, sizeof(uint32_t) * (nh + 2), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->qsa_hbase_lo[k] = c->qsa_off[k][nh];
+    c->qsa_kind_of[k].assign(1 << 16, -1);
+    for (int h = 0; h < nh; h++)
+      if (c->qsa_off[k][h] < (1u << 18)) c->qsa_kind_of[k][c->qsa_off[k][h] >> 2] = (int16_t)keys[h].kind;
     uint32_t max_off = 0;
     for (int h = 0; h < nh; h++) {
       ok = ok && c->qsa_off[k][h] != 0xFFFFFFFFu && (c->qsa_off[k][h] & 3) == 0 && c->qsa_off[k][h] < (1u << 18);
       max_off = std::max(max_off, c->qsa_off[k][h]);
     }
-    // P program entries hold the low 32 bits of absolute handler addresses: they must share
-    // the high half (the kernel keeps it in s19)
-    if (k == 0) ok = ok && (uint64_t)c->qsa_hbase_lo[k] + max_off < (1ull << 32);
+    // P program entries and G's decoded program window hold the low 32 bits of absolute handler
+    // addresses: they must share the high half (the kernels keep it in s19)
+    ok = ok && (uint64_t)c->qsa_hbase_lo[k] + max_off < (1ull << 32);
     c->qsa_off[k].resize(nh);
   }
   // G handler word index -> inline data words that follow it (PUSH_CONSTW)
@@ -506,6 +522,23 @@ static int upload_one(mq_ctx* c, const mq_model_batch* mb) {
       if (v < mb->n_vars && mb->var_width[v] <= 256 && (uint32_t)l < vnl[v]) row = voff[v] + l;
       c->qsa_var_row[8 * v + l] = row;
     }
+  // Bool variables as lane masks (at most 65535 of them; the others are read as rows)
+  {
+    std::vector<uint32_t> brows;
+    c->bmask_of_var.assign(mb->n_vars, -1);
+    for (int v = 0; v < mb->n_vars && brows.size() < 65535; v++)
+      if (mb->var_width[v] == 0) {
+        c->bmask_of_var[v] = (int32_t)brows.size();
+        brows.push_back(voff[v]);
+      }
+    c->n_bmask = (int32_t)brows.size();
+    const int64_t tiles = (M + 63) / 64;
+    HIPCHK(c->bmasks.ensure(std::max<size_t>(8, sizeof(uint64_t) * (size_t)tiles * brows.size())));
+    if (brows.empty()) brows.push_back(0);
+    HIPCHK(c->bmask_rows.upload(brows.data(), brows.size(), c->stream));
+    HIPCHK(launch_pack_bool(c->vars.as<uint32_t>(), c->bmasks.as<uint64_t>(), c->bmask_rows.as<uint32_t>(), nullptr,
+                            c->n_bmask, c->n_bmask, M, c->stream));
+  }
   c->var_off_h.assign(voff.begin(), voff.begin() + mb->n_vars);
   c->var_nl_h.assign(vnl.begin(), vnl.begin() + mb->n_vars);
   c->funcs_h.assign(mb->funcs, mb->funcs + F);
@@ -612,6 +645,25 @@ int mq_models_upload(mq_ctx* c, const mq_model_batch* mb) {
   return MQ_OK;
 }
 
+// Count the handler kinds of one translated program (k = 0: P two-word entries; 1: G words,
+// inline constant words skipped) into hist[QK_COUNT] and, if given, kind bigrams into pairs.
+static void qsa_count(const mq_ctx* c, int k, const std::vector<uint32_t>& tr, std::vector<int64_t>& hist,
+                      std::vector<int64_t>* pairs) {
+  if (hist.size() != (size_t)QK_COUNT) hist.assign(QK_COUNT, 0);
+  if (pairs && pairs->size() != (size_t)QK_COUNT * QK_COUNT) pairs->assign((size_t)QK_COUNT * QK_COUNT, 0);
+  int prev = -1;
+  for (size_t i = 0; i < tr.size();) {
+    const uint32_t key = k == 0 ? ((tr[i] - c->qsa_hbase_lo[0]) >> 2) & 0xFFFFu : tr[i] & 0xFFFFu;
+    const int kind = c->qsa_kind_of[k].empty() ? -1 : c->qsa_kind_of[k][key];
+    i += k == 0 ? 2 : 1;
+    if (kind < 0) continue;
+    hist[kind]++;
+    if (pairs && prev >= 0 && kind != QK_REFILL) (*pairs)[(size_t)prev * QK_COUNT + kind]++;
+    if (kind != QK_REFILL) prev = kind;
+    if (k == 1) i += c->qsa_data_words[key];
+  }
+}
+
 // Translate a compiled stack program into QSA threaded code for kernel k (0 = P, 1 = G).
 // models == false: structural check only (upload time: variable rows and function tables are
 // not known yet, any variable / lookup is assumed expressible).  extra: the tape's derived
@@ -629,10 +681,19 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
   if (x.L != 8 || x.depth > kQsaStack) return false;
   const bool P = k == 0;
   const size_t wpi = P ? 2 : 1;   // program words per interpreter instruction
+  // the last handler word emitted (fusions below rewrite it while it is still the last word)
+  int last_kind = -1, last_d = 0, last_v = -1;
+  uint32_t last_imm = 0;
+  size_t last_pos = 0;
   auto word = [&](int kind, int d, int v, uint32_t imm) -> bool {
     if (d < 0 || d >= kQsaStack || v < -1 || v >= kQsaSel || imm > 0xFFFFu) return false;
     const int h = c->qsa_index[k][kind][d][v + 1];
     if (h < 0) return false;
+    last_kind = kind;
+    last_d = d;
+    last_v = v;
+    last_imm = imm;
+    last_pos = out.size();
     if (P) {   // two-word entry: absolute handler address (low half), immediate
       out.push_back(c->qsa_hbase_lo[0] + c->qsa_off[0][h]);
       out.push_back(imm);
@@ -662,6 +723,28 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
     if ((size_t)off + 8 > x.consts.size()) return false;
     for (int l = 0; l < 8; l++) v[l] = x.consts[off + l];
     return true;
+  };
+  // slot where the last word left a Bool result, or -1 (it is not a fusable Bool producer, or
+  // something was emitted after it)
+  auto last_bool_slot = [&]() -> int {
+    if (last_kind < 0 || out.size() != last_pos + wpi || kQsaKindBoolRes[last_kind] < 0) return -1;
+    return kQsaKindBoolRes[last_kind] == 0 ? last_d : last_d - 1;
+  };
+  // AND / OR at slot d whose right operand the last word just produced: that word's fused form
+  auto fuse_acc = [&](int d, bool is_and) -> bool {
+    if (last_bool_slot() != d) return false;
+    const int fk = is_and ? kQsaKindAndForm[last_kind] : kQsaKindOrForm[last_kind];
+    if (fk < 0 || c->qsa_index[k][fk][last_d][last_v + 1] < 0) return false;
+    out.resize(last_pos);
+    return word(fk, last_d, last_v, last_imm);
+  };
+  // NOT of a compare the last word just made: the complementary compare
+  auto fuse_not = [&](int d) -> bool {
+    if (last_bool_slot() != d || kQsaKindNot[last_kind] < 0) return false;
+    const int nk = kQsaKindNot[last_kind];
+    if (c->qsa_index[k][nk][last_d][last_v + 1] < 0) return false;
+    out.resize(last_pos);
+    return word(nk, last_d, last_v, last_imm);
   };
   uint32_t prev_op = G_END, prev_d = 0, prev_imm = 0;
   size_t prev_out = 0;
@@ -718,6 +801,9 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
           pushed_pre = ps;
         } else if (!models) {
           ok = word(b ? QK_PUSH_MEMB : QK_PUSH_MEM, d, b ? -1 : 7, 0);
+        } else if (b && imm < c->bmask_of_var.size() && c->bmask_of_var[imm] >= 0) {
+          // the tile's lane mask, one scalar load (qs_pack_bool)
+          ok = word(QK_PUSH_PKB, d, -1, (uint32_t)c->bmask_of_var[imm]);
         } else if (gstage && imm < gstage->size() && (*gstage)[imm] >= 0 && c->var_nl_h[imm] <= 8) {
           // a row staged in LDS by the workgroup (gen_qsa.py stage_rows)
           ok = word(b ? QK_PUSH_MEMSB : QK_PUSH_MEMS, d, b ? -1 : (int)c->var_nl_h[imm] - 1, (uint32_t)(*gstage)[imm]);
@@ -751,9 +837,9 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
       case G_STORE_TMP: ok = d == 0 && word(QK_STORE_TMP, 0, -1, imm); break;
       case G_STORE_TMP_B: ok = d == 0 && word(QK_STORE_TMP_BOOL, 0, -1, imm); break;
       case G_PUSH_BOOL: ok = word(QK_PUSH_BOOL, d, -1, imm); break;
-      case G_NOT: ok = word(QK_NOT, d, -1, 0); break;
-      case G_AND: ok = word(QK_AND, d, -1, 0); break;
-      case G_OR: ok = word(QK_OR, d, -1, 0); break;
+      case G_NOT: ok = fuse_not(d) || word(QK_NOT, d, -1, 0); break;
+      case G_AND: ok = fuse_acc(d, true) || word(QK_AND, d, -1, 0); break;
+      case G_OR: ok = fuse_acc(d, false) || word(QK_OR, d, -1, 0); break;
       case G_XOR: ok = word(QK_XOR, d, -1, 0); break;
       case G_IFF: ok = word(QK_IFF, d, -1, 0); break;
       case G_IMPLIES: ok = word(QK_IMPLIES, d, -1, 0); break;
@@ -1166,6 +1252,8 @@ static int set_columns_one(mq_tapes* T, const mq_tape_batch* progs, const int32_
   HIPCHK(hipSetDevice(c->device));
   T->clevels.clear();
   T->col_var.assign(var_index, var_index + n_columns);
+  T->col_level.assign(level, level + n_columns);
+  T->bmask_gen = ~0ull;
   T->col_width.assign(n_columns, 0);
   if (n_columns == 0) return MQ_OK;
   CompileLimits lim;
@@ -1187,10 +1275,10 @@ static int set_columns_one(mq_tapes* T, const mq_tape_batch* progs, const int32_
   }
   std::vector<uint32_t> prog, consts;
   std::vector<GDesc> descs;
-  // G assembly eligibility is structural here, as for tapes (mq_tapes_upload).  Short column
-  // programs stay on the HIP C++ column kernel: per program, qsg_kernel pays a descriptor load
-  // and a dependent program-window load, which a few-node column does not amortise
-  // (profiles/r01p_*: C3's 5.7-node columns took 45 ms on qsg_kernel vs 24 ms on the C++ kernel).
+  // G assembly eligibility is structural here, as for tapes (mq_tapes_upload).  Columns shorter
+  // than kColAsmMinNodes stay on the HIP C++ column kernel.  With slotted counters and the
+  // decoded program window every column size runs faster on qsg_kernel (profiles/r02n_*: C3
+  // 90.5 -> 84.4 ms with all columns there; before, r01p_*, short columns lost 45 vs 24 ms).
   // MQ_G_COL_MIN_NODES overrides the threshold.
   int64_t min_nodes = kColAsmMinNodes;
   if (const char* e = std::getenv("MQ_G_COL_MIN_NODES")) min_nodes = std::atol(e);
@@ -1341,7 +1429,9 @@ static std::vector<int64_t> count_pushes(const mq_ctx* c, const std::vector<Comp
     const auto& pr = cts[i].prog;
     for (size_t pc = 0; pc < pr.size(); pc++) {
       const uint32_t op = pr[pc] & 0xFFu, imm = pr[pc] >> 12;
-      if ((op == G_PUSH_VAR || op == G_PUSH_VAR_B) && imm < pushes.size() && c->var_nl_h[imm] <= 8) pushes[imm]++;
+      if ((op == G_PUSH_VAR || (op == G_PUSH_VAR_B && !(imm < c->bmask_of_var.size() && c->bmask_of_var[imm] >= 0))) &&
+          imm < pushes.size() && c->var_nl_h[imm] <= 8)
+        pushes[imm]++;
       if (op == G_EXTRACT || op == G_CONCAT || op == G_SEXT || op == G_UF1 || op == G_UF2) pc++;
     }
   }
@@ -1393,7 +1483,10 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
     const auto& pr = T->qct[i].prog;
     for (size_t pc = 0; pc < pr.size(); pc++) {
       const uint32_t op = pr[pc] & 0xFFu, imm = pr[pc] >> 12;
-      if ((op == G_PUSH_VAR || op == G_PUSH_VAR_B) && imm < pushes.size() && c->var_nl_h[imm] <= 8) pushes[imm]++;
+      // (Bool variables with a lane mask are neither preloaded nor staged: PUSH_PKB)
+      if ((op == G_PUSH_VAR || (op == G_PUSH_VAR_B && !(imm < c->bmask_of_var.size() && c->bmask_of_var[imm] >= 0))) &&
+          imm < pushes.size() && c->var_nl_h[imm] <= 8)
+        pushes[imm]++;
       if (op == G_EXTRACT || op == G_CONCAT || op == G_SEXT || op == G_UF1 || op == G_UF2) pc++;
     }
   }
@@ -1414,6 +1507,9 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
   for (size_t i = 0; i < T->qct.size(); i++)
     if (!on_p[i]) g_temps = std::max(g_temps, T->qct[i].n_temps);
   plan_stage(c, pushes, &T->gpre, g_temps, T->gstage, T->stage_rows);
+  T->qhist[0].assign(QK_COUNT, 0);
+  T->qhist[1].assign(QK_COUNT, 0);
+  T->qpairs.assign((size_t)QK_COUNT * QK_COUNT, 0);
   for (size_t i = 0; i < T->qct.size(); i++) {
     int k = 0;
     if (!on_p[i] || !qsa_translate(c, 0, true, T->qct[i], &tr, &extra)) {
@@ -1421,6 +1517,7 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
       if (!qsa_translate(c, 1, true, T->qct[i], &tr, &extra, &T->gpre, &T->gstage)) return MQ_OK;
       qsa_window_layout(c, tr);
     }
+    qsa_count(c, k, tr, T->qhist[k], k == 1 ? &T->qpairs : nullptr);
     GDesc d = T->qbase[i];
     d.prog_off = (uint32_t)words[k].size();
     d.prog_len = (uint32_t)tr.size();
@@ -1485,6 +1582,7 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
     const CompiledTape& x = T->cq_ct[i];
     if (!qsa_translate(c, 1, true, x, &tr, &extra, nullptr, &T->cq_stage)) return MQ_OK;
     qsa_window_layout(c, tr);
+    qsa_count(c, 1, tr, T->qhist[2], nullptr);
     const int v = T->cq_var[i];
     GDesc d{};
     d.prog_off = (uint32_t)prog.size();
@@ -1591,6 +1689,22 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     T->cq_gen = ~0ull;
   }
   const uint32_t zero_row = (uint32_t)(c->var_off_h.empty() ? 0 : c->var_off_h.back() + c->var_nl_h.back());
+  if (T->bmask_gen != c->models_gen) {
+    // the mask indices of each level's Bool columns under this model batch
+    T->lvl_bmask_h.assign(T->clevels.size(), {});
+    for (size_t i = 0; i < T->col_var.size(); i++) {
+      const int v = T->col_var[i];
+      if (T->col_width[i] == 0 && v < (int)c->bmask_of_var.size() && c->bmask_of_var[v] >= 0 &&
+          T->col_level[i] < (int)T->clevels.size())
+        T->lvl_bmask_h[T->col_level[i]].push_back(c->bmask_of_var[v]);
+    }
+    T->lvl_bmask.resize(T->clevels.size());
+    for (size_t li = 0; li < T->clevels.size(); li++)
+      if (!T->lvl_bmask_h[li].empty())
+        HIPCHK(T->lvl_bmask[li].upload(T->lvl_bmask_h[li].data(), T->lvl_bmask_h[li].size(), st));
+    HIPCHK(hipStreamSynchronize(st));
+    T->bmask_gen = c->models_gen;
+  }
   for (size_t li = 0; li < T->clevels.size(); li++) {
     const auto& lv = T->clevels[li];
     const mq_tapes::Variant v8 = use_cq ? cut_front(lv.v[0], lv.v8q) : lv.v[0];
@@ -1622,6 +1736,8 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       q.entry_words = c->entry_words.p;
       q.else_words = c->else_words.p;
       q.n_funcs = (uint32_t)c->n_funcs;
+      q.bool_masks = c->bmasks.as<uint64_t>();
+      q.n_bool_masks = (uint32_t)c->n_bmask;
       QArgs* dq = T->cqargs.as<QArgs>() + li;
       if (std::memcmp(&T->cqargs_host[li], &q, sizeof(QArgs)) != 0) {
         HIPCHK(hipMemcpyAsync(dq, &q, sizeof(QArgs), hipMemcpyHostToDevice, st));
@@ -1649,6 +1765,12 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       }
       HIPCHK(start_timer());
       HIPCHK(launch_columns(a, v->L, v->keccak, st));
+    }
+    // the level's Bool columns as lane masks, for the levels and tapes after it
+    if (!T->lvl_bmask_h[li].empty()) {
+      HIPCHK(start_timer());
+      HIPCHK(launch_pack_bool(c->vars.as<uint32_t>(), c->bmasks.as<uint64_t>(), c->bmask_rows.as<uint32_t>(),
+                              T->lvl_bmask[li].as<int32_t>(), (int)T->lvl_bmask_h[li].size(), c->n_bmask, c->M, st));
     }
   }
   for (int k = 0; use_qsa && k < 2; k++) {
@@ -1686,6 +1808,8 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     q.entry_words = c->entry_words.p;
     q.else_words = c->else_words.p;
     q.n_funcs = (uint32_t)c->n_funcs;
+    q.bool_masks = c->bmasks.as<uint64_t>();
+    q.n_bool_masks = (uint32_t)c->n_bmask;
     // the argument block only changes with the output buffer / mode / models: re-upload then
     if (!T->qargs_valid[k] || std::memcmp(&T->qargs_dev_copy[k], &q, sizeof(QArgs)) != 0) {
       HIPCHK(hipMemcpyAsync(T->qargs[k].p, &q, sizeof(QArgs), hipMemcpyHostToDevice, st));
@@ -1970,6 +2094,24 @@ int mq_tapes_qsa_split(mq_tapes* T, int32_t* n_p, int32_t* n_g, int32_t* live) {
   if (n_g) *n_g = T->qsa_live ? T->q_count[1] : 0;
   if (live) *live = T->qsa_live ? 1 : 0;
   return MQ_OK;
+}
+
+int mq_tapes_qsa_histogram(mq_tapes* T, int32_t which, int64_t* hist_out, int32_t cap, int64_t* pairs_out,
+                           int32_t* n_kinds_out) {
+  if (!T || which < 0 || which > 2 || cap < 0) return MQ_ERR_ARG;
+  if (n_kinds_out) *n_kinds_out = QK_COUNT;
+  const int n = std::min<int>(cap, QK_COUNT);
+  const auto& h = T->qhist[which];
+  for (int i = 0; i < n; i++) hist_out[i] = h.empty() ? 0 : h[i];
+  if (pairs_out)
+    for (int i = 0; i < n; i++)
+      for (int j = 0; j < n; j++)
+        pairs_out[(size_t)i * n + j] = (which == 1 && !T->qpairs.empty()) ? T->qpairs[(size_t)i * QK_COUNT + j] : 0;
+  return MQ_OK;
+}
+
+const char* mq_qsa_kind_name(int32_t kind) {
+  return (kind >= 0 && kind < QK_COUNT) ? kQsaKindNames[kind] : nullptr;
 }
 
 int mq_tapes_column_split(mq_tapes* T, int32_t* n_asm, int32_t* live) {

@@ -932,6 +932,29 @@ hipError_t launch_mask_rows(uint32_t* vars, const uint32_t* rowmask, int64_t row
   return hipGetLastError();
 }
 
+// Bool variable rows as 64-bit lane masks per 64-model tile (the G interpreter's PUSH_PKB reads a
+// tile's mask with one scalar load).  One wave per (tile, row).
+__global__ __launch_bounds__(256) void qs_pack_bool(const uint32_t* vars, uint64_t* masks, const uint32_t* rows,
+                                                    const int32_t* list, int n_masks, int64_t M) {
+  const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tile * 64 >= M) return;   // wave-uniform
+  const int j = list ? list[blockIdx.y] : (int)blockIdx.y;
+  const int64_t m = tile * 64 + (threadIdx.x & 63);
+  const bool bit = m < M && vars[(int64_t)rows[j] * M + m] != 0u;
+  const unsigned long long mask = __ballot(bit);
+  if ((threadIdx.x & 63) == 0) masks[tile * n_masks + j] = mask;
+}
+
+hipError_t launch_pack_bool(const uint32_t* vars, uint64_t* masks, const uint32_t* rows, const int32_t* list, int n,
+                            int n_masks, int64_t M, hipStream_t st) {
+  const int64_t tiles = (M + 63) / 64;
+  if (n <= 0 || tiles <= 0) return hipSuccess;
+  if (n > 65535) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(qs_pack_bool, dim3((unsigned)((tiles + 3) / 4), (unsigned)n), dim3(256), 0, st, vars, masks, rows,
+                     list, n_masks, M);
+  return hipGetLastError();
+}
+
 __global__ void qs_init_best(int32_t* best, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) best[i] = 0x7FFFFFFF;

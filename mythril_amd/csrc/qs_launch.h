@@ -86,6 +86,9 @@ struct QArgs {
   uint32_t stage_base;           // 0x188 G: LDS byte offset of the staged rows
   uint32_t pad2;                 // 0x18c
   const uint32_t* stage_rows;    // 0x190 G: global row of each staged slot
+  const uint64_t* bool_masks;    // 0x198 G: packed Bool rows, [tile][n_bool_masks] lane masks
+  uint32_t n_bool_masks;         // 0x1a0
+  uint32_t pad3;                 // 0x1a4
 };
 static_assert(sizeof(void*) == 8, "64-bit");
 static_assert(__builtin_offsetof(QArgs, M) == 0x40, "QArgs layout");
@@ -94,6 +97,8 @@ static_assert(__builtin_offsetof(QArgs, funcs) == 0x160, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, n_funcs) == 0x180, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, n_stage) == 0x184, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, stage_rows) == 0x190, "QArgs layout");
+static_assert(__builtin_offsetof(QArgs, bool_masks) == 0x198, "QArgs layout");
+static_assert(__builtin_offsetof(QArgs, n_bool_masks) == 0x1a0, "QArgs layout");
 
 // variant 0 = P (preloaded variables, qsa_kernel), 1 = G (general, qsg_kernel)
 hipError_t launch_qsa(int variant, const QArgs* d_args, unsigned gx, unsigned gy, size_t lds, hipStream_t st);
@@ -101,6 +106,10 @@ hipError_t launch_qs(const KArgs& a, int L, bool keccak, bool verdict, hipStream
 hipError_t launch_columns(const KArgs& a, int L, bool keccak, hipStream_t st);
 hipError_t launch_init_best(int32_t* best, int n, hipStream_t st);
 hipError_t launch_mask_rows(uint32_t* vars, const uint32_t* rowmask, int64_t rows, int64_t M, hipStream_t st);
+// masks[tile * n_masks + j] = lane mask of (vars[rows[j]][64 * tile + i] != 0), for j in list[0..n)
+// (list == nullptr: j = 0..n-1)
+hipError_t launch_pack_bool(const uint32_t* vars, uint64_t* masks, const uint32_t* rows, const int32_t* list, int n,
+                            int n_masks, int64_t M, hipStream_t st);
 hipError_t launch_finalize_best(int32_t* best, const uint8_t* unsupported, int n, hipStream_t st);
 hipError_t launch_keccak(const uint8_t* data, const int64_t* offsets, int n, uint8_t* out, hipStream_t st);
 

@@ -61,6 +61,10 @@ def load_library(path: str = LIB_PATH):
         L.mq_tapes_info.argtypes = [P] + [C.POINTER(C.c_int32)] * 3
         L.mq_tapes_qsa_split.argtypes = [P] + [C.POINTER(C.c_int32)] * 3
         L.mq_tapes_column_split.argtypes = [P] + [C.POINTER(C.c_int32)] * 2
+        L.mq_tapes_qsa_histogram.argtypes = [P, C.c_int32, C.POINTER(C.c_int64), C.c_int32, C.POINTER(C.c_int64),
+                                             C.POINTER(C.c_int32)]
+        L.mq_qsa_kind_name.argtypes = [C.c_int32]
+        L.mq_qsa_kind_name.restype = C.c_char_p
         L.mq_eval_verdicts.argtypes = [P, C.POINTER(MqTapeBatch), C.POINTER(C.c_uint8), C.POINTER(C.c_int32)]
         L.mq_eval_tapes_verdicts.argtypes = [P, P, C.POINTER(C.c_uint8), C.POINTER(C.c_int32)]
         L.mq_tapes_set_columns.argtypes = [P, C.POINTER(MqTapeBatch), C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_int32]
@@ -218,6 +222,26 @@ class CompiledTapes:
         a, b = C.c_int32(), C.c_int32()
         _check(self.ev.lib.mq_tapes_column_split(self.handle, C.byref(a), C.byref(b)), "mq_tapes_column_split")
         return a.value, bool(b.value)
+
+    def handler_histogram(self, which: int = 1, pairs: bool = False):
+        """After a launch: {handler kind: dispatches per (tape, model) pair, summed over tapes} of
+        the assembly translation (which = 0 P tapes, 1 G tapes, 2 G column programs); with
+        pairs, also {(kind, next kind): count} over the G tapes.  Diagnostic."""
+        lib = self.ev.lib
+        n = C.c_int32()
+        _check(lib.mq_tapes_qsa_histogram(self.handle, which, None, 0, None, C.byref(n)), "mq_tapes_qsa_histogram")
+        k = n.value
+        hist = np.zeros(k, np.int64)
+        pr = np.zeros(k * k, np.int64) if pairs else None
+        _check(lib.mq_tapes_qsa_histogram(self.handle, which, hist.ctypes.data_as(C.POINTER(C.c_int64)), k,
+                                          pr.ctypes.data_as(C.POINTER(C.c_int64)) if pairs else None, C.byref(n)),
+               "mq_tapes_qsa_histogram")
+        names = [lib.mq_qsa_kind_name(i).decode() for i in range(k)]
+        h = {names[i]: int(hist[i]) for i in range(k) if hist[i]}
+        if not pairs:
+            return h
+        pr = pr.reshape(k, k)
+        return h, {(names[i], names[j]): int(pr[i, j]) for i, j in zip(*np.nonzero(pr))}
 
     def free(self) -> None:
         if self.handle:

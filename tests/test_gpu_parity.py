@@ -458,3 +458,81 @@ def test_g_kernel_lds_staged_rows_match_oracle(evaluator, monkeypatch, stage_kb)
     assert (ref == exp).all() and (fh == ref).all()
     v, _ = evaluator.verdicts(ct)
     assert (v == cref.verdicts(tb, mb)).all()
+
+
+# ---------------------------------------------------------------- G kernel: packed Bool masks, fused Bool handlers
+def _bool_heavy_workload(n_tapes, M, seed):
+    """Conjunctions / disjunctions of Bool variables (not preloaded: 24 of them) and compares
+    with constants: PUSH_PKB, PUSH_*_A / _O and the NOT-of-compare peephole on the G kernel."""
+    from mythril_amd.models import ModelBatch
+    from mythril_amd.tape import Tape, TapeBatch
+    rng = np.random.default_rng(seed)
+    NB, NW = 24, 12
+    words = np.concatenate([rng.integers(0, 1 << 32, (8 * NW, M), dtype=np.uint64).astype(np.uint32),
+                            (rng.random((NB, M)) < 0.8).astype(np.uint32) * rng.integers(1, 1 << 32, (NB, M), dtype=np.uint64).astype(np.uint32)])
+    mb = ModelBatch([256] * NW + [0] * NB, words)
+    tapes = []
+    for t in range(n_tapes):
+        tp = Tape()
+        leaves = []
+        for i in range(int(rng.integers(3, 12))):
+            k = int(rng.integers(0, 6))
+            v = int(rng.integers(0, NW))
+            if k <= 1:
+                leaves.append(tp.var(NW + int(rng.integers(0, NB)), 0))
+            elif k == 2:
+                leaves.append(tp.not_(tp.var(NW + int(rng.integers(0, NB)), 0)))
+            elif k == 3:
+                leaves.append(tp.not_(tp.ult(tp.var(v, 256), tp.const(int(rng.integers(0, 1 << 62)) << 190, 256))))
+            elif k == 4:
+                leaves.append(tp.or_(tp.var(NW + int(rng.integers(0, NB)), 0),
+                                     tp.eq(tp.var(v, 256), tp.const(int(words[8 * v, t % M]), 256))))
+            else:
+                leaves.append(tp.not_(tp.eq(tp.var(v, 256), tp.const(12345, 256))))
+        tapes.append(tp.finish(tp.and_(*leaves)))
+    return TapeBatch(tapes), mb
+
+
+@pytest.mark.parametrize("M", [1000, 4096])
+def test_g_kernel_bool_masks_and_fused_handlers_match_oracle(evaluator, M):
+    tb, mb = _bool_heavy_workload(120, M, seed=M)
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    fh = evaluator.first_hit(ct)
+    n_p, n_g, live = ct.asm_split()
+    assert live and n_g > 0, (n_p, n_g)
+    hist = ct.handler_histogram(1)
+    assert hist.get("PUSH_PKB", 0) + hist.get("PUSH_PKB_A", 0) + hist.get("PUSH_PKB_O", 0) > 0, hist
+    assert any(k.endswith("_A") for k in hist), hist
+    ref, _ = cref.first_hit(tb, mb)
+    assert (fh == ref).all(), np.flatnonzero(fh != ref)[:10]
+    v, _ = evaluator.verdicts(ct)
+    assert (v == cref.verdicts(tb, mb)).all()
+
+
+def test_bool_columns_repacked_per_level(evaluator, monkeypatch):
+    """Hoisted Bool sub-terms at two nesting levels: level-1 columns and the tapes read the
+    level-0 Bool columns as packed lane masks, repacked after each level ran."""
+    monkeypatch.setenv("MQ_G_COL_MIN_NODES", "0")
+    from mythril_amd import smt as S
+    from mythril_amd.lower import lower_batch, serialize_models
+    from mythril_amd.smt_model import Model
+    x, y, z = (S.BitVecSym(n, 256) for n in "xyz")
+    c1 = S.ULT(x * y + z, S.BitVecVal(1 << 255, 256))
+    c2 = S.And(c1, S.ULT(x, y + z), S.Not(S.ULT(z ^ x, y)))
+    roots = [S.And(c2, S.ULT(x + S.BitVecVal(i, 256), y)) for i in range(3)] + \
+            [S.Or(c1, S.Not(c2), x == S.BitVecVal(i, 256)) for i in range(3)] + [S.And(c1, S.Not(c2))]
+    rng = np.random.default_rng(11)
+    models = [Model({n: int.from_bytes(rng.bytes(32), "little") >> int(rng.integers(0, 256)) for n in "xyz"})
+              for _ in range(777)]
+    tb, syms, _ = lower_batch(roots, hoist=True, hoist_min_nodes=2)
+    assert tb.columns.n >= 2 and tb.columns.level.max() >= 1
+    tb2, syms2, _ = lower_batch(roots)
+    evaluator.upload_models(serialize_models(models, syms))
+    ct = evaluator.compile(tb)
+    v, fh = evaluator.verdicts(ct)
+    ref = cref.verdicts(tb2, serialize_models(models, syms2))
+    assert (v == ref).all()
+    fh2 = evaluator.first_hit(ct)
+    ref_fh, _ = cref.first_hit(tb2, serialize_models(models, syms2))
+    assert (fh2 == ref_fh).all()
