@@ -183,6 +183,64 @@ def eq_body(d, bl=None):
     return out
 
 
+# inline-constant classes of the G compare-with-constant handlers: 0 = the 16-bit immediate
+# (no data words), 1 = two data words (limbs 0-1), 2 = eight data words
+KCLS = (0, 2, 8)
+
+
+def const_words(nw):
+    """Read the nw inline data words after the handler word into s64.. (s16 past them)."""
+    out = []
+    for i in range(nw):
+        out += [f"v_readlane_b32 s{64 + i}, {WIN}, s16", "s_add_u32 s16, s16, 1"]
+    return out + (["s_nop 1"] if nw else [])     # VALU SGPR write -> VALU read
+
+
+def kconst(l, nw):
+    """Operand for limb l of an inline constant of class nw (immediate in s17 when nw == 0)."""
+    if nw == 0:
+        return "s17" if l == 0 else "0"
+    return f"s{64 + l}" if l < nw else "0"
+
+
+def eq_const_body(xl, nw, dst):
+    """dst = (value with limbs xl(l) == inline constant of class nw): one compare per constant
+    limb, the limbs above it OR-reduced in VALU and compared with 0."""
+    n = max(nw, 1)
+    regs = ["s[34:35]", "s[36:37]", "s[38:39]", "s[60:61]", "s[64:65]", "s[66:67]", "s[68:69]", "s[70:71]"]
+    # (the constant sits in s64.. for nw > 0: its compares go to the low pairs; upper limbs below)
+    out = []
+    for l in range(n):
+        out.append(f"v_cmp_eq_u32_e64 {regs[l] if nw < 8 else regs[l]}, {xl(l)}, {kconst(l, nw)}")
+    if n < L:
+        up = [xl(l) for l in range(n, L)]
+        acc = "v4"
+        out.append(f"v_or3_b32 v4, {up[0]}, {up[1]}, {up[2]}" if len(up) >= 3 else f"v_or_b32 v4, {up[0]}, {up[1]}")
+        rest = up[3:] if len(up) >= 3 else up[2:]
+        while rest:
+            if len(rest) >= 2:
+                out.append(f"v_or3_b32 v4, v4, {rest[0]}, {rest[1]}")
+                rest = rest[2:]
+            else:
+                out.append(f"v_or_b32 v4, v4, {rest[0]}")
+                rest = []
+        out.append(f"v_cmp_eq_u32_e64 {regs[n]}, 0, {acc}")
+        n += 1
+    out.append("s_nop 3")
+    # AND tree over the n masks
+    live = regs[:n]
+    while len(live) > 1:
+        nxt = []
+        for i in range(0, len(live) - 1, 2):
+            out.append(f"s_and_b64 {live[i]}, {live[i]}, {live[i + 1]}")
+            nxt.append(live[i])
+        if len(live) % 2:
+            nxt.append(live[-1])
+        live = nxt
+    out.append(f"s_mov_b64 {dst}, {live[0]}")
+    return out
+
+
 def lt_chain(x, y, dst):
     """dst mask = (x < y) unsigned over 8 limbs; x, y are slot numbers or limb -> register
     functions; borrow chain with hazard nops."""
@@ -510,8 +568,10 @@ def fix(r):
 # Bool producers with fused AND / OR forms (make_handlers); ACC_UNARY leave their result at their
 # own slot d, the others (binary) at d - 1
 ACC_UNARY = ("PUSH_VARB", "PUSH_MEMB", "PUSH_MEMSB", "PUSH_PKB", "PUSH_TMP_BOOL", "NOT")
-ACC_KINDS = ACC_UNARY + ("AND", "OR", "EQ", "EQV", "EQC") + tuple(
-    p + c + sfx for p in "US" for c in ("LT", "GT", "LE", "GE") for sfx in ("", "V", "C") if not (p == "S" and sfx))
+ACC_KINDS = ACC_UNARY + ("AND", "OR", "EQ", "EQV", "EQC", "EQK", "EQVK") + tuple(
+    p + c + sfx for p in "US" for c in ("LT", "GT", "LE", "GE") for sfx in ("", "V", "C", "K") if not (p == "S" and sfx))
+# binary kinds whose result lands at their own slot x (the constant is not on the stack)
+ACC_AT_X = ("EQK", "EQVK", "ULTK", "UGTK", "ULEK", "UGEK")
 # a compare followed by NOT becomes the complementary compare (translator peephole)
 NOT_OF = {"LT": "GE", "GE": "LT", "GT": "LE", "LE": "GT"}
 
@@ -687,6 +747,24 @@ def make_handlers(variant, pfx):
             H(("UGTC", d), ld + tl + lt_chain(T, xa, B(a)))
             H(("ULEC", d), ld + tl + lt_chain(T, xa, "s[38:39]") + ["s_nop 3", f"s_not_b64 {B(a)}, s[38:39]"])
             H(("UGEC", d), ld + tl + lt_chain(xa, T, "s[38:39]") + ["s_nop 3", f"s_not_b64 {B(a)}, s[38:39]"])
+    # ---- G: compares against a constant carried inline (the translator drops the constant's
+    # push): EQK / ULTK / UGTK / ULEK / UGEK (x, cls) compare slot x with it, EQVK (x, 2v + c)
+    # compares preloaded variable v with it; the result lands in B(x).  cls: KCLS
+    if G:
+        for x in range(D - 1):
+            for cls, nw in enumerate(KCLS):
+                kread = const_words(nw)
+                H(("EQK", x, cls), kread + eq_const_body(lambda l, _x=x: S(_x, l), nw, B(x)))
+                tl = [f"v_mov_b32 {T(l)}, {kconst(l, nw)}" for l in range(L)]
+                xa = (lambda l, _x=x: S(_x, l))
+                H(("ULTK", x, cls), kread + tl + lt_chain(xa, T, B(x)))
+                H(("UGTK", x, cls), kread + tl + lt_chain(T, xa, B(x)))
+                H(("ULEK", x, cls), kread + tl + lt_chain(T, xa, "s[38:39]") + ["s_nop 3", f"s_not_b64 {B(x)}, s[38:39]"])
+                H(("UGEK", x, cls), kread + tl + lt_chain(xa, T, "s[38:39]") + ["s_nop 3", f"s_not_b64 {B(x)}, s[38:39]"])
+            for v in range(NVG):
+                for c, nw in enumerate(KCLS[1:]):
+                    H(("EQVK", x, 2 * v + c), const_words(nw) + eq_const_body(lambda l, _v=v: f"v{VBASE + 8 * _v + l}", nw, B(x)),
+                      reads_stack=False)
     # ---- (last: these handlers never branch, so the subroutine calls above stay in s_call range)
     # ---- binary ops whose right operand is a preloaded variable (the translator fuses
     # PUSH_VAR v at slot d with the consuming op at d: no stack copy, one dispatch less)
@@ -714,7 +792,7 @@ def make_handlers(variant, pfx):
     # slot, one dispatch instead of two (AND / OR are ~30 % of the dispatches of EVM-shaped tapes)
     for key, body in acc:
         kind, d = key[0], key[1]
-        r = d if kind in ACC_UNARY else d - 1
+        r = d if (kind in ACC_UNARY or kind in ACC_AT_X) else d - 1
         if r < 1:
             continue
         for suf, ins, ins_n in (("_A", "s_and_b64", "s_andn2_b64"), ("_O", "s_or_b64", "s_orn2_b64")):
@@ -1140,12 +1218,13 @@ def main():
         # 1: slot d - 1, -1: not a fusable producer); the complementary compare (-1: none)
         table("kQsaKindAndForm", lambda n: idx.get(n + "_A", -1))
         table("kQsaKindOrForm", lambda n: idx.get(n + "_O", -1))
-        table("kQsaKindBoolRes", lambda n: (0 if n in ACC_UNARY else 1) if n in ACC_KINDS else -1)
+        table("kQsaKindBoolRes", lambda n: (0 if (n in ACC_UNARY or n in ACC_AT_X) else 1) if n in ACC_KINDS else -1)
 
         def inv(n):
-            m = re.fullmatch(r"([US])(LT|GT|LE|GE)([VC]?)", n)
+            m = re.fullmatch(r"([US])(LT|GT|LE|GE)([VCK]?)", n)
             return idx.get(m.group(1) + NOT_OF[m.group(2)] + m.group(3), -1) if m else -1
         table("kQsaKindNot", inv)
+        f.write(f"constexpr int kQsaKClassWords[] = {{{', '.join(map(str, KCLS))}}};\n")
         f.write("struct QsaHandlerKey { int kind, d, v; };\n")
         for variant, (hs, lines, macro, suffix) in gen.items():
             f.write(f"constexpr int kQsaHandlers{suffix} = {len(hs)};\n")

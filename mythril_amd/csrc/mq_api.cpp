@@ -343,6 +343,16 @@ static int qsa_init(mq_ctx* c) {
       const int h = c->qsa_index[1][QK_PUSH_CONSTW][d][n + 1];
       if (h >= 0) c->qsa_data_words[(c->qsa_off[1][h] >> 2) & 0xFFFFu] = (uint8_t)(n + 1);
     }
+  // compare-with-inline-constant handlers (and their fused forms): kQsaKClassWords[class]
+  for (int h = 0; ok && h < kQsaHandlersG; h++) {
+    const std::string name = kQsaKindNames[kQsaHandlerKeysG[h].kind];
+    const std::string base = name.substr(0, name.find('_'));
+    const int v = kQsaHandlerKeysG[h].v;
+    int words = -1;
+    if (base == "EQVK") words = kQsaKClassWords[1 + (v & 1)];
+    else if (base == "EQK" || base == "ULTK" || base == "UGTK" || base == "ULEK" || base == "UGEK") words = kQsaKClassWords[v];
+    if (words > 0) c->qsa_data_words[(c->qsa_off[1][h] >> 2) & 0xFFFFu] = (uint8_t)words;
+  }
   c->qsa_ready = ok && std::getenv("MQ_DISABLE_QSA") == nullptr;
   return MQ_OK;
 }
@@ -681,19 +691,25 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
   if (x.L != 8 || x.depth > kQsaStack) return false;
   const bool P = k == 0;
   const size_t wpi = P ? 2 : 1;   // program words per interpreter instruction
-  // the last handler word emitted (fusions below rewrite it while it is still the last word)
-  int last_kind = -1, last_d = 0, last_v = -1;
-  uint32_t last_imm = 0;
-  size_t last_pos = 0;
+  // every handler word emitted so far (position, key, immediate, inline data words): the
+  // fusions below rewrite the last ones while nothing follows them
+  struct Emit {
+    size_t pos;
+    int kind, d, v;
+    uint32_t imm;
+    size_t nd;
+  };
+  std::vector<Emit> log;
+  auto ends_at = [&](const Emit& e) { return e.pos + wpi + e.nd; };
+  auto drop_last = [&](size_t n) {   // forget the last n words (and their data)
+    out.resize(log[log.size() - n].pos);
+    log.resize(log.size() - n);
+  };
   auto word = [&](int kind, int d, int v, uint32_t imm) -> bool {
     if (d < 0 || d >= kQsaStack || v < -1 || v >= kQsaSel || imm > 0xFFFFu) return false;
     const int h = c->qsa_index[k][kind][d][v + 1];
     if (h < 0) return false;
-    last_kind = kind;
-    last_d = d;
-    last_v = v;
-    last_imm = imm;
-    last_pos = out.size();
+    log.push_back(Emit{out.size(), kind, d, v, imm, 0});
     if (P) {   // two-word entry: absolute handler address (low half), immediate
       out.push_back(c->qsa_hbase_lo[0] + c->qsa_off[0][h]);
       out.push_back(imm);
@@ -724,27 +740,80 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
     for (int l = 0; l < 8; l++) v[l] = x.consts[off + l];
     return true;
   };
+  // re-emit a word under another kind (same slot, selector, immediate and inline data)
+  auto rekind = [&](int kind) -> bool {
+    const Emit e = log.back();
+    if (c->qsa_index[k][kind][e.d][e.v + 1] < 0) return false;
+    std::vector<uint32_t> data(out.begin() + (long)(e.pos + wpi), out.begin() + (long)ends_at(e));
+    drop_last(1);
+    if (!word(kind, e.d, e.v, e.imm)) return false;
+    out.insert(out.end(), data.begin(), data.end());
+    log.back().nd = data.size();
+    return true;
+  };
   // slot where the last word left a Bool result, or -1 (it is not a fusable Bool producer, or
   // something was emitted after it)
   auto last_bool_slot = [&]() -> int {
-    if (last_kind < 0 || out.size() != last_pos + wpi || kQsaKindBoolRes[last_kind] < 0) return -1;
-    return kQsaKindBoolRes[last_kind] == 0 ? last_d : last_d - 1;
+    if (log.empty() || out.size() != ends_at(log.back()) || kQsaKindBoolRes[log.back().kind] < 0) return -1;
+    return kQsaKindBoolRes[log.back().kind] == 0 ? log.back().d : log.back().d - 1;
   };
   // AND / OR at slot d whose right operand the last word just produced: that word's fused form
   auto fuse_acc = [&](int d, bool is_and) -> bool {
     if (last_bool_slot() != d) return false;
-    const int fk = is_and ? kQsaKindAndForm[last_kind] : kQsaKindOrForm[last_kind];
-    if (fk < 0 || c->qsa_index[k][fk][last_d][last_v + 1] < 0) return false;
-    out.resize(last_pos);
-    return word(fk, last_d, last_v, last_imm);
+    const int fk = is_and ? kQsaKindAndForm[log.back().kind] : kQsaKindOrForm[log.back().kind];
+    return fk >= 0 && rekind(fk);
   };
   // NOT of a compare the last word just made: the complementary compare
   auto fuse_not = [&](int d) -> bool {
-    if (last_bool_slot() != d || kQsaKindNot[last_kind] < 0) return false;
-    const int nk = kQsaKindNot[last_kind];
-    if (c->qsa_index[k][nk][last_d][last_v + 1] < 0) return false;
-    out.resize(last_pos);
-    return word(nk, last_d, last_v, last_imm);
+    if (last_bool_slot() != d || kQsaKindNot[log.back().kind] < 0) return false;
+    return rekind(kQsaKindNot[log.back().kind]);
+  };
+  // G: a constant push as the operand of a compare -> the compare-with-inline-constant handler.
+  // (cls, data words) of the constant pushed by e (PUSH_CONSTI / PUSH_CONSTW), or cls -1
+  auto const_of = [&](const Emit& e, std::vector<uint32_t>& words) -> int {
+    words.clear();
+    if (e.kind == QK_PUSH_CONSTI) return 0;
+    if (e.kind != QK_PUSH_CONSTW) return -1;
+    const size_t n = e.nd;
+    words.assign(out.begin() + (long)(e.pos + 1), out.begin() + (long)(e.pos + 1 + n));
+    const int cls = n <= (size_t)kQsaKClassWords[1] ? 1 : 2;
+    words.resize((size_t)kQsaKClassWords[cls], 0);
+    return cls;
+  };
+  auto emit_k = [&](int kind, int x, int sel, uint32_t imm, const std::vector<uint32_t>& words) -> bool {
+    if (!word(kind, x, sel, imm)) return false;
+    out.insert(out.end(), words.begin(), words.end());
+    log.back().nd = words.size();
+    return true;
+  };
+  // compare `kind` at slot d (operands S(d-1), S(d)); kk = its constant form, mk = the constant
+  // form of the mirrored compare (c OP x == x MIRROR(OP) c)
+  auto fuse_const = [&](int d, int kk, int mk) -> bool {
+    if (P || log.empty() || d < 1) return false;
+    std::vector<uint32_t> words;
+    const Emit e1 = log.back();
+    if (out.size() != ends_at(e1)) return false;
+    // constant on the right: S(d-1) OP c
+    if (e1.d == d) {
+      const int cls = const_of(e1, words);
+      if (cls >= 0 && c->qsa_index[k][kk][d - 1][cls + 1] >= 0) {
+        const uint32_t imm = e1.imm;
+        drop_last(1);
+        return emit_k(kk, d - 1, cls, cls == 0 ? imm : 0, words);
+      }
+    }
+    // constant on the left, value pushed right after it: the value moves down one slot
+    if (log.size() >= 2 && e1.d == d && e1.nd == 0 &&
+        (e1.kind == QK_PUSH_MEM || e1.kind == QK_PUSH_MEMS || e1.kind == QK_PUSH_TMP || e1.kind == QK_PUSH_VAR)) {
+      const Emit e0 = log[log.size() - 2];
+      const int cls = e0.d == d - 1 && ends_at(e0) == e1.pos ? const_of(e0, words) : -1;
+      if (cls >= 0 && c->qsa_index[k][mk][d - 1][cls + 1] >= 0 && c->qsa_index[k][e1.kind][d - 1][e1.v + 1] >= 0) {
+        const uint32_t imm = e0.imm;
+        drop_last(2);
+        return word(e1.kind, d - 1, e1.v, e1.imm) && emit_k(mk, d - 1, cls, cls == 0 ? imm : 0, words);
+      }
+    }
+    return false;
   };
   uint32_t prev_op = G_END, prev_d = 0, prev_imm = 0;
   size_t prev_out = 0;
@@ -759,15 +828,33 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
   // as the fused handler kindv(d, slot) (the push word is dropped)
   // (P) likewise a right operand just pushed from the constants, for the kinds with a kindc
   // handler (operand read from SGPRs)
-  auto binop = [&](int d, int kind, int kindv, int kindc = -1) -> bool {
+  auto binop = [&](int d, int kind, int kindv, int kindc = -1, int kindk = -1, int kindkm = -1) -> bool {
+    // G: EQ of a constant (left) and a preloaded variable (right) -> EQVK, no stack traffic
+    if (!P && kind == QK_EQ && prev_op == G_PUSH_VAR && prev_pre >= 0 && (int)prev_d == d && log.size() >= 2 &&
+        out.size() == prev_out + wpi && log.back().pos == prev_out) {
+      const Emit e0 = log[log.size() - 2];
+      std::vector<uint32_t> words;
+      int cls = e0.d == d - 1 && ends_at(e0) == prev_out ? const_of(e0, words) : -1;
+      if (cls == 0) {   // the 16-bit immediate travels as a two-word constant here
+        words.assign((size_t)kQsaKClassWords[1], 0);
+        words[0] = e0.imm;
+        cls = 1;
+      }
+      const int sel = 2 * prev_pre + (cls - 1);
+      if (cls >= 1 && sel < kQsaSel && c->qsa_index[k][QK_EQVK][d - 1][sel + 1] >= 0) {
+        drop_last(2);
+        return emit_k(QK_EQVK, d - 1, sel, 0, words);
+      }
+    }
+    if (kindk >= 0 && fuse_const(d, kindk, kindkm)) return true;
     if (prev_op == G_PUSH_VAR && prev_pre >= 0 && (int)prev_d == d && out.size() == prev_out + wpi &&
         c->qsa_index[k][kindv][d][prev_pre + 1] >= 0) {
-      out.resize(prev_out);
+      drop_last(1);
       return word(kindv, d, prev_pre, 0);
     }
     if (kindc >= 0 && P && prev_op == G_PUSH_CONST && (int)prev_d == d && out.size() == prev_out + wpi &&
         c->qsa_index[k][kindc][d][0] >= 0) {
-      out.resize(prev_out);
+      drop_last(1);
       return word(kindc, d, -1, prev_imm);
     }
     return word(kind, d, -1, 0);
@@ -829,6 +916,7 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
         } else {
           ok = word(QK_PUSH_CONSTW, d, n - 1, 0);
           for (int l = 0; ok && l < n; l++) out.push_back(cv[l]);
+          if (ok) log.back().nd = (size_t)n;
         }
         break;
       }
@@ -846,11 +934,11 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
       case G_BITE: ok = word(QK_BITE, d, -1, 0); break;
       case G_BITE_EF: ok = word(QK_BITE_EF, d, -1, 0); break;
       // unsigned predicates / bitwise / ite are exact on canonical values of any width <= 256
-      case G_EQ: ok = imm >= 1 && binop(d, QK_EQ, QK_EQV, QK_EQC); break;
-      case G_ULT: ok = imm >= 1 && binop(d, QK_ULT, QK_ULTV, QK_ULTC); break;
-      case G_ULE: ok = imm >= 1 && binop(d, QK_ULE, QK_ULEV, QK_ULEC); break;
-      case G_UGT: ok = imm >= 1 && binop(d, QK_UGT, QK_UGTV, QK_UGTC); break;
-      case G_UGE: ok = imm >= 1 && binop(d, QK_UGE, QK_UGEV, QK_UGEC); break;
+      case G_EQ: ok = imm >= 1 && binop(d, QK_EQ, QK_EQV, QK_EQC, QK_EQK, QK_EQK); break;
+      case G_ULT: ok = imm >= 1 && binop(d, QK_ULT, QK_ULTV, QK_ULTC, QK_ULTK, QK_UGTK); break;
+      case G_ULE: ok = imm >= 1 && binop(d, QK_ULE, QK_ULEV, QK_ULEC, QK_ULEK, QK_UGEK); break;
+      case G_UGT: ok = imm >= 1 && binop(d, QK_UGT, QK_UGTV, QK_UGTC, QK_UGTK, QK_ULTK); break;
+      case G_UGE: ok = imm >= 1 && binop(d, QK_UGE, QK_UGEV, QK_UGEC, QK_UGEK, QK_ULEK); break;
       case G_BAND: ok = binop(d, QK_BAND, QK_BANDV, QK_BANDC); break;
       case G_BOR: ok = binop(d, QK_BOR, QK_BORV, QK_BORC); break;
       case G_BXOR: ok = binop(d, QK_BXOR, QK_BXORV, QK_BXORC); break;
@@ -876,7 +964,8 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
         uint32_t cv[8];
         ok = after_const && d >= 1 && imm >= 1 && imm <= 256 && const_value(prev_imm, cv);
         if (!ok) break;
-        out.resize(prev_out);  // drop the amount push
+        if (log.empty() || log.back().pos != prev_out) return false;
+        drop_last(1);  // drop the amount push
         bool big = false;
         for (int l = 1; l < 8; l++) big = big || cv[l] != 0;
         const uint32_t kb = big || cv[0] >= imm ? imm : cv[0];  // >= width: everything shifted out
@@ -912,7 +1001,8 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
         }
         bool hi = false;
         for (int l = 1; l < 8; l++) hi = hi || cv[l] != 0;
-        out.resize(prev_out);  // drop the divisor push
+        if (log.empty() || log.back().pos != prev_out) return false;
+        drop_last(1);  // drop the divisor push
         if (!sgn && !hi && cv[0] != 0 && (cv[0] & (cv[0] - 1)) == 0) {
           // unsigned power of two: shift / mask
           const uint32_t kb = (uint32_t)__builtin_ctz(cv[0]);
