@@ -323,8 +323,14 @@ int mq_tapes_column_split(mq_tapes* tapes, int32_t* n_asm, int32_t* live);
 int mq_tapes_qsa_histogram(mq_tapes* tapes, int32_t which, int64_t* hist_out, int32_t cap, int64_t* pairs_out,
                            int32_t* n_kinds_out);
 
-/* Name of handler kind `kind` of the assembly interpreters (NULL when out of range). */
+/* Name of handler kind `kind` of the assembly interpreters; past the last kind, the profile's
+   tape-frame entries ("FRAME", "F_HDR", "F_EE", "F_END"); NULL when out of range. */
 const char* mq_qsa_kind_name(int32_t kind);
+
+/* Diagnostic G profile build only (gen_qsa.py QSA_PROF=1): the cycles charged to each handler
+   kind and its dispatch count, interleaved (cycles, count) per kind plus the tape frame, into
+   out[cap]; *n_out = entries (0 in product builds).  reset != 0 zeroes the accumulators. */
+int mq_qsa_profile(mq_ctx* ctx, int64_t* out, int32_t cap, int32_t* n_out, int reset);
 
 /* Static algorithmic cost of a tape; -1 if malformed. */
 double mq_tape_alg_ops(const mq_tape_batch* batch, int32_t t);

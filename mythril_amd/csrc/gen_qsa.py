@@ -59,10 +59,34 @@ BBASE = 48
 STG = "v65"    # G: LDS address of the staged model rows of this lane (stage base + 4 * lane)
 # G early exit: a 64-desc window of the wave's tapes, lane i <-> desc s25 - 1 - 64w - i (w = the
 # window of the current tape counted from the wave's LAST desc); EEA = byte offset of best[tape]
-# of that desc, EEV = best[] as gathered while the previous tape ran (None: scalar check)
+# of that desc, EEV = best[] as gathered when the window was entered (None: scalar check)
 EEA, EEV = "v67", "v66"
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+
+# QSA_PROF=1 at generation: a diagnostic G build that charges the cycles (s_memtime) since the
+# previous handler's end to each handler kind, in a per-wave LDS table flushed to QArgs.prof_out
+# (tools/g_profile.py).  Never the product build: it adds ~12 instructions per dispatch.
+PROF = os.environ.get("QSA_PROF") == "1"
+PROF_VGPR = "v70"     # G: LDS address of this wave's profile table
+# profile entries past the handler kinds: the tape frame split at its waits (tape header load,
+# early-exit check, window / run start) and the tape end bookkeeping
+PROF_EXTRA = ("FRAME", "F_HDR", "F_EE", "F_END")
+
+
+def prof_point(kind):
+    """Charge the cycles since the last profile point to `kind` (offset resolved in main())."""
+    if not PROF:
+        return []
+    return ["s_memtime s[34:35]", "s_waitcnt lgkmcnt(0)",
+            "s_sub_u32 s36, s34, s100",
+            "s_mov_b64 s[100:101], s[34:35]",
+            "s_mov_b64 s[34:35], exec", "s_mov_b64 exec, 1",
+            "v_mov_b32 v4, s36", "v_mov_b32 v5, 0",
+            f"ds_add_u64 {PROF_VGPR}, v[4:5] offset:@PROF:{kind}:0@",
+            "v_mov_b32 v4, 1",
+            f"ds_add_u64 {PROF_VGPR}, v[4:5] offset:@PROF:{kind}:8@",
+            "s_mov_b64 exec, s[34:35]"]
 
 
 def S(d, l):
@@ -107,6 +131,7 @@ def W2(k):
 # two lane reads, one SALU add and the jump: the scalar unit, shared by the CU's four SIMDs, was
 # the binding issue port at six SALU per dispatch.
 WIN, WINA, WINI = "v64", "v68", "v69"
+NWIN = "v71"       # G: the program block after the window, prefetched (load_window)
 
 
 def next_g():
@@ -133,15 +158,29 @@ NEXT_P = [
 ]
 
 
-def load_window(first):
-    """WIN = the 64 program words at s[14:15] (+ 4*s16 unless first); s16 = 0."""
-    out = []
-    if not first:
-        out += ["s_lshl_b32 s34, s16, 2", "s_add_u32 s14, s14, s34", "s_addc_u32 s15, s15, 0"]
-    out += ["v_mbcnt_lo_u32_b32 v5, -1, 0", "v_mbcnt_hi_u32_b32 v5, -1, v5", "v_lshlrev_b32 v5, 2, v5",
-            f"global_load_dword {WIN}, v5, s[14:15]", "s_mov_b32 s16, 0", "s_waitcnt vmcnt(0)",
+def load_window(first, pfx=None):
+    """Make the program's next 64-word block the window (decoded, s16 = 0) and prefetch the one
+    after it into NWIN (mq_api.cpp qsa_window_layout: blocks are aligned and contiguous).
+    first (tape start, s[36:37] = the program's address): the block is NWIN when the previous
+    window's successor is this program (consecutive descriptors), else it is loaded.  Otherwise
+    (REFILL): the block is NWIN, 256 bytes on."""
+    out = ["v_mbcnt_lo_u32_b32 v5, -1, 0", "v_mbcnt_hi_u32_b32 v5, -1, v5", "v_lshlrev_b32 v5, 2, v5"]
+    if first:
+        out += ["s_add_u32 s34, s14, 256", "s_addc_u32 s35, s15, 0",
+                "s_cmp_eq_u64 s[34:35], s[36:37]",
+                "s_mov_b64 s[14:15], s[36:37]",
+                "s_waitcnt vmcnt(0)",
+                f"s_cbranch_scc1 {pfx}_win_pref",
+                f"global_load_dword {NWIN}, v5, s[14:15]",
+                "s_waitcnt vmcnt(0)",
+                f"{pfx}_win_pref:"]
+    else:
+        out += ["s_add_u32 s14, s14, 256", "s_addc_u32 s15, s15, 0", "s_waitcnt vmcnt(0)"]
+    out += [f"v_mov_b32 {WIN}, {NWIN}",
+            f"global_load_dword {NWIN}, v5, s[14:15] offset:256",
+            "s_mov_b32 s16, 0",
             f"v_and_b32 v5, 0xffff, {WIN}",
-            f"v_lshl_add_u32 {WINA}, v5, 2, s12",
+            f"v_lshl_add_u32 {WINA}, v5, {3 if PROF else 2}, s12",
             f"v_lshrrev_b32 {WINI}, 16, {WIN}",
             "s_nop 1"]                      # VALU VGPR write -> v_readlane of it
     return out
@@ -518,11 +557,14 @@ def sub_uf1(pfx):
             "s_waitcnt vmcnt(0)",
             "v_mad_u64_u32 v[136:137], s[34:35], v5, v7, s[68:69]",   # &entry[lo]
             "s_mov_b64 s[60:61], exec",
+            "s_mov_b64 s[64:65], 0",                          # lanes that matched
             f"{P}_uf_loop:",
             "v_cmp_lt_u32_e64 s[34:35], v5, v6",
             "s_nop 3",
             "s_and_b64 exec, exec, s[34:35]",
             f"s_cbranch_execz {P}_uf_done"]
+    # one memory round trip per entry (its key); the value of the first matching entry is read
+    # once after the scan from the remembered entry pointer v[138:139]
     for l in range(L):
         out += [f"s_cmp_le_u32 s36, {l}", f"s_cbranch_scc1 {P}_uf_kl_done",
                 f"global_load_dword v{UBASE + 12 + l}, v[136:137], off offset:{4 * l}"]
@@ -532,24 +574,29 @@ def sub_uf1(pfx):
                 f"v_xor_b32 v149, v{UBASE + 12 + l}, {W(l)}", "v_or_b32 v148, v148, v149"]
     out += [f"{P}_uf_kc_done:",
             "v_cmp_eq_u32_e64 s[34:35], 0, v148",
-            "v_add_co_u32 v150, vcc, s98, v136",
-            "s_nop 1",
-            "v_addc_co_u32 v151, vcc, 0, v137, vcc",
             "s_nop 3",
-            "s_and_saveexec_b64 s[78:79], s[34:35]",
-            f"s_cbranch_execz {P}_uf_nomatch"]
-    for l in range(L):
-        out += [f"s_cmp_le_u32 s37, {l}", f"s_cbranch_scc1 {P}_uf_vl_done",
-                f"global_load_dword v{UBASE + l}, v[150:151], off offset:{4 * l}"]
-    out += [f"{P}_uf_vl_done:", "s_waitcnt vmcnt(0)",
-            f"{P}_uf_nomatch:",
-            "s_andn2_b64 exec, s[78:79], s[34:35]",           # matched lanes are done
+            "s_and_b64 s[34:35], s[34:35], exec",
+            "s_or_b64 s[64:65], s[64:65], s[34:35]",
+            "s_nop 1",
+            "v_cndmask_b32_e64 v138, v138, v136, s[34:35]",
+            "v_cndmask_b32_e64 v139, v139, v137, s[34:35]",
+            "s_andn2_b64 exec, exec, s[34:35]",               # matched lanes are done
             "v_add_u32 v5, 1, v5",
             "v_add_co_u32 v136, vcc, v136, v7",
             "s_nop 1",
             "v_addc_co_u32 v137, vcc, 0, v137, vcc",
             f"s_branch {P}_uf_loop",
             f"{P}_uf_done:",
+            "s_mov_b64 exec, s[64:65]",
+            f"s_cbranch_execz {P}_uf_vl_done",
+            "v_add_co_u32 v150, vcc, s98, v138",
+            "s_nop 1",
+            "v_addc_co_u32 v151, vcc, 0, v139, vcc"]
+    for l in range(L):
+        out += [f"s_cmp_le_u32 s37, {l}", f"s_cbranch_scc1 {P}_uf_vl_issued",
+                f"global_load_dword v{UBASE + l}, v[150:151], off offset:{4 * l}"]
+    out += [f"{P}_uf_vl_issued:", "s_waitcnt vmcnt(0)",
+            f"{P}_uf_vl_done:",
             "s_mov_b64 exec, s[60:61]",
             f"{P}_uf_ret:",
             "s_setpc_b64 s[76:77]"]
@@ -584,7 +631,11 @@ def make_handlers(variant, pfx):
 
     def H(key, body, tail=True, reads_stack=True):
         pre = [VMWAIT] if (G and reads_stack) else []
-        hs.append((key, pre + list(body) + ((NEXT_G if G else NEXT_P) if tail else [])))
+        prof = prof_point(key[0]) if G else []
+        if tail:
+            hs.append((key, pre + list(body) + prof + (NEXT_G if G else NEXT_P)))
+        else:
+            hs.append((key, prof + pre + list(body)))
         if key[0] in ACC_KINDS and tail:
             acc.append((key, pre + list(body)))
 
@@ -800,7 +851,7 @@ def make_handlers(variant, pfx):
                 fused = [f"{ins_n} {B(r - 1)}, {B(r - 1)}, {B(r)}"]
             else:
                 fused = list(body) + (["s_nop 3"] if body[-1].startswith("v_") else []) + [f"{ins} {B(r - 1)}, {B(r - 1)}, {B(r)}"]
-            hs.append(((kind + suf,) + tuple(key[1:]), fused + (NEXT_G if G else NEXT_P)))
+            hs.append(((kind + suf,) + tuple(key[1:]), fused + (prof_point(kind + suf) if G else []) + (NEXT_G if G else NEXT_P)))
     subs = sub_abs_cneg(pfx) + sub_udiv32(pfx) + (sub_uf1(pfx) if G else [])
     return hs, subs
 
@@ -1006,6 +1057,21 @@ def frame(variant, pfx, handlers, subs):
     P += ["s_lshl_b32 s74, s29, 2", "s_lshr_b32 s75, s29, 30"]   # M*4 (after the preload's s[64:79] use)
     if G:
         P += stage_rows(pfx)
+        if PROF:
+            P += ["s_load_dwordx2 s[64:65], s[10:11], 0x184",   # n_stage, stage_base
+                  "s_waitcnt lgkmcnt(0)",
+                  "s_lshl_b32 s64, s64, 8",
+                  "s_add_u32 s64, s64, s65",
+                  "v_lshrrev_b32 v4, 6, v3",
+                  "v_mul_u32_u24 v4, @PROFBYTES@, v4",
+                  f"v_add_u32 {PROF_VGPR}, s64, v4",
+                  "v_mbcnt_lo_u32_b32 v6, -1, 0", "v_mbcnt_hi_u32_b32 v6, -1, v6", "v_lshlrev_b32 v6, 3, v6",
+                  f"v_add_u32 v6, {PROF_VGPR}, v6", "v_mov_b32 v4, 0", "v_mov_b32 v5, 0",
+                  "@PROFZERO@",
+                  "s_waitcnt lgkmcnt(0)",
+                  "s_memtime s[100:101]", "s_waitcnt lgkmcnt(0)"]
+    if G:
+        P += ["s_mov_b64 s[14:15], 0"]   # no window yet (load_window's successor test fails)
     ee = G and EEV is not None
     if ee:
         P += ["s_cmp_lg_u32 s31, 0",
@@ -1026,6 +1092,7 @@ def frame(variant, pfx, handlers, subs):
         "s_addc_u32 s35, s23, 0",
         "s_load_dwordx8 s[80:87], s[34:35], 0x0",
         "s_waitcnt lgkmcnt(0)",
+    ] + (prof_point("F_HDR") if G else []) + [
         "s_lshl_b32 s34, s82, 2",
         "s_add_u32 s72, s26, s34",           # s[72:73] = &best[tape] (handlers never touch s72-s73, s80-s87)
         "s_addc_u32 s73, s27, 0",
@@ -1034,7 +1101,7 @@ def frame(variant, pfx, handlers, subs):
         "s_cmp_eq_u32 s30, 0",
         f"s_cbranch_scc1 {pfx}_run",
     ] + ([
-        # best[tape] from the window gathered while the previous tape ran (a stale value only
+        # best[tape] from the window gathered when the wave entered it (a stale value only
         # costs a tape that a fresher one would have skipped); a new window every 64 tapes
         "s_sub_u32 s34, s25, s24",
         "s_sub_u32 s34, s34, 1",
@@ -1043,18 +1110,15 @@ def frame(variant, pfx, handlers, subs):
         f"s_cbranch_scc1 {pfx}_ee_have",
     ] + ee_window() + [
         f"{pfx}_ee_have:",
-        "s_waitcnt vmcnt(0)",
+    ] + prof_point("F_EE") + [
         "s_and_b32 s35, s34, 63",
         f"v_readlane_b32 s36, {EEV}, s35",
         "s_nop 3",                      # VALU SGPR write -> SALU read
         "s_cmp_ge_i32 s28, s36",
         f"s_cbranch_scc1 {pfx}_next_tape",
-        # refresh the window for the next tape, waited for at its check (the run's first
-        # vmcnt wait usually covers it)
-        "s_mov_b64 s[60:61], exec",
-        "s_mov_b64 exec, -1",
-        f"global_load_dword {EEV}, {EEA}, s[26:27] sc1",
-        "s_mov_b64 exec, s[60:61]",
+        # (no per-tape refresh: vector loads complete in order, so a refresh in flight would hold
+        # up the tape's first operand wait by a coherent round trip; the window is re-gathered
+        # every 64 tapes, and hits found meanwhile only cost tapes a fresher value would skip)
     ] if ee else [
         "s_load_dword s34, s[72:73], 0x0 glc",
         "s_waitcnt lgkmcnt(0)",
@@ -1065,10 +1129,11 @@ def frame(variant, pfx, handlers, subs):
         "s_lshl_b32 s34, s83, 2",
         "s_add_u32 s20, s88, s34",
         "s_addc_u32 s21, s89, 0",
+    ] + (["s_lshl_b32 s34, s80, 2", "s_add_u32 s36, s46, s34", "s_addc_u32 s37, s47, 0"]
+         + load_window(True, pfx) + prof_point("FRAME") + NEXT_G if G else [
         "s_lshl_b32 s34, s80, 2",
         "s_add_u32 s14, s46, s34",
         "s_addc_u32 s15, s47, 0",
-    ] + (load_window(True) + NEXT_G if G else [
         "s_load_dwordx2 s[96:97], s[14:15], 0x0",
         "s_mov_b32 s16, 8",
     ] + NEXT_P) + [
@@ -1116,9 +1181,18 @@ def frame(variant, pfx, handlers, subs):
         "s_mov_b64 exec, s[60:61]",
     ] + ([f"s_branch {pfx}_next_tape"] + store_column(pfx) if G else []) + [
         f"{pfx}_next_tape:",
+    ] + (prof_point("F_END") if G else []) + [
         "s_add_u32 s24, s24, 1",
         f"s_branch {pfx}_tape_loop",
         f"{pfx}_tapes_done:",
+    ] + ([
+        "v_mbcnt_lo_u32_b32 v6, -1, 0", "v_mbcnt_hi_u32_b32 v6, -1, v6", "v_lshlrev_b32 v6, 3, v6",
+        f"v_add_u32 v7, {PROF_VGPR}, v6",
+        "s_load_dwordx2 s[64:65], s[10:11], 0x1a8",
+        "s_waitcnt lgkmcnt(0)",
+        "@PROFFLUSH@",
+        "s_waitcnt vmcnt(0)",
+    ] if (G and PROF) else []) + [
         # the wave's counters go to slot (tile ^ last tape) mod 256 of the slotted counter array
         # (qs_launch.h kCounterSlots): 10^6 waves adding into one cache line serialise in L2
         "s_lshr_b32 s34, s28, 6",
@@ -1145,8 +1219,12 @@ def frame(variant, pfx, handlers, subs):
     P += [f"{pfx}_exit:", "s_getpc_b64 s[34:35]", f"{pfx}_exit_pc:",
           f"s_add_u32 s34, s34, {pfx}_end - {pfx}_exit_pc", "s_addc_u32 s35, s35, 0", "s_setpc_b64 s[34:35]"]
     P += subs
+    if PROF and G:
+        P.append(".p2align 3")
     P.append(f"{pfx}_hbase:")
     for k, (key, body) in enumerate(handlers):
+        if PROF and G:
+            P.append(".p2align 3")
         P.append(f"{pfx}_h{k}:  ; {' '.join(map(str, key))}")
         P += body
     P.append(f"{pfx}_end:")
@@ -1161,14 +1239,14 @@ def set_layout(variant):
     P and G with preloads: the map in the module docstring (G adds the early-exit window v66/v67
     and the decoded program window v68/v69).  Compact G (NVG = 0): UF1 work v[8:31], program
     window v[32:34], staging address v35, stack v[40:87], T/W v[88:95] -> 96 VGPRs."""
-    global SBASE, TBASE, UBASE, WIN, WINA, WINI, STG, NEXT_G, EEA, EEV
+    global SBASE, TBASE, UBASE, WIN, WINA, WINI, NWIN, STG, NEXT_G, EEA, EEV
     if variant == "g" and NVG == 0:
         SBASE, TBASE, UBASE = 40, 88, 8
-        WIN, WINA, WINI, STG = "v32", "v33", "v34", "v35"
+        WIN, WINA, WINI, STG, NWIN = "v32", "v33", "v34", "v35", "v36"
         EEA = EEV = None
     else:
         SBASE, TBASE, UBASE = 72, 120, 40
-        WIN, WINA, WINI, STG = "v64", "v68", "v69", "v65"
+        WIN, WINA, WINI, STG, NWIN = "v64", "v68", "v69", "v65", "v71"
         EEA, EEV = "v67", "v66"
     NEXT_G = next_g()
 
@@ -1182,18 +1260,40 @@ def source_stamp() -> str:
     any change of the generator, independent of file times)."""
     import hashlib
     with open(os.path.abspath(__file__), "rb") as f:
-        return hashlib.sha256(f.read()).hexdigest()[:16]
+        return hashlib.sha256(f.read() + (b"PROF" if PROF else b"")).hexdigest()[:16]
 
 
 def main():
     stamp = source_stamp()
-    sclob = [f'"s{i}"' for i in range(10, 100) if i not in (32, 33)] + ['"vcc"', '"scc"', '"memory"']
+    sclob = [f'"s{i}"' for i in range(10, 102 if PROF else 100) if i not in (32, 33)] + ['"vcc"', '"scc"', '"memory"']
     clob = {v: [f'"v{i}"' for i in range(1, vgprs(v))] + sclob for v in ("p", "g")}
     gen = {}
     for variant, pfx, macro, suffix in VARIANTS:
         set_layout(variant)
         hs, subs = make_handlers(variant, pfx)
         gen[variant] = (hs, frame(variant, pfx, hs, subs), macro, suffix)
+    # (kinds the translator names exist in the enum even when a layout generates no handler)
+    names = sorted({k[0] for hs, *_ in gen.values() for k, _ in hs} | {"EQVK", "PUSH_VAR", "PUSH_VARB"})
+    prof_names = names + list(PROF_EXTRA)
+    prof_bytes = -(-16 * len(prof_names) // 512) * 512 if PROF else 0
+
+    def resolve(ln):
+        if "@" not in ln:
+            return [ln]
+        if "@PROF:" in ln:
+            return [re.sub(r"@PROF:(\w+):(\d+)@", lambda m: str(16 * prof_names.index(m.group(1)) + int(m.group(2))), ln)]
+        if ln == "@PROFZERO@":
+            return [f"ds_write_b64 v6, v[4:5] offset:{512 * j}" for j in range(prof_bytes // 512)]
+        if ln == "@PROFFLUSH@":
+            out = []
+            for j in range(prof_bytes // 512):
+                out += [f"ds_read_b64 v[4:5], v7 offset:{512 * j}", "s_waitcnt lgkmcnt(0)",
+                        f"global_atomic_add_x2 v6, v[4:5], s[64:65] offset:{512 * j}"]
+            return out
+        return [ln.replace("@PROFBYTES@", str(prof_bytes))]
+    for v in gen:
+        hs, lines, macro, suffix = gen[v]
+        gen[v] = (hs, [r for ln in lines for r in resolve(ln)], macro, suffix)
     with open(os.path.join(HERE, "qsa_gen.inc"), "w") as f:
         f.write(f"// GENERATED by gen_qsa.py (source {stamp}) — do not edit\n")
         for variant, (hs, lines, macro, suffix) in gen.items():
@@ -1203,7 +1303,6 @@ def main():
             f.write("  \"\"\n")
         f.write("#define QSA_CLOBBERS_P " + ", ".join(clob["p"]) + "\n")
         f.write("#define QSA_CLOBBERS_G " + ", ".join(clob["g"]) + "\n")
-    names = sorted({k[0] for hs, *_ in gen.values() for k, _ in hs})
     with open(os.path.join(HERE, "qsa_table.h"), "w") as f:
         f.write(f"// GENERATED by gen_qsa.py (source {stamp}) — handler enumerations of the QSA interpreters\n")
         f.write("#ifndef MQ_QSA_TABLE_H\n#define MQ_QSA_TABLE_H\nnamespace mq {\n")
@@ -1225,6 +1324,12 @@ def main():
             return idx.get(m.group(1) + NOT_OF[m.group(2)] + m.group(3), -1) if m else -1
         table("kQsaKindNot", inv)
         f.write(f"constexpr int kQsaKClassWords[] = {{{', '.join(map(str, KCLS))}}};\n")
+        # diagnostic profile build (QSA_PROF=1): per-wave LDS table bytes; entry i = (cycles,
+        # count) of kind i, entry QK_COUNT = the tape frame
+        f.write(f"constexpr int kQsaProfBytes = {prof_bytes};\n")
+        f.write(f"constexpr int kQsaProfExtra = {len(PROF_EXTRA)};\n")
+        f.write("static const char* const kQsaProfExtraNames[] = {" + ", ".join(f'"{n}"' for n in PROF_EXTRA) + "};\n")
+        f.write(f"constexpr int kQsaHandlerShiftG = {3 if PROF else 2};\n")
         f.write("struct QsaHandlerKey { int kind, d, v; };\n")
         for variant, (hs, lines, macro, suffix) in gen.items():
             f.write(f"constexpr int kQsaHandlers{suffix} = {len(hs)};\n")

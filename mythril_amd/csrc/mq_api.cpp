@@ -93,6 +93,7 @@ struct mq_ctx {
   std::vector<int32_t> bmask_of_var;
   int32_t n_bmask = 0;
   DevBuf bmasks, bmask_rows;
+  DevBuf prof;   // G profile build (kQsaProfBytes > 0): per-kind (cycles, count), mq_qsa_profile
   DevBuf verdict_buf;
   // assembly interpreters (qsa.hip): handler byte offsets read back at context creation;
   // k = 0 the P kernel (preloaded variables), k = 1 the G kernel (general)
@@ -301,6 +302,10 @@ const char* mq_strerror(int code) {
   }
 }
 
+// Handler byte offset -> the 16-bit word field that encodes it: P / G handlers are 4-byte
+// aligned (shift 2); the diagnostic G profile build aligns them to 8 bytes (shift 3, 512 KB reach)
+static inline uint32_t hword(int k, uint32_t off) { return off >> (k == 1 ? kQsaHandlerShiftG : 2); }
+
 // Read back the byte offset of every handler of the assembly interpreters (kernel mode 2).
 static int qsa_init(mq_ctx* c) {
   bool ok = true;
@@ -325,10 +330,11 @@ static int qsa_init(mq_ctx* c) {
     c->qsa_hbase_lo[k] = c->qsa_off[k][nh];
     c->qsa_kind_of[k].assign(1 << 16, -1);
     for (int h = 0; h < nh; h++)
-      if (c->qsa_off[k][h] < (1u << 18)) c->qsa_kind_of[k][c->qsa_off[k][h] >> 2] = (int16_t)keys[h].kind;
+      if (hword(k, c->qsa_off[k][h]) < (1u << 16)) c->qsa_kind_of[k][hword(k, c->qsa_off[k][h])] = (int16_t)keys[h].kind;
     uint32_t max_off = 0;
     for (int h = 0; h < nh; h++) {
-      ok = ok && c->qsa_off[k][h] != 0xFFFFFFFFu && (c->qsa_off[k][h] & 3) == 0 && c->qsa_off[k][h] < (1u << 18);
+      ok = ok && c->qsa_off[k][h] != 0xFFFFFFFFu && hword(k, c->qsa_off[k][h]) < (1u << 16) &&
+           (c->qsa_off[k][h] & ((k == 1 ? (1u << kQsaHandlerShiftG) : 4u) - 1)) == 0;
       max_off = std::max(max_off, c->qsa_off[k][h]);
     }
     // P program entries and G's decoded program window hold the low 32 bits of absolute handler
@@ -341,7 +347,7 @@ static int qsa_init(mq_ctx* c) {
   for (int d = 0; ok && d < kQsaStack; d++)
     for (int n = 0; n < 8; n++) {
       const int h = c->qsa_index[1][QK_PUSH_CONSTW][d][n + 1];
-      if (h >= 0) c->qsa_data_words[(c->qsa_off[1][h] >> 2) & 0xFFFFu] = (uint8_t)(n + 1);
+      if (h >= 0) c->qsa_data_words[hword(1, c->qsa_off[1][h]) & 0xFFFFu] = (uint8_t)(n + 1);
     }
   // compare-with-inline-constant handlers (and their fused forms): kQsaKClassWords[class]
   for (int h = 0; ok && h < kQsaHandlersG; h++) {
@@ -351,7 +357,7 @@ static int qsa_init(mq_ctx* c) {
     int words = -1;
     if (base == "EQVK") words = kQsaKClassWords[1 + (v & 1)];
     else if (base == "EQK" || base == "ULTK" || base == "UGTK" || base == "ULEK" || base == "UGEK") words = kQsaKClassWords[v];
-    if (words > 0) c->qsa_data_words[(c->qsa_off[1][h] >> 2) & 0xFFFFu] = (uint8_t)words;
+    if (words > 0) c->qsa_data_words[hword(1, c->qsa_off[1][h]) & 0xFFFFu] = (uint8_t)words;
   }
   c->qsa_ready = ok && std::getenv("MQ_DISABLE_QSA") == nullptr;
   return MQ_OK;
@@ -655,6 +661,16 @@ int mq_models_upload(mq_ctx* c, const mq_model_batch* mb) {
   return MQ_OK;
 }
 
+// G profile build: the zeroed per-kind (cycles, count) accumulator, nullptr in product builds
+static unsigned long long* prof_buffer(mq_ctx* c) {
+  if (kQsaProfBytes <= 0) return nullptr;
+  if (!c->prof.p) {
+    if (c->prof.ensure((size_t)kQsaProfBytes) != hipSuccess) return nullptr;
+    if (hipMemset(c->prof.p, 0, (size_t)kQsaProfBytes) != hipSuccess) return nullptr;
+  }
+  return c->prof.as<unsigned long long>();
+}
+
 // Count the handler kinds of one translated program (k = 0: P two-word entries; 1: G words,
 // inline constant words skipped) into hist[QK_COUNT] and, if given, kind bigrams into pairs.
 static void qsa_count(const mq_ctx* c, int k, const std::vector<uint32_t>& tr, std::vector<int64_t>& hist,
@@ -714,7 +730,7 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
       out.push_back(c->qsa_hbase_lo[0] + c->qsa_off[0][h]);
       out.push_back(imm);
     } else {
-      out.push_back((c->qsa_off[k][h] >> 2) | (imm << 16));
+      out.push_back(hword(k, c->qsa_off[k][h]) | (imm << 16));
     }
     return true;
   };
@@ -1492,21 +1508,30 @@ static KArgs make_col_args(mq_ctx* c, mq_tapes* T, const mq_tapes::Variant& v) {
 // wherever the next handler word and its inline data would not fit in the current window (the
 // refilled window starts right after the REFILL word).
 static void qsa_window_layout(const mq_ctx* c, std::vector<uint32_t>& prog) {
+  // Windows are the program's aligned 64-word blocks: a handler group (word + inline data) that
+  // does not fit the rest of a block is preceded by REFILL and moves to the next block (the gap
+  // is padded with END), and the program is padded to a whole block.  So the window after the
+  // current one is always 256 bytes further, which the kernel prefetches (gen_qsa.py NWIN), and
+  // the programs of consecutive descriptors are contiguous blocks: the next tape's first window
+  // is the prefetch of the current tape's last one.
   const std::vector<uint8_t>& data_words = c->qsa_data_words;
-  const uint32_t refill = c->qsa_off[1][c->qsa_index[1][QK_REFILL][0][0]] >> 2;
+  const uint32_t refill = hword(1, c->qsa_off[1][c->qsa_index[1][QK_REFILL][0][0]]);
+  const uint32_t endw = hword(1, c->qsa_off[1][c->qsa_index[1][QK_END][0][0]]);
   std::vector<uint32_t> out;
-  out.reserve(prog.size() + prog.size() / 48 + 2);
+  out.reserve(prog.size() + prog.size() / 32 + 64);
   size_t pos = 0;
   for (size_t i = 0; i < prog.size();) {
     const size_t g = 1 + (size_t)data_words[prog[i] & 0xFFFFu];
     if (pos + g > 63) {
       out.push_back(refill);
+      out.insert(out.end(), 63 - pos, endw);
       pos = 0;
     }
     for (size_t j = 0; j < g && i + j < prog.size(); j++) out.push_back(prog[i + j]);
     pos += g;
     i += g;
   }
+  if (pos) out.insert(out.end(), 64 - pos, endw);
   prog.swap(out);
 }
 
@@ -1530,12 +1555,20 @@ static std::vector<int64_t> count_pushes(const mq_ctx* c, const std::vector<Comp
 
 // G kernel LDS staging plan: the most pushed variables (not preloaded) whose rows fit the
 // workgroup's staging budget get consecutive LDS slots (gen_qsa.py stage_rows); their pushes
-// become LDS reads.  Budget: MQ_G_STAGE_KB (default 32) KB per workgroup minus the temps of
-// its 4 waves.  stage_rows is padded to a multiple of 8 with the zero row.
+// become LDS reads.  Budget: MQ_G_STAGE_KB (default 40: four workgroups of 4 waves still fit a
+// CU's 160 KB) KB per workgroup minus the temps of its 4 waves.  Every workgroup loads its rows
+// once, so a variable is staged only when the workgroup's tapes (wg_share of the batch's
+// programs) push it at least MQ_G_STAGE_MIN (default 1.5) times on average
+// (profiles/r02t_*: 40 KB with no such floor sped C3 up and slowed C5, whose groups cover few
+// tapes).  stage_rows is padded to a multiple of 8 with the zero row.
+static int64_t g_tapes_per_group(int64_t n, int64_t M);
+
 static void plan_stage(const mq_ctx* c, const std::vector<int64_t>& pushes, const std::vector<int>* gpre, int temps,
-                       std::vector<int>& gstage, std::vector<uint32_t>& rows) {
-  int64_t kb = 32;
+                       double wg_share, std::vector<int>& gstage, std::vector<uint32_t>& rows) {
+  int64_t kb = 40;
   if (const char* e = std::getenv("MQ_G_STAGE_KB")) kb = std::atol(e);
+  double min_pushes = 1.5;
+  if (const char* e = std::getenv("MQ_G_STAGE_MIN")) min_pushes = std::atof(e);
   const int64_t budget = (kb * 1024 - 4 * (int64_t)temps * 2048) / 256;
   gstage.assign(c->var_nl_h.size(), -1);
   rows.clear();
@@ -1545,6 +1578,7 @@ static void plan_stage(const mq_ctx* c, const std::vector<int64_t>& pushes, cons
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return pushes[a] > pushes[b]; });
   for (int v : order) {
     const int64_t nl = c->var_nl_h[v];
+    if ((double)pushes[v] * wg_share < min_pushes) break;   // (sorted by pushes)
     if ((int64_t)rows.size() + nl > budget) continue;
     gstage[v] = (int)rows.size();
     for (int64_t l = 0; l < nl; l++) rows.push_back(c->var_off_h[v] + (uint32_t)l);
@@ -1596,7 +1630,10 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
   int g_temps = 0;
   for (size_t i = 0; i < T->qct.size(); i++)
     if (!on_p[i]) g_temps = std::max(g_temps, T->qct[i].n_temps);
-  plan_stage(c, pushes, &T->gpre, g_temps, T->gstage, T->stage_rows);
+  int64_t n_g = 0;
+  for (size_t i = 0; i < T->qct.size(); i++) n_g += on_p[i] ? 0 : 1;
+  const double g_share = n_g ? std::min(1.0, 4.0 * (double)g_tapes_per_group(n_g, c->M) / (double)n_g) : 1.0;
+  plan_stage(c, pushes, &T->gpre, g_temps, g_share, T->gstage, T->stage_rows);
   T->qhist[0].assign(QK_COUNT, 0);
   T->qhist[1].assign(QK_COUNT, 0);
   T->qpairs.assign((size_t)QK_COUNT * QK_COUNT, 0);
@@ -1627,7 +1664,7 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
     }
     prog.insert(prog.end(), words[k].begin(), words[k].end());
     const uint32_t endo = c->qsa_off[k][c->qsa_index[k][QK_END][0][0]];
-    const uint32_t endw = endo / 4;
+    const uint32_t endw = hword(1, endo);
     if (k == 0) {   // P entries are (handler address, imm) pairs
       for (int r = 0; r < 2; r++) {
         prog.push_back(c->qsa_hbase_lo[0] + endo);
@@ -1638,7 +1675,7 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
       prog.push_back(endw);
     }
     // G's window loads read up to 63 words past a program's last word
-    if (k == 1) prog.insert(prog.end(), 64, endw);
+    if (k == 1) prog.insert(prog.end(), 128, endw);   // window + next-window prefetch past the last END
     T->q_count[k] = (int)ds[k].size();
     T->q_temps[k] = temps[k];
   }
@@ -1666,7 +1703,11 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
   std::vector<GDesc> descs;
   int temps = 0;
   for (const CompiledTape& x : T->cq_ct) temps = std::max(temps, x.n_temps);
-  plan_stage(c, count_pushes(c, T->cq_ct), nullptr, temps, T->cq_stage, T->cq_stage_rows);
+  // (columns run level by level: a workgroup's share is of its level's columns; the batch-wide
+  // share is the conservative estimate)
+  const int64_t n_cq = (int64_t)T->cq_ct.size();
+  const double cq_share = n_cq ? std::min(1.0, 4.0 * (double)g_tapes_per_group(n_cq, c->M) / (double)n_cq) : 1.0;
+  plan_stage(c, count_pushes(c, T->cq_ct), nullptr, temps, cq_share, T->cq_stage, T->cq_stage_rows);
   temps = 0;
   for (size_t i = 0; i < T->cq_ct.size(); i++) {
     const CompiledTape& x = T->cq_ct[i];
@@ -1689,8 +1730,8 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
     descs.push_back(d);
     temps = std::max(temps, x.n_temps);
   }
-  const uint32_t endw = c->qsa_off[1][c->qsa_index[1][QK_END][0][0]] / 4;
-  prog.insert(prog.end(), 66, endw);   // the window loads read up to 63 words past the last END
+  const uint32_t endw = hword(1, c->qsa_off[1][c->qsa_index[1][QK_END][0][0]]);
+  prog.insert(prog.end(), 130, endw);   // the window + next-window prefetch read up to 127 words past the last END
   consts.resize(consts.size() + 16, 0);
   HIPCHK(T->cqdescs.upload(descs.data(), descs.size(), c->stream));
   HIPCHK(T->cqprog.upload(prog.data(), prog.size(), c->stream));
@@ -1828,6 +1869,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       q.n_funcs = (uint32_t)c->n_funcs;
       q.bool_masks = c->bmasks.as<uint64_t>();
       q.n_bool_masks = (uint32_t)c->n_bmask;
+      q.prof_out = prof_buffer(c);
       QArgs* dq = T->cqargs.as<QArgs>() + li;
       if (std::memcmp(&T->cqargs_host[li], &q, sizeof(QArgs)) != 0) {
         HIPCHK(hipMemcpyAsync(dq, &q, sizeof(QArgs), hipMemcpyHostToDevice, st));
@@ -1842,7 +1884,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       }
       HIPCHK(start_timer());
       HIPCHK(launch_qsa(1, dq, 8u * (unsigned)((groups + 3) / 4), (unsigned)rows,
-                        (size_t)q.lds_wave_bytes * 4 + (size_t)q.n_stage * 256, st));
+                        (size_t)q.lds_wave_bytes * 4 + (size_t)q.n_stage * 256 + 4 * (size_t)kQsaProfBytes, st));
     }
     for (int g = 0; g < kGen; g++) {
       const mq_tapes::Variant* v = g == 0 ? &v8 : &lv.v[g];
@@ -1900,6 +1942,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     q.n_funcs = (uint32_t)c->n_funcs;
     q.bool_masks = c->bmasks.as<uint64_t>();
     q.n_bool_masks = (uint32_t)c->n_bmask;
+    if (k == 1) q.prof_out = prof_buffer(c);
     // the argument block only changes with the output buffer / mode / models: re-upload then
     if (!T->qargs_valid[k] || std::memcmp(&T->qargs_dev_copy[k], &q, sizeof(QArgs)) != 0) {
       HIPCHK(hipMemcpyAsync(T->qargs[k].p, &q, sizeof(QArgs), hipMemcpyHostToDevice, st));
@@ -1919,7 +1962,8 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       }
     }
     HIPCHK(start_timer());
-    HIPCHK(launch_qsa(k, T->qargs[k].as<QArgs>(), gx, gy, (size_t)q.lds_wave_bytes * 4 + (size_t)q.n_stage * 256, st));
+    HIPCHK(launch_qsa(k, T->qargs[k].as<QArgs>(), gx, gy,
+                      (size_t)q.lds_wave_bytes * 4 + (size_t)q.n_stage * 256 + (k == 1 ? 4 * (size_t)kQsaProfBytes : 0), st));
   }
   for (const auto& v : cpp) {
     if (v.count <= 0) continue;
@@ -2201,7 +2245,27 @@ int mq_tapes_qsa_histogram(mq_tapes* T, int32_t which, int64_t* hist_out, int32_
 }
 
 const char* mq_qsa_kind_name(int32_t kind) {
+  if (kind >= QK_COUNT && kind < QK_COUNT + kQsaProfExtra) return kQsaProfExtraNames[kind - QK_COUNT];
   return (kind >= 0 && kind < QK_COUNT) ? kQsaKindNames[kind] : nullptr;
+}
+
+int mq_qsa_profile(mq_ctx* c, int64_t* out, int32_t cap, int32_t* n_out, int reset) {
+  if (!c || cap < 0 || (cap > 0 && !out)) return MQ_ERR_ARG;
+  const int n = kQsaProfBytes > 0 ? 2 * (QK_COUNT + kQsaProfExtra) : 0;
+  if (n_out) *n_out = n;
+  if (n == 0) return MQ_OK;
+  std::vector<int64_t> sum(n, 0);
+  for (mq_ctx* d : devices_of(c)) {
+    if (!d->prof.p) continue;
+    HIPCHK(hipSetDevice(d->device));
+    HIPCHK(hipDeviceSynchronize());
+    std::vector<int64_t> v(n);
+    HIPCHK(hipMemcpy(v.data(), d->prof.p, sizeof(int64_t) * n, hipMemcpyDeviceToHost));
+    for (int i = 0; i < n; i++) sum[i] += v[i];
+    if (reset) HIPCHK(hipMemset(d->prof.p, 0, (size_t)kQsaProfBytes));
+  }
+  for (int i = 0; i < std::min(n, cap); i++) out[i] = sum[i];
+  return MQ_OK;
 }
 
 int mq_tapes_column_split(mq_tapes* T, int32_t* n_asm, int32_t* live) {

@@ -89,6 +89,7 @@ struct QArgs {
   const uint64_t* bool_masks;    // 0x198 G: packed Bool rows, [tile][n_bool_masks] lane masks
   uint32_t n_bool_masks;         // 0x1a0
   uint32_t pad3;                 // 0x1a4
+  unsigned long long* prof_out;  // 0x1a8 G profile build only: (cycles, count) per handler kind
 };
 static_assert(sizeof(void*) == 8, "64-bit");
 static_assert(__builtin_offsetof(QArgs, M) == 0x40, "QArgs layout");
@@ -99,6 +100,7 @@ static_assert(__builtin_offsetof(QArgs, n_stage) == 0x184, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, stage_rows) == 0x190, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, bool_masks) == 0x198, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, n_bool_masks) == 0x1a0, "QArgs layout");
+static_assert(__builtin_offsetof(QArgs, prof_out) == 0x1a8, "QArgs layout");
 
 // variant 0 = P (preloaded variables, qsa_kernel), 1 = G (general, qsg_kernel)
 hipError_t launch_qsa(int variant, const QArgs* d_args, unsigned gx, unsigned gy, size_t lds, hipStream_t st);

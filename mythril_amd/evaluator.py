@@ -65,6 +65,7 @@ def load_library(path: str = LIB_PATH):
                                              C.POINTER(C.c_int32)]
         L.mq_qsa_kind_name.argtypes = [C.c_int32]
         L.mq_qsa_kind_name.restype = C.c_char_p
+        L.mq_qsa_profile.argtypes = [P, C.POINTER(C.c_int64), C.c_int32, C.POINTER(C.c_int32), C.c_int]
         L.mq_eval_verdicts.argtypes = [P, C.POINTER(MqTapeBatch), C.POINTER(C.c_uint8), C.POINTER(C.c_int32)]
         L.mq_eval_tapes_verdicts.argtypes = [P, P, C.POINTER(C.c_uint8), C.POINTER(C.c_int32)]
         L.mq_tapes_set_columns.argtypes = [P, C.POINTER(MqTapeBatch), C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_int32]
@@ -346,6 +347,22 @@ class Evaluator:
     def time_kernels(self, on: bool = True) -> None:
         """Bracket the evaluation kernels of every launch with HIP events (clears old ones)."""
         self.set_option(self.OPT_TIME_KERNELS, 1 if on else 0)
+
+    def qsa_profile(self, reset: bool = True) -> dict:
+        """G profile build only (gen_qsa.py QSA_PROF=1): {kind: (cycles, dispatches)} charged
+        since the last reset; {} in product builds."""
+        n = C.c_int32()
+        _check(self.lib.mq_qsa_profile(self.ctx, None, 0, C.byref(n), 0), "mq_qsa_profile")
+        if n.value == 0:
+            return {}
+        out = np.zeros(n.value, np.int64)
+        _check(self.lib.mq_qsa_profile(self.ctx, out.ctypes.data_as(C.POINTER(C.c_int64)), n.value, C.byref(n),
+                                       1 if reset else 0), "mq_qsa_profile")
+        res = {}
+        for i in range(n.value // 2):
+            if out[2 * i + 1]:
+                res[self.lib.mq_qsa_kind_name(i).decode()] = (int(out[2 * i]), int(out[2 * i + 1]))
+        return res
 
     def kernel_times(self, reset: bool = True) -> List[float]:
         """Per-launch device time (ms) of the evaluation kernels since the last reset."""

@@ -225,6 +225,11 @@ def _walk_cut(root: S.Term, cut: Dict[int, int]) -> List[S.Term]:
 
 
 _LEAVES = frozenset({S.SYM, S.VAL, S.TRUE, S.FALSE, S.ARRAY_SYM})
+# a model-table lookup (array select / UF application) counts as this many nodes toward the
+# hoisting size threshold: per (tape, model) it scans the model's entries with one memory round
+# trip each (~12 dispatches of work on the G kernel, profiles/r02s_profile_c3.txt), so a lookup
+# shared by several tapes is worth a column even when its term is small
+_LOOKUP_WEIGHT = 8
 
 
 def shared_subterms(roots: Sequence[S.Term], min_nodes: int = 8, min_tapes: int = 2) -> List[S.Term]:
@@ -243,7 +248,8 @@ def shared_subterms(roots: Sequence[S.Term], min_nodes: int = 8, min_tapes: int 
     def tree_size(t: S.Term) -> int:   # capped tree size (cheap, memoised)
         s = size.get(id(t))
         if s is None:
-            s = 1 + sum(0 if a.kind in _LEAVES else tree_size(a) for a in t.args)
+            s = (_LOOKUP_WEIGHT if t.kind in (S.SELECT, S.APP) else 1) + \
+                sum(0 if a.kind in _LEAVES else tree_size(a) for a in t.args)
             s = min(s, 1 << 20)
             size[id(t)] = s
         return s
