@@ -34,9 +34,11 @@ Register map (both):
 Programs are direct-threaded: each 32-bit word = (handler byte offset / 4) | imm << 16.
 Handler offsets are read back once per context by launching each kernel in mode 2.
 
-gfx950 hazard rule respected throughout: a VALU that writes an SGPR/VCC is followed by >= 2
-wait states before a VALU reads that SGPR (carry chains get s_nop 1; the MUL interleaves three
-carry registers) and >= 4 before a SALU reads it.
+gfx950 hazard rule respected throughout: a VALU that writes an SGPR/VCC is followed by >= 1 wait
+state before a VALU reads it as a carry (carry and borrow chains get s_nop 0, the padding LLVM's
+gfx950 hazard recognizer gives v_add_co -> v_addc; the MUL interleaves three carry registers),
+>= 2 before other VALU reads of it and >= 4 before a SALU reads it.  (tools/issue_probe.py: the
+s_nop 1 padding cost an ADD 45 instead of 36 SIMD cycles at 4 waves per SIMD.)
 
 Outputs: qsa_gen.inc (the two asm texts as C string literals + clobber list) and qsa_table.h
 (handler enumerations used by the host-side translator in mq_api.cpp).
@@ -289,7 +291,7 @@ def lt_chain(x, y, dst):
     cur = "s[34:35]"
     for l in range(1, L):
         nxt = dst if l == L - 1 else ("s[36:37]" if cur == "s[34:35]" else "s[34:35]")
-        out.append("s_nop 1")
+        out.append("s_nop 0")
         out.append(f"v_subb_co_u32_e64 v5, {nxt}, {xl(l)}, {yl(l)}, {cur}")
         cur = nxt
     return out
@@ -302,7 +304,7 @@ def flip_signs(d):
 def carry_chain(first, rest, n=L):
     out = [first(0)]
     for l in range(1, n):
-        out.append("s_nop 1")
+        out.append("s_nop 0")
         out.append(rest(l))
     return out
 

@@ -162,8 +162,9 @@ struct mq_tapes {
   std::vector<uint32_t> stage_rows;
   DevBuf stage_dev;
   // handler-kind histograms of the current translation (mq_tapes_qsa_histogram): [0] P tapes,
-  // [1] G tapes, [2] G column programs; qpairs = (kind, next kind) counts over the G tapes
-  std::vector<int64_t> qhist[3], qpairs;
+  // [1] G tapes, [2] G column programs; qpairs = (kind, next kind) counts over the G tapes,
+  // qpairs_p over the P tapes
+  std::vector<int64_t> qhist[3], qpairs, qpairs_p;
   DevBuf qdescs, qprog, qargs[2];
   QArgs qargs_dev_copy[2];   // what qargs[k] currently holds on the device
   bool qargs_valid[2] = {false, false};
@@ -1637,6 +1638,7 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
   T->qhist[0].assign(QK_COUNT, 0);
   T->qhist[1].assign(QK_COUNT, 0);
   T->qpairs.assign((size_t)QK_COUNT * QK_COUNT, 0);
+  T->qpairs_p.assign((size_t)QK_COUNT * QK_COUNT, 0);
   for (size_t i = 0; i < T->qct.size(); i++) {
     int k = 0;
     if (!on_p[i] || !qsa_translate(c, 0, true, T->qct[i], &tr, &extra)) {
@@ -1644,7 +1646,7 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
       if (!qsa_translate(c, 1, true, T->qct[i], &tr, &extra, &T->gpre, &T->gstage)) return MQ_OK;
       qsa_window_layout(c, tr);
     }
-    qsa_count(c, k, tr, T->qhist[k], k == 1 ? &T->qpairs : nullptr);
+    qsa_count(c, k, tr, T->qhist[k], k == 1 ? &T->qpairs : &T->qpairs_p);
     GDesc d = T->qbase[i];
     d.prog_off = (uint32_t)words[k].size();
     d.prog_len = (uint32_t)tr.size();
@@ -2240,7 +2242,8 @@ int mq_tapes_qsa_histogram(mq_tapes* T, int32_t which, int64_t* hist_out, int32_
   if (pairs_out)
     for (int i = 0; i < n; i++)
       for (int j = 0; j < n; j++)
-        pairs_out[(size_t)i * n + j] = (which == 1 && !T->qpairs.empty()) ? T->qpairs[(size_t)i * QK_COUNT + j] : 0;
+        pairs_out[(size_t)i * n + j] = (which == 1 && !T->qpairs.empty()) ? T->qpairs[(size_t)i * QK_COUNT + j]
+                                       : (which == 0 && !T->qpairs_p.empty()) ? T->qpairs_p[(size_t)i * QK_COUNT + j] : 0;
   return MQ_OK;
 }
 

@@ -23,8 +23,9 @@ for which, name in ((0, "P tapes"), (1, "G tapes"), (2, "G columns")):
     print(f"== {name}: {tot} dispatches per model")
     for k, v in sorted(h.items(), key=lambda kv: -kv[1])[:30]:
         print(f"  {k:16s} {v:9d} {100 * v / max(tot, 1):5.1f}%")
-h, pr = ct.handler_histogram(1, pairs=True)
-tot = sum(pr.values())
-print(f"== G bigrams ({tot})")
-for (a, b), v in sorted(pr.items(), key=lambda kv: -kv[1])[:40]:
-    print(f"  {a:16s} -> {b:16s} {v:9d} {100 * v / max(tot, 1):5.1f}%")
+for which, name in ((0, "P"), (1, "G")):
+    h, pr = ct.handler_histogram(which, pairs=True)
+    tot = sum(pr.values())
+    print(f"== {name} bigrams ({tot})")
+    for (a, b), v in sorted(pr.items(), key=lambda kv: -kv[1])[:40]:
+        print(f"  {a:16s} -> {b:16s} {v:9d} {100 * v / max(tot, 1):5.1f}%")
