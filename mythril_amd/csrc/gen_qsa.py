@@ -365,6 +365,53 @@ def mul_body(d, bl=None):
     return out
 
 
+def mul_to(al, bl, rbase, rel1=False):
+    """v[rbase + k] = word k of a * b mod 2^256 (al(i) / bl(j) = registers of limb i / j; rbase
+    even): mul_body's Comba columns with the even columns accumulating in the result block itself,
+    for operands that are not the destination (no final copy).  rel1: the adds keep their VGPR in
+    src0, so an s_set_gpr_idx_on ... gpr_idx(SRC1) that relocates b's registers leaves them alone."""
+    C = ["s[34:35]", "s[36:37]", "s[38:39]"]
+
+    def R(k):
+        return f"v{rbase + k}"
+
+    def pair(k):
+        if k % 2 == 0:
+            return f"v[{rbase + k}:{rbase + k + 1}]", R(k), R(k + 1)
+        return "v[4:5]", "v4", "v5"
+
+    def addc(ohi, t, c):
+        if rel1:
+            return f"v_addc_co_u32_e64 {ohi}, s[60:61], {'0' if t == 0 else ohi}, 0, {c}"
+        return f"v_addc_co_u32_e64 {ohi}, s[60:61], 0, {'0' if t == 0 else ohi}, {c}"
+
+    p0, lo0, hi0 = pair(0)
+    out = [f"v_mad_u64_u32 {p0}, s[60:61], {al(0)}, {bl(0)}, 0",
+           f"v_mov_b32 v4, {hi0}", "v_mov_b32 v5, 0"]
+    for k in range(1, L):
+        pr, lo, hi = pair(k)
+        prods = [(i, k - i) for i in range(k + 1)]
+        if k == L - 1:
+            for i, j in prods:
+                out.append(f"v_mad_u64_u32 {pr}, s[60:61], {al(i)}, {bl(j)}, {pr}")
+            out.append(f"v_mov_b32 {R(7)}, {lo}")
+            break
+        _, _, ohi = pair(k + 1)
+        mads = [f"v_mad_u64_u32 {pr}, {C[t % 3]}, {al(i)}, {bl(j)}, {pr}" for t, (i, j) in enumerate(prods)]
+        adds = [addc(ohi, t, C[t % 3]) for t in range(len(prods))]
+        n = len(prods)
+        for t in range(n):
+            out.append(mads[t])
+            if t >= 2:
+                out.append(adds[t - 2])
+        out += (["s_nop 0"] if n == 2 else []) + [adds[t] for t in range(max(0, n - 2), n)]
+        if k % 2 == 0:
+            out += [f"v_mov_b32 v4, {hi}"]
+        else:
+            out += [f"v_mov_b32 {R(k)}, v4", f"v_mov_b32 {R(k + 1)}, v5"]
+    return out
+
+
 def lshr_body(d, q, arith):
     """S[d] >>= 32q + s in place (s = imm, 0..31): limb l = (S[l+q+1] : S[l+q]) >> s, ascending
     so every source is read before it is overwritten; ASHR fills with the sign word v4."""
@@ -840,6 +887,45 @@ def make_handlers(variant, pfx):
                 H(("UGTV", d, v), lt_chain(vl, xa, B(a)))
                 H(("ULEV", d, v), lt_chain(vl, xa, "s[38:39]") + ["s_nop 3", f"s_not_b64 {B(a)}, s[38:39]"])
                 H(("UGEV", d, v), lt_chain(xa, vl, "s[38:39]") + ["s_nop 3", f"s_not_b64 {B(a)}, s[38:39]"])
+    # ---- P: binary ops whose BOTH operands are leaves (the translator fuses "PUSH_VAR v1 / PUSH_CONST
+    # c at slot x; PUSH_VAR v2; OP" into one handler at slot x): the right variable v2 is addressed
+    # through M0 (s_set_gpr_idx_on, imm = 8 * v2 in the low byte of an index word), so one handler
+    # serves every v2; no operand copies and one dispatch instead of two
+    #   kindVV (x, v1): S[x] = V[v1] OP V[v2]            imm = 8 * v2
+    #   MULVV (x):      S[x] = V[v1] * V[v2]              imm = 8 * v1 | (8 * v2) << 16
+    #   kindCV (x):     S[x] = C OP V[v2]                 imm = const word offset | (8 * v2) << 16
+    if not G:
+        def vr(l):   # limb l of the M0-relocated variable (V[0] + 8 * v2)
+            return f"v{VBASE + l}"
+        on1 = ["s_set_gpr_idx_on s17, gpr_idx(SRC1)"]
+        off = ["s_set_gpr_idx_off"]
+        for x in range(D - 1):
+            for v1 in range(NV):
+                def v1l(l, v1=v1):
+                    return f"v{VBASE + 8 * v1 + l}"
+                H(("ADDVV", x, v1), on1 + carry_chain(lambda l: f"v_add_co_u32 {S(x, l)}, vcc, {v1l(l)}, {vr(l)}",
+                                                      lambda l: f"v_addc_co_u32 {S(x, l)}, vcc, {v1l(l)}, {vr(l)}, vcc") + off)
+                H(("SUBVV", x, v1), on1 + carry_chain(lambda l: f"v_sub_co_u32 {S(x, l)}, vcc, {v1l(l)}, {vr(l)}",
+                                                      lambda l: f"v_subb_co_u32 {S(x, l)}, vcc, {v1l(l)}, {vr(l)}, vcc") + off)
+                for nm, ins in (("BANDVV", "v_and_b32"), ("BORVV", "v_or_b32"), ("BXORVV", "v_xor_b32")):
+                    H((nm, x, v1), on1 + [f"{ins} {S(x, l)}, {v1l(l)}, {vr(l)}" for l in range(L)] + off)
+            # MULVV: V[v1] copied into S[x] through an SRC0-relocated index, then the MULV body
+            H(("MULVV", x), ["s_set_gpr_idx_on s17, gpr_idx(SRC0)"] + [f"v_mov_b64 {S2(x, l)}, {V2(0, l)}" for l in range(0, L, 2)]
+              + ["s_set_gpr_idx_off", "s_lshr_b32 s35, s17, 16", "s_set_gpr_idx_on s35, gpr_idx(SRC1)"]
+              + mul_to(lambda i: S(x, i), vr, TBASE, rel1=True)
+              + [f"v_mov_b64 {S2(x, l)}, v[{TBASE + l}:{TBASE + l + 1}]" for l in range(0, L, 2)] + off)
+            ld = ["s_and_b32 s34, s17, 0xffff", "s_lshl_b32 s34, s34, 2", "s_load_dwordx8 s[64:71], s[20:21], s34",
+                  "s_lshr_b32 s35, s17, 16", "s_set_gpr_idx_on s35, gpr_idx(SRC1)", "s_waitcnt lgkmcnt(0)"]
+            # carry chains read VCC besides their operands (one SGPR per VALU): the constant goes to
+            # T first, as in ADDC
+            tl = [f"v_mov_b64 v[{TBASE + l}:{TBASE + l + 1}], s[{64 + l}:{65 + l}]" for l in range(0, L, 2)]
+            H(("ADDCV", x), ld + tl + carry_chain(lambda l: f"v_add_co_u32 {S(x, l)}, vcc, {T(l)}, {vr(l)}",
+                                                  lambda l: f"v_addc_co_u32 {S(x, l)}, vcc, {T(l)}, {vr(l)}, vcc") + off)
+            H(("SUBCV", x), ld + tl + carry_chain(lambda l: f"v_sub_co_u32 {S(x, l)}, vcc, {T(l)}, {vr(l)}",
+                                                  lambda l: f"v_subb_co_u32 {S(x, l)}, vcc, {T(l)}, {vr(l)}, vcc") + off)
+            for nm, ins in (("BANDCV", "v_and_b32"), ("BORCV", "v_or_b32"), ("BXORCV", "v_xor_b32")):
+                H((nm, x), ld + [f"{ins} {S(x, l)}, s{64 + l}, {vr(l)}" for l in range(L)] + off)
+            H(("MULCV", x), ld + mul_to(lambda i: f"s{64 + i}", vr, SBASE + 8 * x, rel1=True) + off)
     # ---- Bool producers fused with the AND / OR that consumes their result (kind_A / kind_O):
     # the translator rewrites "X; AND" into "X_A" when X leaves its result at the AND's right
     # slot, one dispatch instead of two (AND / OR are ~30 % of the dispatches of EVM-shaped tapes)

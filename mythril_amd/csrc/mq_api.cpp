@@ -722,8 +722,8 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
     out.resize(log[log.size() - n].pos);
     log.resize(log.size() - n);
   };
-  auto word = [&](int kind, int d, int v, uint32_t imm) -> bool {
-    if (d < 0 || d >= kQsaStack || v < -1 || v >= kQsaSel || imm > 0xFFFFu) return false;
+  auto word = [&](int kind, int d, int v, uint32_t imm, bool imm32 = false) -> bool {
+    if (d < 0 || d >= kQsaStack || v < -1 || v >= kQsaSel || (imm > 0xFFFFu && !(imm32 && P))) return false;
     const int h = c->qsa_index[k][kind][d][v + 1];
     if (h < 0) return false;
     log.push_back(Emit{out.size(), kind, d, v, imm, 0});
@@ -867,6 +867,31 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
     if (prev_op == G_PUSH_VAR && prev_pre >= 0 && (int)prev_d == d && out.size() == prev_out + wpi &&
         c->qsa_index[k][kindv][d][prev_pre + 1] >= 0) {
       drop_last(1);
+      // (P) the left operand is a leaf pushed right before at slot d - 1: both leaves in one
+      // handler at d - 1 (gen_qsa.py kindVV / MULVV / kindCV, the right variable through M0)
+      int kvv = -1, kcv = -1;
+      bool vv_by_v1 = true;
+      switch (kindv) {
+        case QK_ADDV: kvv = QK_ADDVV; kcv = QK_ADDCV; break;
+        case QK_SUBV: kvv = QK_SUBVV; kcv = QK_SUBCV; break;
+        case QK_BANDV: kvv = QK_BANDVV; kcv = QK_BANDCV; break;
+        case QK_BORV: kvv = QK_BORVV; kcv = QK_BORCV; break;
+        case QK_BXORV: kvv = QK_BXORVV; kcv = QK_BXORCV; break;
+        case QK_MULV: kvv = QK_MULVV; kcv = QK_MULCV; vv_by_v1 = false; break;
+        default: break;
+      }
+      if (P && kvv >= 0 && d >= 1 && !log.empty() && out.size() == ends_at(log.back()) && log.back().d == d - 1) {
+        const Emit e0 = log.back();
+        const uint32_t v2 = 8u * (uint32_t)prev_pre;
+        if (e0.kind == QK_PUSH_VAR && e0.v >= 0 && c->qsa_index[k][kvv][d - 1][vv_by_v1 ? e0.v + 1 : 0] >= 0) {
+          drop_last(1);
+          return vv_by_v1 ? word(kvv, d - 1, e0.v, v2) : word(kvv, d - 1, -1, 8u * (uint32_t)e0.v | v2 << 16, true);
+        }
+        if (e0.kind == QK_PUSH_CONST && c->qsa_index[k][kcv][d - 1][0] >= 0) {
+          drop_last(1);
+          return word(kcv, d - 1, -1, e0.imm | v2 << 16, true);
+        }
+      }
       return word(kindv, d, prev_pre, 0);
     }
     if (kindc >= 0 && P && prev_op == G_PUSH_CONST && (int)prev_d == d && out.size() == prev_out + wpi &&
@@ -1914,7 +1939,9 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     // G: 64-model tiles, 4 tape groups per workgroup (one per wave), XCD-interleaved grid
     //    (qsa.hip); groups of g_tapes_per_group() tapes.
     const int64_t tiles256 = (c->M + 255) / 256;
-    int64_t tpg = k == 0 ? (int64_t(n) * tiles256 + 8191) / 8192 : g_tapes_per_group(n, c->M);
+    int64_t p_wg = 8192;   // P: target workgroup count (MQ_P_WG overrides)
+    if (const char* e = std::getenv("MQ_P_WG")) p_wg = std::max(256L, std::atol(e));
+    int64_t tpg = k == 0 ? (int64_t(n) * tiles256 + p_wg - 1) / p_wg : g_tapes_per_group(n, c->M);
     tpg = std::max<int64_t>(1, std::min<int64_t>(tpg, n));
     QArgs q{};
     q.descs = T->qdescs.as<GDesc>() + (k == 0 ? 0 : T->q_count[0]);

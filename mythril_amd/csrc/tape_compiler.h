@@ -13,7 +13,7 @@ constexpr int kMaxWidth = 2048;   // widest value a tape may hold (64 limbs)
 
 // keccak-f[1600] cost per absorbed 136-byte block in 32-bit VALU ops; the
 // per-block instruction mix is counted in profiles/ 
-constexpr double kKeccakOpsPerBlock = 8000.0;
+constexpr double kKeccakOpsPerBlock = 7974.0;  // counted: SQ_INSTS_VALU per lane, 2-block minus 1-block messages (profiles/r02tr/kec_{64,200}.json)
 
 struct CompiledTape {
   bool supported = false;

@@ -19,7 +19,8 @@ from ._abi import MqDagBatch, MqModelBatch, MqNode, MqStats, MqTapeBatch, as_dag
 from .models import ModelBatch
 from .tape import TapeBatch
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmq.so")
+# MQ_LIB: another build of the library (diagnostic A/B runs of generator variants)
+LIB_PATH = os.environ.get("MQ_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmq.so")
 NO_HIT = -1
 UNSUPPORTED = -2
 

@@ -185,6 +185,56 @@ def test_asm_fuzz_matches_oracle_and_generic(evaluator, seed):
     assert (v_gen == ref).all()
 
 
+def _leaf_pair_tapes(rng, n_tapes, n_vars=8):
+    """256-bit tapes whose binary ops have two leaf operands (var/var, const/var, var/const) under
+    ADD/SUB/AND/OR/XOR/MUL, combined and compared: the P translator's leaf-pair fusions."""
+    ops = ("add", "sub", "band", "bor", "bxor", "mul")
+    tapes = []
+    for _ in range(n_tapes):
+        t = Tape()
+
+        def leaf(kind):
+            if kind == "v":
+                return t.var(int(rng.integers(n_vars)), 256)
+            return t.const(int.from_bytes(rng.bytes(32), "little") >> int(rng.integers(0, 250)), 256)
+
+        def pair():
+            a, b = [("v", "v"), ("c", "v"), ("v", "c")][int(rng.integers(3))]
+            return getattr(t, ops[int(rng.integers(len(ops)))])(leaf(a), leaf(b))
+
+        cmps = []
+        for _ in range(3):
+            x = t.add(pair(), pair()) if rng.random() < 0.5 else t.mul(pair(), pair())
+            y = pair()
+            cmps.append(t.ult(x, y) if rng.random() < 0.7 else t.not_(t.eq(x, y)))
+        tapes.append(t.finish(t.and_(*cmps)))
+    return TapeBatch(tapes)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_p_leaf_pair_fusions_match_oracle(evaluator, seed):
+    """Both-leaf operations run as one P handler (kindVV / MULVV / kindCV, the right variable
+    addressed through M0): bit-exact verdicts and first hits against the oracle."""
+    rng = np.random.default_rng(100 + seed)
+    tb = _leaf_pair_tapes(rng, 300)
+    M = 777
+    mb = ModelBatch([256] * 8, rng.integers(0, 1 << 32, (64, M), dtype=np.uint64).astype(np.uint32))
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    v, _ = evaluator.verdicts(tb)
+    ref = cref.verdicts(tb, mb)
+    assert 0 < ref.sum() < ref.size
+    mism = np.argwhere(v != ref)
+    assert len(mism) == 0, f"{len(mism)} mismatches, first {mism[:5]}"
+    fh_ref, _ = cref.first_hit(tb, mb)
+    assert (evaluator.first_hit(ct) == fh_ref).all()
+    assert ct.asm_split()[0] == tb.n_tapes
+    hist = ct.handler_histogram(0)
+    for kind in ("ADDVV", "SUBVV", "BANDVV", "BORVV", "BXORVV", "MULVV", "ADDCV", "SUBCV", "BANDCV", "BORCV",
+                 "BXORCV", "MULCV"):
+        assert hist.get(kind, 0) > 0, (kind, hist)
+
+
 def test_golden_vectors_generic_kernel(evaluator):
     """The same golden fixtures with the assembly path disabled (HIP C++ interpreter only)."""
     entries = load("shift_vectors.json") + load("vmtests_kats.json")
