@@ -147,15 +147,25 @@ def next_g():
 NEXT_G = next_g()
 
 
-# P: two-word program entries (absolute low 32 bits of the handler address, immediate),
-# prefetched one entry ahead into s[96:97]; s[14:15] = program base, s16 = byte offset of the
-# next entry, s19 = high half of the handler addresses (the host checks they share it).
+# P: three-word program entries (absolute low 32 bits of the handler address, immediate,
+# constant-prefetch byte offset), prefetched one entry ahead into s[96:98] (an x4 load: the
+# fourth word belongs to the next entry); s[14:15] = program base, s16 = byte offset of the next
+# entry, s19 = high half of the handler addresses (the host checks they share it).
+# Constant prefetch: the tail that dispatches entry k also loads the 8 words at the tape's
+# constants + entry k's third word into CB = s[80:87], so the constant of entry k + 1 arrives
+# while handler k runs; the PF_ handler variants read it from there instead of issuing their own
+# scalar load and waiting (mq_api.cpp qsa_translate assigns them: never two in a row, and the
+# entry of a PF_ handler whose successor is not one re-loads its own constant, so an in-flight
+# load never changes what a running handler reads).  The frame keeps the descriptor words the
+# tape end needs in s78 / s79 / s100 (s[80:87] is CB while a tape runs).
+PF_CB = 80
 NEXT_P = [
     "s_waitcnt lgkmcnt(0)",
     "s_mov_b32 s18, s96",
     "s_mov_b32 s17, s97",
-    "s_load_dwordx2 s[96:97], s[14:15], s16",
-    "s_add_u32 s16, s16, 8",
+    f"s_load_dwordx8 s[{PF_CB}:{PF_CB + 7}], s[20:21], s98",
+    "s_load_dwordx4 s[96:99], s[14:15], s16",
+    "s_add_u32 s16, s16, 12",
     "s_setpc_b64 s[18:19]",
 ]
 
@@ -926,6 +936,31 @@ def make_handlers(variant, pfx):
             for nm, ins in (("BANDCV", "v_and_b32"), ("BORCV", "v_or_b32"), ("BXORCV", "v_xor_b32")):
                 H((nm, x), ld + [f"{ins} {S(x, l)}, s{64 + l}, {vr(l)}" for l in range(L)] + off)
             H(("MULCV", x), ld + mul_to(lambda i: f"s{64 + i}", vr, SBASE + 8 * x, rel1=True) + off)
+            # prefetched-constant variants: the constant is already in CB (see NEXT_P)
+            cb = (lambda l: f"s{PF_CB + l}")
+            pfo = ["s_lshr_b32 s35, s17, 16", "s_set_gpr_idx_on s35, gpr_idx(SRC1)"]
+            tlb = [f"v_mov_b64 v[{TBASE + l}:{TBASE + l + 1}], s[{PF_CB + l}:{PF_CB + 1 + l}]" for l in range(0, L, 2)]
+            H(("PF_ADDCV", x), pfo + tlb + carry_chain(lambda l: f"v_add_co_u32 {S(x, l)}, vcc, {T(l)}, {vr(l)}",
+                                                       lambda l: f"v_addc_co_u32 {S(x, l)}, vcc, {T(l)}, {vr(l)}, vcc") + off)
+            H(("PF_SUBCV", x), pfo + tlb + carry_chain(lambda l: f"v_sub_co_u32 {S(x, l)}, vcc, {T(l)}, {vr(l)}",
+                                                       lambda l: f"v_subb_co_u32 {S(x, l)}, vcc, {T(l)}, {vr(l)}, vcc") + off)
+            for nm, ins in (("PF_BANDCV", "v_and_b32"), ("PF_BORCV", "v_or_b32"), ("PF_BXORCV", "v_xor_b32")):
+                H((nm, x), pfo + [f"{ins} {S(x, l)}, {cb(l)}, {vr(l)}" for l in range(L)] + off)
+            H(("PF_MULCV", x), pfo + mul_to(cb, vr, SBASE + 8 * x, rel1=True) + off)
+        for d in range(D):
+            H(("PF_PUSH_CONST", d), [f"v_mov_b64 {S2(d, l)}, s[{PF_CB + l}:{PF_CB + 1 + l}]" for l in range(0, L, 2)],
+              reads_stack=False)
+        for d in range(1, D):
+            a = d - 1
+            cb = (lambda l: f"s{PF_CB + l}")
+            for nm, ins in (("PF_BANDC", "v_and_b32"), ("PF_BORC", "v_or_b32"), ("PF_BXORC", "v_xor_b32")):
+                H((nm, d), [f"{ins} {S(a, l)}, {cb(l)}, {S(a, l)}" for l in range(L)])
+            H(("PF_MULC", d), mul_body(d, cb))
+            tlb = [f"v_mov_b64 v[{TBASE + l}:{TBASE + l + 1}], s[{PF_CB + l}:{PF_CB + 1 + l}]" for l in range(0, L, 2)]
+            H(("PF_ADDC", d), tlb + carry_chain(lambda l: f"v_add_co_u32 {S(a, l)}, vcc, {S(a, l)}, {T(l)}",
+                                                lambda l: f"v_addc_co_u32 {S(a, l)}, vcc, {S(a, l)}, {T(l)}, vcc"))
+            H(("PF_SUBC", d), tlb + carry_chain(lambda l: f"v_sub_co_u32 {S(a, l)}, vcc, {S(a, l)}, {T(l)}",
+                                                lambda l: f"v_subb_co_u32 {S(a, l)}, vcc, {S(a, l)}, {T(l)}, vcc"))
     # ---- Bool producers fused with the AND / OR that consumes their result (kind_A / kind_O):
     # the translator rewrites "X; AND" into "X_A" when X leaves its result at the AND's right
     # slot, one dispatch instead of two (AND / OR are ~30 % of the dispatches of EVM-shaped tapes)
@@ -1030,6 +1065,8 @@ def ee_window():
 
 def frame(variant, pfx, handlers, subs):
     G = variant == "g"
+    # descriptor words the tape end reads: node count, algorithmic ops, tape index (P: copies)
+    DN, DA, DT = ("s84", "s87", "s82") if G else ("s78", "s79", "s100")
     P = []
     P += [
         "s_mov_b64 s[10:11], %0",
@@ -1222,8 +1259,12 @@ def frame(variant, pfx, handlers, subs):
         "s_lshl_b32 s34, s80, 2",
         "s_add_u32 s14, s46, s34",
         "s_addc_u32 s15, s47, 0",
-        "s_load_dwordx2 s[96:97], s[14:15], 0x0",
-        "s_mov_b32 s16, 8",
+        "s_load_dwordx4 s[96:99], s[14:15], 0x0",
+        "s_mov_b32 s16, 12",
+        # the tape end's descriptor words, out of CB (s[80:87]) before the first prefetch
+        "s_mov_b32 s78, s84",
+        "s_mov_b32 s79, s87",
+        "s_mov_b32 s100, s82",
     ] + NEXT_P) + [
         f"{pfx}_tape_end:",
         "s_waitcnt lgkmcnt(0)",
@@ -1231,12 +1272,12 @@ def frame(variant, pfx, handlers, subs):
         "s_bcnt1_i32_b64 s38, s[62:63]",
         "s_add_u32 s40, s40, s38",
         "s_addc_u32 s41, s41, 0",
-        "s_mul_i32 s60, s38, s84",
-        "s_mul_hi_u32 s61, s38, s84",
+        f"s_mul_i32 s60, s38, {DN}",
+        f"s_mul_hi_u32 s61, s38, {DN}",
         "s_add_u32 s42, s42, s60",
         "s_addc_u32 s43, s43, s61",
-        "s_mul_i32 s60, s38, s87",
-        "s_mul_hi_u32 s61, s38, s87",
+        f"s_mul_i32 s60, s38, {DA}",
+        f"s_mul_hi_u32 s61, s38, {DA}",
         "s_add_u32 s44, s44, s60",
         "s_addc_u32 s45, s45, s61",
     ] + ([
@@ -1257,8 +1298,8 @@ def frame(variant, pfx, handlers, subs):
         "s_mov_b64 exec, s[60:61]",
         f"s_branch {pfx}_next_tape",
         f"{pfx}_store_verdict:",
-        "s_mul_i32 s38, s82, s29",
-        "s_mul_hi_u32 s39, s82, s29",
+        f"s_mul_i32 s38, {DT}, s29",
+        f"s_mul_hi_u32 s39, {DT}, s29",
         "s_add_u32 s38, s38, s94",
         "s_addc_u32 s39, s39, s95",
         f"v_cndmask_b32_e64 v5, 0, 1, {B(0)}",
@@ -1353,7 +1394,7 @@ def source_stamp() -> str:
 
 def main():
     stamp = source_stamp()
-    sclob = [f'"s{i}"' for i in range(10, 102 if PROF else 100) if i not in (32, 33)] + ['"vcc"', '"scc"', '"memory"']
+    sclob = [f'"s{i}"' for i in range(10, 102) if i not in (32, 33)] + ['"vcc"', '"scc"', '"memory"']
     clob = {v: [f'"v{i}"' for i in range(1, vgprs(v))] + sclob for v in ("p", "g")}
     gen = {}
     for variant, pfx, macro, suffix in VARIANTS:

@@ -672,7 +672,7 @@ static unsigned long long* prof_buffer(mq_ctx* c) {
   return c->prof.as<unsigned long long>();
 }
 
-// Count the handler kinds of one translated program (k = 0: P two-word entries; 1: G words,
+// Count the handler kinds of one translated program (k = 0: P three-word entries; 1: G words,
 // inline constant words skipped) into hist[QK_COUNT] and, if given, kind bigrams into pairs.
 static void qsa_count(const mq_ctx* c, int k, const std::vector<uint32_t>& tr, std::vector<int64_t>& hist,
                       std::vector<int64_t>* pairs) {
@@ -682,7 +682,7 @@ static void qsa_count(const mq_ctx* c, int k, const std::vector<uint32_t>& tr, s
   for (size_t i = 0; i < tr.size();) {
     const uint32_t key = k == 0 ? ((tr[i] - c->qsa_hbase_lo[0]) >> 2) & 0xFFFFu : tr[i] & 0xFFFFu;
     const int kind = c->qsa_kind_of[k].empty() ? -1 : c->qsa_kind_of[k][key];
-    i += k == 0 ? 2 : 1;
+    i += k == 0 ? 3 : 1;
     if (kind < 0) continue;
     hist[kind]++;
     if (pairs && prev >= 0 && kind != QK_REFILL) (*pairs)[(size_t)prev * QK_COUNT + kind]++;
@@ -707,7 +707,7 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
   extra.clear();
   if (x.L != 8 || x.depth > kQsaStack) return false;
   const bool P = k == 0;
-  const size_t wpi = P ? 2 : 1;   // program words per interpreter instruction
+  const size_t wpi = P ? 3 : 1;   // program words per interpreter instruction
   // every handler word emitted so far (position, key, immediate, inline data words): the
   // fusions below rewrite the last ones while nothing follows them
   struct Emit {
@@ -727,9 +727,10 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
     const int h = c->qsa_index[k][kind][d][v + 1];
     if (h < 0) return false;
     log.push_back(Emit{out.size(), kind, d, v, imm, 0});
-    if (P) {   // two-word entry: absolute handler address (low half), immediate
+    if (P) {   // entry: absolute handler address (low half), immediate, constant prefetch
       out.push_back(c->qsa_hbase_lo[0] + c->qsa_off[0][h]);
       out.push_back(imm);
+      out.push_back(0);
     } else {
       out.push_back(hword(k, c->qsa_off[k][h]) | (imm << 16));
     }
@@ -1110,6 +1111,46 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
     prev_out = out_before;
     prev_pre = op == G_PUSH_VAR ? pushed_pre : -1;
   }
+  if (P) {
+    // constant prefetch (gen_qsa.py NEXT_P): a constant handler whose predecessor is not itself
+    // a prefetched one becomes its PF_ variant, and the predecessor's entry names its constant
+    // (the dispatch of the predecessor loads it into CB); a PF_ handler whose successor is not
+    // one re-loads its own constant (an in-flight load then writes CB's current contents)
+    auto pf_kind = [](int kind) -> int {
+      switch (kind) {
+        case QK_PUSH_CONST: return QK_PF_PUSH_CONST;
+        case QK_ADDC: return QK_PF_ADDC;
+        case QK_SUBC: return QK_PF_SUBC;
+        case QK_MULC: return QK_PF_MULC;
+        case QK_BANDC: return QK_PF_BANDC;
+        case QK_BORC: return QK_PF_BORC;
+        case QK_BXORC: return QK_PF_BXORC;
+        case QK_ADDCV: return QK_PF_ADDCV;
+        case QK_SUBCV: return QK_PF_SUBCV;
+        case QK_MULCV: return QK_PF_MULCV;
+        case QK_BANDCV: return QK_PF_BANDCV;
+        case QK_BORCV: return QK_PF_BORCV;
+        case QK_BXORCV: return QK_PF_BXORCV;
+        default: return -1;
+      }
+    };
+    std::vector<char> pf(log.size(), 0);
+    auto coff_bytes = [&](const Emit& e) -> uint32_t {
+      const bool cv = e.kind == QK_ADDCV || e.kind == QK_SUBCV || e.kind == QK_MULCV || e.kind == QK_BANDCV ||
+                      e.kind == QK_BORCV || e.kind == QK_BXORCV;
+      return 4u * (cv ? (e.imm & 0xFFFFu) : e.imm);
+    };
+    for (size_t j = 1; j < log.size(); j++) {
+      const Emit& e = log[j];
+      const int fk = pf_kind(e.kind);
+      if (fk < 0 || pf[j - 1] || c->qsa_index[0][fk][e.d][e.v + 1] < 0) continue;
+      pf[j] = 1;
+      out[e.pos] = c->qsa_hbase_lo[0] + c->qsa_off[0][c->qsa_index[0][fk][e.d][e.v + 1]];
+      out[log[j - 1].pos + 2] = coff_bytes(e);
+    }
+    for (size_t j = 0; j < log.size(); j++)
+      if (pf[j] && !(j + 1 < log.size() && pf[j + 1])) out[log[j].pos + 2] = coff_bytes(log[j]);
+  }
   return x.consts.size() + extra.size() <= 0x10000u;
 }
 
@@ -1187,6 +1228,8 @@ static int tapes_upload_one(mq_ctx* c, int32_t n_tapes, const std::vector<Compil
   HIPCHK(T->qargs[0].ensure(sizeof(QArgs)));
   HIPCHK(T->qargs[1].ensure(sizeof(QArgs)));
   HIPCHK(T->prog.upload(prog.data(), prog.size(), c->stream));
+  // P's constant prefetch reads 8 words at a tape's constants + 0 even for a tape without any
+  consts.insert(consts.end(), 8, 0u);
   HIPCHK(T->consts.upload(consts.data(), consts.size(), c->stream));
   HIPCHK(T->unsup_dev.upload(T->unsupported.data(), T->unsupported.size(), c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -1692,11 +1735,13 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
     prog.insert(prog.end(), words[k].begin(), words[k].end());
     const uint32_t endo = c->qsa_off[k][c->qsa_index[k][QK_END][0][0]];
     const uint32_t endw = hword(1, endo);
-    if (k == 0) {   // P entries are (handler address, imm) pairs
+    if (k == 0) {   // P entries are (handler address, imm, prefetch); the x4 entry load reads one more word
       for (int r = 0; r < 2; r++) {
         prog.push_back(c->qsa_hbase_lo[0] + endo);
         prog.push_back(0);
+        prog.push_back(0);
       }
+      prog.push_back(0);
     } else {
       prog.push_back(endw);
       prog.push_back(endw);
