@@ -1245,7 +1245,11 @@ def frame(variant, pfx, handlers, subs):
         # up the tape's first operand wait by a coherent round trip; the window is re-gathered
         # every 64 tapes, and hits found meanwhile only cost tapes a fresher value would skip)
     ] if ee else [
-        "s_load_dword s34, s[72:73], 0x0 glc",
+        # best[tape] through the scalar cache, NOT glc: a coherent read is an L2 round trip per
+        # tape that every wave waits for (C2 28.3 -> 24.1 ms without it).  A stale value only
+        # skips less: best[] only decreases within a launch (atomicMin from INT32_MAX, set by
+        # qs_init_best before it), and the dispatch's acquire invalidates the scalar cache
+        "s_load_dword s34, s[72:73], 0x0",
         "s_waitcnt lgkmcnt(0)",
         "s_cmp_ge_i32 s28, s34",
         f"s_cbranch_scc1 {pfx}_next_tape",

@@ -803,7 +803,9 @@ __global__ __launch_bounds__(64) void qs_first_hit_kernel(KArgs args) {
     const uint64_t vmask = __ballot(valid);
     for (int i = gbeg; i < gend; i++) {
       const GDesc dsc = load_desc(args.descs, i);
-      int32_t cur = __hip_atomic_load(&args.best[dsc.tape], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // workgroup scope: an ordinary (L1-cached) load, not a coherent L2 round trip per tape; a
+      // stale value only skips less (best[] only decreases within a launch)
+      int32_t cur = __hip_atomic_load(&args.best[dsc.tape], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       cur = __builtin_amdgcn_readfirstlane(cur);
       if (args.early_exit && gfirst >= cur) continue;
       cx.consts = CONSTP(cu32p, args.consts) + dsc.const_base;
