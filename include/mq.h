@@ -314,6 +314,12 @@ int mq_tapes_qsa_split(mq_tapes* tapes, int32_t* n_p, int32_t* n_g, int32_t* liv
    when it did not, run on the HIP C++ column kernel).  Introspection for tests and the bench. */
 int mq_tapes_column_split(mq_tapes* tapes, int32_t* n_asm, int32_t* live);
 
+/* Hoisted columns that are exactly keccak256(concat of model variables and constants) — the
+   keccak applications of kfm.py:95-114 / instructions.py:1043-1052 over candidate models —
+   evaluated by the dedicated keccak-f[1600] column kernel instead of an interpreter.
+   Introspection for tests and the bench (MQ_NO_KECCAK_COLUMNS=1 disables the path). */
+int mq_tapes_column_keccak(mq_tapes* tapes, int32_t* n_keccak_columns);
+
 /* After a launch: handler-kind histogram of the current assembly translation (which = 0: P
    tapes, 1: G tapes, 2: G column programs) into hist_out[cap]; each tape's program runs once per
    (tape, model) pair, so these are the dispatches per pair summed over tapes.  pairs_out

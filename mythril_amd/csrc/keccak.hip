@@ -79,6 +79,62 @@ __global__ __launch_bounds__(64) void keccak256_kernel(const uint8_t* __restrict
     for (int b = 0; b < 8; b++) out[(int64_t)i * 32 + 8 * w + b] = (uint8_t)(A[w] >> (8 * b));
 }
 
+// Keccak columns: grid.y = column, grid.x = 256-model blocks; the column's message layout is
+// uniform (scalar loads), the variable words are coalesced SoA rows.  The digest read big-endian
+// is the 256-bit value (mq.h MQ_OP_KECCAK), stored into the column's 8 variable rows.
+__global__ __launch_bounds__(256) void keccak_column_kernel(const KcCol* __restrict__ cols,
+                                                            const KcMapEntry* __restrict__ map,
+                                                            uint32_t* __restrict__ vars, int64_t M,
+                                                            unsigned long long* __restrict__ counters) {
+  const KcCol col = cols[blockIdx.y];
+  const int64_t m0 = (int64_t)blockIdx.x * 256;
+  const int64_t m = m0 + threadIdx.x;
+  if (threadIdx.x == 0 && counters) {
+    const unsigned long long nvalid = (unsigned long long)min<int64_t>(256, M - m0);
+    unsigned long long* cnt = counters + ((blockIdx.x + blockIdx.y) % kCounterSlots) * kCounterStride;
+    atomicAdd(&cnt[1], nvalid * col.n_nodes);
+    atomicAdd(&cnt[2], nvalid * col.alg_ops);
+  }
+  if (m >= M) return;
+  const KcMapEntry* e = map + col.map_off;
+  const uint32_t nw = col.nwords;
+  const uint32_t nblocks = (4u * nw) / 136u + 1u;
+  uint64_t A[25];
+#pragma unroll
+  for (int k = 0; k < 25; k++) A[k] = 0;
+#pragma unroll
+  for (int b = 0; b < 2; b++) {
+    if ((uint32_t)b >= nblocks) break;
+#pragma unroll
+    for (int p = 0; p < 34; p++) {
+      const uint32_t gi = 34u * b + p;
+      uint32_t w = 0;
+      if (gi < nw) {
+        const KcMapEntry x = e[gi];
+        w = __builtin_bswap32(x.row == ~0u ? x.value : vars[(int64_t)x.row * M + m]);
+      } else if (gi == nw) {
+        w = 0x01u;   // pad byte at message position 4 nw
+      }
+      A[p >> 1] ^= (uint64_t)w << (32 * (p & 1));
+    }
+    if ((uint32_t)b == nblocks - 1u) A[16] ^= 0x8000000000000000ull;
+    keccak_f(A);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint64_t q = A[(7 - i) >> 1];
+    vars[(int64_t)(col.target_row + i) * M + m] = __builtin_bswap32((uint32_t)(((7 - i) & 1) ? (q >> 32) : q));
+  }
+}
+
+hipError_t launch_keccak_columns(const KcCol* cols, int n_cols, const KcMapEntry* map, uint32_t* vars, int64_t M,
+                                 unsigned long long* counters, hipStream_t st) {
+  if (n_cols <= 0 || M <= 0) return hipSuccess;
+  hipLaunchKernelGGL(keccak_column_kernel, dim3((unsigned)((M + 255) / 256), (unsigned)n_cols), dim3(256), 0, st, cols,
+                     map, vars, M, counters);
+  return hipGetLastError();
+}
+
 hipError_t launch_keccak(const uint8_t* data, const int64_t* offsets, int n, uint8_t* out, hipStream_t st) {
   hipLaunchKernelGGL(keccak256_kernel, dim3((n + 63) / 64), dim3(64), 0, st, data, offsets, n, out);
   return hipGetLastError();

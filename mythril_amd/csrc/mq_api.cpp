@@ -87,6 +87,7 @@ struct mq_ctx {
   DevBuf counters;
   DevBuf best_tmp;  // scratch first-hit buffer for the synchronous API
   DevBuf scratch;   // per-wave temp slots of the HIP C++ interpreter (persistent grid)
+  DevBuf kec_data, kec_off, kec_out;   // mq_keccak256 buffers, grown and kept across calls
   DevBuf rowmask;   // per-row masks applied to uploaded variable words
   // Bool variables as packed lane masks [tile][n_bmask] (G kernel PUSH_PKB): bmask_of_var[v] =
   // mask index of Bool variable v (-1: none); bmask_rows[j] = its variable row
@@ -196,6 +197,23 @@ struct mq_tapes {
   std::vector<int> cq_stage;         // staged rows of the G column programs (as gstage)
   std::vector<uint32_t> cq_stage_rows;
   DevBuf cq_stage_dev;
+  // keccak columns (launch_keccak_columns): columns that are exactly keccak(concat of variables
+  // and constants); per column its pieces, most significant first (var >= 0: a model variable of
+  // nl limbs; var < 0: nl constant limbs at kc_consts[coff]); grouped by level
+  struct KcPiece {
+    int32_t var;
+    uint32_t nl, coff;
+  };
+  struct KcHost {
+    int32_t target;
+    uint32_t n_nodes, alg_ops;
+    std::vector<KcPiece> pieces;
+  };
+  std::vector<KcHost> kc;
+  std::vector<uint32_t> kc_consts;
+  std::vector<std::pair<int, int>> kc_level;   // (first, count) in kc, per column level
+  uint64_t kc_gen = ~0ull;                      // models_gen of the uploaded map
+  DevBuf kc_cols_dev, kc_map_dev;
   // multi-device context: the same batch compiled on each peer device (ctx->peers order)
   std::vector<mq_tapes*> peers;
   ~mq_tapes() {
@@ -1421,6 +1439,55 @@ int mq_dag_expand(const mq_dag_batch* dag, int32_t t, mq_node* nodes_out, int64_
 
 void mq_tapes_free(mq_tapes* t) { delete t; }
 
+// A column program that is exactly keccak256(concat of variables and constants) with every piece
+// a whole number of 32-bit words and at most 2048 bits in all (lower.py keccak_subterms makes
+// them): its pieces, most significant first, for the keccak column kernel.
+static bool kc_match(const mq_tape_batch* progs, int32_t k, std::vector<mq_tapes::KcPiece>& pieces,
+                     std::vector<uint32_t>& consts) {
+  const int64_t base = progs->tape_offsets[k];
+  const int64_t nn = progs->tape_offsets[k + 1] - base;
+  if (nn < 2) return false;
+  const mq_node* nd = progs->nodes + base;
+  const mq_node& root = nd[nn - 1];
+  if (root.op != MQ_OP_KECCAK || root.width != 256 || root.a >= (uint32_t)(nn - 1)) return false;
+  pieces.clear();
+  const size_t c0 = consts.size();
+  uint32_t words = 0;
+  std::vector<uint32_t> stack{root.a};
+  while (!stack.empty()) {
+    const uint32_t i = stack.back();
+    stack.pop_back();
+    const mq_node& n = nd[i];
+    if (n.op == MQ_OP_CONCAT) {
+      if (n.a >= i || n.b >= i) return false;
+      stack.push_back(n.b);   // low part after the high part
+      stack.push_back(n.a);
+      continue;
+    }
+    if ((n.op != MQ_OP_VAR && n.op != MQ_OP_CONST) || n.width == 0 || n.width % 32) {
+      consts.resize(c0);
+      return false;
+    }
+    const uint32_t nl = n.width / 32;
+    words += nl;
+    if (n.op == MQ_OP_VAR) {
+      pieces.push_back(mq_tapes::KcPiece{(int32_t)n.a, nl, 0});
+    } else {
+      if ((int64_t)n.a + nl > progs->n_const_words) {
+        consts.resize(c0);
+        return false;
+      }
+      pieces.push_back(mq_tapes::KcPiece{-1, nl, (uint32_t)consts.size()});
+      consts.insert(consts.end(), progs->const_words + n.a, progs->const_words + n.a + nl);
+    }
+  }
+  if (words == 0 || words > 64) {
+    consts.resize(c0);
+    return false;
+  }
+  return true;
+}
+
 static int set_columns_one(mq_tapes* T, const mq_tape_batch* progs, const int32_t* var_index, const int32_t* level,
                            int32_t n_columns) {
   mq_ctx* c = T->ctx;
@@ -1457,11 +1524,33 @@ static int set_columns_one(mq_tapes* T, const mq_tape_batch* progs, const int32_
   // MQ_G_COL_MIN_NODES overrides the threshold.
   int64_t min_nodes = kColAsmMinNodes;
   if (const char* e = std::getenv("MQ_G_COL_MIN_NODES")) min_nodes = std::atol(e);
+  // keccak columns, level by level (MQ_NO_KECCAK_COLUMNS=1: leave them to the interpreters)
+  std::vector<char> kcm(n_columns, 0);
+  T->kc.clear();
+  T->kc_consts.clear();
+  T->kc_gen = ~0ull;
+  T->kc_level.assign((size_t)max_level + 1, {0, 0});
+  if (!std::getenv("MQ_NO_KECCAK_COLUMNS")) {
+    for (int lv = 0; lv <= max_level; lv++) {
+      T->kc_level[lv].first = (int)T->kc.size();
+      for (int k = 0; k < n_columns; k++) {
+        if (level[k] != lv) continue;
+        mq_tapes::KcHost h;
+        if (!kc_match(progs, k, h.pieces, T->kc_consts)) continue;
+        h.target = var_index[k];
+        h.n_nodes = ct[k].n_nodes;
+        h.alg_ops = (uint32_t)std::min(ct[k].alg_ops, 4.0e9);
+        T->kc.push_back(std::move(h));
+        kcm[k] = 1;
+      }
+      T->kc_level[lv].second = (int)T->kc.size() - T->kc_level[lv].first;
+    }
+  }
   std::vector<char> gq(n_columns, 0);
   if (c->qsa_ready)
     for (int k = 0; k < n_columns; k++)
-      gq[k] = ct[k].L == 8 && !ct[k].keccak && ct[k].n_temps <= kQsaMaxTemps && (int64_t)ct[k].n_nodes >= min_nodes &&
-              qsa_translate(c, 1, false, ct[k], nullptr, nullptr);
+      gq[k] = !kcm[k] && ct[k].L == 8 && !ct[k].keccak && ct[k].n_temps <= kQsaMaxTemps &&
+              (int64_t)ct[k].n_nodes >= min_nodes && qsa_translate(c, 1, false, ct[k], nullptr, nullptr);
   T->cq_ct.clear();
   T->cq_var.clear();
   T->cq_bool.clear();
@@ -1478,7 +1567,7 @@ static int set_columns_one(mq_tapes* T, const mq_tape_batch* progs, const int32_
       if (pass != 0) v.begin = (int)descs.size();
       for (int k = 0; k < n_columns; k++) {
         const CompiledTape& x = ct[k];
-        if (level[k] != lv) continue;
+        if (level[k] != lv || kcm[k]) continue;
         if (pass == -1 && !gq[k]) continue;
         if (pass >= 0 && (gen_kind(x) != pass || (pass == 0 && gq[k]))) continue;
         GDesc d{};
@@ -1908,8 +1997,45 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     HIPCHK(hipStreamSynchronize(st));
     T->bmask_gen = c->models_gen;
   }
+  if (!T->kc.empty() && T->kc_gen != c->models_gen) {
+    // the keccak columns' message maps under this model batch's variable rows
+    std::vector<KcCol> cols;
+    std::vector<KcMapEntry> map;
+    for (const auto& h : T->kc) {
+      if (h.target < 0 || h.target >= c->n_vars || c->var_nl_h[h.target] != 8) {
+        g_last_error = "keccak column target is not a 256-bit variable of the uploaded model batch";
+        return MQ_ERR_ARG;
+      }
+      KcCol kc{};
+      kc.map_off = (uint32_t)map.size();
+      kc.target_row = c->var_off_h[h.target];
+      kc.n_nodes = h.n_nodes;
+      kc.alg_ops = h.alg_ops;
+      for (const auto& p : h.pieces) {
+        if (p.var >= 0 && (p.var >= c->n_vars || c->var_nl_h[p.var] != p.nl)) {
+          g_last_error = "keccak column piece does not match the uploaded model batch";
+          return MQ_ERR_ARG;
+        }
+        for (int l = (int)p.nl - 1; l >= 0; l--)
+          map.push_back(p.var >= 0 ? KcMapEntry{c->var_off_h[p.var] + (uint32_t)l, 0u}
+                                   : KcMapEntry{~0u, T->kc_consts[p.coff + (uint32_t)l]});
+      }
+      kc.nwords = (uint32_t)map.size() - kc.map_off;
+      cols.push_back(kc);
+    }
+    HIPCHK(T->kc_cols_dev.upload(cols.data(), cols.size(), st));
+    HIPCHK(T->kc_map_dev.upload(map.data(), map.size(), st));
+    HIPCHK(hipStreamSynchronize(st));
+    T->kc_gen = c->models_gen;
+  }
   for (size_t li = 0; li < T->clevels.size(); li++) {
     const auto& lv = T->clevels[li];
+    if (li < T->kc_level.size() && T->kc_level[li].second > 0) {
+      HIPCHK(start_timer());
+      HIPCHK(launch_keccak_columns(T->kc_cols_dev.as<KcCol>() + T->kc_level[li].first, T->kc_level[li].second,
+                                   T->kc_map_dev.as<KcMapEntry>(), const_cast<uint32_t*>(c->vars.as<uint32_t>()), c->M,
+                                   c->counters.as<unsigned long long>(), st));
+    }
     const mq_tapes::Variant v8 = use_cq ? cut_front(lv.v[0], lv.v8q) : lv.v[0];
     if (use_cq && lv.v8q > 0) {
       // the level's G columns on qsg_kernel, mode 3 (no preloaded variables)
@@ -2350,6 +2476,12 @@ int mq_tapes_column_split(mq_tapes* T, int32_t* n_asm, int32_t* live) {
   return MQ_OK;
 }
 
+int mq_tapes_column_keccak(mq_tapes* T, int32_t* n_keccak_columns) {
+  if (!T || !n_keccak_columns) return MQ_ERR_ARG;
+  *n_keccak_columns = (int32_t)T->kc.size();
+  return MQ_OK;
+}
+
 int mq_tapes_info(mq_tapes* T, int32_t* n_asm, int32_t* n_generic_l8, int32_t* n_generic_l16) {
   if (!T) return MQ_ERR_ARG;
   if (n_asm) *n_asm = T->qsa.count;
@@ -2370,7 +2502,10 @@ int mq_keccak256(mq_ctx* c, const uint8_t* data, const int64_t* offsets, int32_t
   if (n == 0) return MQ_OK;
   HIPCHK(hipSetDevice(c->device));
   const int64_t total = offsets[n];
-  DevBuf d_data, d_off, d_out;
+  // (kept in the context: a hipMalloc / hipFree pair per call cost more than the hashing)
+  DevBuf& d_data = c->kec_data;
+  DevBuf& d_off = c->kec_off;
+  DevBuf& d_out = c->kec_out;
   HIPCHK(d_data.upload(data, (size_t)std::max<int64_t>(total, 1), c->stream));
   HIPCHK(d_off.upload(offsets, (size_t)n + 1, c->stream));
   HIPCHK(d_out.ensure((size_t)32 * n));

@@ -115,5 +115,24 @@ hipError_t launch_pack_bool(const uint32_t* vars, uint64_t* masks, const uint32_
 hipError_t launch_finalize_best(int32_t* best, const uint8_t* unsupported, int n, hipStream_t st);
 hipError_t launch_keccak(const uint8_t* data, const int64_t* offsets, int n, uint8_t* out, hipStream_t st);
 
+// Keccak columns (mq_api.cpp kc_*): a hoisted column that is exactly keccak256(concat of model
+// variables and constants), evaluated by a dedicated keccak-f[1600] kernel, one model per lane.
+// Message word i (little-endian u32 of the big-endian message bytes) = bswap32 of map entry i:
+// a variable row (vars[row * M + m]) or, with row == ~0u, the constant word `value`.
+struct KcMapEntry {
+  uint32_t row;
+  uint32_t value;
+};
+struct KcCol {
+  uint32_t map_off;     // first map entry of the column
+  uint32_t nwords;      // message words (<= 64: at most 2048 bits, two 136-byte blocks)
+  uint32_t target_row;  // first of the 8 rows of the column's variable
+  uint32_t n_nodes;     // DAG nodes of the column program (metric)
+  uint32_t alg_ops;     // SURVEY §8(d) algorithmic ops of the program (metric)
+  uint32_t pad[3];
+};
+hipError_t launch_keccak_columns(const KcCol* cols, int n_cols, const KcMapEntry* map, uint32_t* vars, int64_t M,
+                                 unsigned long long* counters, hipStream_t st);
+
 }  // namespace mq
 #endif

@@ -62,6 +62,7 @@ def load_library(path: str = LIB_PATH):
         L.mq_tapes_info.argtypes = [P] + [C.POINTER(C.c_int32)] * 3
         L.mq_tapes_qsa_split.argtypes = [P] + [C.POINTER(C.c_int32)] * 3
         L.mq_tapes_column_split.argtypes = [P] + [C.POINTER(C.c_int32)] * 2
+        L.mq_tapes_column_keccak.argtypes = [P, C.POINTER(C.c_int32)]
         L.mq_tapes_qsa_histogram.argtypes = [P, C.c_int32, C.POINTER(C.c_int64), C.c_int32, C.POINTER(C.c_int64),
                                              C.POINTER(C.c_int32)]
         L.mq_qsa_kind_name.argtypes = [C.c_int32]
@@ -224,6 +225,12 @@ class CompiledTapes:
         a, b = C.c_int32(), C.c_int32()
         _check(self.ev.lib.mq_tapes_column_split(self.handle, C.byref(a), C.byref(b)), "mq_tapes_column_split")
         return a.value, bool(b.value)
+
+    def keccak_columns(self) -> int:
+        """Hoisted columns computed by the keccak-f[1600] column kernel (mq_tapes_column_keccak)."""
+        n = C.c_int32()
+        _check(self.ev.lib.mq_tapes_column_keccak(self.handle, C.byref(n)), "mq_tapes_column_keccak")
+        return n.value
 
     def handler_histogram(self, which: int = 1, pairs: bool = False):
         """After a launch: {handler kind: dispatches per (tape, model) pair, summed over tapes} of

@@ -275,6 +275,36 @@ def shared_subterms(roots: Sequence[S.Term], min_nodes: int = 8, min_tapes: int 
     return list(chosen.values())
 
 
+def keccak_subterms(terms: Sequence[S.Term], syms, chosen: Sequence[S.Term]) -> List[S.Term]:
+    """Hoisting companion for interpreted keccak (C4): every keccak application under ``terms``
+    becomes a column of its own — its argument's Concat pieces too, unless they are leaves — so
+    the column is exactly ``keccak(concat(variables, constants))``, which mq_api.cpp computes
+    with a dedicated keccak-f[1600] kernel instead of the interpreter (mq_tapes_column_keccak).
+    Returns the new column terms (not already in ``chosen``), pieces before the keccaks."""
+    have = {id(t) for t in chosen}
+    out: List[S.Term] = []
+    seen = set()
+    for r in terms:
+        for t in S.walk(r):
+            if id(t) in seen:
+                continue
+            seen.add(id(t))
+            if not (t.kind == S.KECCAK or (t.kind == S.APP and syms.interpret_keccak and _is_keccak_uf(t.params[0]))):
+                continue
+            stack, pieces = [t.args[0]], []
+            while stack:   # Concat pieces, most significant first
+                x = stack.pop()
+                if x.kind == S.CONCAT:
+                    stack.extend(reversed(x.args))
+                else:
+                    pieces.append(x)
+            for x in pieces + [t]:
+                if x.kind not in _LEAVES and id(x) not in have:
+                    have.add(id(x))
+                    out.append(x)
+    return out
+
+
 def _is_keccak_uf(name: str) -> bool:
     """``keccak256_<n>`` (keccak_function_manager.py:77), not its inverse ``keccak256_<n>-1``."""
     return name.startswith("keccak256_") and name[10:].isdigit()
@@ -299,6 +329,7 @@ def lower_batch(roots: Sequence[S.Term], syms: Optional[SymbolTable] = None, hoi
     col_terms: List[S.Term] = []
     if hoist and len(roots) > 1:
         col_terms = shared_subterms(roots, hoist_min_nodes)
+        col_terms += keccak_subterms(list(roots), syms, col_terms)
         for k, t in enumerate(col_terms):
             hoisted[id(t)] = syms.var(f"@h{k}", t.width)
             syms.hoisted_vars.add(hoisted[id(t)])

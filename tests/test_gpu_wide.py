@@ -82,3 +82,51 @@ def test_keccak_op_wide_widths(evaluator):
     assert (fh != -2).all()
     assert v_gpu[:, 0].all()
     assert (v_gpu == cref.verdicts(tb, mb)).all()
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_keccak_columns_match_unhoisted_oracle(evaluator, monkeypatch, seed):
+    """Interpreted keccak of Concat(variables, constants) at 256..2048 bits, shared by several
+    conjunctions: hoisted into keccak columns computed by the dedicated keccak-f[1600] kernel
+    (mq_tapes_column_keccak), then read by the tapes.  Verdicts equal the oracle's on the
+    UNhoisted lowering and the interpreter path's (MQ_NO_KECCAK_COLUMNS=1)."""
+    from mythril_amd import smt as S
+    from mythril_amd.lower import SymbolTable, lower_batch, serialize_models
+    from mythril_amd.smt_model import Model
+    rng = np.random.default_rng(70 + seed)
+    words = [S.BitVecSym(f"w{i}", 256) for i in range(6)]
+    sel = S.BitVecSym("sel", 32)
+    msgs = [S.Concat(words[0], S.BitVecVal(1, 256)),                                   # mapping slot (512)
+            S.Concat(sel, words[1], S.BitVecVal(7, 256)),                              # 544
+            S.Concat(words[2], words[3], S.BitVecVal(2, 256)),                         # 768
+            S.Concat(words[4], S.BitVecVal(3, 256), words[5], words[0], S.BitVecVal(9, 32)),   # 1056
+            S.Concat(*(words + [S.BitVecVal(5, 256), words[1]])),                      # 2048 (two blocks)
+            words[3]]                                                                  # 256
+    hs = [S.Keccak256(m) for m in msgs]
+    roots = []
+    for i in range(40):
+        h = hs[int(rng.integers(len(hs)))]
+        g = hs[int(rng.integers(len(hs)))]
+        c = int(rng.integers(0, 1 << 32))
+        hi = 7 if i % 2 else 15   # a byte (a hit among 600 models is likely) or 16 bits (unlikely)
+        roots.append(S.And(S.ULT(S.BitVecVal(c, 256), h),
+                           S.Extract(hi, 0, g) == S.BitVecVal(int(rng.integers(0, 1 << (hi + 1))), hi + 1)))
+    models = [Model({**{f"w{i}": int.from_bytes(rng.bytes(32), "little") for i in range(6)},
+                     "sel": int(rng.integers(0, 1 << 32))}) for _ in range(600)]
+    syms = SymbolTable(interpret_keccak=True)
+    tb0, syms0, ok0 = lower_batch(roots, syms)
+    ref, _ = cref.first_hit(tb0, serialize_models(models, syms0))
+    syms = SymbolTable(interpret_keccak=True)
+    tb, syms1, ok1 = lower_batch(roots, syms, hoist=True)
+    assert ok0.all() and ok1.all() and tb.columns is not None
+    mb = serialize_models(models, syms1)
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    assert ct.keccak_columns() == len(hs)
+    fh = evaluator.first_hit(ct)
+    v, _ = evaluator.verdicts(tb)
+    assert (fh == ref).all() and 0 < (ref >= 0).sum() < len(ref)
+    assert (v == cref.verdicts(tb0, serialize_models(models, syms0))).all()
+    monkeypatch.setenv("MQ_NO_KECCAK_COLUMNS", "1")
+    ct2 = evaluator.compile(tb)
+    assert ct2.keccak_columns() == 0 and (evaluator.first_hit(ct2) == ref).all()
