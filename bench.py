@@ -47,7 +47,8 @@ WORKLOADS = {
     "c4": (200, 1_000_000, 4, "C4: 200 keccak-heavy token-transfer paths over 2 txs (balances[key] = storage at "
            "keccak256(key ++ slot), store chains, keccak UF axioms of keccak_function_manager) x 10^6 "
            "keccak-consistent models per GPU, keccak256_512 evaluated IN-KERNEL (keccak-f[1600]), seed 4, 10% planted",
-           "qs_first_hit_kernel<16,6,keccak> (HIP C++ interpreter + keccak-f[1600])"),
+           "mq::qsg_kernel (G tapes + mode-3 columns) + keccak_column_kernel (keccak-f[1600] columns) + "
+           "qs_column_kernel<16> (512-bit columns); whole-step alg ops / kernel time"),
     "c5": (256, 1_250_000, 5, "C5: 256 deep EVM-shaped paths over 5 txs (~1900 DAG nodes) x 1.25*10^6 models per GPU "
            "(10^7 over 8 GPUs), seed 5, 10% planted",
            "mq::qsg_kernel (gfx950 assembly interpreter, variables from HBM) + qs_column_kernel<8> (hoisted columns)"),
