@@ -1221,6 +1221,14 @@ def frame(variant, pfx, handlers, subs):
         "s_lshl_b32 s34, s82, 2",
         "s_add_u32 s72, s26, s34",           # s[72:73] = &best[tape] (handlers never touch s72-s73, s80-s87)
         "s_addc_u32 s73, s27, 0",
+    ] + ([] if G else [
+        # P: the first program entry is requested together with best[tape] (one round trip for
+        # both; a skipped tape wasted a scalar load)
+        "s_lshl_b32 s34, s80, 2",
+        "s_add_u32 s14, s46, s34",
+        "s_addc_u32 s15, s47, 0",
+        "s_load_dwordx4 s[96:99], s[14:15], 0x0",
+    ]) + [
         "s_cmp_eq_u32 s31, 1",
         f"s_cbranch_scc1 {pfx}_run",
         "s_cmp_eq_u32 s30, 0",
@@ -1260,10 +1268,6 @@ def frame(variant, pfx, handlers, subs):
         "s_addc_u32 s21, s89, 0",
     ] + (["s_lshl_b32 s34, s80, 2", "s_add_u32 s36, s46, s34", "s_addc_u32 s37, s47, 0"]
          + load_window(True, pfx) + prof_point("FRAME") + NEXT_G if G else [
-        "s_lshl_b32 s34, s80, 2",
-        "s_add_u32 s14, s46, s34",
-        "s_addc_u32 s15, s47, 0",
-        "s_load_dwordx4 s[96:99], s[14:15], 0x0",
         "s_mov_b32 s16, 12",
         # the tape end's descriptor words, out of CB (s[80:87]) before the first prefetch
         "s_mov_b32 s78, s84",
