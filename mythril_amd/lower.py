@@ -16,6 +16,8 @@ model ("Equivalence lets the lowering choose its input").
 """
 from __future__ import annotations
 
+import os
+
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -316,19 +318,24 @@ _BIN = {S.ADD: "add", S.SUB: "sub", S.MUL: "mul", S.UDIV: "udiv", S.UREM: "urem"
 
 
 def lower_batch(roots: Sequence[S.Term], syms: Optional[SymbolTable] = None, hoist: bool = False,
-                hoist_min_nodes: int = 8):
+                hoist_min_nodes: int = 2):
     """Lower N conjunctions over one shared symbol table.  Returns ``(TapeBatch | None, syms,
     supported_mask)``: a root that fails to lower is replaced by a FALSE placeholder tape and
     flagged unsupported (the caller routes it to z3).
 
     ``hoist``: sub-terms shared by several roots are evaluated once per model into derived
     columns (``TapeBatch.columns``, variables named ``@h<k>``) instead of once per (tape, model).
-    Verdicts are unchanged: a sub-term's value depends only on the model."""
+    Verdicts are unchanged: a sub-term's value depends only on the model.  Every shared sub-term
+    of >= 2 (weighted) nodes is hoisted: on MI355X a column read is cheaper than re-evaluating
+    even a two-node sub-term in each tape (C3 46.2 -> 36.1 ms, C5 61.6 -> 51.4 ms, C4 11.5 ->
+    10.2 ms against the earlier threshold of 8; profiles/r02hm*)."""
     syms = syms or SymbolTable()
     hoisted: Dict[int, int] = {}
     col_terms: List[S.Term] = []
     if hoist and len(roots) > 1:
-        col_terms = shared_subterms(roots, hoist_min_nodes)
+        # (MQ_HOIST_MIN_NODES / MQ_HOIST_MIN_TAPES: diagnostic overrides of the hoisting threshold)
+        col_terms = shared_subterms(roots, int(os.environ.get("MQ_HOIST_MIN_NODES", hoist_min_nodes)),
+                                    int(os.environ.get("MQ_HOIST_MIN_TAPES", 2)))
         col_terms += keccak_subterms(list(roots), syms, col_terms)
         for k, t in enumerate(col_terms):
             hoisted[id(t)] = syms.var(f"@h{k}", t.width)
