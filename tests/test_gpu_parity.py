@@ -237,6 +237,38 @@ def test_p_leaf_pair_fusions_match_oracle(evaluator, seed):
     assert sum(v for k, v in hist.items() if k.startswith("PF_")) > 0, hist
 
 
+def test_p_constant_prefetch_runs_match_oracle(evaluator):
+    """Runs of consecutive constant handlers (x + c1) * c2 & c3 - c4 ... on the P interpreter:
+    the translator alternates prefetched (PF_) and self-loading handlers; a PF_ handler whose
+    successor is not one re-loads its own constant.  Bit-exact against the oracle."""
+    rng = np.random.default_rng(31)
+    tapes = []
+    for i in range(200):
+        t = Tape()
+        acc = t.var(int(rng.integers(8)), 256)
+        for k in range(int(rng.integers(1, 12))):
+            c = t.const(int.from_bytes(rng.bytes(32), "little") >> int(rng.integers(0, 255)), 256)
+            op = ("add", "mul", "band", "sub", "bor", "bxor")[int(rng.integers(6))]
+            acc = getattr(t, op)(acc, c)
+            if rng.random() < 0.2:   # a variable operand between runs
+                acc = t.add(acc, t.var(int(rng.integers(8)), 256))
+        bound = t.const(int.from_bytes(rng.bytes(32), "little"), 256)
+        tapes.append(t.finish(t.ult(acc, bound) if i % 2 else t.not_(t.eq(acc, bound))))
+    tb = TapeBatch(tapes)
+    M = 641
+    mb = ModelBatch([256] * 8, rng.integers(0, 1 << 32, (64, M), dtype=np.uint64).astype(np.uint32))
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    v, _ = evaluator.verdicts(tb)
+    assert (v == cref.verdicts(tb, mb)).all()
+    fh_ref, _ = cref.first_hit(tb, mb)
+    assert (evaluator.first_hit(ct) == fh_ref).all()
+    hist, pairs = ct.handler_histogram(0, pairs=True)
+    assert ct.asm_split()[0] == tb.n_tapes
+    pf = sum(n for k, n in hist.items() if k.startswith("PF_"))
+    assert pf > 0 and sum(n for (a, b), n in pairs.items() if a.startswith("PF_") and b.startswith("PF_")) == 0
+
+
 def test_golden_vectors_generic_kernel(evaluator):
     """The same golden fixtures with the assembly path disabled (HIP C++ interpreter only)."""
     entries = load("shift_vectors.json") + load("vmtests_kats.json")
