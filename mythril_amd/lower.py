@@ -95,20 +95,50 @@ def _w(t: S.Term) -> int:
 
 
 def lower_term(root: S.Term, syms: SymbolTable, hoisted: Optional[Dict[int, int]] = None,
-               value_root: bool = False) -> Tape:
+               value_root: bool = False, narrow: Optional[Dict[int, int]] = None) -> Tape:
     """Lower one Bool term (the quick-sat conjunction) to a tape; iterative over the DAG.
-    ``hoisted``: id(term) -> variable index of terms replaced by derived columns."""
+    ``hoisted``: id(term) -> variable index of terms replaced by derived columns; ``narrow``:
+    id(term) -> the fewer bits its column stores (its value's upper bits are zero: read back
+    zero-extended; a column program of a narrow root ends in an Extract of those bits)."""
     if root.sort != "bool" and not value_root:
         raise LoweringError("quick-sat root must be Bool")
     hoisted = hoisted or {}
+    narrow = narrow or {}
     tp = Tape()
     node: Dict[int, int] = {}
     for t in _walk_cut(root, hoisted):
         if id(t) in hoisted and t is not root:
-            node[id(t)] = tp.var(hoisted[id(t)], _w(t))
+            nw = narrow.get(id(t))
+            if nw is None:
+                node[id(t)] = tp.var(hoisted[id(t)], _w(t))
+            else:
+                node[id(t)] = tp.zext(_w(t) - nw, tp.var(hoisted[id(t)], nw))
             continue
         node[id(t)] = _lower_one(t, [node[id(x)] for x in t.args], tp, syms, node)
-    return tp.finish(node[id(root)], value_root=value_root)
+    r = node[id(root)]
+    if value_root and id(root) in narrow:
+        r = tp.extract(narrow[id(root)] - 1, 0, r)
+    return tp.finish(r, value_root=value_root)
+
+
+def _column_bits(t: S.Term) -> int:
+    """An upper bound on the significant bits of a hoisted BV term's value (its width when
+    nothing better is known): x >> c, x urem c, x & c for constants c, zero-extensions."""
+    w = t.width
+    if t.sort != "bv" or w <= 32:
+        return w
+    a = t.args
+    if t.kind == S.LSHR and a[1].kind == S.VAL:
+        return max(1, w - min(a[1].params[0], w))
+    if t.kind == S.UREM and a[1].kind == S.VAL and a[1].params[0] > 0:
+        return max(1, (a[1].params[0] - 1).bit_length())
+    if t.kind == S.BAND:
+        consts = [x.params[0] for x in a if x.kind == S.VAL]
+        if consts:
+            return max(1, min(c.bit_length() for c in consts))
+    if t.kind == S.ZEXT:
+        return a[0].width
+    return w
 
 
 def _lower_one(t: S.Term, a: List[int], tp: Tape, syms: SymbolTable, node: Dict[int, int]) -> int:
@@ -331,19 +361,27 @@ def lower_batch(roots: Sequence[S.Term], syms: Optional[SymbolTable] = None, hoi
     10.2 ms against the earlier threshold of 8; profiles/r02hm*)."""
     syms = syms or SymbolTable()
     hoisted: Dict[int, int] = {}
+    narrow: Dict[int, int] = {}
     col_terms: List[S.Term] = []
     if hoist and len(roots) > 1:
         # (MQ_HOIST_MIN_NODES / MQ_HOIST_MIN_TAPES: diagnostic overrides of the hoisting threshold)
         col_terms = shared_subterms(roots, int(os.environ.get("MQ_HOIST_MIN_NODES", hoist_min_nodes)),
                                     int(os.environ.get("MQ_HOIST_MIN_TAPES", 2)))
+        n_shared = len(col_terms)
         col_terms += keccak_subterms(list(roots), syms, col_terms)
         for k, t in enumerate(col_terms):
-            hoisted[id(t)] = syms.var(f"@h{k}", t.width)
+            # a column whose value has fewer significant bits stores only those (selectors
+            # x >> 224, x urem 2^160, masks): fewer rows written and read; keccak columns and
+            # their pieces keep their width (the keccak column kernel reads whole words)
+            bits = _column_bits(t) if k < n_shared else t.width
+            if (bits + 31) // 32 < (t.width + 31) // 32:
+                narrow[id(t)] = bits
+            hoisted[id(t)] = syms.var(f"@h{k}", narrow.get(id(t), t.width))
             syms.hoisted_vars.add(hoisted[id(t)])
     tapes, ok = [], np.ones(len(roots), bool)
     for i, r in enumerate(roots):
         try:
-            tapes.append(lower_term(r, syms, hoisted))
+            tapes.append(lower_term(r, syms, hoisted, narrow=narrow))
         except (LoweringError, TypeError):
             ok[i] = False
             t = Tape()
@@ -355,7 +393,7 @@ def lower_batch(roots: Sequence[S.Term], syms: Optional[SymbolTable] = None, hoi
         for t in col_terms:   # column programs; a column may read columns nested inside it
             inner = [h for h in _walk_cut(t, hoisted) if id(h) in hoisted and h is not t]
             lvl[id(t)] = 0
-            progs.append(lower_term(t, syms, hoisted, value_root=True))
+            progs.append(lower_term(t, syms, hoisted, value_root=True, narrow=narrow))
         # levels: longest chain of nested columns (terms are acyclic)
         changed = True
         while changed:
