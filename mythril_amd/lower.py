@@ -111,23 +111,30 @@ def lower_term(root: S.Term, syms: SymbolTable, hoisted: Optional[Dict[int, int]
             nw = narrow.get(id(t))
             if nw is None:
                 node[id(t)] = tp.var(hoisted[id(t)], _w(t))
-            else:
+            elif nw > 0:
                 node[id(t)] = tp.zext(_w(t) - nw, tp.var(hoisted[id(t)], nw))
+            else:   # sign-extended column (-bits)
+                node[id(t)] = tp.sext(_w(t) + nw, tp.var(hoisted[id(t)], -nw))
             continue
         node[id(t)] = _lower_one(t, [node[id(x)] for x in t.args], tp, syms, node)
     r = node[id(root)]
     if value_root and id(root) in narrow:
-        r = tp.extract(narrow[id(root)] - 1, 0, r)
+        r = tp.extract(abs(narrow[id(root)]) - 1, 0, r)
     return tp.finish(r, value_root=value_root)
 
 
 def _column_bits(t: S.Term) -> int:
     """An upper bound on the significant bits of a hoisted BV term's value (its width when
-    nothing better is known): x >> c, x urem c, x & c for constants c, zero-extensions."""
+    nothing better is known): x >> c, x urem c, x & c for constants c, zero-extensions; negative
+    for values that are sign extensions of their low -bits (arithmetic x >> c, sign-extensions)."""
     w = t.width
     if t.sort != "bv" or w <= 32:
         return w
     a = t.args
+    if t.kind == S.ASHR and a[1].kind == S.VAL:
+        return -max(1, w - min(a[1].params[0], w - 1))
+    if t.kind == S.SEXT:
+        return -a[0].width
     if t.kind == S.LSHR and a[1].kind == S.VAL:
         return max(1, w - min(a[1].params[0], w))
     if t.kind == S.UREM and a[1].kind == S.VAL and a[1].params[0] > 0:
@@ -374,9 +381,9 @@ def lower_batch(roots: Sequence[S.Term], syms: Optional[SymbolTable] = None, hoi
             # x >> 224, x urem 2^160, masks): fewer rows written and read; keccak columns and
             # their pieces keep their width (the keccak column kernel reads whole words)
             bits = _column_bits(t) if k < n_shared else t.width
-            if (bits + 31) // 32 < (t.width + 31) // 32:
+            if (abs(bits) + 31) // 32 < (t.width + 31) // 32:
                 narrow[id(t)] = bits
-            hoisted[id(t)] = syms.var(f"@h{k}", narrow.get(id(t), t.width))
+            hoisted[id(t)] = syms.var(f"@h{k}", abs(narrow.get(id(t), t.width)))
             syms.hoisted_vars.add(hoisted[id(t)])
     tapes, ok = [], np.ones(len(roots), bool)
     for i, r in enumerate(roots):
