@@ -139,12 +139,16 @@ def _column_bits(t: S.Term) -> int:
         return max(1, w - min(a[1].params[0], w))
     if t.kind == S.UREM and a[1].kind == S.VAL and a[1].params[0] > 0:
         return max(1, (a[1].params[0] - 1).bit_length())
+    if t.kind == S.UDIV and a[1].kind == S.VAL and a[1].params[0] > 0:   # selector: x / 2^224
+        return max(1, w - (a[1].params[0].bit_length() - 1))
     if t.kind == S.BAND:
         consts = [x.params[0] for x in a if x.kind == S.VAL]
         if consts:
             return max(1, min(c.bit_length() for c in consts))
     if t.kind == S.ZEXT:
         return a[0].width
+    if t.kind == S.CONCAT and a[0].kind == S.VAL:   # Concat(c, x): EVM BYTE is Concat(0, byte)
+        return max(1, a[1].width + a[0].params[0].bit_length()) if a[0].params[0] else a[1].width
     return w
 
 
