@@ -1122,7 +1122,12 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
       }
       default: ok = false;
     }
-    if (!ok) return false;
+    if (!ok) {
+      // MQ_QSA_DEBUG=1: name the stack-program instruction a translation stops at (diagnostic)
+      static const bool dbg = std::getenv("MQ_QSA_DEBUG") != nullptr;
+      if (dbg) std::fprintf(stderr, "qsa_translate(%s): op %u at slot %d imm %u not translated\n", P ? "P" : "G", op, d, imm);
+      return false;
+    }
     prev_op = op;
     prev_d = (uint32_t)d;
     prev_imm = imm;
