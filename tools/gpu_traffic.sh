@@ -7,8 +7,8 @@ TAG="${1:?tag}"; CFGS="${2:-c2 c3 c5}"; R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out
 summ() { local db; db=$(find "$3" -name '*.db' | head -1); [ -n "$db" ] && python3 "$R/tools/rocpd_summary.py" "$OUT/$1.json" "$2=$db" > /dev/null; rm -rf "$3"; }
 for c in $CFGS; do
   for ctr in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 240 rocprofv3 --pmc $ctr -d /tmp/p_$c_$ctr -o run -- python3 "$R/bench.py" --config $c --steps 1 --warmup 1 --no-cpu-baseline --no-dropin > "$OUT/${c}_$ctr.log" 2>&1 || exit 11
-    summ ${c}_$ctr pmc /tmp/p_$c_$ctr
+    timeout -s KILL 240 rocprofv3 --pmc $ctr -d /tmp/p_${c}_$ctr -o run -- python3 "$R/bench.py" --config $c --steps 1 --warmup 1 --no-cpu-baseline --no-dropin > "$OUT/${c}_$ctr.log" 2>&1 || exit 11
+    summ ${c}_$ctr pmc /tmp/p_${c}_$ctr
   done
 done
 for nb in 64 200; do
