@@ -498,7 +498,7 @@ class IncrementalLowering:
     def __init__(self) -> None:
         self.syms = SymbolTable()
         self._reset_dag()
-        self._models: Dict[int, Tuple[object, List[np.ndarray], Dict[int, Tuple[np.ndarray, np.ndarray]]]] = {}
+        self._models: Dict[int, list] = {}
 
     def _reset_dag(self) -> None:
         self.tape = Tape()
@@ -632,16 +632,17 @@ class IncrementalLowering:
         M = len(models)
         cols, fcache = [], []
         for mod in models:
+            # per model: [model, its column of the variables seen so far (extended when new
+            # variables appear), how many variables that is, its function tables]
             ent = self._models.get(id(mod))
             if ent is None or ent[0] is not mod:
-                ent = (mod, [], {})
-                self._models[id(mod)] = ent
-            vl = ent[1]
-            if len(vl) < nv:
+                ent = self._models[id(mod)] = [mod, np.zeros(0, np.uint32), 0, {}]
+            if ent[2] < nv:
                 rec = as_record(mod)
-                vl.extend(self._var_words(rec, v) for v in range(len(vl), nv))
-            cols.append(np.concatenate(vl) if nv else np.zeros(0, np.uint32))
-            fcache.append((mod, ent[2]))
+                ent[1] = np.concatenate([ent[1]] + [self._var_words(rec, v) for v in range(ent[2], nv)])
+                ent[2] = nv
+            cols.append(ent[1])
+            fcache.append((mod, ent[3]))
         rows = sum(limbs(w) for w in syms.var_widths)
         words = np.stack(cols, axis=1) if M else np.zeros((rows, 0), np.uint32)
         if len(self._models) > 4 * M + 256:   # forget models that left the candidate set

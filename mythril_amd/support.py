@@ -48,6 +48,7 @@ import numpy as np
 
 from . import smt as S
 from .exceptions import SolverTimeOutException, UnsatError
+from .lower import DagBatch
 from .smt_model import Model, as_record
 
 log = logging.getLogger(__name__)
@@ -125,6 +126,25 @@ time_handler = TimeHandler()
 
 
 # ---------------------------------------------------------------------------- verdict engine
+def split_conjuncts(db: DagBatch, groups: int) -> Tuple[DagBatch, Optional[np.ndarray]]:
+    """Each tape of ``db`` (a conjunction: its list of conjunct roots) as up to ``groups``
+    tapes over contiguous runs of its conjuncts (consecutive conjuncts of a path share the most
+    sub-terms).  Returns the split batch and the index of each original tape's first group, or
+    ``(db, None)`` when nothing splits."""
+    offs = db.root_offsets
+    n_conj = np.diff(offs)
+    k = np.minimum(n_conj, max(1, int(groups)))
+    if groups <= 1 or not np.any(k > 1):
+        return db, None
+    new = [0]
+    for q in range(db.n_tapes):
+        a, kq = int(offs[q]), int(max(k[q], 1))
+        bounds = a + (np.arange(1, kq + 1) * int(n_conj[q])) // kq
+        new.extend(int(x) for x in bounds)
+    starts = np.concatenate(([0], np.cumsum(np.maximum(k, 1))[:-1])).astype(np.int64)
+    return DagBatch(db.nodes, db.consts, np.asarray(new, np.int64), db.roots), starts
+
+
 class VerdictEngine:
     """Lowers conjunctions + candidate models and evaluates them on the GPU.
 
@@ -140,6 +160,12 @@ class VerdictEngine:
     # the incremental lowering (cached conjunct fragments and model rows) is used instead
     hoist_min_batch = 8
     hoist_min_models = 1024
+    # a small batch leaves the GPU idle and a single conjunction is one wave's serial walk over
+    # its ~1 000 nodes: its conjuncts are split into up to ``split_tapes // N`` contiguous groups,
+    # each its own tape (one wave each), and the group verdict rows are AND-ed (the conjunction
+    # holds iff every conjunct does).  Shared sub-terms are then re-evaluated per group — more
+    # work, less latency; 0 disables
+    split_tapes = int(os.environ.get("MQ_SPLIT_TAPES", "256"))
     STAGES = ("lower", "serialize", "upload", "compile", "evaluate")
 
     def __init__(self, evaluator=None):
@@ -241,8 +267,14 @@ class VerdictEngine:
             return [np.zeros(0, bool) for _ in exprs]
         hoist = len(exprs) >= self.hoist_min_batch and len(models) >= self.hoist_min_models
         tb, mb, ok = self._lower(exprs, models, hoist)
+        starts = None
+        if isinstance(tb, DagBatch) and self.split_tapes:
+            tb, starts = split_conjuncts(tb, self.split_tapes // len(exprs))
         try:
             v, fh = self._evaluate(tb, mb)
+            if starts is not None:
+                v = np.logical_and.reduceat(v, starts, axis=0)
+                fh = np.where(np.minimum.reduceat(fh, starts) == -2, -2, 0)
         except Exception:
             if getattr(tb, "columns", None) is None:
                 raise
