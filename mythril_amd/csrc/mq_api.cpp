@@ -112,6 +112,7 @@ struct mq_ctx {
   uint64_t models_gen = 0;      // bumped by every mq_models_upload
   int use_asm = 1;      // MQ_OPT_USE_ASM
   int early_exit = 1;   // MQ_OPT_EARLY_EXIT
+  int64_t latency_waves = 0;   // MQ_OPT_LATENCY_WAVES
   // MQ_OPT_TIME_KERNELS: one HIP event pair bracketing the evaluation kernels of each launch
   int time_kernels = 0;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> kev;
@@ -1935,6 +1936,8 @@ static int64_t g_tapes_per_group(int64_t n, int64_t M) {
 // the rest.  verdicts == nullptr -> first-hit mode into best.
 static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, hipStream_t st) {
   bool use_qsa = c->qsa_ready && c->use_asm && T->qsa.count > 0;
+  // latency-bound launch (a few tapes over a few models): one C++ launch, no P / G translation
+  if (use_qsa && (int64_t)T->n_tapes * ((c->M + 63) / 64) <= c->latency_waves) use_qsa = false;
   if (use_qsa) {
     const int rc = qsa_prepare(c, T);
     if (rc) return rc;
@@ -2418,6 +2421,7 @@ int mq_ctx_set_option(mq_ctx* c, int option, int value) {
   switch (option) {
     case MQ_OPT_USE_ASM: c->use_asm = value ? 1 : 0; return MQ_OK;
     case MQ_OPT_EARLY_EXIT: c->early_exit = value ? 1 : 0; return MQ_OK;
+    case MQ_OPT_LATENCY_WAVES: c->latency_waves = value > 0 ? value : 0; return MQ_OK;
     case MQ_OPT_ASM_READY: return c->qsa_ready ? 1 : 0;
     case MQ_OPT_TIME_KERNELS:
       c->time_kernels = value ? 1 : 0;

@@ -286,7 +286,7 @@ class Evaluator:
             self.set_option(self.OPT_USE_RCCL, 1)
 
     OPT_USE_ASM, OPT_EARLY_EXIT, OPT_ASM_READY, OPT_TIME_KERNELS = 1, 2, 3, 4
-    OPT_USE_RCCL, OPT_RCCL_ACTIVE = 5, 6
+    OPT_USE_RCCL, OPT_RCCL_ACTIVE, OPT_LATENCY_WAVES = 5, 6, 7
 
     @property
     def rccl_active(self) -> bool:

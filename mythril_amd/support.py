@@ -164,8 +164,11 @@ class VerdictEngine:
     # its ~1 000 nodes: its conjuncts are split into up to ``split_tapes // N`` contiguous groups,
     # each its own tape (one wave each), and the group verdict rows are AND-ed (the conjunction
     # holds iff every conjunct does).  Shared sub-terms are then re-evaluated per group — more
-    # work, less latency; 0 disables
-    split_tapes = int(os.environ.get("MQ_SPLIT_TAPES", "256"))
+    # work (and compile time), less latency: one query x 16 models 0.85 -> 0.18 ms of kernel
+    # (profiles/r02lat); from N = 32 the compile cost outweighs it (profiles/r02sp); 0 disables
+    split_tapes = int(os.environ.get("MQ_SPLIT_TAPES", "32"))
+    # launches of at most this many waves run on ONE HIP C++ kernel launch (MQ_OPT_LATENCY_WAVES)
+    latency_waves = int(os.environ.get("MQ_LATENCY_WAVES", "1024"))
     STAGES = ("lower", "serialize", "upload", "compile", "evaluate")
 
     def __init__(self, evaluator=None):
@@ -207,6 +210,11 @@ class VerdictEngine:
         self.timing["serialize"] += clock() - t1
         return tb, mb, ok
 
+    @staticmethod
+    def _latency_mode(ev, waves: int) -> None:
+        if hasattr(ev, "OPT_LATENCY_WAVES"):
+            ev.set_option(ev.OPT_LATENCY_WAVES, waves)
+
     def _evaluate(self, tb, mb):
         clock = time.perf_counter
         ev = self.evaluator
@@ -215,9 +223,11 @@ class VerdictEngine:
         t1 = clock()
         ct = ev.compile(tb)
         t2 = clock()
+        self._latency_mode(ev, self.latency_waves)
         try:
             v, fh = ev.verdicts(ct)
         finally:
+            self._latency_mode(ev, 0)
             ct.free()
         self.timing["upload"] += t1 - t0
         self.timing["compile"] += t2 - t1
@@ -254,9 +264,11 @@ class VerdictEngine:
         t3 = clock()
         ct = ev.compile(tb)
         t4 = clock()
+        self._latency_mode(ev, self.latency_waves)
         try:
             fh = ev.first_hit(ct)
         finally:
+            self._latency_mode(ev, 0)
             ct.free()
         return fh, t3, t4
 
