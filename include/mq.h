@@ -286,9 +286,9 @@ int mq_keccak256(mq_ctx* ctx, const uint8_t* data, const int64_t* offsets, int32
    all-reduce; 1 on a single-device context runs that path with one rank (0 is refused when
    n_dev > 1).  MQ_OPT_RCCL_ACTIVE (query): 1 if the context reduces over RCCL.
    MQ_OPT_LATENCY_WAVES (default 0 = off): a launch of at most this many waves (tapes x 64-model
-   tiles) runs every 256-bit tape on the HIP C++ kernel in ONE launch instead of the P / G / C++
-   sequence: a few tapes over a few models are latency-bound, and one launch has the shortest
-   critical path (the drop-in path at the reference's shape sets it). */
+   tiles) runs the general assembly kernel with one tape per wave instead of several tapes per
+   wave: a few tapes over a few models are latency-bound (the drop-in path at the reference's
+   shape sets it). */
 enum mq_option {
   MQ_OPT_USE_ASM = 1,
   MQ_OPT_EARLY_EXIT = 2,

@@ -566,6 +566,50 @@ def sub_udiv32(pfx):
     return out
 
 
+def sub_udivv(pfx):
+    """G: unsigned 256-bit division by a variable divisor (bvudiv / bvurem, SMT-LIB: x / 0 = all
+    ones, x % 0 = x).  In: dividend U[0:8], divisor U[8:16] (U = the UF1 work registers).  Out:
+    quotient U[0:8], remainder W[0:8]; U[16:24] is the trial difference.  Restoring radix-2
+    division over the dividend's significant limbs only (n = the wave's maximum, at least 1):
+    the dividend is pre-shifted by 8 - n limbs, then 32n steps each shift (r:a) left by one bit,
+    subtract the divisor from r, keep the difference when it did not borrow (or r overflowed
+    256 bits), and shift the quotient bit into a.  Loops are wave-uniform (SALU counters)."""
+    A = [f"v{UBASE + l}" for l in range(L)]
+    Bv = [f"v{UBASE + 8 + l}" for l in range(L)]
+    Tv = [f"v{UBASE + 16 + l}" for l in range(L)]
+    out = [f"{pfx}_sub_udivv:", "s_mov_b32 s64, 1"]
+    for l in range(1, L):   # s64 = 1 + the highest limb any lane's dividend uses
+        out += [f"v_cmp_ne_u32_e64 s[34:35], 0, {A[l]}", "s_nop 3", "s_cmp_lg_u64 s[34:35], 0",
+                f"s_cselect_b32 s64, {l + 1}, s64"]
+    out += ["s_sub_u32 s65, 8, s64", f"{pfx}_udivv_pre:", "s_cmp_eq_u32 s65, 0", f"s_cbranch_scc1 {pfx}_udivv_go"]
+    out += [f"v_mov_b32 {A[l]}, {A[l - 1]}" for l in range(L - 1, 0, -1)] + [f"v_mov_b32 {A[0]}, 0",
+                                                                              "s_sub_u32 s65, s65, 1",
+                                                                              f"s_branch {pfx}_udivv_pre"]
+    out += [f"{pfx}_udivv_go:", "s_lshl_b32 s66, s64, 5"] + [f"v_mov_b32 {W(l)}, 0" for l in range(L)]
+    out += [f"{pfx}_udivv_step:",
+            f"v_lshrrev_b32 v4, 31, {W(L - 1)}",
+            "v_cmp_ne_u32_e64 s[36:37], 0, v4"]                  # r's top bit before the shift
+    out += [f"v_alignbit_b32 {W(l)}, {W(l)}, {W(l - 1)}, 31" for l in range(L - 1, 0, -1)]
+    out += [f"v_alignbit_b32 {W(0)}, {W(0)}, {A[L - 1]}, 31"]
+    out += [f"v_alignbit_b32 {A[l]}, {A[l]}, {A[l - 1]}, 31" for l in range(L - 1, 0, -1)]
+    out += [f"v_lshlrev_b32 {A[0]}, 1, {A[0]}"]
+    out += carry_chain(lambda l: f"v_sub_co_u32 {Tv[l]}, vcc, {W(l)}, {Bv[l]}",
+                       lambda l: f"v_subb_co_u32 {Tv[l]}, vcc, {W(l)}, {Bv[l]}, vcc")
+    out += ["s_nop 3",
+            "s_not_b64 s[38:39], vcc",
+            "s_or_b64 s[38:39], s[38:39], s[36:37]"]            # r >= b
+    out += [f"v_cndmask_b32_e64 {W(l)}, {W(l)}, {Tv[l]}, s[38:39]" for l in range(L)]
+    out += ["v_cndmask_b32_e64 v5, 0, 1, s[38:39]", f"v_or_b32 {A[0]}, {A[0]}, v5",
+            "s_sub_u32 s66, s66, 1", "s_cmp_lg_u32 s66, 0", f"s_cbranch_scc1 {pfx}_udivv_step"]
+    # divisor 0: the quotient is all ones (the remainder already equals the dividend)
+    out += [f"v_or3_b32 v5, {Bv[0]}, {Bv[1]}, {Bv[2]}", f"v_or3_b32 v5, v5, {Bv[3]}, {Bv[4]}",
+            f"v_or3_b32 v5, v5, {Bv[5]}, {Bv[6]}", f"v_or_b32 v5, v5, {Bv[7]}",
+            "v_cmp_eq_u32_e64 s[34:35], 0, v5", "s_nop 1"]
+    out += [f"v_cndmask_b32_e64 {A[l]}, {A[l]}, -1, s[34:35]" for l in range(L)]
+    out += ["s_setpc_b64 s[76:77]"]
+    return out
+
+
 def sub_uf1(pfx):
     """Arity-1 model function lookup (UF / as-array select, z3 completion: the else value when no
     entry matches): key W[0..7] (canonical), s98 = function id; result in v[UBASE:UBASE+7].
@@ -827,6 +871,14 @@ def make_handlers(variant, pfx):
     for x in range(D - 1):
         for kind in ("UDIVC", "UREMC", "SREMC", "SMODCP", "SMODCN", "SDIVCP", "SDIVCN"):
             H((kind, x), divc_body(x, kind, pfx))
+    # ---- G: division by a variable divisor (operand slots x, x + 1; sub_udivv)
+    if G:
+        for x in range(D - 1):
+            cin = [f"v_mov_b64 v[{UBASE + l}:{UBASE + l + 1}], {S2(x, l)}" for l in range(0, L, 2)]
+            cin += [f"v_mov_b64 v[{UBASE + 8 + l}:{UBASE + 9 + l}], {S2(x + 1, l)}" for l in range(0, L, 2)]
+            call = [f"s_call_b64 s[76:77], {pfx}_sub_udivv"]
+            H(("UDIVV", x), cin + call + [f"v_mov_b64 {S2(x, l)}, v[{UBASE + l}:{UBASE + l + 1}]" for l in range(0, L, 2)])
+            H(("UREMV", x), cin + call + copy_from_w(x))
     # ---- model function lookup (G: uses v[8:31])
     if G:
         for d in range(D):
@@ -975,7 +1027,7 @@ def make_handlers(variant, pfx):
             else:
                 fused = list(body) + (["s_nop 3"] if body[-1].startswith("v_") else []) + [f"{ins} {B(r - 1)}, {B(r - 1)}, {B(r)}"]
             hs.append(((kind + suf,) + tuple(key[1:]), fused + (prof_point(kind + suf) if G else []) + (NEXT_G if G else NEXT_P)))
-    subs = sub_abs_cneg(pfx) + sub_udiv32(pfx) + (sub_uf1(pfx) if G else [])
+    subs = sub_abs_cneg(pfx) + sub_udiv32(pfx) + (sub_uf1(pfx) + sub_udivv(pfx) if G else [])
     return hs, subs
 
 

@@ -1045,6 +1045,17 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
       // division by a constant divisor (the previous instruction pushed it), in place on d-1
       case G_UDIV: case G_UREM: case G_SDIV: case G_SREM: case G_SMOD: {
         uint32_t cv[8];
+        if (op == G_UDIV || op == G_UREM) {
+          // unsigned by a divisor that is not a non-zero 32-bit constant: G's UDIVV / UREMV
+          // (both slots; the quotient of x / 0 is all ones, masked back to the width)
+          bool small = after_const && const_value(prev_imm, cv) && cv[0] != 0;
+          for (int l = 1; small && l < 8; l++) small = cv[l] == 0;
+          if (!small) {
+            ok = d >= 1 && imm >= 1 && imm <= 256 && word(op == G_UDIV ? QK_UDIVV : QK_UREMV, d - 1, -1, 0) &&
+                 (op == G_UREM || mask(d - 1, imm));
+            break;
+          }
+        }
         ok = after_const && d >= 1 && imm >= 1 && imm <= 256 && const_value(prev_imm, cv);
         if (!ok) break;
         const bool sgn = op == G_SDIV || op == G_SREM || op == G_SMOD;
@@ -1936,8 +1947,9 @@ static int64_t g_tapes_per_group(int64_t n, int64_t M) {
 // the rest.  verdicts == nullptr -> first-hit mode into best.
 static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, hipStream_t st) {
   bool use_qsa = c->qsa_ready && c->use_asm && T->qsa.count > 0;
-  // latency-bound launch (a few tapes over a few models): one C++ launch, no P / G translation
-  if (use_qsa && (int64_t)T->n_tapes * ((c->M + 63) / 64) <= c->latency_waves) use_qsa = false;
+  // latency-bound launch (a few tapes over a few models): G runs one tape per wave instead of
+  // batching tapes per wave for throughput
+  const bool latency = (int64_t)T->n_tapes * ((c->M + 63) / 64) <= c->latency_waves;
   if (use_qsa) {
     const int rc = qsa_prepare(c, T);
     if (rc) return rc;
@@ -2120,7 +2132,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     const int64_t tiles256 = (c->M + 255) / 256;
     int64_t p_wg = 8192;   // P: target workgroup count (MQ_P_WG overrides)
     if (const char* e = std::getenv("MQ_P_WG")) p_wg = std::max(256L, std::atol(e));
-    int64_t tpg = k == 0 ? (int64_t(n) * tiles256 + p_wg - 1) / p_wg : g_tapes_per_group(n, c->M);
+    int64_t tpg = k == 0 ? (int64_t(n) * tiles256 + p_wg - 1) / p_wg : latency ? 1 : g_tapes_per_group(n, c->M);
     tpg = std::max<int64_t>(1, std::min<int64_t>(tpg, n));
     QArgs q{};
     q.descs = T->qdescs.as<GDesc>() + (k == 0 ? 0 : T->q_count[0]);

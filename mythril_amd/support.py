@@ -164,10 +164,10 @@ class VerdictEngine:
     # its ~1 000 nodes: its conjuncts are split into up to ``split_tapes // N`` contiguous groups,
     # each its own tape (one wave each), and the group verdict rows are AND-ed (the conjunction
     # holds iff every conjunct does).  Shared sub-terms are then re-evaluated per group — more
-    # work (and compile time), less latency: one query x 16 models 0.85 -> 0.18 ms of kernel
-    # (profiles/r02lat); from N = 32 the compile cost outweighs it (profiles/r02sp); 0 disables
+    # work (and compile time), less latency (profiles/r02lat*, r02sp); from N = 32 the compile
+    # cost outweighs it; 0 disables
     split_tapes = int(os.environ.get("MQ_SPLIT_TAPES", "32"))
-    # launches of at most this many waves run on ONE HIP C++ kernel launch (MQ_OPT_LATENCY_WAVES)
+    # launches of at most this many waves run the G kernel one tape per wave (MQ_OPT_LATENCY_WAVES)
     latency_waves = int(os.environ.get("MQ_LATENCY_WAVES", "1024"))
     STAGES = ("lower", "serialize", "upload", "compile", "evaluate")
 

@@ -1,6 +1,6 @@
 """GPU parity of the drop-in path's latency mode: a single EVM-shaped conjunction split into its
-conjuncts (support.py split_conjuncts) and evaluated with MQ_OPT_LATENCY_WAVES (one HIP C++
-launch, no P / G translation) gives the oracle's verdicts, the same as the P / G / C++ sequence."""
+conjuncts (support.py split_conjuncts) and evaluated with MQ_OPT_LATENCY_WAVES (the G kernel with
+one tape per wave) gives the oracle's verdicts, the same as the throughput launch."""
 import numpy as np
 import pytest
 
@@ -35,9 +35,8 @@ def test_latency_mode_split_matches_oracle(evaluator, n, m):
             evaluator.set_option(evaluator.OPT_LATENCY_WAVES, 0)
         assert (v == ref).all()
         assert np.array_equal(np.logical_and.reduceat(v, starts, axis=0), whole_ref)
-    assert out[1 << 20][1] is False          # latency mode: no assembly translation ran
-    if evaluator.asm_ready:
-        assert out[0][1] is True             # otherwise the conjuncts without division ran on P / G
+    if evaluator.asm_ready:                  # the EVM-shaped conjuncts (variable divisions too) run on P / G
+        assert out[0][1] is True and out[1 << 20][1] is True
 
 
 def test_verdict_engine_small_batch_answers(evaluator):

@@ -620,3 +620,93 @@ def test_bool_columns_repacked_per_level(evaluator, monkeypatch):
     fh2 = evaluator.first_hit(ct)
     ref_fh, _ = cref.first_hit(tb2, serialize_models(models, syms2))
     assert (fh2 == ref_fh).all()
+
+
+# ---------------------------------------------------------------- G kernel: division by a variable
+def _var_division_workload(M, seed):
+    """x / y and x % y with variable (and wide-constant / zero-constant) divisors at 256 and 64
+    bits, against per-model quotients q and remainders r (perturbed in ~30 % of the models),
+    plus the SafeMath multiplication check: zero, one, equal, larger and multi-limb divisors."""
+    from mythril_amd.models import ModelBatch
+    from mythril_amd.tape import Tape, TapeBatch
+    rng = np.random.default_rng(seed)
+
+    def draw(bits, n):
+        kind = rng.integers(0, 6, n)
+        out = []
+        for k in kind:
+            if k == 0:
+                out.append(0)
+            elif k == 1:
+                out.append(1)
+            elif k == 2:
+                out.append(int(rng.integers(2, 1 << 16)))
+            elif k == 3:
+                out.append(int(rng.integers(1, 1 << 62)) << int(rng.integers(0, bits - 62)))
+            else:
+                out.append(int.from_bytes(rng.bytes(bits // 8), "little"))
+        return out
+
+    cols = {}
+    for w in (256, 64):
+        mask = (1 << w) - 1
+        xs, ys = draw(w, M), draw(w, M)
+        for m in range(M):
+            if rng.random() < 0.15:
+                ys[m] = xs[m]
+            elif rng.random() < 0.1:
+                ys[m] = (xs[m] + int(rng.integers(1, 1000))) & mask
+        qs = [mask if y == 0 else x // y for x, y in zip(xs, ys)]
+        rs = [x if y == 0 else x % y for x, y in zip(xs, ys)]
+        for arr in (qs, rs):
+            for m in range(M):
+                if rng.random() < 0.3:
+                    arr[m] = (arr[m] + 1) & mask
+        cols[w] = (xs, ys, qs, rs)
+    widths, rows = [], []
+    for w in (256, 64):
+        for vals in cols[w]:
+            widths.append(w)
+            nl = w // 32
+            rows += [[(v >> (32 * l)) & 0xFFFFFFFF for v in vals] for l in range(nl)]
+    mb = ModelBatch(widths, np.asarray(rows, np.uint32))
+    big = (1 << 200) + 12345
+    tapes = []
+    for i, w in enumerate((256, 64)):
+        x, y, q, r = (4 * i + k for k in range(4))
+        for form in range(6):
+            tp = Tape()
+            X, Y, Q, R = tp.var(x, w), tp.var(y, w), tp.var(q, w), tp.var(r, w)
+            if form == 0:
+                root = tp.eq(tp.udiv(X, Y), Q)
+            elif form == 1:
+                root = tp.eq(tp.urem(X, Y), R)
+            elif form == 2:
+                root = tp.and_(tp.eq(tp.udiv(X, Y), Q), tp.not_(tp.eq(tp.urem(X, Y), R)))
+            elif form == 3:   # SafeMath: x == 0 or (x * y) / x == y
+                root = tp.or_(tp.eq(X, tp.const(0, w)), tp.eq(tp.udiv(tp.mul(X, Y), X), Y))
+            elif form == 4:   # wide and zero constant divisors
+                root = tp.and_(tp.ult(tp.udiv(X, tp.const(big & ((1 << w) - 1), w)), Q),
+                               tp.eq(tp.udiv(X, tp.const(0, w)), tp.const((1 << w) - 1, w)))
+            else:
+                root = tp.ule(tp.urem(tp.add(X, Q), tp.udiv(Y, tp.const(3, w))), R)
+            tapes.append(tp.finish(root))
+    return TapeBatch(tapes), mb
+
+
+@pytest.mark.parametrize("M", [64, 1000])
+def test_g_kernel_variable_division_matches_oracle(evaluator, M):
+    tb, mb = _var_division_workload(M, seed=M)
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    v, fh = evaluator.verdicts(ct)
+    n_p, n_g, live = ct.asm_split()
+    assert live and n_g >= 8, (n_p, n_g, ct.split())
+    hist = ct.handler_histogram(1)
+    assert hist.get("UDIVV", 0) > 0 and hist.get("UREMV", 0) > 0, hist
+    ref = cref.verdicts(tb, mb)
+    mism = np.argwhere(v != ref)
+    assert len(mism) == 0, f"{len(mism)} mismatches, first {mism[:5]}"
+    assert ref.any(axis=1).sum() >= 6 and (~ref).any(axis=1).sum() >= 6
+    fh_ref, _ = cref.first_hit(tb, mb)
+    assert (evaluator.first_hit(ct) == fh_ref).all()
