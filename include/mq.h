@@ -288,7 +288,8 @@ int mq_keccak256(mq_ctx* ctx, const uint8_t* data, const int64_t* offsets, int32
    MQ_OPT_LATENCY_WAVES (default 0 = off): a launch of at most this many waves (tapes x 64-model
    tiles) runs the general assembly kernel with one tape per wave instead of several tapes per
    wave: a few tapes over a few models are latency-bound (the drop-in path at the reference's
-   shape sets it). */
+   shape sets it).  Such a launch with more than 16 384 tape nodes skips the assembly
+   translation (host time) and runs on the HIP C++ kernel. */
 enum mq_option {
   MQ_OPT_USE_ASM = 1,
   MQ_OPT_EARLY_EXIT = 2,

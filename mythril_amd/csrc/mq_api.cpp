@@ -1945,11 +1945,20 @@ static int64_t g_tapes_per_group(int64_t n, int64_t M) {
 // Launch every evaluation kernel for a compiled batch: the assembly interpreter for the
 // QSA-eligible tapes (when the model batch fits its register file), the HIP C++ kernels for
 // the rest.  verdicts == nullptr -> first-hit mode into best.
+constexpr int64_t kLatencyAsmNodes = 16384;
+
 static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, hipStream_t st) {
   bool use_qsa = c->qsa_ready && c->use_asm && T->qsa.count > 0;
   // latency-bound launch (a few tapes over a few models): G runs one tape per wave instead of
-  // batching tapes per wave for throughput
+  // batching tapes per wave for throughput -- unless the batch is large enough that translating
+  // it for P / G (host, ~50 ns per node) costs more than the C++ kernel's extra latency
+  // (profiles/r02dv2: 256 EVM-shaped queries x 100 models, 13 ms of translation for 0.6 ms)
   const bool latency = (int64_t)T->n_tapes * ((c->M + 63) / 64) <= c->latency_waves;
+  if (use_qsa && latency) {
+    int64_t nodes = 0;
+    for (int64_t n : T->n_nodes) nodes += n;
+    if (nodes > kLatencyAsmNodes) use_qsa = false;
+  }
   if (use_qsa) {
     const int rc = qsa_prepare(c, T);
     if (rc) return rc;
