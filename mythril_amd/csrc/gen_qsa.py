@@ -573,7 +573,9 @@ def sub_udivv(pfx):
     division over the dividend's significant limbs only (n = the wave's maximum, at least 1):
     the dividend is pre-shifted by 8 - n limbs, then 32n steps each shift (r:a) left by one bit,
     subtract the divisor from r, keep the difference when it did not borrow (or r overflowed
-    256 bits), and shift the quotient bit into a.  Loops are wave-uniform (SALU counters)."""
+    256 bits), and shift the quotient bit into a.  The first steps, while r is shorter than
+    every lane's divisor, produce 0 bits and are taken a whole limb at a time (so a 256-bit
+    divisor costs 32 steps, not 256).  Loops are wave-uniform (SALU counters)."""
     A = [f"v{UBASE + l}" for l in range(L)]
     Bv = [f"v{UBASE + 8 + l}" for l in range(L)]
     Tv = [f"v{UBASE + 16 + l}" for l in range(L)]
@@ -585,7 +587,25 @@ def sub_udivv(pfx):
     out += [f"v_mov_b32 {A[l]}, {A[l - 1]}" for l in range(L - 1, 0, -1)] + [f"v_mov_b32 {A[0]}, 0",
                                                                               "s_sub_u32 s65, s65, 1",
                                                                               f"s_branch {pfx}_udivv_pre"]
-    out += [f"{pfx}_udivv_go:", "s_lshl_b32 s66, s64, 5"] + [f"v_mov_b32 {W(l)}, 0" for l in range(L)]
+    out += [f"{pfx}_udivv_go:"] + [f"v_mov_b32 {W(l)}, 0" for l in range(L)]
+    # while r has fewer limbs than every lane's divisor, a step only moves a bit of a into r:
+    # s67 = the number of limbs below the top nonzero limb of the divisor, minimum over the
+    # wave (0 if any divisor is 0); those steps are limb moves, min(s67, s64) of them
+    out += ["s_mov_b32 s67, 0", f"v_mov_b32 v5, {Bv[L - 1]}"]
+    for l in range(L - 1, 0, -1):
+        out += ([f"v_or_b32 v5, v5, {Bv[l]}"] if l < L - 1 else []) + [
+            "v_cmp_ne_u32_e64 s[34:35], 0, v5", "s_nop 3", "s_cmp_eq_u64 s[34:35], exec",
+            f"s_cbranch_scc1 {pfx}_udivv_nb{l}"]
+    out += [f"s_branch {pfx}_udivv_skip"]
+    for l in range(L - 1, 0, -1):
+        out += [f"{pfx}_udivv_nb{l}:", f"s_mov_b32 s67, {l}", f"s_branch {pfx}_udivv_skip"]
+    out += [f"{pfx}_udivv_skip:", "s_min_u32 s67, s67, s64", "s_sub_u32 s66, s64, s67", "s_lshl_b32 s66, s66, 5",
+            f"{pfx}_udivv_mv:", "s_cmp_eq_u32 s67, 0", f"s_cbranch_scc1 {pfx}_udivv_steps"]
+    out += [f"v_mov_b32 {W(l)}, {W(l - 1)}" for l in range(L - 1, 0, -1)] + [f"v_mov_b32 {W(0)}, {A[L - 1]}"]
+    out += [f"v_mov_b32 {A[l]}, {A[l - 1]}" for l in range(L - 1, 0, -1)] + [f"v_mov_b32 {A[0]}, 0",
+                                                                              "s_sub_u32 s67, s67, 1",
+                                                                              f"s_branch {pfx}_udivv_mv"]
+    out += [f"{pfx}_udivv_steps:", "s_cmp_eq_u32 s66, 0", f"s_cbranch_scc1 {pfx}_udivv_done"]
     out += [f"{pfx}_udivv_step:",
             f"v_lshrrev_b32 v4, 31, {W(L - 1)}",
             "v_cmp_ne_u32_e64 s[36:37], 0, v4"]                  # r's top bit before the shift
@@ -602,7 +622,7 @@ def sub_udivv(pfx):
     out += ["v_cndmask_b32_e64 v5, 0, 1, s[38:39]", f"v_or_b32 {A[0]}, {A[0]}, v5",
             "s_sub_u32 s66, s66, 1", "s_cmp_lg_u32 s66, 0", f"s_cbranch_scc1 {pfx}_udivv_step"]
     # divisor 0: the quotient is all ones (the remainder already equals the dividend)
-    out += [f"v_or3_b32 v5, {Bv[0]}, {Bv[1]}, {Bv[2]}", f"v_or3_b32 v5, v5, {Bv[3]}, {Bv[4]}",
+    out += [f"{pfx}_udivv_done:", f"v_or3_b32 v5, {Bv[0]}, {Bv[1]}, {Bv[2]}", f"v_or3_b32 v5, v5, {Bv[3]}, {Bv[4]}",
             f"v_or3_b32 v5, v5, {Bv[5]}, {Bv[6]}", f"v_or_b32 v5, v5, {Bv[7]}",
             "v_cmp_eq_u32_e64 s[34:35], 0, v5", "s_nop 1"]
     out += [f"v_cndmask_b32_e64 {A[l]}, {A[l]}, -1, s[34:35]" for l in range(L)]

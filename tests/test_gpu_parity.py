@@ -691,6 +691,14 @@ def _var_division_workload(M, seed):
             else:
                 root = tp.ule(tp.urem(tp.add(X, Q), tp.udiv(Y, tp.const(3, w))), R)
             tapes.append(tp.finish(root))
+        # divisors forced above 2^k in every lane (the limb-skipping start of G's division):
+        # q * d + r == x and r < d hold in every model iff the division is right
+        for k in ((200, 255, 40, 33) if w == 256 else (40, 63, 33)):
+            tp = Tape()
+            X, Y = tp.var(x, w), tp.var(y, w)
+            D = tp.bor(Y, tp.const(1 << k, w))
+            q_, r_ = tp.udiv(X, D), tp.urem(X, D)
+            tapes.append(tp.finish(tp.and_(tp.eq(tp.add(tp.mul(q_, D), r_), X), tp.ult(r_, D))))
     return TapeBatch(tapes), mb
 
 
