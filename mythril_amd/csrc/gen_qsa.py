@@ -630,6 +630,46 @@ def sub_udivv(pfx):
     return out
 
 
+def cneg(regs, m):
+    """regs (a 256-bit value, limbs) = -regs where the lane mask VGPR m is all ones: (x ^ m) - m."""
+    return [f"v_xor_b32 {r}, {r}, {m}" for r in regs] + carry_chain(
+        lambda l: f"v_sub_co_u32 {regs[l]}, vcc, {regs[l]}, {m}",
+        lambda l: f"v_subb_co_u32 {regs[l]}, vcc, {regs[l]}, {m}, vcc")
+
+
+def sdivv_body(x, kind, cin_call):
+    """G: bvsdiv / bvsrem / bvsmod at 256 bits by a variable divisor (slots x, x + 1): the
+    unsigned division of |a| by |b| (sub_udivv), then the SMT-LIB sign rules; v6 / v7 = sign
+    masks of a / b.  A zero divisor needs no case of its own: |a| / 0 = all ones gives -1 or 1,
+    |a| % 0 = |a| gives a back."""
+    A = [f"v{UBASE + l}" for l in range(L)]
+    Bv = [f"v{UBASE + 8 + l}" for l in range(L)]
+    Tv = [f"v{UBASE + 16 + l}" for l in range(L)]
+    cin, call = cin_call[:-1], cin_call[-1:]
+    out = cin + [f"v_ashrrev_i32 v6, 31, {A[L - 1]}", f"v_ashrrev_i32 v7, 31, {Bv[L - 1]}"]
+    out += cneg(A, "v6") + cneg(Bv, "v7") + call
+    Wr = [W(l) for l in range(L)]
+    if kind == "SDIVV":
+        out += ["v_xor_b32 v6, v6, v7"] + cneg(A, "v6")
+        out += [f"v_mov_b64 {S2(x, l)}, v[{UBASE + l}:{UBASE + l + 1}]" for l in range(0, L, 2)]
+    elif kind == "SREMV":
+        out += cneg(Wr, "v6") + copy_from_w(x)
+    else:
+        # t = sa ? -u : u, plus b (the original divisor, slot x + 1) when the signs differ and u != 0
+        out += [f"v_or3_b32 v5, {Wr[0]}, {Wr[1]}, {Wr[2]}", f"v_or3_b32 v5, v5, {Wr[3]}, {Wr[4]}",
+                f"v_or3_b32 v5, v5, {Wr[5]}, {Wr[6]}", f"v_or_b32 v5, v5, {Wr[7]}",
+                "v_cmp_ne_u32_e64 s[34:35], 0, v5",
+                "v_xor_b32 v7, v6, v7",
+                "v_cmp_ne_u32_e64 s[36:37], 0, v7"]
+        out += cneg(Wr, "v6")
+        out += ["s_nop 3", "s_and_b64 s[38:39], s[34:35], s[36:37]"]
+        out += [f"v_cndmask_b32_e64 {Tv[l]}, 0, {S(x + 1, l)}, s[38:39]" for l in range(L)]
+        out += carry_chain(lambda l: f"v_add_co_u32 {Wr[l]}, vcc, {Wr[l]}, {Tv[l]}",
+                           lambda l: f"v_addc_co_u32 {Wr[l]}, vcc, {Wr[l]}, {Tv[l]}, vcc")
+        out += copy_from_w(x)
+    return out
+
+
 def sub_uf1(pfx):
     """Arity-1 model function lookup (UF / as-array select, z3 completion: the else value when no
     entry matches): key W[0..7] (canonical), s98 = function id; result in v[UBASE:UBASE+7].
@@ -899,6 +939,8 @@ def make_handlers(variant, pfx):
             call = [f"s_call_b64 s[76:77], {pfx}_sub_udivv"]
             H(("UDIVV", x), cin + call + [f"v_mov_b64 {S2(x, l)}, v[{UBASE + l}:{UBASE + l + 1}]" for l in range(0, L, 2)])
             H(("UREMV", x), cin + call + copy_from_w(x))
+            for kind in ("SDIVV", "SREMV", "SMODV"):
+                H((kind, x), sdivv_body(x, kind, cin + call))
     # ---- model function lookup (G: uses v[8:31])
     if G:
         for d in range(D):

@@ -1045,10 +1045,19 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
       // division by a constant divisor (the previous instruction pushed it), in place on d-1
       case G_UDIV: case G_UREM: case G_SDIV: case G_SREM: case G_SMOD: {
         uint32_t cv[8];
+        if (!after_const) {
+          // by a variable divisor: G's UDIVV / UREMV (both slots; the quotient of x / 0 is all
+          // ones, masked back to the width) and, at 256 bits, SDIVV / SREMV / SMODV
+          int kind = op == G_UDIV ? QK_UDIVV : op == G_UREM ? QK_UREMV : op == G_SDIV ? QK_SDIVV
+                   : op == G_SREM ? QK_SREMV : QK_SMODV;
+          const bool sgn = op == G_SDIV || op == G_SREM || op == G_SMOD;
+          ok = d >= 1 && imm >= 1 && imm <= 256 && (!sgn || imm == 256) && word(kind, d - 1, -1, 0) &&
+               (op != G_UDIV || mask(d - 1, imm));
+          break;
+        }
         if (op == G_UDIV || op == G_UREM) {
-          // unsigned by a divisor that is not a non-zero 32-bit constant: G's UDIVV / UREMV
-          // (both slots; the quotient of x / 0 is all ones, masked back to the width)
-          bool small = after_const && const_value(prev_imm, cv) && cv[0] != 0;
+          // unsigned by a constant that is not a non-zero 32-bit value: UDIVV / UREMV on it
+          bool small = const_value(prev_imm, cv) && cv[0] != 0;
           for (int l = 1; small && l < 8; l++) small = cv[l] == 0;
           if (!small) {
             ok = d >= 1 && imm >= 1 && imm <= 256 && word(op == G_UDIV ? QK_UDIVV : QK_UREMV, d - 1, -1, 0) &&

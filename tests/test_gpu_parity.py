@@ -718,3 +718,73 @@ def test_g_kernel_variable_division_matches_oracle(evaluator, M):
     assert ref.any(axis=1).sum() >= 6 and (~ref).any(axis=1).sum() >= 6
     fh_ref, _ = cref.first_hit(tb, mb)
     assert (evaluator.first_hit(ct) == fh_ref).all()
+
+
+def _signed_division_workload(M, seed):
+    """bvsdiv / bvsrem / bvsmod by a variable at 256 bits: the identities a = q * b + r and
+    smod = srem (+ b when the signs differ and srem != 0), and compares against a third
+    variable, over zero, +-1, MIN, small and full-width operands of both signs."""
+    from mythril_amd.models import ModelBatch
+    from mythril_amd.tape import Tape, TapeBatch
+    rng = np.random.default_rng(seed)
+    MIN, MASK = 1 << 255, (1 << 256) - 1
+
+    def draw(n):
+        out = []
+        for k in rng.integers(0, 7, n):
+            if k == 0:
+                out.append(0)
+            elif k == 1:
+                out.append(int(rng.choice([1, MASK, MIN])))
+            elif k == 2:
+                out.append(int(rng.integers(1, 1 << 20)))
+            elif k == 3:
+                out.append((-int(rng.integers(1, 1 << 20))) & MASK)
+            else:
+                out.append(int.from_bytes(rng.bytes(32), "little"))
+        return out
+
+    cols = [draw(M), draw(M), draw(M)]
+    rows = [[(v >> (32 * l)) & 0xFFFFFFFF for v in vals] for vals in cols for l in range(8)]
+    mb = ModelBatch([256, 256, 256], np.asarray(rows, np.uint32))
+    tapes = []
+    for form in range(7):
+        tp = Tape()
+        X, Y, Z = tp.var(0, 256), tp.var(1, 256), tp.var(2, 256)
+        q, r, md = tp.sdiv(X, Y), tp.srem(X, Y), tp.smod(X, Y)
+        zero = tp.const(0, 256)
+        if form == 0:
+            root = tp.eq(tp.add(tp.mul(q, Y), r), X)
+        elif form == 1:
+            same = tp.eq(tp.slt(X, zero), tp.slt(Y, zero))
+            root = tp.eq(md, tp.ite(tp.or_(tp.eq(r, zero), same), r, tp.add(r, Y)))
+        elif form == 2:
+            root = tp.slt(q, Z)
+        elif form == 3:
+            root = tp.slt(r, Z)
+        elif form == 4:
+            root = tp.sle(md, Z)
+        elif form == 5:
+            root = tp.eq(tp.sdiv(X, Z), tp.sdiv(Y, Z))
+        else:
+            root = tp.ult(tp.smod(Z, Y), tp.srem(Z, X))
+        tapes.append(tp.finish(root))
+    return TapeBatch(tapes), mb
+
+
+@pytest.mark.parametrize("M", [64, 700])
+def test_g_kernel_signed_variable_division_matches_oracle(evaluator, M):
+    tb, mb = _signed_division_workload(M, seed=M + 1)
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    v, fh = evaluator.verdicts(ct)
+    n_p, n_g, live = ct.asm_split()
+    assert live and n_g == tb.n_tapes, (n_p, n_g, ct.split())
+    hist = ct.handler_histogram(1)
+    assert all(hist.get(k, 0) > 0 for k in ("SDIVV", "SREMV", "SMODV")), hist
+    ref = cref.verdicts(tb, mb)
+    assert ref[:2].all()                      # the identities hold in every model (oracle)
+    mism = np.argwhere(v != ref)
+    assert len(mism) == 0, f"{len(mism)} mismatches, first {mism[:5]}"
+    fh_ref, _ = cref.first_hit(tb, mb)
+    assert (evaluator.first_hit(ct) == fh_ref).all()
