@@ -630,6 +630,42 @@ def sub_udivv(pfx):
     return out
 
 
+def shiftv_body(x, kind):
+    """G: S[x] shifted by the variable amount S[x + 1] (per lane; imm = the width W): amounts
+    >= W (or with high limbs) give 0 (ASHR, at 256 bits only: the sign fill).  A barrel shift:
+    whole limbs in three conditional stages (4, 2, 1 limbs), then the bit shift with per-lane
+    v_alignbit / 64-bit shifts."""
+    X = [S(x, l) for l in range(L)]
+    amt = [S(x + 1, l) for l in range(L)]
+    right = kind != "SHLV"
+    fill = "v6" if kind == "ASHRV" else "0"
+    out = [f"v_or3_b32 v5, {amt[1]}, {amt[2]}, {amt[3]}", f"v_or3_b32 v5, v5, {amt[4]}, {amt[5]}",
+           f"v_or3_b32 v5, v5, {amt[6]}, {amt[7]}",
+           "v_cmp_ne_u32_e64 s[34:35], 0, v5", f"v_cmp_le_u32_e64 s[36:37], s17, {amt[0]}",
+           f"v_bfe_u32 v7, {amt[0]}, 5, 3", f"v_and_b32 v3, 31, {amt[0]}"]
+    if kind == "ASHRV":
+        out.append(f"v_ashrrev_i32 v6, 31, {X[L - 1]}")
+    for k in (4, 2, 1):
+        out += [f"v_and_b32 v5, {k}, v7", "v_cmp_ne_u32_e64 vcc, 0, v5", "s_nop 1"]
+        order = range(L) if right else range(L - 1, -1, -1)
+        for i in order:
+            j = i + k if right else i - k
+            src = X[j] if 0 <= j < L else fill
+            out.append(f"v_cndmask_b32_e64 {X[i]}, {X[i]}, {src}, vcc")
+    if right:
+        for i in range(L):
+            hi = X[i + 1] if i + 1 < L else ("v6" if kind == "ASHRV" else "0")
+            out.append(f"v_alignbit_b32 {X[i]}, {hi}, {X[i]}, v3")
+    else:
+        for i in range(L - 1, 0, -1):
+            out += [f"v_mov_b32 v4, {X[i - 1]}", f"v_mov_b32 v5, {X[i]}", "v_lshlrev_b64 v[4:5], v3, v[4:5]",
+                    f"v_mov_b32 {X[i]}, v5"]
+        out.append(f"v_lshlrev_b32 {X[0]}, v3, {X[0]}")
+    out += ["s_nop 1", "s_or_b64 s[38:39], s[34:35], s[36:37]"]
+    out += [f"v_cndmask_b32_e64 {X[i]}, {X[i]}, {fill}, s[38:39]" for i in range(L)]
+    return out
+
+
 def cneg(regs, m):
     """regs (a 256-bit value, limbs) = -regs where the lane mask VGPR m is all ones: (x ^ m) - m."""
     return [f"v_xor_b32 {r}, {r}, {m}" for r in regs] + carry_chain(
@@ -941,6 +977,8 @@ def make_handlers(variant, pfx):
             H(("UREMV", x), cin + call + copy_from_w(x))
             for kind in ("SDIVV", "SREMV", "SMODV"):
                 H((kind, x), sdivv_body(x, kind, cin + call))
+            for kind in ("SHLV", "LSHRV", "ASHRV"):
+                H((kind, x), shiftv_body(x, kind))
     # ---- model function lookup (G: uses v[8:31])
     if G:
         for d in range(D):

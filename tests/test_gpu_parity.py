@@ -788,3 +788,56 @@ def test_g_kernel_signed_variable_division_matches_oracle(evaluator, M):
     assert len(mism) == 0, f"{len(mism)} mismatches, first {mism[:5]}"
     fh_ref, _ = cref.first_hit(tb, mb)
     assert (evaluator.first_hit(ct) == fh_ref).all()
+
+
+def _variable_shift_workload(M, seed):
+    """shl / lshr / ashr by a per-model amount (0 .. W+9, and amounts with high limbs) at 256
+    and 64 bits: the identity (x >> a) << a == x & (ones << a) and compares with a third
+    variable (sensitive verdicts, checked against the oracle)."""
+    from mythril_amd.models import ModelBatch
+    from mythril_amd.tape import Tape, TapeBatch
+    rng = np.random.default_rng(seed)
+    widths, rows = [], []
+    for w in (256, 64):
+        xs = [int.from_bytes(rng.bytes(w // 8), "little") for _ in range(M)]
+        zs = [int.from_bytes(rng.bytes(w // 8), "little") for _ in range(M)]
+        amts = [int(rng.integers(0, w + 10)) if rng.random() < 0.85 else
+                (int(rng.integers(1, 1 << 30)) << 64) & ((1 << w) - 1) | int(rng.integers(0, 8)) for _ in range(M)]
+        for vals in (xs, zs, amts):
+            widths.append(w)
+            rows += [[(v >> (32 * l)) & 0xFFFFFFFF for v in vals] for l in range(w // 32)]
+    mb = ModelBatch(widths, np.asarray(rows, np.uint32))
+    tapes = []
+    for i, w in enumerate((256, 64)):
+        ones = (1 << w) - 1
+        for form in range(5 if w == 256 else 4):
+            tp = Tape()
+            X, Z, A = tp.var(3 * i, w), tp.var(3 * i + 1, w), tp.var(3 * i + 2, w)
+            if form == 0:
+                root = tp.eq(tp.shl(tp.lshr(X, A), A), tp.band(X, tp.shl(tp.const(ones, w), A)))
+            elif form == 1:
+                root = tp.ult(tp.lshr(X, A), tp.lshr(Z, tp.const(3, w)))
+            elif form == 2:
+                root = tp.ult(tp.shl(X, A), Z)
+            elif form == 3:
+                root = tp.eq(tp.lshr(tp.shl(X, A), A), tp.lshr(tp.shl(Z, A), A))
+            else:
+                root = tp.slt(tp.ashr(X, A), tp.ashr(Z, tp.const(7, w)))
+            tapes.append(tp.finish(root))
+    return TapeBatch(tapes), mb
+
+
+@pytest.mark.parametrize("M", [64, 700])
+def test_g_kernel_variable_shifts_match_oracle(evaluator, M):
+    tb, mb = _variable_shift_workload(M, seed=M + 2)
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    v, fh = evaluator.verdicts(ct)
+    n_p, n_g, live = ct.asm_split()
+    assert live and n_p + n_g == tb.n_tapes, (n_p, n_g, ct.split())
+    ref = cref.verdicts(tb, mb)
+    assert ref[0].all() and ref[5].all()      # the identity holds in every model (oracle)
+    mism = np.argwhere(v != ref)
+    assert len(mism) == 0, f"{len(mism)} mismatches, first {mism[:5]}"
+    fh_ref, _ = cref.first_hit(tb, mb)
+    assert (evaluator.first_hit(ct) == fh_ref).all()
