@@ -1024,9 +1024,10 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
       // shifts by a constant amount (the previous instruction pushed it): in place on slot d-1
       case G_SHL: case G_LSHR: case G_ASHR: {
         uint32_t cv[8];
-        if (!after_const) {   // by a variable amount: G's SHLV / LSHRV / ASHRV (ASHR at 256 bits)
+        if (!after_const) {   // by a variable amount: G's SHLV / LSHRV / ASHRV (ASHR at 256 bits);
+          // the immediate is the width W: the handler replaces results of amounts >= W by the fill
           ok = d >= 1 && imm >= 1 && imm <= 256 && (op != G_ASHR || imm == 256) &&
-               word(op == G_SHL ? QK_SHLV : op == G_LSHR ? QK_LSHRV : QK_ASHRV, d - 1, -1, 0) &&
+               word(op == G_SHL ? QK_SHLV : op == G_LSHR ? QK_LSHRV : QK_ASHRV, d - 1, -1, imm) &&
                (op != G_SHL || mask(d - 1, imm));
           break;
         }

@@ -790,53 +790,92 @@ def test_g_kernel_signed_variable_division_matches_oracle(evaluator, M):
     assert (evaluator.first_hit(ct) == fh_ref).all()
 
 
+SHIFT_WIDTHS = (256, 160, 64, 8)
+
+
+def _shift_amounts(rng, w, M):
+    """Per-model shift amounts at width w: the edge amounts 0, 1, 31, 32, 33, 63, 64, 255, 256,
+    257, W-1, W, W+1, 2^32, 2^32+1, 2^64, 2^255 (reduced mod 2^W), uniform amounts below W + 10
+    and amounts with high limbs set."""
+    edge = [0, 1, 31, 32, 33, 63, 64, 255, 256, 257, w - 1, w, w + 1, 1 << 32, (1 << 32) + 1, 1 << 64, 1 << 255]
+    out = []
+    for m in range(M):
+        r = rng.random()
+        if m < len(edge):
+            a = edge[m]
+        elif r < 0.5:
+            a = int(rng.integers(0, w + 10))
+        elif r < 0.8:
+            a = edge[int(rng.integers(0, len(edge)))]
+        else:
+            a = int.from_bytes(rng.bytes(32), "little")
+        out.append(a & ((1 << w) - 1))
+    return out
+
+
 def _variable_shift_workload(M, seed):
-    """shl / lshr / ashr by a per-model amount (0 .. W+9, and amounts with high limbs) at 256
-    and 64 bits: the identity (x >> a) << a == x & (ones << a) and compares with a third
-    variable (sensitive verdicts, checked against the oracle)."""
+    """shl / lshr / ashr by a per-model amount at widths 256, 160, 64 and 8 (_shift_amounts):
+    the identity (x >> a) << a == x & (ones << a), compares with a third variable (sensitive
+    verdicts, checked against the oracle), and EVM SIGNEXTEND's shape at 256 bits
+    (instructions.py:645-672: testbit = 8 * s + 7, shl(1, testbit) masks, ite on s <= 31)."""
     from mythril_amd.models import ModelBatch
     from mythril_amd.tape import Tape, TapeBatch
     rng = np.random.default_rng(seed)
     widths, rows = [], []
-    for w in (256, 64):
-        xs = [int.from_bytes(rng.bytes(w // 8), "little") for _ in range(M)]
-        zs = [int.from_bytes(rng.bytes(w // 8), "little") for _ in range(M)]
-        amts = [int(rng.integers(0, w + 10)) if rng.random() < 0.85 else
-                (int(rng.integers(1, 1 << 30)) << 64) & ((1 << w) - 1) | int(rng.integers(0, 8)) for _ in range(M)]
+    for w in SHIFT_WIDTHS:
+        xs = [int.from_bytes(rng.bytes(32), "little") & ((1 << w) - 1) for _ in range(M)]
+        zs = [int.from_bytes(rng.bytes(32), "little") & ((1 << w) - 1) for _ in range(M)]
+        amts = _shift_amounts(rng, w, M)
         for vals in (xs, zs, amts):
             widths.append(w)
-            rows += [[(v >> (32 * l)) & 0xFFFFFFFF for v in vals] for l in range(w // 32)]
+            rows += [[(v >> (32 * l)) & 0xFFFFFFFF for v in vals] for l in range((w + 31) // 32)]
     mb = ModelBatch(widths, np.asarray(rows, np.uint32))
-    tapes = []
-    for i, w in enumerate((256, 64)):
+    tapes, identities = [], []
+    for i, w in enumerate(SHIFT_WIDTHS):
         ones = (1 << w) - 1
-        for form in range(5 if w == 256 else 4):
+        for form in range(6 if w == 256 else 4):
             tp = Tape()
             X, Z, A = tp.var(3 * i, w), tp.var(3 * i + 1, w), tp.var(3 * i + 2, w)
             if form == 0:
+                identities.append(len(tapes))
                 root = tp.eq(tp.shl(tp.lshr(X, A), A), tp.band(X, tp.shl(tp.const(ones, w), A)))
             elif form == 1:
-                root = tp.ult(tp.lshr(X, A), tp.lshr(Z, tp.const(3, w)))
+                root = tp.ult(tp.lshr(X, A), tp.lshr(Z, tp.const(min(3, w - 1), w)))
             elif form == 2:
                 root = tp.ult(tp.shl(X, A), Z)
             elif form == 3:
                 root = tp.eq(tp.lshr(tp.shl(X, A), A), tp.lshr(tp.shl(Z, A), A))
-            else:
+            elif form == 4:
                 root = tp.slt(tp.ashr(X, A), tp.ashr(Z, tp.const(7, w)))
+            else:
+                # SIGNEXTEND(s = A & 31, x = X) compared with Z's low byte sign-extended
+                s = tp.band(A, tp.const(31, w))
+                testbit = tp.add(tp.mul(s, tp.const(8, w)), tp.const(7, w))
+                bit = tp.shl(tp.const(1, w), testbit)
+                setm = tp.sub(bit, tp.const(1, w))
+                neg = tp.distinct(tp.band(X, bit), tp.const(0, w))
+                se = tp.ite(neg, tp.bor(X, tp.bnot(setm)), tp.band(X, setm))
+                root = tp.ule(se, Z)
             tapes.append(tp.finish(root))
-    return TapeBatch(tapes), mb
+    return TapeBatch(tapes), mb, identities
 
 
 @pytest.mark.parametrize("M", [64, 700])
 def test_g_kernel_variable_shifts_match_oracle(evaluator, M):
-    tb, mb = _variable_shift_workload(M, seed=M + 2)
+    """Shifts by a variable amount run on G's SHLV / LSHRV / ASHRV handlers (no tape left on the
+    HIP C++ interpreter) and match the oracle bit for bit."""
+    tb, mb, identities = _variable_shift_workload(M, seed=M + 2)
     evaluator.upload_models(mb)
     ct = evaluator.compile(tb)
     v, fh = evaluator.verdicts(ct)
     n_p, n_g, live = ct.asm_split()
     assert live and n_p + n_g == tb.n_tapes, (n_p, n_g, ct.split())
+    hist = ct.handler_histogram(1)
+    for kind in ("SHLV", "LSHRV", "ASHRV"):
+        assert hist.get(kind, 0) > 0, (kind, hist)
     ref = cref.verdicts(tb, mb)
-    assert ref[0].all() and ref[5].all()      # the identity holds in every model (oracle)
+    for t in identities:
+        assert ref[t].all()          # the identity holds in every model (oracle)
     mism = np.argwhere(v != ref)
     assert len(mism) == 0, f"{len(mism)} mismatches, first {mism[:5]}"
     fh_ref, _ = cref.first_hit(tb, mb)
