@@ -97,6 +97,9 @@ def parse():
     p.add_argument("--no-hoist", action="store_true", help="c3/c4/c5: lower without batch-level hoisting")
     p.add_argument("--no-dropin", action="store_true", help="skip the drop-in leg (ModelCache at N<=256, M<=100)")
     p.add_argument("--no-early-exit", action="store_true", help="diagnostic: evaluate every (tape, model) pair")
+    p.add_argument("--context", action="store_true",
+                   help="drive the GPUs through one multi-device mq_ctx even at --gpus 1 (in-library RCCL with "
+                        "one rank: a 1-GPU rehearsal of the one-process N-GPU path)")
     return p.parse_args()
 
 
@@ -256,10 +259,37 @@ def pmc_traffic(workload_key: str):
     return None if e is None else {"bytes": e["fetch_bytes"] + e["write_bytes"], "source": e["source"]}
 
 
+def launch_mode(args):
+    """How the N GPUs of ``--gpus N`` are driven:
+    * ``torchrun``: WORLD_SIZE > 1 in the environment (the driver's N > 1 launch): one process per
+      GPU, torch.distributed over RCCL, this process is one rank;
+    * ``context``: ``--gpus N > 1`` without WORLD_SIZE: ONE process drives N devices through one
+      multi-device ``mq_ctx`` (mq_ctx_create(N, ids): the candidate axis is sharded inside
+      mq_models_upload, first hits are MIN-reduced by an in-library ncclAllReduce) — the way
+      Mythril itself, a single process (mythril_analyzer.py:136-185), would use N GPUs;
+    * ``single``: one GPU.
+    Returns (mode, n_gpus); exits non-zero with a message when N cannot be honoured."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        if args.gpus not in (1, world):
+            raise SystemExit(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world}")
+        return "torchrun", world
+    if args.gpus > 1 or getattr(args, "context", False):
+        import torch
+        have = torch.cuda.device_count()   # does not initialise the GPU
+        if have < args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} requested but only {have} GPU device(s) are visible")
+        return "context", args.gpus
+    if args.gpus < 1:
+        raise SystemExit(f"bench.py: --gpus {args.gpus}: need at least one GPU")
+    return "single", 1
+
+
 def main():
     args = parse()
+    mode, n_gpus = launch_mode(args)
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = n_gpus if mode == "torchrun" else 1     # processes
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.device is not None:
         local = args.device
@@ -290,10 +320,14 @@ def main():
     args.seed = d_seed if args.seed is None else args.seed
     t_gen = time.perf_counter()
     M = args.models
-    tb, mb, expected = build_workload(args.config, args.tapes, M, args.seed, rank, world, hoist=not args.no_hoist)
+    if mode == "context":
+        # the whole global candidate list (n_gpus x M); mq_models_upload shards it over the devices
+        tb, mb, expected = build_workload(args.config, args.tapes, M * n_gpus, args.seed, 0, 1, hoist=not args.no_hoist)
+    else:
+        tb, mb, expected = build_workload(args.config, args.tapes, M, args.seed, rank, world, hoist=not args.no_hoist)
     t_gen = time.perf_counter() - t_gen
 
-    ev = Evaluator(local)
+    ev = Evaluator(devices=list(range(n_gpus)), use_rccl=True) if mode == "context" else Evaluator(local)
     if args.no_early_exit:
         ev.set_option(Evaluator.OPT_EARLY_EXIT, 0)
     ev.upload_models(mb)
@@ -313,9 +347,13 @@ def main():
         all_reduce(best, dist.ReduceOp.MIN)
         ev.finalize_first_hit(ct, best.data_ptr(), sptr)
 
+    def sync_all():
+        for d in (range(n_gpus) if mode == "context" else [local]):
+            torch.cuda.synchronize(d)
+
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
+    sync_all()
     # correctness gate on the benchmark workload itself (planted first hits)
     got = best.cpu().numpy()
     ok = bool((got == expected).all())
@@ -328,11 +366,11 @@ def main():
     ev.time_kernels(True)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync_all()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step()
-    torch.cuda.synchronize(dev)
+    sync_all()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -354,7 +392,7 @@ def main():
     hits = int((got >= 0).sum())
 
     if rank == 0:
-        per_launch_ops = alg_ops / args.steps / world
+        per_launch_ops = alg_ops / args.steps / n_gpus
         achieved_tops = per_launch_ops / (kern_ms * 1e-3) / 1e12
         model_bytes = mb.var_words.nbytes
         tape_bytes = tb.nodes.nbytes + tb.consts.nbytes + 4 * tb.n_tapes
@@ -365,7 +403,7 @@ def main():
             "metric": "256-bit constraint-node x model evals/s",
             "value": node_evals / elapsed,
             "unit": "node-evals/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
@@ -376,11 +414,16 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": workload_text,
-                "n_tapes": tb.n_tapes, "models_per_gpu": M, "models_total": M * world,
+                "n_tapes": tb.n_tapes, "models_per_gpu": M, "models_total": M * n_gpus,
                 "avg_tape_nodes": float(tb.sizes().mean()), "seed": args.seed,
                 "hoisted_columns": int(tb.columns.n) if getattr(tb, "columns", None) is not None else 0,
                 "column_nodes_per_model": int(tb.columns.programs.sizes().sum()) if getattr(tb, "columns", None) is not None else 0,
-                "parallelism": f"model-axis shard x{world} + RCCL min-allreduce" if world > 1 else "single GPU",
+                "parallelism": {"torchrun": f"one process per GPU x{n_gpus}: model-axis shard + torch.distributed RCCL "
+                                            f"min-allreduce",
+                                "context": f"one-process context x{n_gpus}: model-axis shard inside mq_models_upload + "
+                                           f"in-library RCCL min (ncclAllReduce)",
+                                "single": "single GPU"}[mode],
+                "rccl_in_library": bool(ev.rccl_active),
             },
             "roofline": {
                 "bound": "valu", "achieved": achieved_tops, "peak": VALU_PEAK_TOPS, "unit": "TOPS (int32 VALU)",
@@ -395,10 +438,10 @@ def main():
             "z3_calls_avoided": {"quick_sat_hits": hits, "queries": tb.n_tapes, "fraction": hits / tb.n_tapes},
             "parity_ok": ok,
             "pairs_evaluated": pairs,
-            "nominal_node_evals_per_step": float(tb.sizes().sum()) * M * world,
+            "nominal_node_evals_per_step": float(tb.sizes().sum()) * M * n_gpus,
             "gen_seconds": t_gen,
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if n_gpus == 1 and not args.no_cpu_baseline:
             if getattr(tb, "columns", None) is not None:
                 # the reference evaluates every conjunction in full per model: time the oracle on
                 # the same conjunctions lowered without hoisting
@@ -408,7 +451,7 @@ def main():
                 cb = cpu_baseline(tb, mb, args.cpu_seconds)
             out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample", "single_core_value", "host")}
             out["gpu_over_cpu"] = out["value"] / cb["value"]
-        if world == 1 and not args.no_dropin:
+        if n_gpus == 1 and not args.no_dropin:
             out["dropin"] = dropin_leg(ev)
             out["keccak_service"] = keccak_leg(ev)
         print(json.dumps(out), flush=True)

@@ -1,0 +1,43 @@
+"""bench.py's --gpus contract on a host without enough GPUs (CPU test): the run must fail loudly,
+never report fewer GPUs than asked for."""
+import os
+import subprocess
+import sys
+import types
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def _args(gpus):
+    return types.SimpleNamespace(gpus=gpus)
+
+
+def test_gpus_2_on_a_host_with_fewer_devices_exits_nonzero():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HIP_VISIBLE_DEVICES"] = ""      # (this container has no GPU anyway)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode != 0
+    assert "--gpus 2 requested but only" in r.stderr
+    assert '"n_gpus"' not in r.stdout
+
+
+def test_launch_modes(monkeypatch):
+    import torch
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    assert bench.launch_mode(_args(1)) == ("single", 1)
+    assert bench.launch_mode(_args(8)) == ("context", 8)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 4)
+    with pytest.raises(SystemExit, match="only 4 GPU"):
+        bench.launch_mode(_args(8))
+    # the driver's N > 1 launch (torchrun): one rank per GPU, --gpus agrees with WORLD_SIZE
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    assert bench.launch_mode(_args(4)) == ("torchrun", 4)
+    assert bench.launch_mode(_args(1)) == ("torchrun", 4)
+    with pytest.raises(SystemExit, match="disagrees"):
+        bench.launch_mode(_args(2))
