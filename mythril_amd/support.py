@@ -382,7 +382,8 @@ class ModelCache:
         not answer, search the LRU models followed by up to ``quick_sat_candidate_budget``
         generated candidates in ONE launch.  Returns per expression a satisfying model (an LRU
         model, or a generated candidate materialized as a Model: never inserted into the cache)
-        or False.  Only for callers that use the verdict, never the model's contents."""
+        or False.  get_model caches a candidate answer in the LRU as the solver's model would be
+        (model.py:125), so the model differs from z3's: see INTEGRATION.md, "Generated candidates"."""
         from .candidates import CandidateGenerator
         exprs = list(exprs)
         out = [False] * len(exprs)
@@ -525,6 +526,7 @@ def get_model(constraints, minimize=(), maximize=(), solver_timeout=None, verdic
     whether a model exists (``Constraints.is_possible``); with ``Args.quick_sat_candidates`` a
     quick-sat miss then also tries generated candidates before the solver."""
     counters["get_model_calls"] += 1
+    asked, asked_timeout = constraints, solver_timeout
     solver_timeout = solver_timeout or args.solver_timeout
     solver_timeout = min(solver_timeout, time_handler.time_remaining())
     if solver_timeout <= 0:
@@ -547,7 +549,16 @@ def get_model(constraints, minimize=(), maximize=(), solver_timeout=None, verdic
             cand = model_cache.candidate_for(simplify(S.And(*constraints)))
             if cand is not False:
                 counters["candidate_answers"] += 1
+                # the candidate stands in for the solver's sat answer, and is cached as that
+                # answer would be (model.py:125): later quick-sat queries see it in the LRU
+                model_cache.put(cand, 1)
                 return cand
+            # a candidate miss goes to the solver under the plain get_model key, so that a later
+            # Constraints.get_model() of the same state finds the answer in this memo as the
+            # reference's would (the verdict-only key is an extension the reference does not have)
+            counters["get_model_calls"] -= 1
+            # (same call form as Constraints.get_model: lru_cache keys depend on it)
+            return get_model(asked, solver_timeout=asked_timeout)
     counters["solver_calls"] += 1
     pool = ThreadPool(1)
     try:

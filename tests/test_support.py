@@ -306,8 +306,7 @@ def test_keccak_manager_reset_keeps_index_counter():
 def test_generated_candidates_answer_fork_verdicts(fresh):
     """Args.quick_sat_candidates: forks the LRU misses (fork_workload: a cached path + one new
     branch condition) are answered by generated candidates without the solver; every answer is
-    a model that satisfies the query under direct term evaluation, and is NOT inserted into the
-    LRU (the cache contents stay the solver's)."""
+    a model that satisfies the query under direct term evaluation."""
     import term_eval
     from mythril_amd.synth_evm import fork_workload
     exprs, recs, parents = fork_workload(24, 40, seed=9)
@@ -315,7 +314,6 @@ def test_generated_candidates_answer_fork_verdicts(fresh):
     sp.set_solver_backend(solver)
     for m in reversed(recs):
         sp.model_cache.put(m, 1)
-    before = list(sp.model_cache.model_cache.lru_cache)
     sp.args.quick_sat_candidates, budget = True, sp.args.quick_sat_candidate_budget
     sp.args.quick_sat_candidate_budget = 6000
     try:
@@ -323,14 +321,59 @@ def test_generated_candidates_answer_fork_verdicts(fresh):
         got = sp.is_possible_batch(states)
     finally:
         sp.args.quick_sat_candidates, sp.args.quick_sat_candidate_budget = False, budget
-    assert sp.counters["candidate_answers"] == sum(got) > 0
+    # a candidate answer enters the LRU, so a later fork may hit it in quick-sat instead
+    assert sp.counters["candidate_answers"] > 0
+    assert sp.counters["candidate_answers"] + sp.counters["quick_sat_answers"] == sum(got)
     assert solver.calls == len(states) - sum(got)
-    assert list(sp.model_cache.model_cache.lru_cache) == before
-    # each answered state: the candidate model found for it satisfies the full query
-    cs_answers = [sp.model_cache.candidates([e])[0] for e, ok in zip(exprs, got) if ok]
-    assert all(a is not False for a in cs_answers)
-    for e, a in zip([e for e, ok in zip(exprs, got) if ok], cs_answers):
-        assert term_eval.is_true(e, a)
+    # each answered state: get_model (memoized) returns a model that satisfies the full query
+    for st, e, ok in zip(states, exprs, got):
+        if ok:
+            a = sp.get_model(st, solver_timeout=None, verdict_only=True)   # is_possible's call form
+            assert term_eval.is_true(e, a)
+
+
+def test_candidate_answers_enter_the_lru_like_solver_answers(fresh):
+    """INTEGRATION.md "Generated candidates": a candidate answer is cached in the LRU where z3's
+    sat model would be (model.py:125) and answers a later state through quick-sat; a candidate
+    miss is solved under the plain get_model key (a later Constraints.get_model() does not call
+    the solver again)."""
+    import term_eval
+    from mythril_amd.synth_evm import fork_workload
+    exprs, recs, _ = fork_workload(6, 20, seed=9)
+    solved = Model({"sender_1": 1})
+    solver = ScriptedSolver(lambda cs: solved)
+    sp.set_solver_backend(solver)
+    for m in reversed(recs):
+        sp.model_cache.put(m, 1)
+    sp.args.quick_sat_candidates, budget = True, sp.args.quick_sat_candidate_budget
+    sp.args.quick_sat_candidate_budget = 6000
+    try:
+        states = [sp.Constraints(list(e.args)) for e in exprs]
+        answered = []
+        for st, e in zip(states, exprs):
+            n_lru = len(sp.model_cache.model_cache.lru_cache)
+            before = sp.counters["candidate_answers"]
+            assert st.is_possible()
+            if sp.counters["candidate_answers"] > before:
+                # the candidate is now the MRU entry, and it satisfies the state
+                mru = next(reversed(sp.model_cache.model_cache.lru_cache))
+                assert len(sp.model_cache.model_cache.lru_cache) == min(n_lru + 1, 100)
+                assert term_eval.is_true(e, mru)
+                answered.append((st, e, mru))
+        assert answered, "no fork was answered by a generated candidate"
+        # the same state again, read by a model-content caller: quick-sat returns the candidate
+        st, e, mru = answered[0]
+        sp.get_model.cache_clear()
+        sp.model_cache._memo.clear()
+        assert sp.get_model(st) is mru
+        # a state no candidate satisfies: the solver runs once, under the plain key
+        contra = sp.Constraints(list(exprs[0].args) + [S.Not(exprs[0].args[0])])
+        calls = solver.calls
+        assert contra.is_possible()
+        assert solver.calls == calls + 1
+        assert contra.get_model() is not None and solver.calls == calls + 1
+    finally:
+        sp.args.quick_sat_candidates, sp.args.quick_sat_candidate_budget = False, budget
 
 
 def test_candidates_off_by_default(fresh):
