@@ -218,6 +218,52 @@ def dropin_leg(ev, grid=((1, 16), (1, 100), (32, 16), (32, 100), (256, 16), (256
     return out
 
 
+def calls_avoided_leg(ev, n_forks: int = 256, n_models: int = 100, seed: int = 21, budget: int = 100_000):
+    """"z3 solver calls avoided", counted where SURVEY Appendix E says: at ``get_model``
+    (``support.counters``: calls, answers from quick-sat at model.py:101-103, answers from
+    generated candidates, calls that reach ``solver_worker`` model.py:28).
+
+    Stream: the per-fork check of svm.py:351-358 on ``n_forks`` JUMPIs.  Each fork's parent path
+    is satisfied by a cached model (fork_workload: 100 models in the LRU, MRU first); its two
+    successors are path + cond (the parent model falsifies cond) and path + Not(cond).  All
+    2 * n_forks states go through ``is_possible_batch`` (one launch, answers sequentially exact),
+    with ``Args.quick_sat_candidates`` off (the reference's behaviour) and on.  There is no z3 on
+    the box: the solver stand-in answers ``unknown`` (what z3 does on a timeout), so a call that
+    reaches it prunes the state (constraints.py:37-38) instead of adding a model."""
+    from mythril_amd import smt as S
+    from mythril_amd import support as sp
+    from mythril_amd.synth_evm import fork_workload
+    exprs, recs, _ = fork_workload(n_forks, n_models, seed=seed)
+    states = []
+    for e in exprs:
+        path, cond = list(e.args[:-1]), e.args[-1]
+        states += [sp.Constraints(path + [cond]), sp.Constraints(path + [S.Not(cond)])]
+    out = {"stream": f"svm.py:351-358 fork checks: {n_forks} forks x 2 successors over {n_models} cached models "
+                     f"(fork_workload seed {seed}); solver stand-in answers unknown (no z3 on the box)"}
+    saved = (sp.model_cache, sp.args.quick_sat_candidates, sp.args.quick_sat_candidate_budget)
+    try:
+        for cand in (False, True):
+            sp.reset_caches()
+            sp.model_cache = sp.ModelCache(sp.VerdictEngine(ev))
+            sp.set_solver_backend(sp.NoSolver())
+            sp.args.quick_sat_candidates, sp.args.quick_sat_candidate_budget = cand, budget
+            for m in reversed(recs):
+                sp.model_cache.put(m, 1)
+            t0 = time.perf_counter()
+            alive = sp.is_possible_batch(states)
+            dt = time.perf_counter() - t0
+            c = dict(sp.counters)
+            avoided = c["get_model_calls"] - c["solver_calls"]
+            out["candidates_on" if cand else "candidates_off"] = {
+                **c, "states_alive": int(sum(alive)), "solver_calls_avoided": avoided,
+                "fraction_avoided": avoided / max(c["get_model_calls"], 1), "ms_per_state": dt * 1e3 / len(states),
+                "candidate_budget": budget if cand else 0}
+    finally:
+        sp.model_cache, sp.args.quick_sat_candidates, sp.args.quick_sat_candidate_budget = saved
+        sp.set_solver_backend(None)
+    return out
+
+
 def keccak_leg(ev, sizes=(1, 64, 4096, 262144), msg_bytes: int = 64):
     """Concrete keccak service (mythril_amd.keccak_service): GPU mq_keccak256 per-call latency by
     batch size vs the per-call CPU keccak the reference uses (eth_hash from Python, here the
@@ -435,7 +481,7 @@ def main():
                 "alg_ops_per_launch": per_launch_ops,
                 "hbm_alg_GBps": hbm_gbs, "hbm_frac": hbm_gbs / HBM_PEAK_GBS,
             },
-            "z3_calls_avoided": {"quick_sat_hits": hits, "queries": tb.n_tapes, "fraction": hits / tb.n_tapes},
+            "planted_first_hits": {"hits": hits, "tapes": tb.n_tapes},
             "parity_ok": ok,
             "pairs_evaluated": pairs,
             "nominal_node_evals_per_step": float(tb.sizes().sum()) * M * n_gpus,
@@ -453,6 +499,7 @@ def main():
             out["gpu_over_cpu"] = out["value"] / cb["value"]
         if n_gpus == 1 and not args.no_dropin:
             out["dropin"] = dropin_leg(ev)
+            out["z3_calls_avoided"] = calls_avoided_leg(ev)
             out["keccak_service"] = keccak_leg(ev)
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -41,3 +41,20 @@ def test_launch_modes(monkeypatch):
     assert bench.launch_mode(_args(1)) == ("torchrun", 4)
     with pytest.raises(SystemExit, match="disagrees"):
         bench.launch_mode(_args(2))
+
+
+def test_calls_avoided_leg_counts_at_get_model(monkeypatch):
+    """The bench's "z3 calls avoided" leg on the oracle engine (small): counted at get_model,
+    off = quick-sat hits only (each fork's not-taken side hits the parent's model), on = at least
+    as many, and calls = quick-sat + candidate answers + solver calls."""
+    import test_support as ts
+    from mythril_amd import support as sp
+    monkeypatch.setattr(sp, "VerdictEngine", lambda ev: ts.OracleEngine())
+    r = bench.calls_avoided_leg(None, n_forks=12, budget=2000)
+    off, on = r["candidates_off"], r["candidates_on"]
+    for d in (off, on):
+        assert d["get_model_calls"] == 24
+        assert d["quick_sat_answers"] + d["candidate_answers"] + d["solver_calls"] == d["get_model_calls"]
+        assert d["solver_calls_avoided"] == d["get_model_calls"] - d["solver_calls"]
+    assert off["candidate_answers"] == 0 and off["quick_sat_answers"] == 12
+    assert on["solver_calls_avoided"] >= off["solver_calls_avoided"]
