@@ -49,8 +49,9 @@ WORKLOADS = {
            "keccak-consistent models per GPU, keccak256_512 evaluated IN-KERNEL (keccak-f[1600]), seed 4, 10% planted",
            "mq::qsg_kernel (G tapes + mode-3 columns) + keccak_column_kernel (keccak-f[1600] columns) + "
            "qs_column_kernel<16> (512-bit columns); whole-step alg ops / kernel time"),
-    "c5": (256, 1_250_000, 5, "C5: 256 deep EVM-shaped paths over 5 txs (~1900 DAG nodes) x 1.25*10^6 models per GPU "
-           "(10^7 over 8 GPUs), seed 5, 10% planted",
+    "c5": (256, 1_250_000, 5, "C5: 256 deep EVM-shaped paths over 5 txs (-t 5), 5 ABI words per call, 18-24 checks "
+           "per tx (~4090 DAG nodes per conjunction before hoisting) x 1.25*10^6 models per GPU (10^7 over 8 GPUs), "
+           "seed 5, 10% planted",
            "mq::qsg_kernel (gfx950 assembly interpreter, variables from HBM) + qs_column_kernel<8> (hoisted columns)"),
 }
 
@@ -72,7 +73,7 @@ def build_workload(cfg: str, n_tapes: int, M: int, seed: int, rank: int, world: 
                                                     hasher_many=default_evaluator().keccak256_array, hoist=hoist)
     elif cfg == "c5":
         tb, mb, expected, _ = synth_evm.c3_workload(n_tapes, M * world, seed=seed, shard=shard, n_tx=5,
-                                                    checks_per_tx=(10, 14), hoist=hoist)
+                                                    checks_per_tx=(18, 24), n_args=5, hoist=hoist)
     else:
         tb, mb, expected, _ = synth_evm.c3_workload(n_tapes, M * world, seed=seed, shard=shard, hoist=hoist)
     return tb, mb, expected
@@ -462,6 +463,7 @@ def main():
                 "workload": workload_text,
                 "n_tapes": tb.n_tapes, "models_per_gpu": M, "models_total": M * n_gpus,
                 "avg_tape_nodes": float(tb.sizes().mean()), "seed": args.seed,
+                "avg_tape_nodes_unhoisted": float(np.mean(getattr(tb, "unhoisted_nodes", tb.sizes()))),
                 "hoisted_columns": int(tb.columns.n) if getattr(tb, "columns", None) is not None else 0,
                 "column_nodes_per_model": int(tb.columns.programs.sizes().sum()) if getattr(tb, "columns", None) is not None else 0,
                 "parallelism": {"torchrun": f"one process per GPU x{n_gpus}: model-axis shard + torch.distributed RCCL "

@@ -57,7 +57,7 @@ BLOCK = 1 << 16  # models are generated in independently seeded blocks (any rank
 
 
 class _Block:
-    def __init__(self, seed: int, b: int, n: int, n_tx: int, address_args: bool = False):
+    def __init__(self, seed: int, b: int, n: int, n_tx: int, address_args: bool = False, n_bytes: int = N_BYTES):
         rng = np.random.Generator(np.random.PCG64([seed, b]))
         self.sender, self.value, self.cds, self.cdata = [], [], [], []
         for _ in range(n_tx):
@@ -70,8 +70,8 @@ class _Block:
             v = rng.integers(0, 1 << 40, n, dtype=np.uint64)
             v[rng.random(n) < 0.4] = 0
             self.value.append(_to_limbs(v))
-            self.cds.append(_to_limbs(rng.integers(4, 100, n, dtype=np.uint64)))
-            cd = rng.integers(0, 256, (N_BYTES, n), dtype=np.uint64).astype(np.uint8)
+            self.cds.append(_to_limbs(rng.integers(4, n_bytes + 32, n, dtype=np.uint64)))
+            cd = rng.integers(0, 256, (n_bytes, n), dtype=np.uint64).astype(np.uint8)
             if address_args:
                 # first ABI argument is an address: 12 zero bytes + an actor (90 %) or random bytes
                 cd[4:16] = 0
@@ -90,10 +90,12 @@ class EvmModels:
     Senders are actors 90 % of the time, call values are 0 (40 %) or < 2^40, calldatasize is
     uniform in [4, 100), calldata bytes are uniform, balances have entries for the 3 actors."""
 
-    def __init__(self, seed: int, M: int, n_tx: int, lo: int = 0, hi: int = None, address_args: bool = False):
+    def __init__(self, seed: int, M: int, n_tx: int, lo: int = 0, hi: int = None, address_args: bool = False,
+                 n_bytes: int = N_BYTES):
         hi = M if hi is None else hi
         self.seed, self.M, self.n_tx, self.lo, self.hi = seed, M, n_tx, lo, hi
         self.address_args = address_args
+        self.n_bytes = n_bytes   # calldata bytes per tx (selector + ABI words); calldatasize in [4, n_bytes + 32)
         blocks = [self._block(b) for b in range(lo // BLOCK, (hi + BLOCK - 1) // BLOCK)] if hi > lo else []
         off = lo - (lo // BLOCK) * BLOCK
         n = hi - lo
@@ -112,14 +114,14 @@ class EvmModels:
 
     def _block(self, b: int) -> _Block:
         n = min(BLOCK, self.M - b * BLOCK)
-        return _Block(self.seed, b, n, self.n_tx, self.address_args)
+        return _Block(self.seed, b, n, self.n_tx, self.address_args, self.n_bytes)
 
     def derived_column(self, fname: str, args, nl: int, n: int) -> np.ndarray:
         """Interpretation of ``fname`` at constant ``args`` for every stored model."""
         r = np.zeros((nl, n), np.uint32)
         if fname.endswith("_calldata"):
             k, idx = int(fname.split("_")[0]) - 1, args[0]
-            if idx < N_BYTES:
+            if idx < self.n_bytes:
                 r[0] = self.cdata[k][idx].astype(np.uint32)
             return r
         raise ValueError(f"no derived column for {fname}{args}")
@@ -261,8 +263,11 @@ def _holds(cond: S.Term, truth: bool) -> S.Term:
     return cond if truth else S.Not(cond)
 
 
-def evm_path(rng: np.random.Generator, wit: Dict, n_tx: int, checks_per_tx: Tuple[int, int] = (3, 6)) -> S.Term:
-    """One path conjunction whose every branch is the one ``wit`` takes."""
+def evm_path(rng: np.random.Generator, wit: Dict, n_tx: int, checks_per_tx: Tuple[int, int] = (3, 6),
+             n_args: int = 2) -> S.Term:
+    """One path conjunction whose every branch is the one ``wit`` takes.  ``n_args`` ABI words per
+    call (at 4, 36, 68, ...); with more than two, every check draws the pair of words it relates
+    (the default keeps the round-1/2 C3 stream bit for bit)."""
     cs: List[S.Term] = []
     storage = S.K(256, 256, 0)
     for k in range(n_tx):
@@ -270,6 +275,8 @@ def evm_path(rng: np.random.Generator, wit: Dict, n_tx: int, checks_per_tx: Tupl
         snd, cv, cds, B = wit["sender"][k], wit["value"][k], wit["cds"][k], wit["bytes"][k]
         W0, W1, W2 = _word_val(B, cds, 0), _word_val(B, cds, 4), _word_val(B, cds, 36)
         w0, w1, w2 = tx.word(0), tx.word(4), tx.word(36)
+        a_vals = [_word_val(B, cds, 4 + 32 * i) for i in range(n_args)]
+        a_terms = [tx.word(4 + 32 * i) for i in range(n_args)]
         cs.append(S.Or(*[tx.sender == a for a in ACTORS]))  # always asserted (symbolic.py:217-219)
         cs.append(_holds(S.ULT(tx.cds, S.BitVecVal(4, 256)), cds < 4))
         sel = W0 >> 224
@@ -282,6 +289,9 @@ def evm_path(rng: np.random.Generator, wit: Dict, n_tx: int, checks_per_tx: Tupl
             cs.append((S.UDiv(w0, S.BitVecVal(1 << 224, 256)) & 0xFFFFFFFF) == sel)
         n_checks = int(rng.integers(checks_per_tx[0], checks_per_tx[1] + 1))
         for _ in range(n_checks):
+            if n_args > 2:
+                i, j = (int(x) for x in rng.choice(n_args, 2, replace=False))
+                W1, W2, w1, w2 = a_vals[i], a_vals[j], a_terms[i], a_terms[j]
             c = int(rng.integers(14))
             if c == 0:
                 m160 = (1 << 160) - 1
@@ -333,22 +343,24 @@ def evm_path(rng: np.random.Generator, wit: Dict, n_tx: int, checks_per_tx: Tupl
             cs.append(_holds(S.Select(storage, S.BitVecVal(slot, 256)) == 0, wit["_storage"].get(slot, 0) == 0))
         wit.setdefault("_storage", {})
         slot = int(rng.integers(0, 4))
-        storage = S.Store(storage, S.BitVecVal(slot, 256), w1)
-        wit["_storage"][slot] = W1
+        storage = S.Store(storage, S.BitVecVal(slot, 256), a_terms[0])
+        wit["_storage"][slot] = a_vals[0]
     wit.pop("_storage", None)
     return S.And(*cs)
 
 
 def c3_workload(n_tapes: int = 1000, n_models: int = 1_000_000, seed: int = 3, planted_frac: float = 0.1,
                 n_tx: int = 3, shard: Tuple[int, int] = None, checks_per_tx: Tuple[int, int] = (3, 6),
-                hoist: bool = False):
+                hoist: bool = False, n_args: int = 2):
     """Config C3 substitute: ``n_tapes`` EVM-shaped path conjunctions over ``n_tx`` transactions x
-    ``n_models`` candidates.  ``shard=(lo, hi)`` materialises only candidates [lo, hi) (multi-GPU);
-    tapes and expected first hits are global.  Returns (tapes, models, expected, symbols)."""
+    ``n_models`` candidates (``n_args`` ABI words per call).  ``shard=(lo, hi)`` materialises only
+    candidates [lo, hi) (multi-GPU); tapes and expected first hits are global.  Returns (tapes,
+    models, expected, symbols)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     lo, hi = shard if shard else (0, n_models)
-    models = EvmModels(seed, n_models, n_tx, lo, hi)
-    ghost = EvmModels(seed + 1_000_003, max(1, n_tapes), n_tx, 0, 0)
+    nb = 4 + 32 * n_args
+    models = EvmModels(seed, n_models, n_tx, lo, hi, n_bytes=nb)
+    ghost = EvmModels(seed + 1_000_003, max(1, n_tapes), n_tx, 0, 0, n_bytes=nb)
     syms = SymbolTable()
     roots, expected = [], np.full(n_tapes, -1, np.int32)
     planted = rng.random(n_tapes) < planted_frac
@@ -362,9 +374,11 @@ def c3_workload(n_tapes: int = 1000, n_models: int = 1_000_000, seed: int = 3, p
             expected[t] = p
         else:
             wit = ghost.witness(t)
-        roots.append(evm_path(rng, wit, n_tx, checks_per_tx))
+        roots.append(evm_path(rng, wit, n_tx, checks_per_tx, n_args))
     tb, syms, ok = lower_batch(roots, syms, hoist=hoist)
     assert ok.all()
+    # DAG nodes per conjunction as the reference evaluates it (no batch-level hoisting)
+    tb.unhoisted_nodes = lower_batch(roots, SymbolTable())[0].sizes() if hoist else tb.sizes()
     return tb, models.batch(syms), expected, syms
 
 

@@ -415,13 +415,24 @@ def test_keccak_op_all_widths(evaluator):
     assert (v_gpu == cref.verdicts(tb, mb)).all()
 
 
-def test_c5_deep_tapes_match_oracle(evaluator):
+@pytest.mark.parametrize("hoist", [False, True])
+def test_c5_deep_tapes_match_oracle(evaluator, hoist):
+    """C5 at the stated depth (-t 5, ~4 096 DAG nodes per conjunction): first hits and the full
+    verdict matrix against the oracle on the unhoisted lowering."""
     from mythril_amd.synth_evm import c3_workload
-    tb, mb, exp, _ = c3_workload(16, 3000, seed=5, planted_frac=0.5, n_tx=5, checks_per_tx=(10, 14))
+    kw = dict(planted_frac=0.5, n_tx=5, checks_per_tx=(18, 24), n_args=5)
+    ptb, pmb, exp, _ = c3_workload(16, 3000, seed=5, **kw)
+    assert ptb.sizes().mean() > 3900
+    tb, mb, exp2, _ = c3_workload(16, 3000, seed=5, hoist=hoist, **kw)
+    assert (exp == exp2).all()
     evaluator.upload_models(mb)
-    fh = evaluator.first_hit(tb)
-    ref, _ = cref.first_hit(tb, mb)
+    ct = evaluator.compile(tb)
+    assert ct.n_unsupported == 0
+    fh = evaluator.first_hit(ct)
+    ref, _ = cref.first_hit(ptb, pmb)
     assert (ref == exp).all() and (fh == ref).all()
+    v, _ = evaluator.verdicts(ct)
+    assert (v == cref.verdicts(ptb, pmb)).all()
 
 
 # ---------------------------------------------------------------- batch-level hoisting (column programs)

@@ -29,8 +29,9 @@ def test_c3_shards_are_slices_of_the_global_set():
 
 
 def test_c5_deep_tapes_planted():
-    tb, mb, exp, _ = c3_workload(12, 800, seed=5, planted_frac=0.5, n_tx=5, checks_per_tx=(10, 14))
-    assert tb.sizes().mean() > 1500
+    """C5's shape (bench.py): -t 5, five ABI words per call, ~4 096 DAG nodes per conjunction."""
+    tb, mb, exp, _ = c3_workload(12, 800, seed=5, planted_frac=0.5, n_tx=5, checks_per_tx=(18, 24), n_args=5)
+    assert 3900 < tb.sizes().mean() < 4300
     fh, _ = cref.first_hit(tb, mb)
     assert (fh == exp).all()
 
