@@ -1090,6 +1090,12 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
         }
         bool hi = false;
         for (int l = 1; l < 8; l++) hi = hi || cv[l] != 0;
+        if (sgn && (hi || cv[0] == 0)) {
+          // a signed divisor of 0 or of magnitude >= 2^32: SDIVV / SREMV / SMODV on the pushed
+          // constant, as the unsigned case routes such divisors to UDIVV / UREMV (G only)
+          ok = word(op == G_SDIV ? QK_SDIVV : op == G_SREM ? QK_SREMV : QK_SMODV, d - 1, -1, 0);
+          break;
+        }
         if (log.empty() || log.back().pos != prev_out) return false;
         drop_last(1);  // drop the divisor push
         if (!sgn && !hi && cv[0] != 0 && (cv[0] & (cv[0] - 1)) == 0) {

@@ -282,6 +282,7 @@ class Evaluator:
         self.device = ids[0]
         self.n_models = 0
         self.index_base = 0
+        self._opts = {}
         if use_rccl and len(ids) == 1:
             self.set_option(self.OPT_USE_RCCL, 1)
 
@@ -296,7 +297,12 @@ class Evaluator:
         rc = self.lib.mq_ctx_set_option(self.ctx, option, value)
         if rc < 0:
             _check(rc, "mq_ctx_set_option")
+        self._opts[option] = value
         return rc
+
+    def option(self, option: int, default: int = 0) -> int:
+        """The last value this process set for a settable option (the library's default if none)."""
+        return self._opts.get(option, default)
 
     @property
     def asm_ready(self) -> bool:

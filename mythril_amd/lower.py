@@ -380,11 +380,14 @@ def lower_batch(roots: Sequence[S.Term], syms: Optional[SymbolTable] = None, hoi
                                     int(os.environ.get("MQ_HOIST_MIN_TAPES", 2)))
         n_shared = len(col_terms)
         col_terms += keccak_subterms(list(roots), syms, col_terms)
+        # every keccak application and Concat piece, also those already chosen as shared terms
+        # (an address key x & (2^160 - 1) is both): never narrowed
+        kpieces = {id(t) for t in keccak_subterms(list(roots), syms, [])}
         for k, t in enumerate(col_terms):
             # a column whose value has fewer significant bits stores only those (selectors
             # x >> 224, x urem 2^160, masks): fewer rows written and read; keccak columns and
             # their pieces keep their width (the keccak column kernel reads whole words)
-            bits = _column_bits(t) if k < n_shared else t.width
+            bits = _column_bits(t) if k < n_shared and id(t) not in kpieces else t.width
             if (abs(bits) + 31) // 32 < (t.width + 31) // 32:
                 narrow[id(t)] = bits
             hoisted[id(t)] = syms.var(f"@h{k}", abs(narrow.get(id(t), t.width)))

@@ -211,9 +211,15 @@ class VerdictEngine:
         return tb, mb, ok
 
     @staticmethod
-    def _latency_mode(ev, waves: int) -> None:
-        if hasattr(ev, "OPT_LATENCY_WAVES"):
+    def _latency_mode(ev, waves: Optional[int]) -> Optional[int]:
+        """Set the evaluator's latency-mode threshold; returns the previous value (None: the
+        evaluator has no such option).  ``waves=None`` leaves it unchanged."""
+        if not hasattr(ev, "OPT_LATENCY_WAVES"):
+            return None
+        prev = ev.option(ev.OPT_LATENCY_WAVES) if hasattr(ev, "option") else 0
+        if waves is not None:
             ev.set_option(ev.OPT_LATENCY_WAVES, waves)
+        return prev
 
     def _evaluate(self, tb, mb):
         clock = time.perf_counter
@@ -223,11 +229,11 @@ class VerdictEngine:
         t1 = clock()
         ct = ev.compile(tb)
         t2 = clock()
-        self._latency_mode(ev, self.latency_waves)
+        prev = self._latency_mode(ev, self.latency_waves)
         try:
             v, fh = ev.verdicts(ct)
         finally:
-            self._latency_mode(ev, 0)
+            self._latency_mode(ev, prev)   # (the caller's own setting, not 0)
             ct.free()
         self.timing["upload"] += t1 - t0
         self.timing["compile"] += t2 - t1
@@ -264,11 +270,11 @@ class VerdictEngine:
         t3 = clock()
         ct = ev.compile(tb)
         t4 = clock()
-        self._latency_mode(ev, self.latency_waves)
+        prev = self._latency_mode(ev, self.latency_waves)
         try:
             fh = ev.first_hit(ct)
         finally:
-            self._latency_mode(ev, 0)
+            self._latency_mode(ev, prev)
             ct.free()
         return fh, t3, t4
 
@@ -295,7 +301,7 @@ class VerdictEngine:
             tb, mb, ok = self._lower(exprs, models, False)
             v, fh = self._evaluate(tb, mb)
         self.launches += 1
-        self.pairs += tb.n_tapes * mb.n_models
+        self.pairs += len(exprs) * mb.n_models   # (queries, not the conjunct groups split_conjuncts made)
         out: List[Optional[np.ndarray]] = []
         for i in range(len(exprs)):
             out.append(v[i].copy() if ok[i] and fh[i] != -2 else None)

@@ -801,6 +801,40 @@ def test_g_kernel_signed_variable_division_matches_oracle(evaluator, M):
     assert (evaluator.first_hit(ct) == fh_ref).all()
 
 
+
+@pytest.mark.parametrize("M", [64, 700])
+def test_g_kernel_signed_division_by_wide_and_zero_constants(evaluator, M):
+    """bvsdiv / bvsrem / bvsmod by a constant divisor that is 0 or of magnitude >= 2^32:
+    G runs them as SDIVV / SREMV / SMODV on the pushed constant (no tape left on the C++ kernel),
+    bit-exact with the oracle; the 32-bit constant path (SDIVC*) stays for small divisors."""
+    rng = np.random.default_rng(M + 9)
+    MASK = (1 << 256) - 1
+    xs = [int.from_bytes(rng.bytes(32), "little") if i % 3 else (-int(rng.integers(1, 1 << 40))) & MASK
+          for i in range(M)]
+    zs = [int.from_bytes(rng.bytes(32), "little") for _ in range(M)]
+    rows = [[(v >> (32 * l)) & 0xFFFFFFFF for v in vals] for vals in (xs, zs) for l in range(8)]
+    mb = ModelBatch([256, 256], np.asarray(rows, np.uint32))
+    consts = [0, 1 << 32, (1 << 32) + 7, (-(1 << 40)) & MASK, (-((1 << 32) + 1)) & MASK, 1 << 255,
+              MASK, (1 << 200) + 12345, 3, (-5) & MASK]
+    tapes = []
+    for c in consts:
+        for op in ("sdiv", "srem", "smod"):
+            tp = Tape()
+            X, Z = tp.var(0, 256), tp.var(1, 256)
+            tapes.append(tp.finish(tp.slt(getattr(tp, op)(X, tp.const(c, 256)), Z)))
+    tb = TapeBatch(tapes)
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    v, fh = evaluator.verdicts(ct)
+    n_p, n_g, live = ct.asm_split()
+    assert live and n_p + n_g == tb.n_tapes, (n_p, n_g, ct.split())
+    hist = ct.handler_histogram(1)
+    assert all(hist.get(k, 0) > 0 for k in ("SDIVV", "SREMV", "SMODV")), hist
+    ref = cref.verdicts(tb, mb)
+    mism = np.argwhere(v != ref)
+    assert len(mism) == 0, f"{len(mism)} mismatches, first {mism[:5]}"
+    assert 0.05 < ref.mean() < 0.95
+
 SHIFT_WIDTHS = (256, 160, 64, 8)
 
 

@@ -130,3 +130,20 @@ def test_keccak_columns_match_unhoisted_oracle(evaluator, monkeypatch, seed):
     monkeypatch.setenv("MQ_NO_KECCAK_COLUMNS", "1")
     ct2 = evaluator.compile(tb)
     assert ct2.keccak_columns() == 0 and (evaluator.first_hit(ct2) == ref).all()
+
+
+@pytest.mark.gpu
+def test_address_key_mapping_uses_keccak_columns(evaluator):
+    from mythril_amd.lower import SymbolTable, lower_batch, serialize_models
+    from mythril_amd.smt_model import Model
+    rng = np.random.default_rng(6)
+    from test_lowering import _address_key_roots
+    roots, xs, keys, hs = _address_key_roots(rng)
+    models = [Model({f"a{i}": int.from_bytes(rng.bytes(32), "little") for i in range(3)}) for _ in range(700)]
+    tb0, syms0, _ = lower_batch(roots, SymbolTable(interpret_keccak=True))
+    ref, _ = cref.first_hit(tb0, serialize_models(models, syms0))
+    tb, syms1, ok = lower_batch(roots, SymbolTable(interpret_keccak=True), hoist=True)
+    evaluator.upload_models(serialize_models(models, syms1))
+    ct = evaluator.compile(tb)
+    assert ct.keccak_columns() == len(hs)
+    assert (evaluator.first_hit(ct) == ref).all() and (ref >= 0).any()

@@ -193,3 +193,38 @@ def test_c4_wide_planted_hits_hold_in_the_oracle():
     tb, mb, exp, recs = c4_wide_workload(8, 40, seed=46, hasher=keccak_ref.keccak256)
     v = cref.verdicts(tb, mb)
     assert (v[exp >= 0, exp[exp >= 0]]).all()
+
+
+def _address_key_roots(rng, n=40):
+    """Mapping reads balances[x & (2^160 - 1)] (an address key, instructions.py:1306 masks) whose
+    masked key also appears on its own in other conjuncts: the key is a shared sub-term AND a
+    keccak Concat piece (it must not be narrowed, or the keccak column kernel rejects
+    the column)."""
+    from mythril_amd import smt as S
+    xs = [S.BitVecSym(f"a{i}", 256) for i in range(3)]
+    m160 = S.BitVecVal((1 << 160) - 1, 256)
+    # (a key of >= 2 nodes, as a calldata word's is: a one-node x & m is not worth a column)
+    keys = [(x + S.BitVecVal(i, 256)) & m160 for i, x in enumerate(xs)]
+    hs = [S.Keccak256(S.Concat(k, S.BitVecVal(1, 256))) for k in keys]
+    roots = []
+    for i in range(n):
+        j = int(rng.integers(3))
+        c = int(rng.integers(0, 1 << 32))
+        roots.append(S.And(S.ULT(S.BitVecVal(c, 256), hs[j]),
+                           S.ULT(keys[(j + 1) % 3], S.BitVecVal(int.from_bytes(rng.bytes(20), "big") | 1, 256))))
+    return roots, xs, keys, hs
+
+
+def test_address_key_piece_is_not_narrowed():
+    from mythril_amd.lower import SymbolTable, lower_batch
+    roots, xs, keys, hs = _address_key_roots(np.random.default_rng(5))
+    syms = SymbolTable(interpret_keccak=True)
+    tb, syms, ok = lower_batch(roots, syms, hoist=True)
+    assert ok.all() and tb.columns is not None
+    widths = dict(syms.vars)
+    hoisted = [w for (name, w) in syms.vars if name.startswith("@h")]
+    # the masked keys keep 256 bits (narrowed they would be 160-bit columns), as do the keccak
+    # results
+    assert hoisted and 160 not in hoisted and hoisted.count(256) == 6, widths
+
+
