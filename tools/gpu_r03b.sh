@@ -12,3 +12,9 @@ timeout -k 10 300 python -u bench.py --context --no-cpu-baseline --no-dropin > $
 python -c "import json; d=json.loads(open('$O/bench_c2_ctx.json').read().strip().splitlines()[-1]); print('ctx', d['n_gpus'], round(d['ms_per_step'],2), d['config']['parallelism'], d['config']['rccl_in_library'], d['parity_ok'])"
 timeout -k 10 600 python -u bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline --no-dropin > $O/bench_c5.json 2> $O/bench_c5.err || { tail -20 $O/bench_c5.err; exit 6; }
 python -c "import json; d=json.loads(open('$O/bench_c5.json').read().strip().splitlines()[-1]); c=d['config']; print('c5', round(d['ms_per_step'],2), round(d['roofline']['frac'],4), d['parity_ok'], c['avg_tape_nodes'], c['avg_tape_nodes_unhoisted'], d['value'])"
+# diagnostics: handler mix and per-handler profile (profile build through MQ_LIB)
+for c in c3 c5; do
+  timeout -k 10 300 python -u tools/qsa_mix.py $c > $O/mix_$c.txt 2>&1 || { tail -20 $O/mix_$c.txt; exit 7; }
+  MQ_LIB=mythril_amd/prof/libmq.so timeout -k 10 300 python -u tools/g_profile.py $c > $O/gprof_$c.txt 2>&1 || { tail -20 $O/gprof_$c.txt; exit 8; }
+  head -25 $O/gprof_$c.txt
+done
