@@ -822,6 +822,26 @@ ACC_AT_X = ("EQK", "EQVK", "ULTK", "UGTK", "ULEK", "UGEK")
 NOT_OF = {"LT": "GE", "GE": "LT", "GT": "LE", "LE": "GT"}
 
 
+_LONG_CALLS = [0]
+
+
+def long_calls(body):
+    """Profile build only: its longer handlers put the subroutines out of s_call's 16-bit reach,
+    so a handler's ``s_call_b64 s[76:77], sub`` becomes a 64-bit pc-relative call through the
+    subroutine scratch s[78:79] (the subroutines sit before the handlers: a negative offset)."""
+    out = []
+    for ln in body:
+        if ln.startswith("s_call_b64 s[76:77], "):
+            target = ln.split(", ", 1)[1]
+            k = _LONG_CALLS[0]
+            _LONG_CALLS[0] += 1
+            out += ["s_getpc_b64 s[78:79]", f".Llc{k}:", f"s_add_u32 s78, s78, {target} - .Llc{k}",
+                    "s_addc_u32 s79, s79, 0xffffffff", "s_swappc_b64 s[76:77], s[78:79]"]
+        else:
+            out.append(ln)
+    return out
+
+
 def make_handlers(variant, pfx):
     """(key, body lines) for the variant; key = (kind, d, v)."""
     G = variant == "g"
@@ -829,6 +849,8 @@ def make_handlers(variant, pfx):
     acc = []   # (key, body without the dispatch tail) of the Bool producers that get _A/_O forms
 
     def H(key, body, tail=True, reads_stack=True):
+        if PROF and G:
+            body = long_calls(body)
         pre = [VMWAIT] if (G and reads_stack) else []
         prof = prof_point(key[0]) if G else []
         if tail:
