@@ -568,65 +568,162 @@ def sub_udiv32(pfx):
 
 def sub_udivv(pfx):
     """G: unsigned 256-bit division by a variable divisor (bvudiv / bvurem, SMT-LIB: x / 0 = all
-    ones, x % 0 = x).  In: dividend U[0:8], divisor U[8:16] (U = the UF1 work registers).  Out:
-    quotient U[0:8], remainder W[0:8]; U[16:24] is the trial difference.  Restoring radix-2
-    division over the dividend's significant limbs only (n = the wave's maximum, at least 1):
-    the dividend is pre-shifted by 8 - n limbs, then 32n steps each shift (r:a) left by one bit,
-    subtract the divisor from r, keep the difference when it did not borrow (or r overflowed
-    256 bits), and shift the quotient bit into a.  The first steps, while r is shorter than
-    every lane's divisor, produce 0 bits and are taken a whole limb at a time (so a 256-bit
-    divisor costs 32 steps, not 256).  Loops are wave-uniform (SALU counters)."""
-    A = [f"v{UBASE + l}" for l in range(L)]
-    Bv = [f"v{UBASE + 8 + l}" for l in range(L)]
-    Tv = [f"v{UBASE + 16 + l}" for l in range(L)]
-    out = [f"{pfx}_sub_udivv:", "s_mov_b32 s64, 1"]
-    for l in range(1, L):   # s64 = 1 + the highest limb any lane's dividend uses
-        out += [f"v_cmp_ne_u32_e64 s[34:35], 0, {A[l]}", "s_nop 3", "s_cmp_lg_u64 s[34:35], 0",
-                f"s_cselect_b32 s64, {l + 1}, s64"]
-    out += ["s_sub_u32 s65, 8, s64", f"{pfx}_udivv_pre:", "s_cmp_eq_u32 s65, 0", f"s_cbranch_scc1 {pfx}_udivv_go"]
-    out += [f"v_mov_b32 {A[l]}, {A[l - 1]}" for l in range(L - 1, 0, -1)] + [f"v_mov_b32 {A[0]}, 0",
-                                                                              "s_sub_u32 s65, s65, 1",
-                                                                              f"s_branch {pfx}_udivv_pre"]
-    out += [f"{pfx}_udivv_go:"] + [f"v_mov_b32 {W(l)}, 0" for l in range(L)]
-    # while r has fewer limbs than every lane's divisor, a step only moves a bit of a into r:
-    # s67 = the number of limbs below the top nonzero limb of the divisor, minimum over the
-    # wave (0 if any divisor is 0); those steps are limb moves, min(s67, s64) of them
-    out += ["s_mov_b32 s67, 0", f"v_mov_b32 v5, {Bv[L - 1]}"]
-    for l in range(L - 1, 0, -1):
-        out += ([f"v_or_b32 v5, v5, {Bv[l]}"] if l < L - 1 else []) + [
-            "v_cmp_ne_u32_e64 s[34:35], 0, v5", "s_nop 3", "s_cmp_eq_u64 s[34:35], exec",
-            f"s_cbranch_scc1 {pfx}_udivv_nb{l}"]
-    out += [f"s_branch {pfx}_udivv_skip"]
-    for l in range(L - 1, 0, -1):
-        out += [f"{pfx}_udivv_nb{l}:", f"s_mov_b32 s67, {l}", f"s_branch {pfx}_udivv_skip"]
-    out += [f"{pfx}_udivv_skip:", "s_min_u32 s67, s67, s64", "s_sub_u32 s66, s64, s67", "s_lshl_b32 s66, s66, 5",
-            f"{pfx}_udivv_mv:", "s_cmp_eq_u32 s67, 0", f"s_cbranch_scc1 {pfx}_udivv_steps"]
-    out += [f"v_mov_b32 {W(l)}, {W(l - 1)}" for l in range(L - 1, 0, -1)] + [f"v_mov_b32 {W(0)}, {A[L - 1]}"]
-    out += [f"v_mov_b32 {A[l]}, {A[l - 1]}" for l in range(L - 1, 0, -1)] + [f"v_mov_b32 {A[0]}, 0",
-                                                                              "s_sub_u32 s67, s67, 1",
-                                                                              f"s_branch {pfx}_udivv_mv"]
-    out += [f"{pfx}_udivv_steps:", "s_cmp_eq_u32 s66, 0", f"s_cbranch_scc1 {pfx}_udivv_done"]
-    out += [f"{pfx}_udivv_step:",
-            f"v_lshrrev_b32 v4, 31, {W(L - 1)}",
-            "v_cmp_ne_u32_e64 s[36:37], 0, v4"]                  # r's top bit before the shift
-    out += [f"v_alignbit_b32 {W(l)}, {W(l)}, {W(l - 1)}, 31" for l in range(L - 1, 0, -1)]
-    out += [f"v_alignbit_b32 {W(0)}, {W(0)}, {A[L - 1]}, 31"]
-    out += [f"v_alignbit_b32 {A[l]}, {A[l]}, {A[l - 1]}, 31" for l in range(L - 1, 0, -1)]
-    out += [f"v_lshlrev_b32 {A[0]}, 1, {A[0]}"]
-    out += carry_chain(lambda l: f"v_sub_co_u32 {Tv[l]}, vcc, {W(l)}, {Bv[l]}",
-                       lambda l: f"v_subb_co_u32 {Tv[l]}, vcc, {W(l)}, {Bv[l]}, vcc")
-    out += ["s_nop 3",
-            "s_not_b64 s[38:39], vcc",
-            "s_or_b64 s[38:39], s[38:39], s[36:37]"]            # r >= b
-    out += [f"v_cndmask_b32_e64 {W(l)}, {W(l)}, {Tv[l]}, s[38:39]" for l in range(L)]
-    out += ["v_cndmask_b32_e64 v5, 0, 1, s[38:39]", f"v_or_b32 {A[0]}, {A[0]}, v5",
-            "s_sub_u32 s66, s66, 1", "s_cmp_lg_u32 s66, 0", f"s_cbranch_scc1 {pfx}_udivv_step"]
-    # divisor 0: the quotient is all ones (the remainder already equals the dividend)
-    out += [f"{pfx}_udivv_done:", f"v_or3_b32 v5, {Bv[0]}, {Bv[1]}, {Bv[2]}", f"v_or3_b32 v5, v5, {Bv[3]}, {Bv[4]}",
-            f"v_or3_b32 v5, v5, {Bv[5]}, {Bv[6]}", f"v_or_b32 v5, v5, {Bv[7]}",
-            "v_cmp_eq_u32_e64 s[34:35], 0, v5", "s_nop 1"]
-    out += [f"v_cndmask_b32_e64 {A[l]}, {A[l]}, -1, s[34:35]" for l in range(L)]
-    out += ["s_setpc_b64 s[76:77]"]
+    ones, x % 0 = x).  In: dividend U[0:8], divisor U[16:24] (U = the UF1 work registers).  Out:
+    quotient U[0:8], remainder W[0:8].  Clobbers U, W, v3-v7 and s[34:39], s[60:61], s[64:71].
+
+    Normalised schoolbook division (Knuth, TAOCP 4.3.1 Algorithm D), per lane: the divisor is
+    shifted left by s = 32k + b bits (k whole limbs in three conditional stages, then b bits) so
+    its top bit is set, the dividend by the same amount into 16 limbs u'; the quotient is then
+    8 base-2^32 digits, j = 7 .. 0.  Each digit is estimated from the window's top two limbs by a
+    2-by-1 division with the divisor's reciprocal (Moller & Granlund 2011, Alg. 4; the reciprocal
+    floor((2^64 - 1) / d1) - 2^32 comes from an fp64 estimate plus an exact integer fix-up), refined
+    against the second divisor limb (step D3, <= 2 decrements), multiplied back and subtracted
+    from the 9-limb window; the rare borrow adds the divisor back once.  The digit replaces the
+    window's top limb (zero after the step), so u'[8:16] ends as the quotient and u'[0:8] as the
+    normalised remainder.  A digit every lane's window shows to be 0 (top limb 0, next limb below
+    d1) is skipped wave-uniformly.  A zero divisor divides by 1 and is patched at the end.
+    ~650 VALU per call (the radix-2 loop it replaces took 32 steps per significant limb, ~58 VALU
+    each).  Algorithm model: tools/udivv_model.py."""
+    U = [f"v{UBASE + l}" for l in range(16)]           # u' (16 limbs)
+    Vd = [f"v{UBASE + 16 + l}" for l in range(8)]      # v' (normalised divisor)
+    d1, d0 = Vd[7], Vd[6]
+    P, PL, PH = W2(0), W(0), W(1)                      # 64-bit products
+    NR, RH = W2(2), W(3)                               # (n_, rhat) pair
+    QH, INV = W(4), W(5)
+    AD, ADL = W2(6), W(6)                              # multiply-subtract addend (carry, 0)
+    out = [f"{pfx}_sub_udivv:"]
+    out += [f"v_mov_b64 v[{UBASE + 8 + l}:{UBASE + 9 + l}], 0" for l in range(0, 8, 2)]
+    # zero divisor lanes (s[64:65]) divide by 1
+    out += [f"v_or3_b32 v5, {Vd[0]}, {Vd[1]}, {Vd[2]}", f"v_or3_b32 v5, v5, {Vd[3]}, {Vd[4]}",
+            f"v_or3_b32 v5, v5, {Vd[5]}, {Vd[6]}", f"v_or_b32 v5, v5, {Vd[7]}",
+            "v_cmp_eq_u32_e64 s[64:65], 0, v5", "s_nop 1",
+            f"v_cndmask_b32_e64 {Vd[0]}, {Vd[0]}, 1, s[64:65]"]
+    # v6 = top nonzero limb of the divisor, v3 = k = zero limbs above it, v7 = b = its leading zeros
+    out += [f"v_mov_b32 v6, {Vd[7]}", "v_mov_b32 v3, 0"]
+    for l in range(6, -1, -1):
+        out += ["v_cmp_eq_u32_e64 vcc, 0, v6", "s_nop 1",
+                f"v_cndmask_b32_e64 v6, v6, {Vd[l]}, vcc",
+                "v_addc_co_u32_e64 v3, vcc, v3, 0, vcc"]
+    out += ["v_ffbh_u32 v7, v6",
+            "v_and_b32 v5, 4, v3", "v_cmp_ne_u32_e64 s[66:67], 0, v5",
+            "v_and_b32 v5, 2, v3", "v_cmp_ne_u32_e64 s[68:69], 0, v5",
+            "v_and_b32 v5, 1, v3", "v_cmp_ne_u32_e64 s[70:71], 0, v5",
+            "v_cmp_eq_u32_e64 s[36:37], 0, v7",
+            "v_sub_u32 v5, 32, v7",
+            "s_nop 1"]
+    # whole-limb shift left by k (stages of 4, 2, 1 limbs), highest limb first
+    for st, m, hi in ((4, "s[66:67]", 11), (2, "s[68:69]", 13), (1, "s[70:71]", 14)):
+        out += [f"v_cndmask_b32_e64 {U[i]}, {U[i]}, {U[i - st]}, {m}" for i in range(hi, st - 1, -1)]
+        out += [f"v_cndmask_b32_e64 {U[i]}, {U[i]}, 0, {m}" for i in range(st - 1, -1, -1)]
+        out += [f"v_cndmask_b32_e64 {Vd[i]}, {Vd[i]}, {Vd[i - st]}, {m}" for i in range(7, st - 1, -1)]
+        out += [f"v_cndmask_b32_e64 {Vd[i]}, {Vd[i]}, 0, {m}" for i in range(st - 1, -1, -1)]
+    # bit shift left by b (v_alignbit by 32 - b; b = 0 keeps the limb: s[36:37])
+    for R, n in ((U, 16), (Vd, 8)):
+        for i in range(n - 1, 0, -1):
+            out += [f"v_alignbit_b32 v6, {R[i]}, {R[i - 1]}, v5", f"v_cndmask_b32_e64 {R[i]}, v6, {R[i]}, s[36:37]"]
+        out.append(f"v_lshlrev_b32 {R[0]}, v7, {R[0]}")
+    # INV = floor((2^64 - 1) / d1) - 2^32: fp64 reciprocal (one Newton step), then exact fix-up
+    # with p = (INV + 2^32) * d1: p >= 2^64 -> INV - 1; p + d1 < 2^64 -> INV + 1
+    out += [f"v_cvt_f64_u32 {P}, {d1}",
+            f"v_rcp_f64 {NR}, {P}",
+            "s_nop 1",
+            f"v_fma_f64 {AD}, -{P}, {NR}, 1.0",
+            f"v_fma_f64 {NR}, {NR}, {AD}, {NR}",
+            f"v_ldexp_f64 {NR}, {NR}, 64",
+            "s_mov_b32 s34, 0", "s_mov_b32 s35, 0xc1f00000",
+            f"v_add_f64 {NR}, {NR}, s[34:35]",
+            f"v_cvt_u32_f64 {INV}, {NR}",
+            "v_mov_b32 v4, 0", f"v_mov_b32 v5, {d1}",
+            f"v_mad_u64_u32 {P}, s[34:35], {INV}, {d1}, v[4:5]",
+            f"v_add_co_u32 v4, vcc, {PL}, {d1}",
+            "s_nop 0",
+            f"v_addc_co_u32 v5, vcc, {PH}, 0, vcc",
+            "s_nop 3",
+            "s_or_b64 s[36:37], s[34:35], vcc",
+            "s_not_b64 s[36:37], s[36:37]",
+            f"v_add_u32 v4, -1, {INV}", f"v_add_u32 v5, 1, {INV}",
+            f"v_cndmask_b32_e64 {INV}, {INV}, v4, s[34:35]",
+            f"v_cndmask_b32_e64 {INV}, {INV}, v5, s[36:37]"]
+    for j in range(7, -1, -1):
+        n1, n0, nn = U[j + 8], U[j + 7], U[j + 6]
+        lbl = f"{pfx}_udv_j{j}"
+        out += [f"v_cmp_eq_u32_e64 s[34:35], 0, {n1}",
+                f"v_cmp_lt_u32_e64 s[36:37], {n0}, {d1}",
+                "s_nop 3",
+                "s_and_b64 s[34:35], s[34:35], s[36:37]",
+                "s_cmp_eq_u64 s[34:35], exec",
+                f"s_cbranch_scc1 {lbl}"]
+        # (QH, RH) = divmod(n1:n0, d1) for n1 < d1 (Moller-Granlund)
+        out += [f"v_mov_b32 v4, {n0}", f"v_mov_b32 v5, {n1}",
+                f"v_mad_u64_u32 {P}, s[38:39], {INV}, {n1}, v[4:5]",
+                f"v_add_u32 {PH}, 1, {PH}",
+                f"v_mul_lo_u32 v6, {PH}, {d1}",
+                f"v_sub_u32 v3, {n0}, v6",
+                f"v_cmp_gt_u32_e64 s[34:35], v3, {PL}",
+                f"v_add_u32 v6, {d1}, v3",
+                f"v_add_u32 {QH}, -1, {PH}",
+                f"v_cndmask_b32_e64 v3, v3, v6, s[34:35]",
+                f"v_cndmask_b32_e64 {QH}, {PH}, {QH}, s[34:35]",
+                f"v_cmp_le_u32_e64 s[36:37], {d1}, v3",
+                f"v_subrev_u32 v6, {d1}, v3",
+                f"v_add_u32 {PH}, 1, {QH}",
+                f"v_cndmask_b32_e64 {RH}, v3, v6, s[36:37]",
+                f"v_cndmask_b32_e64 {QH}, {QH}, {PH}, s[36:37]"]
+        # n1 == d1: QH = 2^32 - 1, RH = n0 + d1 (s[60:61] = lanes where that overflowed)
+        out += [f"v_cmp_eq_u32_e64 s[34:35], {n1}, {d1}",
+                f"v_add_co_u32 v6, s[36:37], {n0}, {d1}",
+                "s_nop 1",
+                f"v_cndmask_b32_e64 {QH}, {QH}, -1, s[34:35]",
+                f"v_cndmask_b32_e64 {RH}, {RH}, v6, s[34:35]",
+                "s_nop 2",
+                "s_and_b64 s[60:61], s[34:35], s[36:37]",
+                f"v_mov_b32 {W(2)}, {nn}"]
+        # D3: while RH < 2^32 and QH * d0 > (RH : n_): QH -= 1, RH += d1 (at most twice)
+        for it in range(2):
+            out += [f"v_mad_u64_u32 {P}, s[38:39], {QH}, {d0}, 0",
+                    f"v_cmp_gt_u64_e64 s[34:35], {P}, {NR}",
+                    "s_nop 3",
+                    "s_andn2_b64 s[34:35], s[34:35], s[60:61]",
+                    "s_cmp_eq_u64 s[34:35], 0",
+                    f"s_cbranch_scc1 {pfx}_udv_d3_{j}",
+                    f"v_add_u32 v6, -1, {QH}",
+                    f"v_add_co_u32 v3, s[36:37], {RH}, {d1}",
+                    f"v_cndmask_b32_e64 {QH}, {QH}, v6, s[34:35]",
+                    f"v_cndmask_b32_e64 {RH}, {RH}, v3, s[34:35]",
+                    "s_nop 2",
+                    "s_and_b64 s[36:37], s[36:37], s[34:35]",
+                    "s_or_b64 s[60:61], s[60:61], s[36:37]"]
+        out += [f"{pfx}_udv_d3_{j}:"]
+        # window u'[j .. j+8] -= QH * v'; vcc = lanes that borrowed
+        out += [f"v_mov_b64 {AD}, 0"]
+        for i in range(8):
+            out.append(f"v_mad_u64_u32 {P}, s[38:39], {QH}, {Vd[i]}, {AD}")
+            out.append(f"v_sub_co_u32 {U[j + i]}, vcc, {U[j + i]}, {PL}" if i == 0
+                       else f"v_subb_co_u32 {U[j + i]}, vcc, {U[j + i]}, {PL}, vcc")
+            out.append(f"v_mov_b32 {ADL}, {PH}")
+        out += [f"v_subb_co_u32 v6, vcc, {n1}, {ADL}, vcc",
+                "s_nop 3",
+                "s_cmp_eq_u64 vcc, 0",
+                f"s_cbranch_scc1 {pfx}_udv_ok{j}",
+                "s_mov_b64 s[34:35], vcc",
+                f"v_add_u32 v6, -1, {QH}",
+                f"v_cndmask_b32_e64 {QH}, {QH}, v6, s[34:35]"]
+        for i in range(8):
+            out += [f"v_cndmask_b32_e64 v3, 0, {Vd[i]}, s[34:35]",
+                    f"v_add_co_u32 {U[j]}, vcc, {U[j]}, v3" if i == 0
+                    else f"v_addc_co_u32 {U[j + i]}, vcc, {U[j + i]}, v3, vcc"]
+        out += [f"{pfx}_udv_ok{j}:", f"v_mov_b32 {n1}, {QH}", f"{lbl}:"]
+    # remainder = u'[0:8] >> (32k + b): bits first, then whole limbs
+    out += [f"v_alignbit_b32 {W(i)}, {U[i + 1]}, {U[i]}, v7" for i in range(7)]
+    out += [f"v_lshrrev_b32 {W(7)}, v7, {U[7]}"]
+    for st, m in ((4, "s[66:67]"), (2, "s[68:69]"), (1, "s[70:71]")):
+        out += [f"v_cndmask_b32_e64 {W(i)}, {W(i)}, {W(i + st) if i + st < L else 0}, {m}" for i in range(L)]
+    out += [f"v_mov_b64 v[{UBASE + l}:{UBASE + l + 1}], v[{UBASE + 8 + l}:{UBASE + 9 + l}]" for l in range(0, L, 2)]
+    # divisor 0: quotient all ones, remainder the dividend (= the quotient by 1)
+    out += ["s_cmp_eq_u64 s[64:65], 0", f"s_cbranch_scc1 {pfx}_udv_nz"]
+    out += [f"v_cndmask_b32_e64 {W(l)}, {W(l)}, {U[l]}, s[64:65]" for l in range(L)]
+    out += [f"v_cndmask_b32_e64 {U[l]}, {U[l]}, -1, s[64:65]" for l in range(L)]
+    out += [f"{pfx}_udv_nz:", "s_setpc_b64 s[76:77]"]
     return out
 
 
@@ -676,14 +773,16 @@ def cneg(regs, m):
 def sdivv_body(x, kind, cin_call):
     """G: bvsdiv / bvsrem / bvsmod at 256 bits by a variable divisor (slots x, x + 1): the
     unsigned division of |a| by |b| (sub_udivv), then the SMT-LIB sign rules; v6 / v7 = sign
-    masks of a / b.  A zero divisor needs no case of its own: |a| / 0 = all ones gives -1 or 1,
+    masks of a / b (slots x / x + 1 still hold a and b).  A zero divisor needs no case of its own: |a| / 0 = all ones gives -1 or 1,
     |a| % 0 = |a| gives a back."""
     A = [f"v{UBASE + l}" for l in range(L)]
-    Bv = [f"v{UBASE + 8 + l}" for l in range(L)]
+    Bv = [f"v{UBASE + 16 + l}" for l in range(L)]
     Tv = [f"v{UBASE + 16 + l}" for l in range(L)]
     cin, call = cin_call[:-1], cin_call[-1:]
     out = cin + [f"v_ashrrev_i32 v6, 31, {A[L - 1]}", f"v_ashrrev_i32 v7, 31, {Bv[L - 1]}"]
+    # (sub_udivv clobbers v6 / v7: the sign masks are re-read from the operand slots after it)
     out += cneg(A, "v6") + cneg(Bv, "v7") + call
+    out += [f"v_ashrrev_i32 v6, 31, {S(x, L - 1)}", f"v_ashrrev_i32 v7, 31, {S(x + 1, L - 1)}"]
     Wr = [W(l) for l in range(L)]
     if kind == "SDIVV":
         out += ["v_xor_b32 v6, v6, v7"] + cneg(A, "v6")
@@ -993,7 +1092,7 @@ def make_handlers(variant, pfx):
     if G:
         for x in range(D - 1):
             cin = [f"v_mov_b64 v[{UBASE + l}:{UBASE + l + 1}], {S2(x, l)}" for l in range(0, L, 2)]
-            cin += [f"v_mov_b64 v[{UBASE + 8 + l}:{UBASE + 9 + l}], {S2(x + 1, l)}" for l in range(0, L, 2)]
+            cin += [f"v_mov_b64 v[{UBASE + 16 + l}:{UBASE + 17 + l}], {S2(x + 1, l)}" for l in range(0, L, 2)]
             call = [f"s_call_b64 s[76:77], {pfx}_sub_udivv"]
             H(("UDIVV", x), cin + call + [f"v_mov_b64 {S2(x, l)}, v[{UBASE + l}:{UBASE + l + 1}]" for l in range(0, L, 2)])
             H(("UREMV", x), cin + call + copy_from_w(x))
