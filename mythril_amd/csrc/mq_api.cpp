@@ -9,10 +9,14 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -29,21 +33,129 @@ namespace {
 
 inline int nl_of(int w) { return w == 0 ? 1 : (w + 31) / 32; }
 
+// Device allocations are cached per device by size class instead of going back to hipFree: the
+// drop-in path builds a fresh mq_tapes (a dozen buffers) per query batch, and a hipMalloc /
+// hipFree pair per buffer (hipFree synchronises the device) cost more than compiling the batch.
+// A released block may be handed out again at once, so whoever releases a buffer must have
+// ordered the kernels that read it before any later use: every product path synchronises its
+// stream before freeing (mq_tapes_free, mq_ctx_destroy).
+class DevPool {
+ public:
+  static DevPool& get() {
+    static DevPool* p = new DevPool();
+    return *p;
+  }
+  static size_t size_class(size_t n) {
+    n = std::max<size_t>(n, 256);
+    if (n <= (size_t(64) << 20)) {
+      size_t c = 256;
+      while (c < n) c <<= 1;
+      return c;
+    }
+    const size_t g = size_t(2) << 20;
+    return (n + g - 1) / g * g;
+  }
+  void* take(int dev, size_t cls) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto& fl = free_[dev & 15];
+    auto it = fl.find(cls);
+    if (it == fl.end()) return nullptr;
+    void* p = it->second;
+    fl.erase(it);
+    cached_[dev & 15] -= cls;
+    return p;
+  }
+  // a kernel was launched on a caller's stream (mq_launch_first_hit): a block released on this
+  // device may still be read there, so the next release synchronises the device first (what
+  // hipFree would have done)
+  void mark_foreign(int dev) { foreign_[dev & 15].store(true); }
+  void put(int dev, void* p, size_t cls) {
+    if (foreign_[dev & 15].exchange(false)) {
+      int cur = 0;
+      (void)hipGetDevice(&cur);
+      (void)hipSetDevice(dev);
+      (void)hipDeviceSynchronize();
+      (void)hipSetDevice(cur);
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (cached_[dev & 15] + cls <= kMaxCached) {
+        free_[dev & 15].emplace(cls, p);
+        cached_[dev & 15] += cls;
+        return;
+      }
+    }
+    (void)hipFree(p);
+  }
+  void trim(int dev) {   // give the cached blocks back (an allocation failed)
+    std::multimap<size_t, void*> fl;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      fl.swap(free_[dev & 15]);
+      cached_[dev & 15] = 0;
+    }
+    for (auto& kv : fl) (void)hipFree(kv.second);
+  }
+
+ private:
+  static constexpr size_t kMaxCached = size_t(4) << 30;
+  std::mutex mu_;
+  std::multimap<size_t, void*> free_[16];
+  size_t cached_[16] = {};
+  std::atomic<bool> foreign_[16] = {};
+};
+
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
+  int dev = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes), dev(o.dev) {
+    o.p = nullptr;
+    o.bytes = 0;
+  }
+  DevBuf& operator=(DevBuf&& o) noexcept {
+    if (this != &o) {
+      release();
+      p = o.p;
+      bytes = o.bytes;
+      dev = o.dev;
+      o.p = nullptr;
+      o.bytes = 0;
+    }
+    return *this;
+  }
   ~DevBuf() { release(); }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) DevPool::get().put(dev, p, bytes);
     p = nullptr;
     bytes = 0;
   }
   hipError_t ensure(size_t n) {
     if (n <= bytes && p) return hipSuccess;
     release();
-    hipError_t e = hipMalloc(&p, std::max<size_t>(n, 16));
-    if (e == hipSuccess) bytes = std::max<size_t>(n, 16);
-    return e;
+    int d = 0;
+    hipError_t e = hipGetDevice(&d);
+    if (e != hipSuccess) return e;
+    const size_t cls = DevPool::size_class(n);
+    p = DevPool::get().take(d, cls);
+    if (!p) {
+      e = hipMalloc(&p, cls);
+      if (e != hipSuccess) {
+        (void)hipGetLastError();
+        DevPool::get().trim(d);
+        e = hipMalloc(&p, cls);
+      }
+      if (e != hipSuccess) {
+        p = nullptr;
+        return e;
+      }
+    }
+    bytes = cls;
+    dev = d;
+    return hipSuccess;
   }
   template <class T>
   hipError_t upload(const T* src, size_t count, hipStream_t st) {
@@ -237,33 +349,85 @@ static void sum_counter_slots(const std::vector<unsigned long long>& raw, unsign
 // chunks off a shared counter.  Threads: MQ_HOST_THREADS, else OMP_NUM_THREADS, else the
 // hardware concurrency, at most 64.  (No OpenMP runtime: the library shares its process with
 // torch's own.)
+// The workers are created once and park on a condition variable between calls: a drop-in query
+// compiles a few dozen tapes, and spawning threads per call cost more than the compilation.
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool* p = new HostPool();   // (never destroyed: workers may outlive static dtors)
+    return *p;
+  }
+  int threads() const { return n_; }
+  // run job(tid) on tids 0 .. k-1 (0 on the caller), return when all are done
+  void run(int k, const std::function<void(int)>& job) {
+    std::lock_guard<std::mutex> serial(call_mu_);   // one parallel region at a time
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      job_ = &job;
+      want_ = k - 1;
+      done_ = 0;
+      epoch_++;
+    }
+    cv_.notify_all();
+    job(0);
+    std::unique_lock<std::mutex> g(mu_);
+    done_cv_.wait(g, [&] { return done_ == want_; });
+    job_ = nullptr;
+  }
+
+ private:
+  HostPool() {
+    n_ = [] {
+      for (const char* v : {"MQ_HOST_THREADS", "OMP_NUM_THREADS"})
+        if (const char* e = std::getenv(v)) {
+          const int t = std::atoi(e);
+          if (t > 0) return std::min(t, 64);
+        }
+      return (int)std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
+    }();
+    for (int t = 1; t < n_; t++) std::thread([this, t] { loop(t); }).detach();
+  }
+  void loop(int tid) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)>* job;
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return epoch_ != seen; });
+        seen = epoch_;
+        if (tid > want_) continue;   // not needed this time
+        job = job_;
+      }
+      (*job)(tid);
+      std::lock_guard<std::mutex> g(mu_);
+      if (++done_ == want_) done_cv_.notify_one();
+    }
+  }
+  int n_ = 1;
+  std::mutex call_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int)>* job_ = nullptr;
+  int want_ = 0, done_ = 0;
+  uint64_t epoch_ = 0;
+};
+
 template <class F>
 static void parallel_for(int64_t n, int64_t chunk, F&& fn) {
-  static const int kThreads = [] {
-    for (const char* v : {"MQ_HOST_THREADS", "OMP_NUM_THREADS"})
-      if (const char* e = std::getenv(v)) {
-        const int t = std::atoi(e);
-        if (t > 0) return std::min(t, 64);
-      }
-    return (int)std::max(1u, std::min(64u, std::thread::hardware_concurrency()));
-  }();
-  const int T = (int)std::min<int64_t>(kThreads, (n + chunk - 1) / std::max<int64_t>(chunk, 1));
+  HostPool& pool = HostPool::get();
+  const int T = (int)std::min<int64_t>(pool.threads(), (n + chunk - 1) / std::max<int64_t>(chunk, 1));
   if (T <= 1) {
     fn(0, 0, n);
     return;
   }
   std::atomic<int64_t> next{0};
-  auto work = [&](int tid) {
+  const std::function<void(int)> work = [&](int tid) {
     for (;;) {
       const int64_t b = next.fetch_add(chunk);
       if (b >= n) break;
       fn(tid, b, std::min(n, b + chunk));
     }
   };
-  std::vector<std::thread> pool;
-  for (int t = 1; t < T; t++) pool.emplace_back(work, t);
-  work(0);
-  for (auto& th : pool) th.join();
+  pool.run(T, work);
 }
 
 static int hip_fail(hipError_t e, const char* what) {
@@ -1476,7 +1640,12 @@ int mq_dag_expand(const mq_dag_batch* dag, int32_t t, mq_node* nodes_out, int64_
   return MQ_OK;
 }
 
-void mq_tapes_free(mq_tapes* t) { delete t; }
+void mq_tapes_free(mq_tapes* t) {
+  // the batch's buffers go back to the pool: the launches on the context streams that read them
+  // must be done (caller streams: DevPool::mark_foreign)
+  if (t && t->ctx && t->ctx->stream) (void)hipStreamSynchronize(t->ctx->stream);
+  delete t;
+}
 
 // A column program that is exactly keccak256(concat of variables and constants) with every piece
 // a whole number of 32-bit words and at most 2048 bits in all (lower.py keccak_subterms makes
@@ -1796,10 +1965,13 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
   int temps[2] = {0, 0};
   // pass 1: tapes the P kernel takes; the others go to G, which preloads the (at most 8)
   // variables of at most 256 bits those tapes push most often
-  std::vector<char> on_p(T->qct.size(), 0);
+  const int64_t nq = (int64_t)T->qct.size();
+  std::vector<char> on_p(nq, 0);
+  parallel_for(nq, 8, [&](int, int64_t b, int64_t e) {
+    for (int64_t i = b; i < e; i++) on_p[i] = qsa_translate(c, 0, true, T->qct[i], nullptr, nullptr) ? 1 : 0;
+  });
   std::vector<int64_t> pushes(c->var_nl_h.size(), 0);
   for (size_t i = 0; i < T->qct.size(); i++) {
-    on_p[i] = qsa_translate(c, 0, true, T->qct[i], nullptr, nullptr) ? 1 : 0;
     if (on_p[i]) continue;
     const auto& pr = T->qct[i].prog;
     for (size_t pc = 0; pc < pr.size(); pc++) {
@@ -1835,18 +2007,31 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
   T->qhist[1].assign(QK_COUNT, 0);
   T->qpairs.assign((size_t)QK_COUNT * QK_COUNT, 0);
   T->qpairs_p.assign((size_t)QK_COUNT * QK_COUNT, 0);
-  for (size_t i = 0; i < T->qct.size(); i++) {
-    int k = 0;
-    if (!on_p[i] || !qsa_translate(c, 0, true, T->qct[i], &tr, &extra)) {
-      k = 1;
-      if (!qsa_translate(c, 1, true, T->qct[i], &tr, &extra, &T->gpre, &T->gstage)) return MQ_OK;
-      qsa_window_layout(c, tr);
+  // per-tape translations in parallel (independent; ~50 ns per node), then concatenated in order
+  std::vector<std::vector<uint32_t>> trs(nq);
+  std::vector<char> kind_of(nq, 0);
+  std::atomic<bool> g_fail{false};
+  parallel_for(nq, 8, [&](int, int64_t b, int64_t e) {
+    std::vector<uint32_t> ex;
+    for (int64_t i = b; i < e && !g_fail.load(std::memory_order_relaxed); i++) {
+      if (on_p[i] && qsa_translate(c, 0, true, T->qct[i], &trs[i], &ex)) continue;
+      kind_of[i] = 1;
+      if (!qsa_translate(c, 1, true, T->qct[i], &trs[i], &ex, &T->gpre, &T->gstage)) {
+        g_fail = true;
+        break;
+      }
+      qsa_window_layout(c, trs[i]);
     }
-    qsa_count(c, k, tr, T->qhist[k], k == 1 ? &T->qpairs : &T->qpairs_p);
+  });
+  if (g_fail) return MQ_OK;
+  for (int64_t i = 0; i < nq; i++) {
+    const int k = kind_of[i];
+    const std::vector<uint32_t>& t = trs[i];
+    qsa_count(c, k, t, T->qhist[k], k == 1 ? &T->qpairs : &T->qpairs_p);
     GDesc d = T->qbase[i];
     d.prog_off = (uint32_t)words[k].size();
-    d.prog_len = (uint32_t)tr.size();
-    words[k].insert(words[k].end(), tr.begin(), tr.end());
+    d.prog_len = (uint32_t)t.size();
+    words[k].insert(words[k].end(), t.begin(), t.end());
     ds[k].push_back(d);
     temps[k] = std::max(temps[k], T->qct[i].n_temps);
   }
@@ -1967,7 +2152,15 @@ static int64_t g_tapes_per_group(int64_t n, int64_t M) {
 // Launch every evaluation kernel for a compiled batch: the assembly interpreter for the
 // QSA-eligible tapes (when the model batch fits its register file), the HIP C++ kernels for
 // the rest.  verdicts == nullptr -> first-hit mode into best.
-constexpr int64_t kLatencyAsmNodes = 16384;
+// (MQ_LATENCY_ASM_NODES overrides; the translation runs on the host pool, ~50 ns per node per
+// thread)
+static int64_t latency_asm_nodes() {
+  static const int64_t v = [] {
+    if (const char* e = std::getenv("MQ_LATENCY_ASM_NODES")) return (int64_t)std::atoll(e);
+    return (int64_t)131072;
+  }();
+  return v;
+}
 
 static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, hipStream_t st) {
   bool use_qsa = c->qsa_ready && c->use_asm && T->qsa.count > 0;
@@ -1979,7 +2172,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
   if (use_qsa && latency) {
     int64_t nodes = 0;
     for (int64_t n : T->n_nodes) nodes += n;
-    if (nodes > kLatencyAsmNodes) use_qsa = false;
+    if (nodes > latency_asm_nodes()) use_qsa = false;
   }
   if (use_qsa) {
     const int rc = qsa_prepare(c, T);
@@ -2279,6 +2472,7 @@ int mq_launch_first_hit(mq_ctx* c, mq_tapes* T, int32_t* d_best, void* stream) {
   if (!c->have_models) return MQ_ERR_NO_MODELS;
   if (T->ctx != c || T->peers.size() != c->peers.size()) return MQ_ERR_STATE;
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  if (st != c->stream) DevPool::get().mark_foreign(c->device);
   int rc = launch_one(c, T, d_best, st);
   if (rc || c->comms.empty()) return rc;
   // every device evaluates its contiguous shard of candidates (global indices), then ONE RCCL
