@@ -219,6 +219,58 @@ def dropin_leg(ev, grid=((1, 16), (1, 100), (32, 16), (32, 100), (256, 16), (256
     return out
 
 
+def dropin_stream_leg(ev, grid=((1, 16), (1, 100), (16, 100), (128, 100)), seed: int = 7):
+    """The drop-in path on a LASER-shaped stream (svm.py:351-358): N parent paths are checked
+    (``check_quick_sat_batch``), then their 2N JUMPI successors (parent + cond, parent +
+    Not(cond); synth_evm.fork_children) are timed — what the next fork / transaction round asks.
+    Answers are compared with the reference loop replayed on the oracle's verdicts."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cref  # oracle: CPU comparison only
+    from mythril_amd import support as sp
+    from mythril_amd.synth_evm import dropin_workload, fork_children
+    out = []
+    for n, m in grid:
+        eng = sp.VerdictEngine(ev)
+        warm, recs, _ = dropin_workload(n, m, seed=seed)
+        cache = sp.ModelCache(eng)
+        for r in reversed(recs):
+            cache.put(r, 1)
+        cache.check_quick_sat_batch(warm)
+        kids = fork_children(warm, seed=seed + n)
+        order_before = list(reversed(cache.model_cache.lru_cache.keys()))
+        before = dict(eng.timing)
+        st0 = dict(eng.stats)
+        ev.time_kernels(True)
+        t0 = time.perf_counter()
+        answers = cache.check_quick_sat_batch(kids)
+        wall = time.perf_counter() - t0
+        kt = ev.kernel_times(reset=True)
+        ev.time_kernels(False)
+        stages = {k: (eng.timing[k] - before[k]) * 1e3 for k in eng.timing}
+        db, ok = eng.incremental.lower(kids)
+        tb = db.to_tapes()
+        mb = eng.incremental.serialize(order_before)
+        t1 = time.perf_counter()
+        cref.first_hit(tb, mb, nthreads=1)
+        cpu_eval = time.perf_counter() - t1
+        v = cref.verdicts(tb, mb)
+        order, ref = list(range(len(order_before))), []
+        for q in range(len(kids)):
+            hit = next((i for i in order if v[q, i]), None)
+            if hit is not None:
+                order.remove(hit)
+                order.insert(0, hit)
+            ref.append(False if hit is None else order_before[hit])
+        same = all((a is False and b is False) or a is b for a, b in zip(answers, ref))
+        out.append({"n_parents": n, "n_queries": len(kids), "n_models": m, "ms_per_batch": wall * 1e3,
+                    "ms_per_query": wall * 1e3 / len(kids), "stage_ms": stages, "kernel_ms": float(sum(kt)),
+                    "conjuncts_evaluated": eng.stats["conjuncts_evaluated"] - st0["conjuncts_evaluated"],
+                    "conjuncts_cached": eng.stats["conjuncts_cached"] - st0["conjuncts_cached"],
+                    "hits": int(sum(a is not False for a in answers)),
+                    "cpu_oracle_eval_ms_1thread": cpu_eval * 1e3, "answers_match_reference_loop": bool(same)})
+    return out
+
+
 def calls_avoided_leg(ev, n_forks: int = 256, n_models: int = 100, seed: int = 21, budget: int = 100_000):
     """"z3 solver calls avoided", counted where SURVEY Appendix E says: at ``get_model``
     (``support.counters``: calls, answers from quick-sat at model.py:101-103, answers from
@@ -501,6 +553,7 @@ def main():
             out["gpu_over_cpu"] = out["value"] / cb["value"]
         if n_gpus == 1 and not args.no_dropin:
             out["dropin"] = dropin_leg(ev)
+            out["dropin_stream"] = dropin_stream_leg(ev)
             out["z3_calls_avoided"] = calls_avoided_leg(ev)
             out["keccak_service"] = keccak_leg(ev)
         print(json.dumps(out), flush=True)

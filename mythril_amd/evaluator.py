@@ -323,8 +323,11 @@ class Evaluator:
             pass
 
     # ------------------------------------------------------------ models
+    upload_seq = 0   # bumped by every upload: lets a caller tell its own batch is still resident
+
     def upload_models(self, mb: ModelBatch) -> None:
         s, keep = as_model_batch(mb)
+        self.upload_seq += 1
         _check(self.lib.mq_models_upload(self.ctx, C.byref(s)), "mq_models_upload")
         self.n_models = mb.n_models
         self.index_base = mb.index_base

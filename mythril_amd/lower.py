@@ -501,9 +501,10 @@ class IncrementalLowering:
     def __init__(self) -> None:
         self.syms = SymbolTable()
         self._reset_dag()
-        self._models: Dict[int, list] = {}
+        self._reset_models()
 
     def _reset_dag(self) -> None:
+        self.dag_gen = getattr(self, "dag_gen", 0) + 1   # node ids are valid within one generation
         self.tape = Tape()
         self._node: Dict[int, int] = {}       # id(term) -> DAG node
         self._keep: Dict[int, S.Term] = {}    # keeps those terms (and their ids) alive
@@ -593,7 +594,19 @@ class IncrementalLowering:
         return DagBatch(nodes, consts, np.asarray(offs, np.int64), np.asarray(flat, np.uint32)), ok
 
     # ------------------------------------------------------------ models
-    def _var_words(self, rec: Model, v: int) -> np.ndarray:
+    # Candidate models live in SLOTS: a model's variable rows are serialized once, column-major
+    # into ``_words[rows, slot]``; a variable that first appears in a later query adds its rows
+    # for every slot at once (one value lookup per model), and a batch is a column gather.  Slots
+    # are compacted (``slot_epoch`` bumps) when models that left the candidate set pile up.
+    def _reset_models(self) -> None:
+        self._slot: Dict[int, int] = {}      # id(model) -> slot
+        self._slot_model: List[object] = []  # slot -> model (kept alive: the id stays valid)
+        self._ftabs: List[Dict[int, Tuple[np.ndarray, np.ndarray]]] = []   # slot -> {f: table}
+        self._ser_nv = 0                     # variables serialized so far
+        self._words = np.zeros((0, 64), np.uint32)
+        self.slot_epoch = getattr(self, "slot_epoch", 0) + 1
+
+    def _var_value(self, rec: Model, v: int) -> int:
         name, w = self._var_names[v]
         if v in self.syms.derived:
             fname, fargs = self.syms.derived[v]
@@ -601,8 +614,64 @@ class IncrementalLowering:
             val = 0 if interp is None else interp[0].get(fargs, interp[1])
         else:
             val = rec.assignment.get(name)
-        val = 0 if val is None else int(val) & ((1 << max(w, 1)) - 1)
-        return np.asarray(to_words(val, w), np.uint32)
+        return 0 if val is None else int(val) & ((1 << max(w, 1)) - 1)
+
+    def _var_words(self, rec: Model, v: int) -> np.ndarray:
+        return np.asarray(to_words(self._var_value(rec, v), self._var_names[v][1]), np.uint32)
+
+    def _rows_of(self, recs: Sequence[Model], v0: int, v1: int) -> np.ndarray:
+        """Rows of variables [v0, v1) for the model records ``recs`` (one column each)."""
+        widths = self.syms.var_widths
+        blocks = []
+        for v in range(v0, v1):
+            vals = [self._var_value(r, v) for r in recs]
+            nl = limbs(widths[v])
+            blk = np.empty((nl, len(recs)), np.uint32)
+            for l in range(nl):
+                blk[l] = [(x >> (32 * l)) & 0xFFFFFFFF for x in vals]
+            blocks.append(blk)
+        return np.concatenate(blocks, axis=0) if blocks else np.zeros((0, len(recs)), np.uint32)
+
+    def _sync_names(self) -> int:
+        nv = len(self.syms.var_widths)
+        if getattr(self, "_names_n", -1) != nv:
+            self._var_names = {i: k for k, i in self.syms.vars.items()}
+            self._names_n = nv
+        return nv
+
+    def slots(self, models: Sequence) -> List[int]:
+        """Slot of each model (new models get one, with the rows of every serialized variable);
+        then the rows of variables the symbol table gained since the last call, for every slot."""
+        if not hasattr(self, "_slot"):
+            self._reset_models()
+        nv = self._sync_names()
+        if len(self._slot_model) > 4 * len(models) + 256:
+            self._reset_models()   # models that left the candidate set piled up: start over
+        out, new = [], []
+        for mod in models:
+            s = self._slot.get(id(mod))
+            if s is None or self._slot_model[s] is not mod:
+                s = len(self._slot_model)
+                self._slot[id(mod)] = s
+                self._slot_model.append(mod)
+                self._ftabs.append({})
+                new.append(s)
+            out.append(s)
+        n = len(self._slot_model)
+        if n > self._words.shape[1]:
+            grow = np.zeros((self._words.shape[0], max(n, 2 * self._words.shape[1])), np.uint32)
+            grow[:, :self._words.shape[1]] = self._words
+            self._words = grow
+        if new and self._ser_nv:
+            self._words[:, new] = self._rows_of([as_record(self._slot_model[s]) for s in new], 0, self._ser_nv)
+        if nv > self._ser_nv:
+            recs = [as_record(m) for m in self._slot_model]
+            add = self._rows_of(recs, self._ser_nv, nv)
+            rows = np.zeros((add.shape[0], self._words.shape[1]), np.uint32)
+            rows[:, :n] = add
+            self._words = np.concatenate([self._words, rows], axis=0)
+            self._ser_nv = nv
+        return out
 
     def _func_table(self, rec: Model, f: int) -> Tuple[np.ndarray, np.ndarray]:
         spec, name = self.syms.func_specs[f], self.syms.func_names[f]
@@ -623,35 +692,12 @@ class IncrementalLowering:
         ent = np.asarray(rows, np.uint32).reshape(-1, spec.stride)
         return ent, np.asarray(to_words(int(els), spec.result_width), np.uint32)
 
-    def serialize(self, models: Sequence, index_base: int = 0) -> ModelBatch:
-        """All variables / functions of the symbol table for ``models`` in global candidate
-        order, WITHOUT completion (absent: 0 / no entries, else 0).  A model's rows are computed
-        once per variable and function and reused by every later batch."""
+    def batch_of_slots(self, slots: Sequence[int], index_base: int = 0) -> ModelBatch:
+        """The ``mq_model_batch`` of the given slots, in that order, WITHOUT completion (absent:
+        0 / no entries, else 0)."""
         syms = self.syms
-        nv = len(syms.var_widths)
-        if getattr(self, "_names_n", -1) != nv:
-            self._var_names = {i: k for k, i in syms.vars.items()}
-            self._names_n = nv
-        M = len(models)
-        cols, fcache = [], []
-        for mod in models:
-            # per model: [model, its column of the variables seen so far (extended when new
-            # variables appear), how many variables that is, its function tables]
-            ent = self._models.get(id(mod))
-            if ent is None or ent[0] is not mod:
-                ent = self._models[id(mod)] = [mod, np.zeros(0, np.uint32), 0, {}]
-            if ent[2] < nv:
-                rec = as_record(mod)
-                ent[1] = np.concatenate([ent[1]] + [self._var_words(rec, v) for v in range(ent[2], nv)])
-                ent[2] = nv
-            cols.append(ent[1])
-            fcache.append((mod, ent[3]))
-        rows = sum(limbs(w) for w in syms.var_widths)
-        words = np.stack(cols, axis=1) if M else np.zeros((rows, 0), np.uint32)
-        if len(self._models) > 4 * M + 256:   # forget models that left the candidate set
-            live = {id(m) for m in models}
-            for k in [k for k in self._models if k not in live]:
-                del self._models[k]
+        M = len(slots)
+        words = self._words[:, list(slots)] if M else np.zeros((self._words.shape[0], 0), np.uint32)
         F = len(syms.func_specs)
         if not F:
             return ModelBatch(syms.var_widths, words, index_base=index_base)
@@ -662,10 +708,11 @@ class IncrementalLowering:
         wpos = epos = 0
         for f in range(F):
             tabs = []
-            for mod, fc in fcache:
+            for s in slots:
+                fc = self._ftabs[s]
                 t = fc.get(f)
                 if t is None:
-                    t = fc[f] = self._func_table(as_record(mod), f)
+                    t = fc[f] = self._func_table(as_record(self._slot_model[s]), f)
                 tabs.append(t)
             counts = np.fromiter((len(t[0]) for t in tabs), np.int64, M)
             eptr[f, 1:] = np.cumsum(counts)
@@ -679,3 +726,12 @@ class IncrementalLowering:
             epos += el.size
         return ModelBatch(syms.var_widths, words, list(syms.func_specs), eptr, np.concatenate(ew_chunks), ebase,
                           np.concatenate(el_chunks), elb, index_base)
+
+    def serialize(self, models: Sequence, index_base: int = 0) -> ModelBatch:
+        """All variables / functions of the symbol table for ``models`` in global candidate
+        order (index 0 = MRU), WITHOUT completion."""
+        return self.batch_of_slots(self.slots(models), index_base)
+
+    def model_key(self, slots: Sequence[int]) -> tuple:
+        """Identity of the batch ``batch_of_slots(slots)`` would build: equal keys, equal batches."""
+        return (self.slot_epoch, tuple(slots), self._ser_nv, len(self.syms.func_specs))

@@ -145,12 +145,60 @@ def split_conjuncts(db: DagBatch, groups: int) -> Tuple[DagBatch, Optional[np.nd
     return DagBatch(db.nodes, db.consts, np.asarray(new, np.int64), db.roots), starts
 
 
+class ConjunctRows:
+    """Verdicts of single conjuncts under single models, kept across calls: ``R[row, slot]`` is
+    -1 (not evaluated), 0 or 1 for the conjunct DAG node of ``row`` under the model in ``slot``
+    (:class:`~mythril_amd.lower.IncrementalLowering` slots).  A conjunction is true under a model
+    iff each of its conjuncts is, so a query whose conjuncts were all seen before (a forked path's
+    parent constraints, svm.py:351-358; the keccak axioms riding on every query,
+    constraints.py:127-128) needs no device work for the models already evaluated.  Valid for one
+    DAG generation and slot epoch (``key``); past ``MAX_ROWS`` conjuncts it starts over."""
+
+    MAX_ROWS = 1 << 16
+
+    def __init__(self) -> None:
+        self.reset(None)
+
+    def reset(self, key) -> None:
+        self.key = key
+        self.row: Dict[int, int] = {}
+        self.R = np.full((256, 128), -1, np.int8)
+        self.bad: set = set()   # conjunct nodes whose tape the evaluator does not support
+
+    def sync(self, key) -> None:
+        if key != self.key or len(self.row) > self.MAX_ROWS:
+            self.reset(key)
+
+    def rows_for(self, nodes: np.ndarray, n_slots: int) -> np.ndarray:
+        row = self.row
+        out = np.empty(len(nodes), np.int64)
+        for i, x in enumerate(nodes.tolist()):
+            r = row.get(x)
+            if r is None:
+                r = row[x] = len(row)
+            out[i] = r
+        nr, ns = self.R.shape
+        if len(row) > nr or n_slots > ns:
+            grow = np.full((max(nr, 2 * len(row)) if len(row) > nr else nr,
+                            max(ns, 2 * n_slots) if n_slots > ns else ns), -1, np.int8)
+            grow[:nr, :ns] = self.R
+            self.R = grow
+        return out
+
+
 class VerdictEngine:
     """Lowers conjunctions + candidate models and evaluates them on the GPU.
 
     ``rows(exprs, models)`` -> one ``bool[len(models)]`` verdict row per expression (``None`` =
     unsupported: fail closed).  Works on z3-free terms (:mod:`mythril_amd.smt`) and, on a z3 host,
     on z3 ``BoolRef`` (lowered by :mod:`mythril_amd.lower_z3`).
+
+    The drop-in path (z3-free terms, the LRU's <= 100 models) keeps three things across calls:
+    the hash-consed DAG of every lowered term, the candidate models' serialized rows (resident on
+    the device in slot order, so an LRU bump re-uploads nothing), and per-conjunct verdict rows
+    (:class:`ConjunctRows`).  A call evaluates only the conjuncts not yet known under the current
+    models, one tape each, when there are at most ``conj_tapes`` of them; a batch of mostly new
+    paths is evaluated as whole conjunctions instead (split into conjunct groups when small).
 
     ``timing`` accumulates host seconds per stage of every call (lower, serialize, upload,
     compile, evaluate = launch + readback) — the drop-in leg of bench.py reports it."""
@@ -160,15 +208,20 @@ class VerdictEngine:
     # the incremental lowering (cached conjunct fragments and model rows) is used instead
     hoist_min_batch = 8
     hoist_min_models = 1024
-    # a small batch leaves the GPU idle and a single conjunction is one wave's serial walk over
-    # its ~1 000 nodes: its conjuncts are split into up to ``split_tapes // N`` contiguous groups,
-    # each its own tape (one wave each), and the group verdict rows are AND-ed (the conjunction
-    # holds iff every conjunct does).  Shared sub-terms are then re-evaluated per group — more
-    # work (and compile time), less latency (profiles/r02lat*, r02sp); from N = 32 the compile
-    # cost outweighs it; 0 disables
+    # a small batch of new paths leaves the GPU idle and a single conjunction is one wave's
+    # serial walk over its ~1 000 nodes: its conjuncts are split into up to ``split_tapes // N``
+    # contiguous groups, each its own tape (one wave each), and the group verdict rows are AND-ed.
+    # Shared sub-terms are then re-evaluated per group — more work (and compile time), less
+    # latency (profiles/r02lat*, r02sp); from N = 32 the compile cost outweighs it; 0 disables
     split_tapes = int(os.environ.get("MQ_SPLIT_TAPES", "32"))
+    # at most this many unknown conjuncts are evaluated one tape each (and cached); more are
+    # evaluated as whole conjunctions.  One tape per conjunct re-evaluates shared sub-terms per
+    # conjunct, yet it measured no slower on batches of new paths either (one wave per short
+    # tape; profiles/r03c) and it is what lets forked paths reuse their parents' rows, so the
+    # default is unbounded.  0 disables the conjunct cache
+    conj_tapes = int(os.environ.get("MQ_CONJ_TAPES", str(1 << 30)))
     # launches of at most this many waves run the G kernel one tape per wave (MQ_OPT_LATENCY_WAVES)
-    latency_waves = int(os.environ.get("MQ_LATENCY_WAVES", "1024"))
+    latency_waves = int(os.environ.get("MQ_LATENCY_WAVES", "4096"))
     STAGES = ("lower", "serialize", "upload", "compile", "evaluate")
 
     def __init__(self, evaluator=None):
@@ -178,6 +231,9 @@ class VerdictEngine:
         self.pairs = 0
         self.timing = dict.fromkeys(self.STAGES, 0.0)
         self.incremental = IncrementalLowering()
+        self.conjuncts = ConjunctRows()
+        self.stats = {"conjuncts_evaluated": 0, "conjuncts_cached": 0, "whole_query_batches": 0}
+        self._resident = None   # (model key, evaluator upload_seq) of the batch on the device
 
     @property
     def evaluator(self):
@@ -221,11 +277,14 @@ class VerdictEngine:
             ev.set_option(ev.OPT_LATENCY_WAVES, waves)
         return prev
 
-    def _evaluate(self, tb, mb):
+    def _evaluate(self, tb, mb, upload: bool = True):
+        """Device hook: (verdicts [n_tapes, M], first hits) of ``tb`` over ``mb``; ``upload``
+        False when ``mb`` is already the evaluator's resident batch."""
         clock = time.perf_counter
         ev = self.evaluator
         t0 = clock()
-        ev.upload_models(mb)
+        if upload:
+            ev.upload_models(mb)
         t1 = clock()
         ct = ev.compile(tb)
         t2 = clock()
@@ -238,6 +297,22 @@ class VerdictEngine:
         self.timing["upload"] += t1 - t0
         self.timing["compile"] += t2 - t1
         self.timing["evaluate"] += clock() - t2
+        return v, fh
+
+    def _evaluate_resident(self, tb, slots):
+        """``_evaluate`` over the models of ``slots`` (sorted), uploading them only when the
+        evaluator no longer holds the batch this engine last uploaded for the same slots."""
+        t0 = time.perf_counter()
+        key = self.incremental.model_key(slots)
+        seq = getattr(self._ev, "upload_seq", None)
+        if self._resident is not None and self._resident[:2] == (key, seq) and seq is not None:
+            mb, upload = self._resident[2], False
+        else:
+            mb, upload = self.incremental.batch_of_slots(slots), True
+        self.timing["serialize"] += time.perf_counter() - t0
+        v, fh = self._evaluate(tb, mb, upload)
+        if upload:
+            self._resident = (key, getattr(self._ev, "upload_seq", None), mb)
         return v, fh
 
     def candidate_first_hits(self, exprs: Sequence, models: Sequence, generator):
@@ -284,15 +359,11 @@ class VerdictEngine:
         if not models:
             return [np.zeros(0, bool) for _ in exprs]
         hoist = len(exprs) >= self.hoist_min_batch and len(models) >= self.hoist_min_models
+        if not hoist and all(isinstance(e, S.Term) for e in exprs):
+            return self._rows_incremental(exprs, models)
         tb, mb, ok = self._lower(exprs, models, hoist)
-        starts = None
-        if isinstance(tb, DagBatch) and self.split_tapes:
-            tb, starts = split_conjuncts(tb, self.split_tapes // len(exprs))
         try:
             v, fh = self._evaluate(tb, mb)
-            if starts is not None:
-                v = np.logical_and.reduceat(v, starts, axis=0)
-                fh = np.where(np.minimum.reduceat(fh, starts) == -2, -2, 0)
         except Exception:
             if getattr(tb, "columns", None) is None:
                 raise
@@ -300,12 +371,73 @@ class VerdictEngine:
             # evaluate the batch without hoisting instead
             tb, mb, ok = self._lower(exprs, models, False)
             v, fh = self._evaluate(tb, mb)
+        self._resident = None
         self.launches += 1
-        self.pairs += len(exprs) * mb.n_models   # (queries, not the conjunct groups split_conjuncts made)
+        self.pairs += len(exprs) * mb.n_models
+        return [v[i].copy() if ok[i] and fh[i] != -2 else None for i in range(len(exprs))]
+
+    def _rows_incremental(self, exprs: Sequence, models: Sequence) -> List[Optional[np.ndarray]]:
+        clock = time.perf_counter
+        inc = self.incremental
+        t0 = clock()
+        db, ok = inc.lower(exprs)
+        t1 = clock()
+        slots = np.asarray(inc.slots(models), np.int64)
+        dev_slots = sorted(set(slots.tolist()))
+        self.timing["lower"] += t1 - t0
+        self.timing["serialize"] += clock() - t1
+        cache = self.conjuncts
+        cache.sync((inc.dag_gen, inc.slot_epoch))
+        uroots, inv = np.unique(db.roots, return_inverse=True)
+        urows = cache.rows_for(uroots, int(slots.max()) + 1)
+        unk = (cache.R[np.ix_(urows, slots)] < 0).any(axis=1)
+        n_unk = int(unk.sum())
+        self.stats["conjuncts_cached"] += int(len(uroots) - n_unk)
+        if n_unk > self.conj_tapes:
+            return self._rows_whole(db, ok, slots, dev_slots, len(exprs))
+        if n_unk:
+            from .lower import DagBatch
+            todo = uroots[unk]
+            tb = DagBatch(db.nodes, db.consts, np.arange(n_unk + 1, dtype=np.int64), todo)
+            v, fh = self._evaluate_resident(tb, dev_slots)
+            cache.R[np.ix_(urows[unk], np.asarray(dev_slots, np.int64))] = v.astype(np.int8)
+            for x in todo[fh == -2].tolist():
+                cache.bad.add(int(x))
+            self.stats["conjuncts_evaluated"] += n_unk
+            self.launches += 1
+            self.pairs += n_unk * len(dev_slots)
+        # each query: the AND of its conjuncts' rows, in the caller's model order
+        occ = cache.R[np.ix_(urows[inv], slots)] > 0
+        offs = db.root_offsets
+        lens = np.diff(offs)
         out: List[Optional[np.ndarray]] = []
-        for i in range(len(exprs)):
-            out.append(v[i].copy() if ok[i] and fh[i] != -2 else None)
+        bad = cache.bad
+        for q in range(len(exprs)):
+            a, b = int(offs[q]), int(offs[q + 1])
+            if not ok[q] or (bad and any(int(x) in bad for x in db.roots[a:b])):
+                out.append(None)
+            elif lens[q] == 0:
+                out.append(np.ones(len(slots), bool))
+            else:
+                out.append(occ[a:b].all(axis=0))
         return out
+
+    def _rows_whole(self, db, ok, slots, dev_slots, n_exprs) -> List[Optional[np.ndarray]]:
+        """Whole conjunctions, one tape each (a small batch: conjunct groups, rows AND-ed), on the
+        resident model batch; nothing is cached per conjunct."""
+        tb, starts = db, None
+        if self.split_tapes:
+            tb, starts = split_conjuncts(db, self.split_tapes // n_exprs)
+        v, fh = self._evaluate_resident(tb, dev_slots)
+        if starts is not None:
+            v = np.logical_and.reduceat(v, starts, axis=0)
+            fh = np.where(np.minimum.reduceat(fh, starts) == -2, -2, 0)
+        pos = {s: i for i, s in enumerate(dev_slots)}
+        v = v[:, [pos[s] for s in slots.tolist()]]
+        self.stats["whole_query_batches"] += 1
+        self.launches += 1
+        self.pairs += n_exprs * len(dev_slots)   # (queries, not the conjunct groups split_conjuncts made)
+        return [v[i].copy() if ok[i] and fh[i] != -2 else None for i in range(n_exprs)]
 
 
 _UNSUPPORTED = object()

@@ -738,3 +738,24 @@ def fork_workload(n_queries: int, n_models: int, seed: int = 8, n_tx: int = 3,
         exprs.append(S.And(*(path.args + (cond,))))
         parents.append(p)
     return exprs, records, parents
+
+
+def fork_children(parents: Sequence[S.Term], n_tx: int = 3, seed: int = 9) -> List[S.Term]:
+    """The two successors of a JUMPI after each parent path (svm.py:351-358): ``parent + cond``
+    and ``parent + Not(cond)``, with ``cond`` a branch condition on the last transaction's
+    calldata (an argument compare, a flag byte or a calldata-size check).  The children reuse
+    the parents' conjunct terms (interned), as LASER's forked states share their constraints."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    tx = _Tx(n_tx)
+    out = []
+    for p in parents:
+        kind = int(rng.integers(3))
+        if kind == 0:
+            cond = S.ULT(tx.word(36), S.BitVecVal(int(rng.integers(1, 1 << 16)), 256))
+        elif kind == 1:
+            cond = S.Extract(7, 0, tx.word(4)) == int(rng.integers(0, 256))
+        else:
+            cond = S.ULT(tx.cds, S.BitVecVal(int(rng.integers(4, 100)), 256))
+        conj = list(p.args) if p.kind == S.AND else [p]
+        out += [S.And(*(conj + [cond])), S.And(*(conj + [S.Not(cond)]))]
+    return out

@@ -33,7 +33,7 @@ class OracleEngine(VerdictEngine):
         t = time.perf_counter()
         return cref.first_hit(tb, mb)[0], t, t
 
-    def _evaluate(self, tb, mb):
+    def _evaluate(self, tb, mb, upload=True):
         if hasattr(tb, "root_offsets"):   # DagBatch -> self-contained tapes
             tb = tb.to_tapes()
         fh, _ = cref.first_hit(tb, mb)

@@ -384,3 +384,87 @@ def test_candidates_off_by_default(fresh):
         sp.model_cache.put(m, 1)
     assert sp.is_possible_batch([sp.Constraints(list(e.args)) for e in exprs]) == [False] * 4
     assert sp.counters["candidate_answers"] == 0
+
+
+class CountingOracleEngine(OracleEngine):
+    """OracleEngine that records what reaches the device hook (tapes, uploads)."""
+
+    def __init__(self):
+        super().__init__()
+        self.uploads = 0
+        self.tapes = []
+
+    def _evaluate(self, tb, mb, upload=True):
+        self.uploads += int(upload)
+        self.tapes.append(tb.n_tapes)
+        self.upload_seq_fake = self.uploads
+        return super()._evaluate(tb, mb, upload)
+
+
+def test_child_paths_reuse_cached_conjunct_rows():
+    """A stream of forked paths (each query = a previous path + new conjuncts, svm.py:351-358):
+    only conjuncts never seen under the current models reach the device, one tape each, and the
+    answers equal the reference loop's (term_eval, independent of the lowering)."""
+    from mythril_amd.synth_evm import dropin_workload
+    exprs, recs, _ = dropin_workload(6, 20, seed=11)
+    eng = CountingOracleEngine()
+    cache, ref = sp.ModelCache(eng), ReferenceLoopCache()
+    for r in reversed(recs):
+        cache.put(r, 1)
+        ref.put(r, 1)
+    rng = random.Random(3)
+    stream = list(exprs)
+    for e in exprs:   # children: the parent's conjuncts plus one or two new ones
+        extra = [S.ULT(S.BitVecVal(rng.randrange(1 << 20), 256), S.BitVecVal(rng.randrange(1 << 20), 256))
+                 for _ in range(rng.randrange(1, 3))]
+        stream.append(S.And(*(list(e.args) + extra)))
+    got = cache.check_quick_sat_batch(stream[:6])
+    n_first = sum(eng.tapes)
+    got += cache.check_quick_sat_batch(stream[6:])
+    want = [ref.check_quick_sat(e) for e in stream]
+    assert all((a is False and b is False) or a is b for a, b in zip(got, want))
+    st = eng.stats
+    assert st["conjuncts_cached"] > 0
+    # the children added at most 2 new conjuncts each (plus nothing else)
+    assert sum(eng.tapes) - n_first <= 2 * 6
+    assert list(cache.model_cache.lru_cache.keys()) == list(ref.lru.keys())
+
+
+def test_conjunct_rows_follow_new_models():
+    """A model inserted between two batches (a solver answer, model.py:125) is evaluated for the
+    cached conjuncts too; a query over it is answered exactly."""
+    x, y = S.BitVecSym("x", 256), S.BitVecSym("y", 256)
+    c1, c2 = S.ULT(x, S.BitVecVal(10, 256)), x + y == S.BitVecVal(7, 256)
+    m_old = Model({"x": 100, "y": 0})
+    m_new = Model({"x": 3, "y": 4})
+    eng = CountingOracleEngine()
+    assert eng.rows([S.And(c1, c2)], [m_old])[0].tolist() == [False]
+    rows = eng.rows([S.And(c1, c2), c1], [m_new, m_old])
+    assert rows[0].tolist() == [True, False] and rows[1].tolist() == [True, False]
+    n = len(eng.tapes)
+    rows = eng.rows([S.And(c2, c1)], [m_old, m_new])   # same conjuncts, same models: no launch
+    assert rows[0].tolist() == [False, True] and len(eng.tapes) == n
+    assert eng.stats["conjuncts_cached"] >= 2
+
+
+def test_resident_models_are_not_reuploaded():
+    """The device batch is the candidate set in slot order: a new order of the same models (an
+    LRU bump) and repeated calls upload nothing new; a new model does."""
+    x = S.BitVecSym("x", 256)
+    ms = [Model({"x": i}) for i in range(5)]
+
+    class FakeEv:
+        upload_seq = 1
+
+    eng = CountingOracleEngine()
+    eng._ev = FakeEv()
+    eng.conj_tapes = 0   # whole-query path: every call reaches the device hook
+    q = [S.ULT(x, S.BitVecVal(3, 256))]
+    eng.rows(q, ms)
+    eng.rows([S.ULT(x, S.BitVecVal(4, 256))], list(reversed(ms)))
+    assert eng.uploads == 1
+    r = eng.rows([S.ULT(x, S.BitVecVal(2, 256))], ms[2:] + ms[:2])
+    assert r[0].tolist() == [False, False, False, True, True]
+    assert eng.uploads == 1
+    eng.rows(q, ms + [Model({"x": 0})])
+    assert eng.uploads == 2
