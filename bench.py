@@ -188,12 +188,14 @@ def dropin_leg(ev, grid=((1, 16), (1, 100), (32, 16), (32, 100), (256, 16), (256
             cache.put(r, 1)
         before = dict(eng.timing)
         ev.time_kernels(True)
+        ev.host_times(reset=True)
         t0 = time.perf_counter()
         answers = cache.check_quick_sat_batch(exprs)
         wall = time.perf_counter() - t0
         kt = ev.kernel_times(reset=True)
         ev.time_kernels(False)
         stages = {k: (eng.timing[k] - before[k]) * 1e3 for k in eng.timing}
+        lib_ms = {k: v * 1e3 for k, v in ev.host_times(reset=True).items()}
         # the oracle on the same lowered tapes x models (candidate index = position in recs,
         # MRU first), then the reference loop replayed on its verdicts: first hit in the current
         # order, bump to MRU (support_utils.py:62-66)
@@ -214,6 +216,7 @@ def dropin_leg(ev, grid=((1, 16), (1, 100), (32, 16), (32, 100), (256, 16), (256
         same = all((a is False and b is False) or a is b for a, b in zip(answers, ref))
         out.append({"n_queries": n, "n_models": m, "avg_tape_nodes": float(tb.sizes().mean()),
                     "ms_per_batch": wall * 1e3, "ms_per_query": wall * 1e3 / n, "stage_ms": stages,
+                    "library_phase_ms": lib_ms,
                     "kernel_ms": float(sum(kt)), "hits": int(sum(a is not False for a in answers)),
                     "cpu_oracle_eval_ms_1thread": cpu_eval * 1e3, "answers_match_reference_loop": bool(same)})
     return out
@@ -241,12 +244,14 @@ def dropin_stream_leg(ev, grid=((1, 16), (1, 100), (16, 100), (128, 100)), seed:
         before = dict(eng.timing)
         st0 = dict(eng.stats)
         ev.time_kernels(True)
+        ev.host_times(reset=True)
         t0 = time.perf_counter()
         answers = cache.check_quick_sat_batch(kids)
         wall = time.perf_counter() - t0
         kt = ev.kernel_times(reset=True)
         ev.time_kernels(False)
         stages = {k: (eng.timing[k] - before[k]) * 1e3 for k in eng.timing}
+        lib_ms = {k: v * 1e3 for k, v in ev.host_times(reset=True).items()}
         db, ok = eng.incremental.lower(kids)
         tb = db.to_tapes()
         mb = eng.incremental.serialize(order_before)
@@ -263,7 +268,8 @@ def dropin_stream_leg(ev, grid=((1, 16), (1, 100), (16, 100), (128, 100)), seed:
             ref.append(False if hit is None else order_before[hit])
         same = all((a is False and b is False) or a is b for a, b in zip(answers, ref))
         out.append({"n_parents": n, "n_queries": len(kids), "n_models": m, "ms_per_batch": wall * 1e3,
-                    "ms_per_query": wall * 1e3 / len(kids), "stage_ms": stages, "kernel_ms": float(sum(kt)),
+                    "ms_per_query": wall * 1e3 / len(kids), "stage_ms": stages, "library_phase_ms": lib_ms,
+                    "kernel_ms": float(sum(kt)),
                     "conjuncts_evaluated": eng.stats["conjuncts_evaluated"] - st0["conjuncts_evaluated"],
                     "conjuncts_cached": eng.stats["conjuncts_cached"] - st0["conjuncts_cached"],
                     "hits": int(sum(a is not False for a in answers)),

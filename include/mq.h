@@ -288,8 +288,8 @@ int mq_keccak256(mq_ctx* ctx, const uint8_t* data, const int64_t* offsets, int32
    MQ_OPT_LATENCY_WAVES (default 0 = off): a launch of at most this many waves (tapes x 64-model
    tiles) runs the general assembly kernel with one tape per wave instead of several tapes per
    wave: a few tapes over a few models are latency-bound (the drop-in path at the reference's
-   shape sets it).  Such a launch with more than 16 384 tape nodes skips the assembly
-   translation (host time) and runs on the HIP C++ kernel. */
+   shape sets it).  Such a launch with more than 131 072 tape nodes (MQ_LATENCY_ASM_NODES)
+   skips the assembly translation (host time) and runs on the HIP C++ kernel. */
 enum mq_option {
   MQ_OPT_USE_ASM = 1,
   MQ_OPT_EARLY_EXIT = 2,
@@ -305,6 +305,14 @@ int mq_ctx_set_option(mq_ctx* ctx, int option, int value);
    launch order (MQ_OPT_TIME_KERNELS on; several devices: the slowest device per launch).  Waits for those launches.  *n_out = number recorded
    (may exceed max_out; only max_out are written).  reset != 0 forgets them. */
 int mq_kernel_times(mq_ctx* ctx, float* out_ms, int32_t max_out, int32_t* n_out, int reset);
+
+/* Diagnostic: host seconds this context spent per phase since the last reset (out[i], i <
+   MQ_HOST_PHASES; *n_out = MQ_HOST_PHASES): 0 DAG expansion + tape compilation, 1 structural
+   P/G translation at upload, 2 tape upload, 3 P translation at launch, 4 G translation at
+   launch, 5 translated-program upload, 6 kernel-argument upload, 7 launch + readback, 8 model
+   upload, 9 tape release.  No reference counterpart (the drop-in leg's host-time breakdown). */
+#define MQ_HOST_PHASES 10
+int mq_host_times(mq_ctx* ctx, double* out, int32_t max_out, int32_t* n_out, int reset);
 
 /* How a compiled batch is split: tapes on the assembly interpreter, on the generic 256-bit
    and on the wider (512 / 1024 / 2048-bit) HIP C++ kernels (any pointer may be NULL). */

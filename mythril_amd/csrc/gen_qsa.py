@@ -996,6 +996,21 @@ def make_handlers(variant, pfx):
             # tile's masks): one scalar load straight into the Bool stack
             H(("PUSH_PKB", d), ["s_lshl_b32 s34, s17, 3", f"s_load_dwordx2 {B(d)}, s[96:97], s34", "s_waitcnt lgkmcnt(0)"],
               reads_stack=False)
+        if G and d >= 1:
+            # a run of n + 1 packed Bool masks AND-ed into B(d - 1) (the translator merges
+            # consecutive PUSH_PKB_A at slot d): imm = the first mask, n inline data words the
+            # others; all n + 1 scalar loads are in flight behind one wait
+            for n in range(1, 4):
+                body = ["s_lshl_b32 s34, s17, 3", "s_load_dwordx2 s[64:65], s[96:97], s34"]
+                for i in range(n):
+                    body += [f"v_readlane_b32 s{35 + i}, {WIN}, s16", "s_add_u32 s16, s16, 1"]
+                body += ["s_nop 3"]
+                for i in range(n):
+                    body += [f"s_lshl_b32 s{35 + i}, s{35 + i}, 3",
+                             f"s_load_dwordx2 s[{66 + 2 * i}:{67 + 2 * i}], s[96:97], s{35 + i}"]
+                body += ["s_waitcnt lgkmcnt(0)"]
+                body += [f"s_and_b64 {B(d - 1)}, {B(d - 1)}, s[{64 + 2 * i}:{65 + 2 * i}]" for i in range(n + 1)]
+                H(("PKBN_A", d, n), body, reads_stack=False)
         H(("PUSH_CONST", d), ["s_lshl_b32 s34, s17, 2", "s_load_dwordx8 s[64:71], s[20:21], s34", "s_waitcnt lgkmcnt(0)"]
           + [f"v_mov_b64 {S2(d, l)}, s[{64 + l}:{65 + l}]" for l in range(0, L, 2)], reads_stack=False)
         if G:

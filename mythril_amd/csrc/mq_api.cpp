@@ -233,6 +233,7 @@ struct mq_ctx {
   // the lead (dev_ids[0]); peers[i] is a single-device context on dev_ids[i + 1].  The candidate
   // axis is split contiguously over [lead, peers...] (shard_lo[g] = first local model of device
   // g); per-tape first hits are combined by an in-library RCCL MIN all-reduce (comms, lead first).
+  double host_t[MQ_HOST_PHASES] = {};   // mq_host_times
   std::vector<mq_ctx*> peers;
   std::vector<ncclComm_t> comms;
   std::vector<int64_t> shard_lo;
@@ -430,6 +431,14 @@ static void parallel_for(int64_t n, int64_t chunk, F&& fn) {
   pool.run(T, work);
 }
 
+// adds the scope's wall time to ctx->host_t[phase] (mq_host_times)
+struct PhaseTimer {
+  double* acc;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  explicit PhaseTimer(double* a) : acc(a) {}
+  ~PhaseTimer() { *acc += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); }
+};
+
 static int hip_fail(hipError_t e, const char* what) {
   g_last_error = std::string(what) + ": " + hipGetErrorString(e);
   return MQ_ERR_HIP;
@@ -541,6 +550,7 @@ static int qsa_init(mq_ctx* c) {
     int words = -1;
     if (base == "EQVK") words = kQsaKClassWords[1 + (v & 1)];
     else if (base == "EQK" || base == "ULTK" || base == "UGTK" || base == "ULEK" || base == "UGEK") words = kQsaKClassWords[v];
+    else if (base == "PKBN") words = v;   // the run's other mask indices
     if (words > 0) c->qsa_data_words[hword(1, c->qsa_off[1][h]) & 0xFFFFu] = (uint8_t)words;
   }
   c->qsa_ready = ok && std::getenv("MQ_DISABLE_QSA") == nullptr;
@@ -822,6 +832,7 @@ void mq_models_shard_free(void* handle) { delete static_cast<ShardBuffers*>(hand
 
 int mq_models_upload(mq_ctx* c, const mq_model_batch* mb) {
   if (!c || !mb || mb->n_models < 0) return MQ_ERR_ARG;
+  PhaseTimer pt(&c->host_t[8]);
   if (c->peers.empty()) {
     c->shard_lo.assign(1, 0);
     c->M_total = mb->n_models;
@@ -1016,6 +1027,25 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
     }
     return false;
   };
+  // G: consecutive "B(d - 1) &= packed mask" words (PUSH_PKB_A at slot d) as one PKBN_A word
+  // with up to four masks: their scalar loads share one wait
+  auto merge_pkb = [&](int d) {
+    if (log.size() < 2) return;
+    const Emit e1 = log.back();
+    if (e1.kind != QK_PUSH_PKB_A || e1.d != d || out.size() != ends_at(e1)) return;
+    const Emit e0 = log[log.size() - 2];
+    if (ends_at(e0) != e1.pos || e0.d != d) return;
+    int n0;   // masks after the first one in e0
+    if (e0.kind == QK_PUSH_PKB_A) n0 = 0;
+    else if (e0.kind == QK_PKBN_A) n0 = e0.v;
+    else return;
+    if (n0 + 1 > 3 || c->qsa_index[k][QK_PKBN_A][d][n0 + 2] < 0) return;
+    std::vector<uint32_t> data(out.begin() + (long)(e0.pos + 1), out.begin() + (long)ends_at(e0));
+    data.push_back(e1.imm);
+    const uint32_t imm0 = e0.imm;
+    drop_last(2);
+    emit_k(QK_PKBN_A, d, n0 + 1, imm0, data);
+  };
   uint32_t prev_op = G_END, prev_d = 0, prev_imm = 0;
   size_t prev_out = 0;
   int prev_pre = -1;   // preload slot of the variable the previous instruction pushed
@@ -1152,7 +1182,10 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
       case G_STORE_TMP_B: ok = d == 0 && word(QK_STORE_TMP_BOOL, 0, -1, imm); break;
       case G_PUSH_BOOL: ok = word(QK_PUSH_BOOL, d, -1, imm); break;
       case G_NOT: ok = fuse_not(d) || word(QK_NOT, d, -1, 0); break;
-      case G_AND: ok = fuse_acc(d, true) || word(QK_AND, d, -1, 0); break;
+      case G_AND:
+        ok = fuse_acc(d, true) || word(QK_AND, d, -1, 0);
+        if (ok && !P) merge_pkb(d);
+        break;
       case G_OR: ok = fuse_acc(d, false) || word(QK_OR, d, -1, 0); break;
       case G_XOR: ok = word(QK_XOR, d, -1, 0); break;
       case G_IFF: ok = word(QK_IFF, d, -1, 0); break;
@@ -1407,10 +1440,14 @@ static int tapes_upload_one(mq_ctx* c, int32_t n_tapes, const std::vector<Compil
   // constants of an eligible tape (divisor reciprocals) follow its own constants in the pool
   std::vector<char> qsa_ok(n_tapes, 0);
   std::vector<std::vector<uint32_t>> qextra(n_tapes);
+  std::unique_ptr<PhaseTimer> pt(new PhaseTimer(&c->host_t[1]));
   if (c->qsa_ready)
-    for (int t = 0; t < n_tapes; t++)
-      if (ct[t].supported && ct[t].L == 8 && ct[t].n_temps <= kQsaMaxTemps)
-        qsa_ok[t] = qsa_translate(c, 1, false, ct[t], nullptr, &qextra[t]) ? 1 : 0;
+    parallel_for(n_tapes, 8, [&](int, int64_t b, int64_t e) {
+      for (int64_t t = b; t < e; t++)
+        if (ct[t].supported && ct[t].L == 8 && ct[t].n_temps <= kQsaMaxTemps)
+          qsa_ok[t] = qsa_translate(c, 1, false, ct[t], nullptr, &qextra[t]) ? 1 : 0;
+    });
+  pt.reset(new PhaseTimer(&c->host_t[2]));
   for (int pass = -1; pass < kGen; pass++) {
     mq_tapes::Variant& v = pass < 0 ? T->qsa : T->gen[pass];
     v.L = pass < 0 ? 8 : kGenL[pass];
@@ -1485,9 +1522,12 @@ int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t*
   // compile once (independent per tape), upload to every device of the context
   CompileLimits lim;
   std::vector<CompiledTape> ct(tb->n_tapes);
-  parallel_for(tb->n_tapes, 16, [&](int, int64_t b, int64_t e) {
-    for (int64_t t = b; t < e; t++) ct[t] = compile_tape(tb, (int32_t)t, lim);
-  });
+  {
+    PhaseTimer pt(&c->host_t[0]);
+    parallel_for(tb->n_tapes, 16, [&](int, int64_t b, int64_t e) {
+      for (int64_t t = b; t < e; t++) ct[t] = compile_tape(tb, (int32_t)t, lim);
+    });
+  }
   return tapes_upload_all(c, tb->n_tapes, ct, out, n_unsup_out);
 }
 
@@ -1598,15 +1638,21 @@ static bool dag_ok(const mq_dag_batch* d) {
 // Compile every tape of a DAG batch (parallel over tapes).
 static std::vector<CompiledTape> compile_dag(const mq_dag_batch* dag, const CompileLimits& lim) {
   std::vector<CompiledTape> ct(dag->n_tapes);
+  // per-thread scratch kept across calls: the mark array spans the whole persistent DAG (up to
+  // 2^20 nodes), so re-zeroing it per call cost more than compiling a query's few tapes; stamps
+  // keep increasing across calls instead (the array is reset only when it grows or they wrap)
   struct Scratch {
     std::vector<int32_t> mark;
     std::vector<mq_node> block;
     int32_t stamp = 0;
   };
-  std::vector<Scratch> scratch(64);
-  parallel_for(dag->n_tapes, 4, [&](int tid, int64_t b, int64_t e) {
-    Scratch& sc = scratch[tid];
-    if (sc.mark.empty()) sc.mark.assign((size_t)std::max<int64_t>(dag->n_nodes, 1), 0);
+  static thread_local Scratch sc_tls;
+  parallel_for(dag->n_tapes, 4, [&](int, int64_t b, int64_t e) {
+    Scratch& sc = sc_tls;
+    if ((int64_t)sc.mark.size() < dag->n_nodes || sc.stamp > (1 << 30)) {
+      sc.mark.assign((size_t)std::max<int64_t>(dag->n_nodes, 1), 0);
+      sc.stamp = 0;
+    }
     for (int64_t t = b; t < e; t++) {
       if (!expand_dag_tape(dag, (int32_t)t, sc.mark, ++sc.stamp, sc.block)) {
         ct[t].why = "malformed DAG (operand does not precede its user)";
@@ -1626,7 +1672,11 @@ int mq_tapes_upload_dag(mq_ctx* c, const mq_dag_batch* dag, mq_tapes** out, int3
   for (int t = 0; t < dag->n_tapes; t++)
     if (dag->root_offsets[t + 1] < dag->root_offsets[t]) return MQ_ERR_ARG;
   CompileLimits lim;
-  const std::vector<CompiledTape> ct = compile_dag(dag, lim);
+  std::vector<CompiledTape> ct;
+  {
+    PhaseTimer pt(&c->host_t[0]);
+    ct = compile_dag(dag, lim);
+  }
   return tapes_upload_all(c, dag->n_tapes, ct, out, n_unsup_out);
 }
 
@@ -1643,7 +1693,11 @@ int mq_dag_expand(const mq_dag_batch* dag, int32_t t, mq_node* nodes_out, int64_
 void mq_tapes_free(mq_tapes* t) {
   // the batch's buffers go back to the pool: the launches on the context streams that read them
   // must be done (caller streams: DevPool::mark_foreign)
-  if (t && t->ctx && t->ctx->stream) (void)hipStreamSynchronize(t->ctx->stream);
+  if (!t) return;
+  double* acc = t->ctx ? &t->ctx->host_t[9] : nullptr;
+  double dummy = 0;
+  PhaseTimer pt(acc ? acc : &dummy);
+  if (t->ctx && t->ctx->stream) (void)hipStreamSynchronize(t->ctx->stream);
   delete t;
 }
 
@@ -1967,8 +2021,19 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
   // variables of at most 256 bits those tapes push most often
   const int64_t nq = (int64_t)T->qct.size();
   std::vector<char> on_p(nq, 0);
+  std::unique_ptr<PhaseTimer> pt(new PhaseTimer(&c->host_t[3]));
+  // (P preloads variables 0-7 only: a program pushing any other variable is not tried on P)
+  auto p_candidate = [](const CompiledTape& x) {
+    for (size_t pc = 0; pc < x.prog.size(); pc++) {
+      const uint32_t op = x.prog[pc] & 0xFFu;
+      if ((op == G_PUSH_VAR || op == G_PUSH_VAR_B) && (x.prog[pc] >> 12) >= (uint32_t)kQsaVars) return false;
+      if (op == G_EXTRACT || op == G_CONCAT || op == G_SEXT || op == G_UF1 || op == G_UF2) pc++;
+    }
+    return true;
+  };
   parallel_for(nq, 8, [&](int, int64_t b, int64_t e) {
-    for (int64_t i = b; i < e; i++) on_p[i] = qsa_translate(c, 0, true, T->qct[i], nullptr, nullptr) ? 1 : 0;
+    for (int64_t i = b; i < e; i++)
+      on_p[i] = p_candidate(T->qct[i]) && qsa_translate(c, 0, true, T->qct[i], nullptr, nullptr) ? 1 : 0;
   });
   std::vector<int64_t> pushes(c->var_nl_h.size(), 0);
   for (size_t i = 0; i < T->qct.size(); i++) {
@@ -2008,6 +2073,7 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
   T->qpairs.assign((size_t)QK_COUNT * QK_COUNT, 0);
   T->qpairs_p.assign((size_t)QK_COUNT * QK_COUNT, 0);
   // per-tape translations in parallel (independent; ~50 ns per node), then concatenated in order
+  pt.reset(new PhaseTimer(&c->host_t[4]));
   std::vector<std::vector<uint32_t>> trs(nq);
   std::vector<char> kind_of(nq, 0);
   std::atomic<bool> g_fail{false};
@@ -2037,6 +2103,7 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
   }
   // [P programs | END END | G programs | END END]: the dispatch tail prefetches one word past
   // each program's END
+  pt.reset(new PhaseTimer(&c->host_t[5]));
   std::vector<uint32_t> prog;
   std::vector<GDesc> descs;
   for (int k = 0; k < 2; k++) {
@@ -2314,6 +2381,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       q.prof_out = prof_buffer(c);
       QArgs* dq = T->cqargs.as<QArgs>() + li;
       if (std::memcmp(&T->cqargs_host[li], &q, sizeof(QArgs)) != 0) {
+        PhaseTimer pq(&c->host_t[6]);
         HIPCHK(hipMemcpyAsync(dq, &q, sizeof(QArgs), hipMemcpyHostToDevice, st));
         HIPCHK(hipStreamSynchronize(st));  // q is host memory
         T->cqargs_host[li] = q;
@@ -2389,6 +2457,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     if (k == 1) q.prof_out = prof_buffer(c);
     // the argument block only changes with the output buffer / mode / models: re-upload then
     if (!T->qargs_valid[k] || std::memcmp(&T->qargs_dev_copy[k], &q, sizeof(QArgs)) != 0) {
+      PhaseTimer pq(&c->host_t[6]);
       HIPCHK(hipMemcpyAsync(T->qargs[k].p, &q, sizeof(QArgs), hipMemcpyHostToDevice, st));
       HIPCHK(hipStreamSynchronize(st));  // q is host memory
       T->qargs_dev_copy[k] = q;
@@ -2509,6 +2578,15 @@ int mq_finalize_first_hit(mq_ctx* c, mq_tapes* T, int32_t* d_best, void* stream)
   return MQ_OK;
 }
 
+int mq_host_times(mq_ctx* c, double* out, int32_t max_out, int32_t* n_out, int reset) {
+  if (!c || !n_out || (max_out > 0 && !out)) return MQ_ERR_ARG;
+  *n_out = MQ_HOST_PHASES;
+  for (int i = 0; i < MQ_HOST_PHASES && i < max_out; i++) out[i] = c->host_t[i];
+  if (reset)
+    for (double& x : c->host_t) x = 0;
+  return MQ_OK;
+}
+
 int mq_counters(mq_ctx* c, double* out3, int reset) {
   if (!c || !out3) return MQ_ERR_ARG;
   for (int i = 0; i < 3; i++) out3[i] = 0;
@@ -2598,6 +2676,7 @@ int mq_eval_verdicts(mq_ctx* c, const mq_tape_batch* tb, uint8_t* bits, int32_t*
 // verdict bytes [tape][local model] of ONE device
 static int verdict_bytes_one(mq_ctx* c, mq_tapes* T, std::vector<uint8_t>& host) {
   if (!c->have_models) return MQ_ERR_NO_MODELS;
+  PhaseTimer pt(&c->host_t[7]);   // (includes phases 3-6 of this launch)
   HIPCHK(hipSetDevice(c->device));
   const size_t nbytes = (size_t)T->n_tapes * (size_t)c->M;
   HIPCHK(c->verdict_buf.ensure(std::max<size_t>(nbytes, 1)));

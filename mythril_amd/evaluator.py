@@ -59,6 +59,7 @@ def load_library(path: str = LIB_PATH):
         L.mq_counters.argtypes = [P, C.POINTER(C.c_double), C.c_int]
         L.mq_ctx_set_option.argtypes = [P, C.c_int, C.c_int]
         L.mq_kernel_times.argtypes = [P, C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_int32), C.c_int]
+        L.mq_host_times.argtypes = [P, C.POINTER(C.c_double), C.c_int32, C.POINTER(C.c_int32), C.c_int]
         L.mq_tapes_info.argtypes = [P] + [C.POINTER(C.c_int32)] * 3
         L.mq_tapes_qsa_split.argtypes = [P] + [C.POINTER(C.c_int32)] * 3
         L.mq_tapes_column_split.argtypes = [P] + [C.POINTER(C.c_int32)] * 2
@@ -388,6 +389,16 @@ class Evaluator:
         buf = (C.c_float * max(n.value, 1))()
         _check(self.lib.mq_kernel_times(self.ctx, buf, n.value, C.byref(n), 1 if reset else 0), "mq_kernel_times")
         return [float(buf[i]) for i in range(n.value)]
+
+    HOST_PHASES = ("compile", "translate_upload", "tape_upload", "translate_p", "translate_g", "program_upload",
+                   "args_upload", "launch_readback", "model_upload", "tape_free")
+
+    def host_times(self, reset: bool = True) -> dict:
+        """Host seconds per phase of the library (mq_host_times; diagnostic)."""
+        out = (C.c_double * 16)()
+        n = C.c_int32()
+        _check(self.lib.mq_host_times(self.ctx, out, 16, C.byref(n), 1 if reset else 0), "mq_host_times")
+        return {self.HOST_PHASES[i] if i < len(self.HOST_PHASES) else str(i): float(out[i]) for i in range(n.value)}
 
     def counters(self, reset: bool = False):
         """(pairs evaluated, node-evals, algorithmic ops) accumulated on the device."""

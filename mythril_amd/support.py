@@ -72,11 +72,13 @@ class LRUCache:
     def __init__(self, size: int):
         self.size = size
         self.lru_cache: "OrderedDict" = OrderedDict()
+        self.version = 0   # (not in the reference) bumped when the order or the contents change
 
     def get(self, key):
         if key not in self.lru_cache:
             return -1
         self.lru_cache.move_to_end(key)
+        self.version += 1
         return self.lru_cache[key]
 
     def put(self, key, value) -> None:
@@ -85,6 +87,7 @@ class LRUCache:
         elif len(self.lru_cache) >= self.size:
             self.lru_cache.popitem(last=False)
         self.lru_cache[key] = value
+        self.version += 1
 
 
 class Args(metaclass=Singleton):
@@ -452,8 +455,12 @@ class ModelCache:
     def __init__(self, engine: Optional[VerdictEngine] = None):
         self.model_cache = LRUCache(size=100)
         self.engine = engine or VerdictEngine()
-        # expr -> {model: verdict} for conjunctions evaluated ahead of their check_quick_sat call
+        # expr -> int8 verdict row over model slots (-1: not evaluated yet) for conjunctions
+        # evaluated ahead of their check_quick_sat call, or _UNSUPPORTED
         self._rows: Dict[object, object] = {}
+        self._slot: Dict[int, int] = {}      # id(model) -> slot of the rows above
+        self._slot_model: List[object] = []  # keeps those models (and their ids) alive
+        self._order_v = None                 # (LRU version, MRU-first order, its slots)
         self._pending: "OrderedDict[object, None]" = OrderedDict()
         # the memo of check_quick_sat: functools.lru_cache semantics (a hit moves to MRU, the LRU
         # entry is evicted past MEMO_SIZE, exceptions are not cached), kept as a dict so prefetch
@@ -476,20 +483,44 @@ class ModelCache:
             memo.popitem(last=False)
         return result
 
+    def _order(self):
+        """The candidate order (MRU first, support_utils.py:62) and its row slots, recomputed
+        only when the LRU changed."""
+        lru = self.model_cache
+        if not self._rows and len(self._slot_model) > 4 * lru.size + 256:
+            # no pending row refers to a slot: forget the models that left the cache
+            self._slot, self._slot_model, self._order_v = {}, [], None
+        if self._order_v is None or self._order_v[0] != lru.version or len(self._order_v[1]) != len(lru.lru_cache):
+            order = list(reversed(lru.lru_cache.keys()))
+            self._order_v = (lru.version, order, self._slots_of(order))
+        return self._order_v[1], self._order_v[2]
+
+    def _slots_of(self, models) -> np.ndarray:
+        slot, keep = self._slot, self._slot_model
+        out = np.empty(len(models), np.int64)
+        for i, m in enumerate(models):
+            s = slot.get(id(m))
+            if s is None or keep[s] is not m:
+                s = slot[id(m)] = len(keep)
+                keep.append(m)
+            out[i] = s
+        return out
+
     def _check_quick_sat(self, constraints):
         self.stats["queries"] += 1
-        order = list(reversed(self.model_cache.lru_cache.keys()))
-        row = self._verdicts(constraints, order)
+        order, slots = self._order()
+        row = self._verdicts(constraints, order, slots)
         if row is _UNSUPPORTED:
             self.stats["unsupported"] += 1
             self._record(constraints, order, -2)
             return self._fallback(constraints, order)
-        for i, (model, ok) in enumerate(zip(order, row)):
-            if ok:
-                self._record(constraints, order, i)
-                self.model_cache.put(model, self.model_cache.get(model) + 1)
-                self.stats["hits"] += 1
-                return model
+        i = int(np.argmax(row)) if len(row) else 0
+        if len(row) and row[i]:
+            model = order[i]
+            self._record(constraints, order, i)
+            self.model_cache.put(model, self.model_cache.get(model) + 1)
+            self.stats["hits"] += 1
+            return model
         self._record(constraints, order, -1)
         return False
 
@@ -507,12 +538,12 @@ class ModelCache:
         """Evaluate pending conjunctions against the current cache in one launch (a10).
         Conjunctions the memo already answers never reach the evaluator again: they are skipped."""
         exprs = [e for e in dict.fromkeys(exprs) if e not in self._rows and e not in self._memo]
-        order = list(reversed(self.model_cache.lru_cache.keys()))
+        order, slots = self._order()
         for e in exprs:
-            self._rows[e] = {}
+            self._rows[e] = self._empty_row()
             self._pending[e] = None
         if exprs and order:
-            self._fill(exprs, order)
+            self._fill(exprs, order, slots)
 
     # -------------------------------------------------------------- generated candidates
     def candidates(self, exprs: Sequence) -> list:
@@ -544,7 +575,7 @@ class ModelCache:
         miss = []
         for e in dict.fromkeys(exprs):
             d = self._rows.get(e)
-            if isinstance(d, dict) and d and not any(d.values()) and e not in self._cand:
+            if isinstance(d, np.ndarray) and (d >= 0).any() and not (d > 0).any() and e not in self._cand:
                 miss.append(e)
         for e, r in zip(miss, self.candidates(miss)):
             self._cand[e] = r
@@ -569,8 +600,12 @@ class ModelCache:
         finally:
             self.discard(exprs)
 
-    def _fill(self, exprs: List, models: List) -> None:
+    def _empty_row(self) -> np.ndarray:
+        return np.full(max(len(self._slot_model), 16), -1, np.int8)
+
+    def _fill(self, exprs: List, models: List, slots: np.ndarray) -> None:
         rows = self.engine.rows(exprs, models)
+        n = len(self._slot_model)
         for e, r in zip(exprs, rows):
             d = self._rows[e]
             if d is _UNSUPPORTED:
@@ -578,26 +613,29 @@ class ModelCache:
             if r is None:
                 self._rows[e] = _UNSUPPORTED
                 continue
-            for m, ok in zip(models, r):
-                d[m] = bool(ok)
+            if len(d) < n:
+                d = self._rows[e] = np.concatenate([d, np.full(max(n, 2 * len(d)) - len(d), -1, np.int8)])
+            d[slots] = r
 
-    def _verdicts(self, expr, order):
+    def _verdicts(self, expr, order, slots):
         if expr not in self._rows:
-            self._rows[expr] = {}
+            self._rows[expr] = self._empty_row()
             self._pending[expr] = None
         d = self._rows[expr]
         if d is not _UNSUPPORTED:
-            missing = [m for m in order if m not in d]
-            if missing:
+            got = d[slots] if slots.size and int(slots.max()) < len(d) else None
+            if got is None or (got < 0).any():
                 # evaluate every still-pending conjunction against the new models in one launch
+                known = np.zeros(len(slots), bool) if got is None else got >= 0
+                miss = np.flatnonzero(~known)
                 batch = [expr] + [e for e in self._pending if e is not expr and self._rows.get(e) is not _UNSUPPORTED]
-                self._fill(batch, missing)
+                self._fill(batch, [order[i] for i in miss], slots[miss])
                 d = self._rows[expr]
         self._rows.pop(expr, None)
         self._pending.pop(expr, None)
         if d is _UNSUPPORTED:
             return _UNSUPPORTED
-        return [d[m] for m in order]
+        return d[slots] > 0
 
     def _fallback(self, constraints, order):
         """Unsupported conjunction: the reference's own loop where z3 exists, else no quick answer."""

@@ -458,6 +458,10 @@ def test_c3_hoisted_columns_match_unhoisted_oracle(evaluator, monkeypatch, col_m
     vref = cref.verdicts(plain[0], plain[1])
     v, _ = evaluator.verdicts(ct)
     assert (v == vref).all()
+    # runs of hoisted Bool columns AND-ed into the conjunction are fused (PKBN_A: one wait for
+    # up to four mask loads)
+    hist = ct.handler_histogram(1)
+    assert hist.get("PKBN_A", 0) > 0, hist
     # the same columns on the HIP C++ column kernel
     evaluator.use_asm(False)
     try:

@@ -10,7 +10,7 @@ for ln in open('$1'):
     c = json.loads(ln)
     n = c.get('n_parents')
     tag = ('s%d' % n) if n is not None else ''
-    print(tag, c['n_queries'], c['n_models'], round(c['ms_per_batch'], 3), {k: round(v, 3) for k, v in c['stage_ms'].items()}, 'k', round(c['kernel_ms'], 3), 'cpu1', round(c['cpu_oracle_eval_ms_1thread'], 3), c.get('conjuncts_evaluated', ''), c['answers_match_reference_loop'])"
+    print(tag, c['n_queries'], c['n_models'], round(c['ms_per_batch'], 3), {k: round(v, 3) for k, v in c['stage_ms'].items()}, 'k', round(c['kernel_ms'], 3), 'cpu1', round(c['cpu_oracle_eval_ms_1thread'], 3), c.get('conjuncts_evaluated', ''), c['answers_match_reference_loop']); print('   lib', {k: round(v, 3) for k, v in c.get('library_phase_ms', {}).items() if v > 0.005})"
 }
 i=0
 for V in "$@"; do
