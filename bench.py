@@ -524,6 +524,7 @@ def main():
                 "avg_tape_nodes_unhoisted": float(np.mean(getattr(tb, "unhoisted_nodes", tb.sizes()))),
                 "hoisted_columns": int(tb.columns.n) if getattr(tb, "columns", None) is not None else 0,
                 "column_nodes_per_model": int(tb.columns.programs.sizes().sum()) if getattr(tb, "columns", None) is not None else 0,
+                "keccak_columns": int(ct.keccak_columns()) if getattr(tb, "columns", None) is not None else 0,
                 "parallelism": {"torchrun": f"one process per GPU x{n_gpus}: model-axis shard + torch.distributed RCCL "
                                             f"min-allreduce",
                                 "context": f"one-process context x{n_gpus}: model-axis shard inside mq_models_upload + "

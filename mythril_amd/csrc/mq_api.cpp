@@ -2206,14 +2206,16 @@ static mq_tapes::Variant cut_front(mq_tapes::Variant v, int n) {
 
 // G kernel tape-group size.  Each wave evaluates its group on the 64 models of its workgroup's
 // tile; small groups put many waves on the same tile at once (model rows shared through L1/L2),
-// large ones amortise the per-wave preload of the 8 most pushed variables.  MQ_G_TPG overrides.
+// large ones amortise the per-wave preload of the 8 most pushed variables.  The 4 waves of a
+// workgroup take one group each, so a launch of n <= 64 programs (a column level, a small batch)
+// is cut into 4 groups: min(n, 16) left 3 of 4 waves idle below 16 programs.  MQ_G_TPG overrides.
 static int64_t g_tapes_per_group(int64_t n, int64_t M) {
   (void)M;
   if (const char* e = std::getenv("MQ_G_TPG")) {
     const long v = std::atol(e);
     if (v > 0) return v;
   }
-  return std::min<int64_t>(n, 16);
+  return std::max<int64_t>(1, std::min<int64_t>(16, (n + 3) / 4));
 }
 
 // Launch every evaluation kernel for a compiled batch: the assembly interpreter for the
