@@ -126,16 +126,26 @@ def host_cores():
 
 
 def _timed_first_hit(cref, tb, mb, target_s: float, threads: int):
-    """The first n tapes x all models, n grown until the oracle runs ~target_s."""
-    n = max(4, min(tb.n_tapes, 16))
+    """The first n tapes x the first m models, grown until the oracle runs ~target_s: a short
+    calibration on 4 tapes x <= 4096 models, then all models when the budget allows (else as many
+    as fit) and as many tapes as fit."""
+    n, m = min(tb.n_tapes, 4), min(mb.n_models, 4096)
+    sub = tb.subset(range(n))
+    t0 = time.perf_counter()
+    cref.first_hit(sub, mb.shard(0, m) if m < mb.n_models else mb, nthreads=threads)
+    per_pair = max(time.perf_counter() - t0, 1e-4) / (n * m)
+    m = int(min(mb.n_models, max(m, target_s / per_pair / max(4, min(tb.n_tapes, 16)))))
+    n = int(min(tb.n_tapes, max(4, target_s / per_pair / m)))
     while True:
-        sub = tb.subset(range(n))
+        sub, msub = tb.subset(range(n)), (mb.shard(0, m) if m < mb.n_models else mb)
+        print(f"[cpu_baseline] {n} tapes x {m} models, {threads} threads", file=sys.stderr, flush=True)
         t0 = time.perf_counter()
-        fh, pairs = cref.first_hit(sub, mb, nthreads=threads)
+        fh, pairs = cref.first_hit(sub, msub, nthreads=threads)
         dt = time.perf_counter() - t0
         if dt >= target_s * 0.5 or n >= tb.n_tapes:
             break
         n = min(tb.n_tapes, int(n * max(2.0, target_s / max(dt, 1e-3))))
+    mb = msub
     sizes = sub.sizes()
     # node-evals the oracle performed: the full M for tapes without a hit, first hit + 1 otherwise
     # (cref stops a tape at its first satisfying model, support_utils.py:62-66)
@@ -143,7 +153,7 @@ def _timed_first_hit(cref, tb, mb, target_s: float, threads: int):
     for t in range(sub.n_tapes):
         evals = mb.n_models if fh[t] < 0 else (fh[t] - mb.index_base + 1)
         node_evals += float(evals) * float(sizes[t])
-    return node_evals / dt, n, dt
+    return node_evals / dt, (n, mb.n_models), dt
 
 
 def cpu_baseline(tb, mb, target_s: float):
@@ -156,9 +166,9 @@ def cpu_baseline(tb, mb, target_s: float):
     v_all, n_all, dt_all = _timed_first_hit(cref, tb, mb, target_s * 2 / 3, cores)
     v_one, n_one, dt_one = _timed_first_hit(cref, tb, mb, target_s / 3, 1)
     return {"value": v_all, "unit": "node-evals/s", "cores": cores, "kind": "port",
-            "sample": f"first {n_all} of {tb.n_tapes} tapes x {mb.n_models} models of the same workload, "
-                      f"oracle/cref.c OpenMP over {cores} threads, {dt_all:.1f} s; single core: first {n_one} tapes, "
-                      f"{dt_one:.1f} s",
+            "sample": f"first {n_all[0]} of {tb.n_tapes} tapes x first {n_all[1]} of {mb.n_models} models of the same "
+                      f"workload, oracle/cref.c OpenMP over {cores} threads, {dt_all:.1f} s; single core: first "
+                      f"{n_one[0]} tapes x {n_one[1]} models, {dt_one:.1f} s",
             "single_core_value": v_one, "host": hc, "seconds": dt_all + dt_one}
 
 
