@@ -526,22 +526,27 @@ class IncrementalLowering:
         order: List[S.Term] = []
         seen = set()
         stack = [(root, False)]
+        pop, push, add = stack.pop, stack.append, seen.add
         while stack:
-            t, done = stack.pop()
+            t, done = pop()
             if done:
                 order.append(t)
                 continue
-            if id(t) in seen or id(t) in node:
+            i = id(t)
+            if i in seen or i in node:
                 continue
-            seen.add(id(t))
-            stack.append((t, True))
+            add(i)
+            push((t, True))
             for a in reversed(t.args):
-                if id(a) not in seen and id(a) not in node:
-                    stack.append((a, False))
+                j = id(a)
+                if j not in seen and j not in node:
+                    push((a, False))
+        keep = self._keep
+        get = node.get
         try:
             for t in order:
-                node[id(t)] = _lower_one(t, [node.get(id(x), -1) for x in t.args], tp, syms, node)
-                self._keep[id(t)] = t
+                node[id(t)] = _lower_one(t, [get(id(x), -1) for x in t.args], tp, syms, node)
+                keep[id(t)] = t
         except (LoweringError, TypeError) as e:
             self._bad[id(root)] = root
             raise LoweringError(str(e))

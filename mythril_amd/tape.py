@@ -119,13 +119,13 @@ class Tape:
 
     # ------------------------------------------------------------ internals
     def _add(self, op: Op, width: int, a: int = 0, b: int = 0, c: int = 0, kind: str = "bv") -> int:
-        key = (int(op), width, a, b, c)
+        key = (op.value if isinstance(op, Op) else op, width, a, b, c)
         hit = self._memo.get(key)
         if hit is not None:
             return hit
+        idx = len(self.nodes)
         self.nodes.append(key)
         self.kind.append(kind)
-        idx = len(self.nodes) - 1
         self._memo[key] = idx
         return idx
 

@@ -72,3 +72,29 @@ def test_gpu_get_model_quick_sat_answers():
         assert sp.is_possible_batch([sp.Constraints([x == 4]), sp.Constraints([y == 1, x == 4])]) == [True, True]
     finally:
         sp.reset_caches()
+
+
+def test_gpu_fork_children_reuse_parent_conjuncts():
+    """LASER's fork stream (svm.py:351-358) on EVM-shaped paths: the parents are checked, then
+    their JUMPI successors (parent + cond / parent + Not(cond)).  The children evaluate only the
+    new branch conjuncts on the device (the parents' conjunct rows are cached per model), and every
+    answer and the final LRU order equal the reference loop's (term_eval, independent of the
+    lowering)."""
+    from mythril_amd.synth_evm import dropin_workload, fork_children
+    parents, recs, _ = dropin_workload(12, 60, seed=21)
+    kids = fork_children(parents, seed=5)
+    eng = sp.VerdictEngine()
+    gpu, ref = sp.ModelCache(eng), ReferenceLoopCache()
+    for r in reversed(recs):
+        gpu.put(r, 1)
+        ref.put(r, 1)
+    got = gpu.check_quick_sat_batch(parents)
+    before = dict(eng.stats)
+    got += gpu.check_quick_sat_batch(kids)
+    want = [ref.check_quick_sat(e) for e in parents + kids]
+    assert all((a is False and b is False) or a is b for a, b in zip(got, want))
+    assert list(gpu.model_cache.lru_cache) == list(ref.lru)
+    new = eng.stats["conjuncts_evaluated"] - before["conjuncts_evaluated"]
+    assert 0 < new <= len(kids), new                  # one new branch conjunct per child at most
+    assert eng.stats["conjuncts_cached"] - before["conjuncts_cached"] > 10 * len(parents)
+    assert sum(a is not False for a in got) > 0
