@@ -305,11 +305,11 @@ struct mq_tapes {
   std::vector<uint8_t> cq_bool;
   uint64_t cq_gen = ~0ull;
   bool cq_live = false;
-  int cq_temps = 0;
   DevBuf cqdescs, cqprog, cqconsts, cqargs;
   std::vector<QArgs> cqargs_host;   // what cqargs holds on the device, per level
-  std::vector<int> cq_stage;         // staged rows of the G column programs (as gstage)
-  std::vector<uint32_t> cq_stage_rows;
+  std::vector<uint32_t> cq_stage_rows;                   // staged rows of every level, level by level
+  std::vector<uint32_t> cq_lvl_stage_off, cq_lvl_stage_n;  // per level: its rows in cq_stage_rows
+  std::vector<int> cq_lvl_temps;                         // per level: LDS temp slots
   DevBuf cq_stage_dev;
   // keccak columns (launch_keccak_columns): columns that are exactly keccak(concat of variables
   // and constants); per column its pieces, most significant first (var >= 0: a model variable of
@@ -2153,34 +2153,46 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
   if (T->cq_ct.empty()) return MQ_OK;
   std::vector<uint32_t> prog, consts, tr, extra;
   std::vector<GDesc> descs;
-  int temps = 0;
-  for (const CompiledTape& x : T->cq_ct) temps = std::max(temps, x.n_temps);
-  // (columns run level by level: a workgroup's share is of its level's columns; the batch-wide
-  // share is the conservative estimate)
-  const int64_t n_cq = (int64_t)T->cq_ct.size();
-  const double cq_share = n_cq ? std::min(1.0, 4.0 * (double)g_tapes_per_group(n_cq, c->M) / (double)n_cq) : 1.0;
-  plan_stage(c, count_pushes(c, T->cq_ct), nullptr, temps, cq_share, T->cq_stage, T->cq_stage_rows);
-  temps = 0;
-  for (size_t i = 0; i < T->cq_ct.size(); i++) {
-    const CompiledTape& x = T->cq_ct[i];
-    if (!qsa_translate(c, 1, true, x, &tr, &extra, nullptr, &T->cq_stage)) return MQ_OK;
-    qsa_window_layout(c, tr);
-    qsa_count(c, 1, tr, T->qhist[2], nullptr);
-    const int v = T->cq_var[i];
-    GDesc d{};
-    d.prog_off = (uint32_t)prog.size();
-    d.prog_len = (uint32_t)tr.size();
-    d.tape = c->var_off_h[v];
-    d.const_base = (uint32_t)consts.size();
-    d.n_nodes = x.n_nodes;
-    d.n_temps = c->var_nl_h[v];
-    d.depth = T->cq_bool[i];
-    d.alg_ops = (uint32_t)std::min(x.alg_ops, 4.0e9);
-    prog.insert(prog.end(), tr.begin(), tr.end());
-    consts.insert(consts.end(), x.consts.begin(), x.consts.end());
-    consts.insert(consts.end(), extra.begin(), extra.end());
-    descs.push_back(d);
-    temps = std::max(temps, x.n_temps);
+  // one LDS staging plan per column level: a level's launch stages only the rows its own
+  // programs push (one plan for all levels made every level stage every level's rows)
+  T->cq_stage_rows.clear();
+  T->cq_lvl_stage_off.assign(T->clevels.size(), 0);
+  T->cq_lvl_stage_n.assign(T->clevels.size(), 0);
+  T->cq_lvl_temps.assign(T->clevels.size(), 0);
+  for (size_t li = 0; li < T->clevels.size(); li++) {
+    const int b = T->clevels[li].cq_begin, n = T->clevels[li].v8q;
+    if (n <= 0) continue;
+    const std::vector<CompiledTape> lvl(T->cq_ct.begin() + b, T->cq_ct.begin() + b + n);
+    int temps = 0;
+    for (const CompiledTape& x : lvl) temps = std::max(temps, x.n_temps);
+    const double share = std::min(1.0, 4.0 * (double)g_tapes_per_group(n, c->M) / (double)n);
+    std::vector<int> gstage;
+    std::vector<uint32_t> rows;
+    plan_stage(c, count_pushes(c, lvl), nullptr, temps, share, gstage, rows);
+    T->cq_lvl_stage_off[li] = (uint32_t)T->cq_stage_rows.size();
+    T->cq_lvl_stage_n[li] = (uint32_t)rows.size();
+    T->cq_lvl_temps[li] = temps;
+    T->cq_stage_rows.insert(T->cq_stage_rows.end(), rows.begin(), rows.end());
+    for (int i = b; i < b + n; i++) {
+      const CompiledTape& x = T->cq_ct[i];
+      if (!qsa_translate(c, 1, true, x, &tr, &extra, nullptr, &gstage)) return MQ_OK;
+      qsa_window_layout(c, tr);
+      qsa_count(c, 1, tr, T->qhist[2], nullptr);
+      const int v = T->cq_var[i];
+      GDesc d{};
+      d.prog_off = (uint32_t)prog.size();
+      d.prog_len = (uint32_t)tr.size();
+      d.tape = c->var_off_h[v];
+      d.const_base = (uint32_t)consts.size();
+      d.n_nodes = x.n_nodes;
+      d.n_temps = c->var_nl_h[v];
+      d.depth = T->cq_bool[i];
+      d.alg_ops = (uint32_t)std::min(x.alg_ops, 4.0e9);
+      prog.insert(prog.end(), tr.begin(), tr.end());
+      consts.insert(consts.end(), x.consts.begin(), x.consts.end());
+      consts.insert(consts.end(), extra.begin(), extra.end());
+      descs.push_back(d);
+    }
   }
   const uint32_t endw = hword(1, c->qsa_off[1][c->qsa_index[1][QK_END][0][0]]);
   prog.insert(prog.end(), 130, endw);   // the window + next-window prefetch read up to 127 words past the last END
@@ -2193,7 +2205,6 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
   else HIPCHK(T->cq_stage_dev.upload(T->cq_stage_rows.data(), T->cq_stage_rows.size(), c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   T->cqargs_host.assign(T->clevels.size(), QArgs{});
-  T->cq_temps = temps;
   T->cq_live = true;
   return MQ_OK;
 }
@@ -2368,10 +2379,10 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       q.tapes_per_group = (uint32_t)tpg;
       q.early_exit = 0;
       q.mode = 3;
-      q.lds_wave_bytes = (uint32_t)T->cq_temps * 2048u;
-      q.n_stage = (uint32_t)T->cq_stage_rows.size();
+      q.lds_wave_bytes = (uint32_t)T->cq_lvl_temps[li] * 2048u;
+      q.n_stage = T->cq_lvl_stage_n[li];
       q.stage_base = 4u * q.lds_wave_bytes;
-      q.stage_rows = T->cq_stage_dev.as<uint32_t>();
+      q.stage_rows = T->cq_stage_dev.as<uint32_t>() + T->cq_lvl_stage_off[li];
       for (int j = 0; j < 64; j++) q.var_row[j] = zero_row;
       q.funcs = c->funcs.p;
       q.entry_ptr = c->entry_ptr.p;
