@@ -51,7 +51,8 @@ Segment = Tuple[int, int, int]
 class _BitMaps:
     """Which DAG nodes are one-to-one maps of model-input bits (memoised per node)."""
 
-    def __init__(self, nodes: np.ndarray, consts: np.ndarray):
+    def __init__(self, nodes: np.ndarray, consts: np.ndarray, opaque=frozenset()):
+        self.opaque = opaque   # variables that are not free model inputs (never patched)
         self.op = nodes["op"].astype(np.int64)
         self.w = nodes["width"].astype(np.int64)
         self.a = nodes["a"].astype(np.int64)
@@ -77,7 +78,7 @@ class _BitMaps:
         op, w = int(self.op[n]), int(self.w[n])
         r: Optional[Tuple[Segment, ...]] = None
         fl: Tuple[Tuple[int, int], ...] = ()
-        if op == 2 and w > 0:                                  # VAR
+        if op == 2 and w > 0 and int(self.a[n]) not in self.opaque:   # VAR
             r = ((int(self.a[n]), 0, w),)
         elif op == 1:                                          # CONST
             r = ((-1, self.const_value(n), w),)
@@ -218,7 +219,11 @@ class CandidateGenerator:
     # ------------------------------------------------------------ targets
     def _targets(self, db, syms):
         """Per query: list of (patch-option lists) of its invertible branch conditions."""
-        bm = _BitMaps(db.nodes, db.consts)
+        # a derived variable of a value slice (lower.py _wide_eq) shares its bits with the other
+        # slices of the same function value: patching one alone would split them
+        from .lower import SLICE
+        opaque = frozenset(v for v, (f, _) in syms.derived.items() if SLICE in f)
+        bm = _BitMaps(db.nodes, db.consts, opaque)
         op, a, b = bm.op, bm.a, bm.b
         per_query = []
         for q in range(db.n_tapes):

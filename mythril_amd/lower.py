@@ -73,6 +73,11 @@ class SymbolTable:
             self.var_widths.append(width)
         return i
 
+    def func_slice(self, name: str, arg_widths: Sequence[int], lo: int, hi: int) -> Tuple[int, str]:
+        """The derived function of bits [lo, hi) of ``name``'s values: (id, its name)."""
+        sname = f"{name}{SLICE}{lo}:{hi}"
+        return self.func(sname, arg_widths, hi - lo), sname
+
     def func(self, name: str, arg_widths: Sequence[int], result_width: int) -> int:
         i = self.funcs.get(name)
         spec = FuncSpec(len(arg_widths), result_width, tuple(arg_widths))
@@ -86,6 +91,33 @@ class SymbolTable:
         elif self.func_specs[i] != spec:
             raise LoweringError(f"function {name} used with two signatures")
         return i
+
+
+# "name@@lo:hi" names bits [lo, hi) of model function `name`'s values: a wide equality over a UF
+# result is lowered as equalities of 256-bit slices (_wide_eq), each a lookup in a derived
+# function whose table is the base table with its values sliced (function_interp)
+SLICE = "@@"
+
+
+def split_slice(fname: str) -> Tuple[str, Optional[Tuple[int, int]]]:
+    if SLICE not in fname:
+        return fname, None
+    base, r = fname.rsplit(SLICE, 1)
+    lo, hi = (int(x) for x in r.split(":"))
+    return base, (lo, hi)
+
+
+def function_interp(rec: Model, fname: str):
+    """``(entries, else)`` of model function ``fname`` in ``rec`` (None if absent); a slice name
+    reads the base function's interpretation with its values cut to the slice's bits."""
+    base, sl = split_slice(fname)
+    interp = rec.functions.get(base)
+    if interp is None or sl is None:
+        return interp
+    lo, hi = sl
+    m = (1 << (hi - lo)) - 1
+    table, els = interp
+    return {k: (int(v) >> lo) & m for k, v in table.items()}, (int(els) >> lo) & m
 
 
 def _w(t: S.Term) -> int:
@@ -188,6 +220,10 @@ def _lower_one(t: S.Term, a: List[int], tp: Tape, syms: SymbolTable, node: Dict[
     if k == S.EQ:
         if t.args[0].sort == "array":
             raise LoweringError("array equality")
+        if t.args[0].width > 256:
+            r = _wide_eq(t, tp, syms, node)
+            if r is not None:
+                return r
         return tp.eq(a[0], a[1])
     if k == S.BVULT:
         return tp.ult(a[0], a[1])
@@ -243,6 +279,62 @@ def _lower_one(t: S.Term, a: List[int], tp: Tape, syms: SymbolTable, node: Dict[
             return tp.var(syms.derived_var(name, tuple(x.params[0] for x in t.args), _w(t)), _w(t))
         return tp.uf(fid, t.width, *a)
     raise LoweringError(f"term kind {k!r} not in the tape vocabulary")
+
+
+def _chunk(t: S.Term, lo: int, hi: int, tp: Tape, syms: SymbolTable, node: Dict[int, int]) -> Optional[int]:
+    """Tape node of bits [lo, hi) (<= 256 bits) of the BV term ``t`` built without its full
+    width, or None: constants are cut, concatenations split, a UF result is read through the
+    slice function of its bits.  ``t`` must be a term whose lowering kept its structure (a term
+    cut by hoisting is a variable node: None)."""
+    n = node.get(id(t))
+    if n is None:
+        return None
+    op = tp.nodes[n][0]
+    k = t.kind
+    if k == S.VAL:
+        return tp.const((t.params[0] >> lo) & ((1 << (hi - lo)) - 1), hi - lo)
+    if k == S.CONCAT and op == Op.CONCAT.value:
+        x, y = t.args                       # value = x ++ y (x high)
+        wy = y.width
+        if hi <= wy:
+            return _chunk(y, lo, hi, tp, syms, node)
+        if lo >= wy:
+            return _chunk(x, lo - wy, hi - wy, tp, syms, node)
+        hx, ly = _chunk(x, 0, hi - wy, tp, syms, node), _chunk(y, lo, wy, tp, syms, node)
+        return None if hx is None or ly is None else tp.concat(hx, ly)
+    const_args = all(x.kind == S.VAL for x in t.args)
+    if k == S.APP and t.width > 256 and (op == Op.UF.value or (op == Op.VAR.value and syms.derive and const_args)):
+        name, dom = t.params
+        if syms.interpret_keccak and _is_keccak_uf(name):
+            return None
+        fid, sname = syms.func_slice(name, dom, lo, hi)
+        args = [node.get(id(x)) for x in t.args]
+        if any(x is None for x in args):
+            return None
+        if syms.derive and const_args:
+            return tp.var(syms.derived_var(sname, tuple(x.params[0] for x in t.args), hi - lo), hi - lo)
+        return tp.uf(fid, hi - lo, *args)
+    if t.width <= 256:   # a narrow operand of a split concatenation: itself, or a cut of it
+        return n if hi - lo == t.width else tp.extract(hi - 1, lo, n)
+    return None
+
+
+def _wide_eq(t: S.Term, tp: Tape, syms: SymbolTable, node: Dict[int, int]) -> Optional[int]:
+    """``a == b`` wider than 256 bits as the AND of its 256-bit chunk equalities when both sides
+    split without their full width (_chunk): the keccak axioms' ``keccak256_<n>-1(h) ==
+    key ++ slot`` (keccak_function_manager.py:116-130) then needs no value wider than 256 bits
+    and runs on the 256-bit kernels.  None: lower as one wide equality."""
+    a, b = t.args
+    w = a.width
+    parts = []
+    for lo in range(0, w, 256):
+        hi = min(w, lo + 256)
+        x, y = _chunk(a, lo, hi, tp, syms, node), _chunk(b, lo, hi, tp, syms, node)
+        if x is None or y is None:
+            return None
+        parts.append(tp.eq(x, y))
+    tp.has_dead = True   # the wide operands lowered before it are dead now: finish() prunes them
+    return tp.and_(*parts)
 
 
 def _walk_cut(root: S.Term, cut: Dict[int, int]) -> List[S.Term]:
@@ -440,7 +532,7 @@ def serialize_models(models: Sequence[Model], syms: SymbolTable, index_base: int
         for i, (name, w) in enumerate(names):
             if i in syms.derived:
                 fname, fargs = syms.derived[i]
-                interp = mod.functions.get(fname)
+                interp = function_interp(mod, fname)
                 v = 0 if interp is None else interp[0].get(fargs, interp[1])
             else:
                 v = asg.get(name)
@@ -452,7 +544,7 @@ def serialize_models(models: Sequence[Model], syms: SymbolTable, index_base: int
     for mod in models:
         fm = {}
         for f, name in enumerate(syms.func_names):
-            interp = mod.functions.get(name)
+            interp = function_interp(mod, name)
             if interp is not None:
                 fm[f] = interp
         fmodels.append({"funcs": fm})
@@ -615,7 +707,7 @@ class IncrementalLowering:
         name, w = self._var_names[v]
         if v in self.syms.derived:
             fname, fargs = self.syms.derived[v]
-            interp = rec.functions.get(fname)
+            interp = function_interp(rec, fname)
             val = 0 if interp is None else interp[0].get(fargs, interp[1])
         else:
             val = rec.assignment.get(name)
@@ -680,7 +772,7 @@ class IncrementalLowering:
 
     def _func_table(self, rec: Model, f: int) -> Tuple[np.ndarray, np.ndarray]:
         spec, name = self.syms.func_specs[f], self.syms.func_names[f]
-        interp = rec.functions.get(name)
+        interp = function_interp(rec, name)
         nres = limbs(spec.result_width)
         if interp is None:
             return np.zeros((0, spec.stride), np.uint32), np.zeros(nres, np.uint32)

@@ -31,7 +31,7 @@ from typing import Dict, List, Sequence, Tuple
 import numpy as np
 
 from . import smt as S
-from .lower import SymbolTable, lower_batch, lower_term
+from .lower import SymbolTable, lower_batch, lower_term, split_slice
 from .models import FuncSpec, ModelBatch
 from .tape import TapeBatch, limbs
 
@@ -176,10 +176,16 @@ class EvmModels:
             spec = syms.func_specs[f]
             funcs.append(spec)
             if fname != "balance":
-                t = self.extra_table(fname, spec)
+                base, sl = split_slice(fname)
+                t = self.extra_table(base, spec)
                 if t is None:
                     raise ValueError(f"EvmModels has no table for {fname}")
                 ptr, ent, els = t
+                if sl is not None:   # a slice of the base function's values (lower.py _wide_eq)
+                    kl = sum(limbs(w) for w in spec.arg_widths)
+                    a, b = sl[0] // 32, sl[1] // 32
+                    ent = np.concatenate([ent[..., :kl], ent[..., kl + a:kl + b]], axis=-1)
+                    els = els[..., a:b]
                 ebase.append(wpos)
                 ewords.append(ent.reshape(-1))
                 wpos += ent.size
@@ -450,6 +456,10 @@ class KeccakModels(EvmModels):
         return self._build().get(fname)
 
     def derived_column(self, fname, args, nl, n):
+        base, sl = split_slice(fname)
+        if sl is not None and base in ("keccak256_512", "keccak256_512-1"):
+            full = self.derived_column(base, args, 16 if base.endswith("-1") else 8, n)
+            return np.ascontiguousarray(full[sl[0] // 32:sl[1] // 32][:nl])
         if fname in ("keccak256_512", "keccak256_512-1"):
             ptr, ent, els = self._build()[fname]
             kl = 16 if fname == "keccak256_512" else 8

@@ -163,7 +163,7 @@ class Tape:
                 raise SortError("a column program's root cannot be an array")
         else:
             self._bool(root)
-        if root == len(self.nodes) - 1:
+        if root == len(self.nodes) - 1 and not getattr(self, "has_dead", False):
             return self
         out = Tape()
         remap: Dict[int, int] = {}

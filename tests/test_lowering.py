@@ -228,3 +228,66 @@ def test_address_key_piece_is_not_narrowed():
     assert hoisted and 160 not in hoisted and hoisted.count(256) == 6, widths
 
 
+
+
+def _wide_eq_cases(rng):
+    """Equalities wider than 256 bits of the keccak-axiom shapes (keccak_function_manager.py:
+    116-130: keccak256_<n>-1(h) == key ++ slot) and others, with the models to check them on."""
+    h, x, y, z = (S.BitVecSym(n, 256) for n in ("h", "x", "y", "z"))
+    n8, n100 = S.BitVecSym("n8", 8), S.BitVecSym("n100", 100)
+    inv = S.Function("keccak256_512-1", [256], 512)
+    inv768 = S.Function("keccak256_768-1", [256], 768)
+    c = S.BitVecVal(rng.getrandbits(256), 256)
+    big = S.BitVecVal(rng.getrandbits(512), 512)
+    exprs = [
+        inv(h) == S.Concat(x, c),                       # the axiom shape
+        S.Concat(x, c) == inv(h),
+        inv(h) == big,
+        inv(S.BitVecVal(5, 256)) == S.Concat(x, y),     # constant argument: a derived column
+        inv768(h) == S.Concat(x, y, z),
+        inv(h) == S.Concat(n100, x, S.BitVecSym("n156", 156)),   # chunks straddle the concats
+        S.Concat(n8, x, S.BitVecSym("w248", 248)) == S.Concat(y, S.BitVecSym("w256", 256)),
+        S.Not(inv(h) == S.Concat(x, c)),
+        S.And(inv(h) == S.Concat(x, c), S.ULT(x, y)),
+    ]
+    models = []
+    for _ in range(40):
+        vals = {k: rng.choice([0, 1, 5, rng.getrandbits(256)]) for k in ("h", "x", "y", "z", "w256")}
+        vals["n8"], vals["n100"] = rng.getrandbits(8), rng.getrandbits(100)
+        vals["n156"], vals["w248"] = rng.getrandbits(156), rng.getrandbits(248)
+        pick = rng.random()
+        val = (vals["x"] << 256) | c.params[0] if pick < 0.4 else (big.params[0] if pick < 0.6 else rng.getrandbits(512))
+        t = {(vals["h"],): val, (5,): (vals["x"] << 256) | vals["y"]} if rng.random() < 0.8 else {}
+        t768 = {(vals["h"],): (vals["x"] << 512) | (vals["y"] << 256) | vals["z"]} if rng.random() < 0.5 else {}
+        models.append(Model(vals, {"keccak256_512-1": (t, rng.choice([0, val])),
+                                   "keccak256_768-1": (t768, 0)}))
+    return exprs, models
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_wide_equalities_split_into_256_bit_chunks(seed):
+    """lower.py _wide_eq: an equality over concatenations, constants and UF results wider than 256
+    bits is lowered as 256-bit chunk equalities (UF results read through value-slice functions),
+    so the keccak axioms need no 512-bit value; every verdict equals the independent term
+    evaluator's (tests/term_eval.py) under model completion."""
+    import term_eval
+    rng = random.Random(seed)
+    exprs, models = _wide_eq_cases(rng)
+    tb, syms, ok = lower_batch(exprs)
+    assert ok.all()
+    assert any("@@" in f for f in syms.func_names)
+    for t in range(tb.n_tapes):
+        assert int(tb.tape_nodes(t)["width"].max()) <= 256, t     # no wide value left
+    mb = serialize_models(models, syms)
+    v = cref.verdicts(tb, mb)
+    want = np.array([[term_eval.is_true(e, m) for m in models] for e in exprs])
+    assert (v == want).all(), np.argwhere(v != want)[:5]
+    assert 0 < want.mean() < 1
+
+
+def test_wide_equality_of_opaque_terms_stays_wide():
+    """A side that cannot be split without its full width (here an ite) keeps the wide equality."""
+    x, y = S.BitVecSym("x", 512), S.BitVecSym("y", 512)
+    e = S.If(S.ULT(x, y), x, y) == S.Concat(S.BitVecSym("a", 256), S.BitVecSym("b", 256))
+    tb, syms, ok = lower_batch([e])
+    assert ok.all() and int(tb.tape_nodes(0)["width"].max()) == 512
