@@ -1163,6 +1163,26 @@ def make_handlers(variant, pfx):
                 for c, nw in enumerate(KCLS[1:]):
                     H(("EQVK", x, 2 * v + c), const_words(nw) + eq_const_body(lambda l, _v=v: f"v{VBASE + 8 * _v + l}", nw, B(x)),
                       reads_stack=False)
+        # "push model variable row imm (n limbs) at x; compare it with an inline constant; AND
+        # into B(x - 1)" as one handler (the translator merges PUSH_MEM / PUSH_MEMS + EQK_A): the
+        # value goes to T, never to the stack, and the load wait is the handler's own
+        tl = lambda l: T(l)
+        for x in range(1, D):
+            for n in range(1, L + 1):
+                mem = ["s_mul_i32 s34, s17, s29", "s_mul_hi_u32 s35, s17, s29", "s_lshl_b64 s[34:35], s[34:35], 2",
+                       "s_add_u32 s34, s34, s90", "s_addc_u32 s35, s35, s91"]
+                for l in range(n):
+                    mem.append(f"global_load_dword {T(l)}, v2, s[34:35]")
+                    if l < n - 1:
+                        mem += ["s_add_u32 s34, s34, s74", "s_addc_u32 s35, s35, s75"]
+                lds = ["s_lshl_b32 s34, s17, 8", f"v_add_u32 v5, s34, {STG}"] + \
+                      [f"ds_read_b32 {T(l)}, v5 offset:{256 * l}" for l in range(n)]
+                zero = [f"v_mov_b32 {T(l)}, 0" for l in range(n, L)]
+                for src, load, wait in (("M", mem, "s_waitcnt vmcnt(0)"), ("S", lds, "s_waitcnt lgkmcnt(0)")):
+                    for nw in (2, 8):
+                        H((f"{src}EQK{nw}_A", x, n - 1),
+                          load + zero + const_words(nw) + [wait] + eq_const_body(tl, nw, B(x))
+                          + [f"s_and_b64 {B(x - 1)}, {B(x - 1)}, {B(x)}"], reads_stack=False)
     # ---- (last: these handlers never branch, so the subroutine calls above stay in s_call range)
     # ---- binary ops whose right operand is a preloaded variable (the translator fuses
     # PUSH_VAR v at slot d with the consuming op at d: no stack copy, one dispatch less)
@@ -1455,6 +1475,9 @@ def frame(variant, pfx, handlers, subs):
         "s_add_u32 s96, s64, s68",
         "s_addc_u32 s97, s65, s69",
     ] if G else [])
+    if G:
+        # mode 3 (hoisted column programs) is translated without preloaded variables
+        P += ["s_cmp_eq_u32 s31, 3", f"s_cbranch_scc1 {pfx}_preload_done"]
     if True:
         # preload variables: 64 limb rows (row index table at args+0x60; the host points missing
         # limbs / vars at an all-zero row)
@@ -1467,6 +1490,8 @@ def frame(variant, pfx, handlers, subs):
                       "s_lshl_b64 s[34:35], s[34:35], 2", "s_add_u32 s34, s34, s90", "s_addc_u32 s35, s35, s91",
                       f"global_load_dword v{VBASE + 8 * v + l}, v2, s[34:35]"]
         P += ["s_waitcnt vmcnt(0)"]
+    if G:
+        P += [f"{pfx}_preload_done:"]
     P += ["s_lshl_b32 s74, s29, 2", "s_lshr_b32 s75, s29, 30"]   # M*4 (after the preload's s[64:79] use)
     if G:
         P += stage_rows(pfx)

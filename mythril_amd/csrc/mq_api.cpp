@@ -551,6 +551,8 @@ static int qsa_init(mq_ctx* c) {
     if (base == "EQVK") words = kQsaKClassWords[1 + (v & 1)];
     else if (base == "EQK" || base == "ULTK" || base == "UGTK" || base == "ULEK" || base == "UGEK") words = kQsaKClassWords[v];
     else if (base == "PKBN") words = v;   // the run's other mask indices
+    else if (base == "MEQK2" || base == "SEQK2") words = 2;
+    else if (base == "MEQK8" || base == "SEQK8") words = 8;
     if (words > 0) c->qsa_data_words[hword(1, c->qsa_off[1][h]) & 0xFFFFu] = (uint8_t)words;
   }
   c->qsa_ready = ok && std::getenv("MQ_DISABLE_QSA") == nullptr;
@@ -1046,6 +1048,30 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
     drop_last(2);
     emit_k(QK_PKBN_A, d, n0 + 1, imm0, data);
   };
+  // G: "PUSH_MEM / PUSH_MEMS x (n limbs); EQK_A x" (a model variable compared with an inline
+  // constant, AND-ed into the conjunction) as one M/SEQK{2,8}_A word: row / slot in the
+  // immediate, the constant in 2 or 8 inline data words (a 16-bit immediate constant travels
+  // as two)
+  auto merge_memk = [&]() {
+    if (log.size() < 2) return;
+    const Emit e1 = log.back();
+    if (e1.kind != QK_EQK_A || out.size() != ends_at(e1)) return;
+    const Emit e0 = log[log.size() - 2];
+    if (ends_at(e0) != e1.pos || e0.d != e1.d || e0.nd != 0 || e0.v < 0) return;
+    const bool wide = e1.v == 2;
+    int fk;
+    if (e0.kind == QK_PUSH_MEM) fk = wide ? QK_MEQK8_A : QK_MEQK2_A;
+    else if (e0.kind == QK_PUSH_MEMS) fk = wide ? QK_SEQK8_A : QK_SEQK2_A;
+    else return;
+    if (c->qsa_index[k][fk][e1.d][e0.v + 1] < 0) return;
+    std::vector<uint32_t> data;
+    if (e1.v == 0) data = {e1.imm, 0u};
+    else data.assign(out.begin() + (long)(e1.pos + 1), out.begin() + (long)ends_at(e1));
+    const int x = e1.d, nsel = e0.v;
+    const uint32_t imm0 = e0.imm;
+    drop_last(2);
+    emit_k(fk, x, nsel, imm0, data);
+  };
   uint32_t prev_op = G_END, prev_d = 0, prev_imm = 0;
   size_t prev_out = 0;
   int prev_pre = -1;   // preload slot of the variable the previous instruction pushed
@@ -1185,6 +1211,7 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
       case G_AND:
         ok = fuse_acc(d, true) || word(QK_AND, d, -1, 0);
         if (ok && !P) merge_pkb(d);
+        if (ok && !P) merge_memk();
         break;
       case G_OR: ok = fuse_acc(d, false) || word(QK_OR, d, -1, 0); break;
       case G_XOR: ok = word(QK_XOR, d, -1, 0); break;

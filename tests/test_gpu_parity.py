@@ -462,6 +462,8 @@ def test_c3_hoisted_columns_match_unhoisted_oracle(evaluator, monkeypatch, col_m
     # up to four mask loads)
     hist = ct.handler_histogram(1)
     assert hist.get("PKBN_A", 0) > 0, hist
+    # pushes of a model variable compared with a constant and AND-ed: one M/SEQK*_A handler
+    assert sum(v for k, v in hist.items() if k[1:4] == "EQK" and k[0] in "MS") > 0, hist
     # the same columns on the HIP C++ column kernel
     evaluator.use_asm(False)
     try:
