@@ -73,7 +73,7 @@ PROF = os.environ.get("QSA_PROF") == "1"
 PROF_VGPR = "v70"     # G: LDS address of this wave's profile table
 # profile entries past the handler kinds: the tape frame split at its waits (tape header load,
 # early-exit check, window / run start) and the tape end bookkeeping
-PROF_EXTRA = ("FRAME", "F_HDR", "F_EE", "F_END")
+PROF_EXTRA = ("FRAME", "FRAME_LD", "FRAME3", "FRAME3_LD", "F_HDR", "F_EE", "F_END")
 
 
 def prof_point(kind):
@@ -89,6 +89,18 @@ def prof_point(kind):
             "v_mov_b32 v4, 1",
             f"ds_add_u64 {PROF_VGPR}, v[4:5] offset:@PROF:{kind}:8@",
             "s_mov_b64 exec, s[34:35]"]
+
+
+def frame_prof(pfx):
+    """Profile build: the tape start charged by mode (3 = column programs) and by whether the
+    program's first block was the prefetched successor (FRAME, FRAME3) or loaded (*_LD)."""
+    if not PROF:
+        return []
+    out = ["s_cmp_eq_u32 s31, 3", f"s_cbranch_scc1 {pfx}_fp3", "s_cmp_eq_u32 s39, 1", f"s_cbranch_scc1 {pfx}_fp0s"]
+    out += prof_point("FRAME_LD") + [f"s_branch {pfx}_fpd", f"{pfx}_fp0s:"] + prof_point("FRAME")
+    out += [f"s_branch {pfx}_fpd", f"{pfx}_fp3:", "s_cmp_eq_u32 s39, 1", f"s_cbranch_scc1 {pfx}_fp3s"]
+    out += prof_point("FRAME3_LD") + [f"s_branch {pfx}_fpd", f"{pfx}_fp3s:"] + prof_point("FRAME3") + [f"{pfx}_fpd:"]
+    return out
 
 
 def S(d, l):
@@ -180,7 +192,7 @@ def load_window(first, pfx=None):
     if first:
         out += ["s_add_u32 s34, s14, 256", "s_addc_u32 s35, s15, 0",
                 "s_cmp_eq_u64 s[34:35], s[36:37]",
-                "s_mov_b64 s[14:15], s[36:37]",
+                "s_mov_b64 s[14:15], s[36:37]"] + (["s_cselect_b32 s39, 1, 0"] if PROF else []) + [
                 "s_waitcnt vmcnt(0)",
                 f"s_cbranch_scc1 {pfx}_win_pref",
                 f"global_load_dword {NWIN}, v5, s[14:15]",
@@ -1580,7 +1592,7 @@ def frame(variant, pfx, handlers, subs):
         "s_add_u32 s20, s88, s34",
         "s_addc_u32 s21, s89, 0",
     ] + (["s_lshl_b32 s34, s80, 2", "s_add_u32 s36, s46, s34", "s_addc_u32 s37, s47, 0"]
-         + load_window(True, pfx) + prof_point("FRAME") + NEXT_G if G else [
+         + load_window(True, pfx) + frame_prof(pfx) + NEXT_G if G else [
         "s_mov_b32 s16, 12",
         # the tape end's descriptor words, out of CB (s[80:87]) before the first prefetch
         "s_mov_b32 s78, s84",
