@@ -721,12 +721,9 @@ class IncrementalLowering:
         widths = self.syms.var_widths
         blocks = []
         for v in range(v0, v1):
-            vals = [self._var_value(r, v) for r in recs]
-            nl = limbs(widths[v])
-            blk = np.empty((nl, len(recs)), np.uint32)
-            for l in range(nl):
-                blk[l] = [(x >> (32 * l)) & 0xFFFFFFFF for x in vals]
-            blocks.append(blk)
+            nb = 4 * limbs(widths[v])
+            raw = b"".join(self._var_value(r, v).to_bytes(nb, "little") for r in recs)
+            blocks.append(np.frombuffer(raw, "<u4").reshape(len(recs), nb // 4).T)
         return np.concatenate(blocks, axis=0) if blocks else np.zeros((0, len(recs)), np.uint32)
 
     def _sync_names(self) -> int:
@@ -770,24 +767,35 @@ class IncrementalLowering:
             self._ser_nv = nv
         return out
 
-    def _func_table(self, rec: Model, f: int) -> Tuple[np.ndarray, np.ndarray]:
+    def _func_tables(self, slots: Sequence[int], f: int) -> None:
+        """Serialize function ``f``'s table for the given slots (cached per slot): entries = the
+        arguments' and result's little-endian u32 limbs (``to_words``), else = the result's,
+        built as one byte string for all of them."""
         spec, name = self.syms.func_specs[f], self.syms.func_names[f]
-        interp = function_interp(rec, name)
-        nres = limbs(spec.result_width)
-        if interp is None:
-            return np.zeros((0, spec.stride), np.uint32), np.zeros(nres, np.uint32)
-        table, els = interp
-        rows = []
-        for args, val in table.items():
-            if not isinstance(args, tuple):
-                args = (args,)
-            w = []
-            for aw, av in zip(spec.arg_widths, args):
-                w.extend(to_words(int(av), aw))
-            w.extend(to_words(int(val), spec.result_width))
-            rows.append(w)
-        ent = np.asarray(rows, np.uint32).reshape(-1, spec.stride)
-        return ent, np.asarray(to_words(int(els), spec.result_width), np.uint32)
+        stride, nres = spec.stride, limbs(spec.result_width)
+        fields = [(4 * limbs(w), (1 << max(w, 1)) - 1) for w in list(spec.arg_widths) + [spec.result_width]]
+        rnb, rmask = fields[-1]
+        buf, ebuf, counts = bytearray(), bytearray(), []
+        for s in slots:
+            interp = function_interp(as_record(self._slot_model[s]), name)
+            if interp is None:
+                counts.append(0)
+                ebuf += bytes(rnb)
+                continue
+            table, els = interp
+            counts.append(len(table))
+            for args, val in table.items():
+                if not isinstance(args, tuple):
+                    args = (args,)
+                for (nb, mask), x in zip(fields, list(args) + [val]):
+                    buf += (int(x) & mask).to_bytes(nb, "little")
+            ebuf += (int(els) & rmask).to_bytes(rnb, "little")
+        ent = np.frombuffer(bytes(buf), "<u4").reshape(-1, stride)
+        els_w = np.frombuffer(bytes(ebuf), "<u4").reshape(-1, nres)
+        pos = 0
+        for i, s in enumerate(slots):
+            self._ftabs[s][f] = (ent[pos:pos + counts[i]], els_w[i])
+            pos += counts[i]
 
     def batch_of_slots(self, slots: Sequence[int], index_base: int = 0) -> ModelBatch:
         """The ``mq_model_batch`` of the given slots, in that order, WITHOUT completion (absent:
@@ -804,13 +812,10 @@ class IncrementalLowering:
         ew_chunks, el_chunks = [], []
         wpos = epos = 0
         for f in range(F):
-            tabs = []
-            for s in slots:
-                fc = self._ftabs[s]
-                t = fc.get(f)
-                if t is None:
-                    t = fc[f] = self._func_table(as_record(self._slot_model[s]), f)
-                tabs.append(t)
+            missing = [s for s in dict.fromkeys(slots) if f not in self._ftabs[s]]
+            if missing:
+                self._func_tables(missing, f)
+            tabs = [self._ftabs[s][f] for s in slots]
             counts = np.fromiter((len(t[0]) for t in tabs), np.int64, M)
             eptr[f, 1:] = np.cumsum(counts)
             ebase[f] = wpos

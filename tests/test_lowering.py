@@ -186,6 +186,38 @@ def test_incremental_lowering_shares_the_dag_across_queries():
     assert len(db2.nodes) == n                # nothing new to lower
 
 
+def test_incremental_serialization_matches_whole_batch_serialization():
+    """IncrementalLowering.serialize (rows and function tables cached per model slot, built as
+    byte strings) == serialize_models (the whole-batch form), also after the symbol table grows
+    and for a model order that repeats a model."""
+    from mythril_amd.lower import IncrementalLowering, serialize_models
+    from mythril_amd.synth_evm import dropin_workload
+    warm, recs, _ = dropin_workload(4, 12, seed=5)
+    inc = IncrementalLowering()
+    inc.lower(warm[:1])
+    inc.serialize(recs)
+    exprs, _, _ = dropin_workload(4, 12, seed=5, query_seed=2)
+    inc.lower(list(warm) + list(exprs))             # new variables and functions since the first call
+    for order in (recs, list(reversed(recs)) + recs[:3]):
+        a, b = inc.serialize(order), serialize_models(order, inc.syms)
+        assert (a.var_words == b.var_words).all()
+        assert len(a.funcs) == len(b.funcs) > 0
+        nres = [(f.result_width + 31) // 32 for f in a.funcs]
+        n_entries = 0
+        for f, spec in enumerate(a.funcs):
+            for m in range(len(order)):
+                rows = []
+                for mb in (a, b):
+                    lo, hi = mb.entry_ptr[f, m], mb.entry_ptr[f, m + 1]
+                    base = mb.entry_base[f]
+                    ent = mb.entry_words[base + lo * spec.stride: base + hi * spec.stride]
+                    els = mb.else_words[mb.else_base[f] + m * nres[f]: mb.else_base[f] + (m + 1) * nres[f]]
+                    rows.append((ent.tolist(), els.tolist()))
+                assert rows[0] == rows[1], (f, m)
+                n_entries += len(rows[0][0]) // spec.stride
+        assert n_entries > 0
+
+
 def test_c4_wide_planted_hits_hold_in_the_oracle():
     import cref
     import keccak_ref
