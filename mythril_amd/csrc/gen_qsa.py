@@ -73,7 +73,7 @@ PROF = os.environ.get("QSA_PROF") == "1"
 PROF_VGPR = "v70"     # G: LDS address of this wave's profile table
 # profile entries past the handler kinds: the tape frame split at its waits (tape header load,
 # early-exit check, window / run start) and the tape end bookkeeping
-PROF_EXTRA = ("FRAME", "FRAME_LD", "FRAME3", "FRAME3_LD", "F_HDR", "F_EE", "F_END")
+PROF_EXTRA = ("FRAME", "FRAME_LD", "FRAME3", "FRAME3_LD", "F_HDR", "F_EE", "F_END", "PRELOAD", "STAGE")
 
 
 def prof_point(kind):
@@ -1487,6 +1487,20 @@ def frame(variant, pfx, handlers, subs):
         "s_add_u32 s96, s64, s68",
         "s_addc_u32 s97, s65, s69",
     ] if G else [])
+    if G and PROF:
+        # profile table of this wave, zeroed; the clock starts here (PRELOAD, STAGE: the prologue)
+        P += ["s_load_dwordx2 s[64:65], s[10:11], 0x184",   # n_stage, stage_base
+              "s_waitcnt lgkmcnt(0)",
+              "s_lshl_b32 s64, s64, 8",
+              "s_add_u32 s64, s64, s65",
+              "v_lshrrev_b32 v4, 6, v3",
+              "v_mul_u32_u24 v4, @PROFBYTES@, v4",
+              f"v_add_u32 {PROF_VGPR}, s64, v4",
+              "v_mbcnt_lo_u32_b32 v6, -1, 0", "v_mbcnt_hi_u32_b32 v6, -1, v6", "v_lshlrev_b32 v6, 3, v6",
+              f"v_add_u32 v6, {PROF_VGPR}, v6", "v_mov_b32 v4, 0", "v_mov_b32 v5, 0",
+              "@PROFZERO@",
+              "s_waitcnt lgkmcnt(0)",
+              "s_memtime s[100:101]", "s_waitcnt lgkmcnt(0)"]
     if G:
         # mode 3 (hoisted column programs) is translated without preloaded variables
         P += ["s_cmp_eq_u32 s31, 3", f"s_cbranch_scc1 {pfx}_preload_done"]
@@ -1503,23 +1517,11 @@ def frame(variant, pfx, handlers, subs):
                       f"global_load_dword v{VBASE + 8 * v + l}, v2, s[34:35]"]
         P += ["s_waitcnt vmcnt(0)"]
     if G:
-        P += [f"{pfx}_preload_done:"]
+        P += [f"{pfx}_preload_done:"] + prof_point("PRELOAD")
     P += ["s_lshl_b32 s74, s29, 2", "s_lshr_b32 s75, s29, 30"]   # M*4 (after the preload's s[64:79] use)
     if G:
         P += stage_rows(pfx)
-        if PROF:
-            P += ["s_load_dwordx2 s[64:65], s[10:11], 0x184",   # n_stage, stage_base
-                  "s_waitcnt lgkmcnt(0)",
-                  "s_lshl_b32 s64, s64, 8",
-                  "s_add_u32 s64, s64, s65",
-                  "v_lshrrev_b32 v4, 6, v3",
-                  "v_mul_u32_u24 v4, @PROFBYTES@, v4",
-                  f"v_add_u32 {PROF_VGPR}, s64, v4",
-                  "v_mbcnt_lo_u32_b32 v6, -1, 0", "v_mbcnt_hi_u32_b32 v6, -1, v6", "v_lshlrev_b32 v6, 3, v6",
-                  f"v_add_u32 v6, {PROF_VGPR}, v6", "v_mov_b32 v4, 0", "v_mov_b32 v5, 0",
-                  "@PROFZERO@",
-                  "s_waitcnt lgkmcnt(0)",
-                  "s_memtime s[100:101]", "s_waitcnt lgkmcnt(0)"]
+        P += prof_point("STAGE")
     if G:
         P += ["s_mov_b64 s[14:15], 0"]   # no window yet (load_window's successor test fails)
     ee = G and EEV is not None
@@ -1700,16 +1702,17 @@ def set_layout(variant):
     """Register map of the variant being generated (the body functions read these globals).
     P and G with preloads: the map in the module docstring (G adds the early-exit window v66/v67
     and the decoded program window v68/v69).  Compact G (NVG = 0): UF1 work v[8:31], program
-    window v[32:34], staging address v35, stack v[40:87], T/W v[88:95] -> 96 VGPRs."""
-    global SBASE, TBASE, UBASE, WIN, WINA, WINI, NWIN, STG, NEXT_G, EEA, EEV
+    window v[32:34], staging address v35, next window v36, early-exit window v37/v38 (profile
+    table v39), stack v[40:87], T/W v[88:95] -> 96 VGPRs."""
+    global SBASE, TBASE, UBASE, WIN, WINA, WINI, NWIN, STG, NEXT_G, EEA, EEV, PROF_VGPR
     if variant == "g" and NVG == 0:
         SBASE, TBASE, UBASE = 40, 88, 8
         WIN, WINA, WINI, STG, NWIN = "v32", "v33", "v34", "v35", "v36"
-        EEA = EEV = None
+        EEA, EEV, PROF_VGPR = "v38", "v37", "v39"
     else:
         SBASE, TBASE, UBASE = 72, 120, 40
         WIN, WINA, WINI, STG, NWIN = "v64", "v68", "v69", "v65", "v71"
-        EEA, EEV = "v67", "v66"
+        EEA, EEV, PROF_VGPR = "v67", "v66", "v70"
     NEXT_G = next_g()
 
 
