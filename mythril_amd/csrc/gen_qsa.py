@@ -15,15 +15,18 @@ Two variants are generated from the same handler code (one asm statement each, l
      once per workgroup; PUSH_VAR is a register copy.  C2-shaped batches.
   G ("general", qsg_kernel):  the 4 variables the batch pushes most preloaded, the others
      pushed from the model rows in HBM (PUSH_MEM: the loads are issued by the push and waited
-     for by the first consumer); table-lookup subroutine (UF1); 128 VGPRs so 4 waves per SIMD
-     hide the push latency.  EVM-shaped batches and hoisted column programs (mode 3).
+     for by the first consumer); table-lookup subroutine (UF1).  The product G is the compact
+     layout (NVG = 0, set_layout): no preloaded variables, 96 VGPRs so 5 waves per SIMD hide the
+     push latency (profiles/r03u: C3 26.6 -> 23.8 ms, C4 6.0 -> 5.8 ms, C5 69.1 -> 70.4 ms
+     against the 128-VGPR layout with four preloaded variables).  EVM-shaped batches and hoisted column programs (mode 3).
 
 Register map (both):
   VGPR  v1       LDS temp address (wave base + lane*8)
         v2       model byte offset m*4 (clamped)          v3 sign mask of signed division
         v[4:7]   scratch / MUL accumulator / division step
         v[8:71]  P: preloaded variables V[v][l] = v(8+8v+l), v < 8
-                 G: v[8:39] preloaded variables (v < 4), v[40:63] UF1 work, v64 program window
+                 G with NVG = 4: v[8:39] preloaded variables (v < 4), v[40:63] UF1 work, v64
+                 program window (the compact G map: set_layout)
         v[72:119] operand stack S[d][l] = v(72+8d+l), d < 6 (256-bit values, 8 x u32 limbs)
         v[120:127] MUL column results / division + lookup operand
   SGPR  s[48:59] Bool stack B[d] = s[48+2d : 49+2d] as 64-lane masks (Bool ops are SALU)
@@ -51,7 +54,7 @@ import sys
 
 D = 6          # stack slots
 NV = 8         # preloaded variables (P)
-NVG = 4        # preloaded variables (G); 0 selects the compact G layout (set_layout): 96 VGPRs,
+NVG = 0        # preloaded variables (G); 0 selects the compact G layout (set_layout): 96 VGPRs,
                # 5 waves / SIMD.  4 = v[8:39] preloaded in a 128-VGPR kernel (4 waves / SIMD)
 L = 8          # limbs (256-bit)
 VBASE, SBASE, TBASE = 8, 72, 120
