@@ -13,12 +13,13 @@ Two variants are generated from the same handler code (one asm statement each, l
 
   P ("preload", qsa_kernel):  the wave's 64 models' first 8 variables are preloaded into VGPRs
      once per workgroup; PUSH_VAR is a register copy.  C2-shaped batches.
-  G ("general", qsg_kernel):  the 4 variables the batch pushes most preloaded, the others
-     pushed from the model rows in HBM (PUSH_MEM: the loads are issued by the push and waited
-     for by the first consumer); table-lookup subroutine (UF1).  The product G is the compact
-     layout (NVG = 0, set_layout): no preloaded variables, 96 VGPRs so 5 waves per SIMD hide the
-     push latency (profiles/r03u: C3 26.6 -> 23.8 ms, C4 6.0 -> 5.8 ms, C5 69.1 -> 70.4 ms
-     against the 128-VGPR layout with four preloaded variables).  EVM-shaped batches and hoisted column programs (mode 3).
+  G ("general", qsg_kernel):  variables pushed from the model rows in HBM (PUSH_MEM: the loads
+     are issued by the push and waited for by the first consumer) or from rows staged in LDS;
+     table-lookup subroutine (UF1).  EVM-shaped batches and hoisted column programs (mode 3).
+     The product G is the compact layout (NVG = 0, set_layout): no preloaded variables, 96 VGPRs
+     so 5 waves per SIMD hide the push latency (profiles/r03u: C3 26.6 -> 23.8 ms, C4 6.0 ->
+     5.8 ms, C5 69.1 -> 70.4 ms against the NVG = 4 layout, 128 VGPRs with the 4 variables the
+     batch pushes most preloaded).
 
 Register map (both):
   VGPR  v1       LDS temp address (wave base + lane*8)
@@ -27,8 +28,9 @@ Register map (both):
         v[8:71]  P: preloaded variables V[v][l] = v(8+8v+l), v < 8
                  G with NVG = 4: v[8:39] preloaded variables (v < 4), v[40:63] UF1 work, v64
                  program window (the compact G map: set_layout)
-        v[72:119] operand stack S[d][l] = v(72+8d+l), d < 6 (256-bit values, 8 x u32 limbs)
-        v[120:127] MUL column results / division + lookup operand
+        v[72:119] operand stack S[d][l] = v(72+8d+l), d < 6 (256-bit values, 8 x u32 limbs;
+                 compact G: v[40:87])
+        v[120:127] MUL column results / division + lookup operand (compact G: v[88:95])
   SGPR  s[48:59] Bool stack B[d] = s[48+2d : 49+2d] as 64-lane masks (Bool ops are SALU)
         s[12:13] handler base, s[14:15] program pointer, s16 next word, s17 immediate
         s[74:75] M*4 (model row stride in bytes), s[76:77] subroutine return address,
