@@ -2009,6 +2009,7 @@ static std::vector<int64_t> count_pushes(const mq_ctx* c, const std::vector<Comp
 // (profiles/r02t_*: 40 KB with no such floor sped C3 up and slowed C5, whose groups cover few
 // tapes).  stage_rows is padded to a multiple of 8 with the zero row.
 static int64_t g_tapes_per_group(int64_t n, int64_t M);
+static int64_t cq_tapes_per_group(int64_t n, int64_t M);
 
 static void plan_stage(const mq_ctx* c, const std::vector<int64_t>& pushes, const std::vector<int>* gpre, int temps,
                        double wg_share, std::vector<int>& gstage, std::vector<uint32_t>& rows) {
@@ -2192,7 +2193,7 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
     const std::vector<CompiledTape> lvl(T->cq_ct.begin() + b, T->cq_ct.begin() + b + n);
     int temps = 0;
     for (const CompiledTape& x : lvl) temps = std::max(temps, x.n_temps);
-    const double share = std::min(1.0, 4.0 * (double)g_tapes_per_group(n, c->M) / (double)n);
+    const double share = std::min(1.0, 4.0 * (double)cq_tapes_per_group(n, c->M) / (double)n);
     std::vector<int> gstage;
     std::vector<uint32_t> rows;
     plan_stage(c, count_pushes(c, lvl), nullptr, temps, share, gstage, rows);
@@ -2254,6 +2255,15 @@ static int64_t g_tapes_per_group(int64_t n, int64_t M) {
     if (v > 0) return v;
   }
   return std::max<int64_t>(1, std::min<int64_t>(16, (n + 3) / 4));
+}
+
+// programs per wave of a hoisted-column level launch (mode 3); MQ_CQ_TPG overrides
+static int64_t cq_tapes_per_group(int64_t n, int64_t M) {
+  if (const char* e = std::getenv("MQ_CQ_TPG")) {
+    const long v = std::atol(e);
+    if (v > 0) return v;
+  }
+  return g_tapes_per_group(n, M);
 }
 
 // Launch every evaluation kernel for a compiled batch: the assembly interpreter for the
@@ -2391,7 +2401,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     if (use_cq && lv.v8q > 0) {
       // the level's G columns on qsg_kernel, mode 3 (no preloaded variables)
       const int n = lv.v8q;
-      const int64_t tpg = std::max<int64_t>(1, std::min<int64_t>(g_tapes_per_group(n, c->M), n));
+      const int64_t tpg = std::max<int64_t>(1, std::min<int64_t>(cq_tapes_per_group(n, c->M), n));
       QArgs q{};
       q.descs = T->cqdescs.as<GDesc>() + lv.cq_begin;
       q.prog = T->cqprog.p;
