@@ -43,16 +43,16 @@ WORKLOADS = {
     "c3": (1_000, 1_000_000, 3, "C3 substitute: 10^3 EVM-shaped path conjunctions over 3 txs (calldata bytes/words, "
            "dispatch, SafeMath udiv/urem/smod, shifts, extract/concat/signext, balance table, storage store chains; "
            "~1060 DAG nodes) x 10^6 models per GPU, seed 3, 10% planted",
-           "mq::qsg_kernel (gfx950 assembly interpreter, variables from HBM) + qs_column_kernel<8> (hoisted columns)"),
+           "mq::qsg_kernel (gfx950 assembly interpreter: tapes, and hoisted columns in mode 3)"),
     "c4": (200, 1_000_000, 4, "C4: 200 keccak-heavy token-transfer paths over 2 txs (balances[key] = storage at "
            "keccak256(key ++ slot), store chains, keccak UF axioms of keccak_function_manager) x 10^6 "
            "keccak-consistent models per GPU, keccak256_512 evaluated IN-KERNEL (keccak-f[1600]), seed 4, 10% planted",
-           "mq::qsg_kernel (G tapes + mode-3 columns) + keccak_column_kernel (keccak-f[1600] columns) + "
-           "qs_column_kernel<16> (512-bit columns); whole-step alg ops / kernel time"),
+           "mq::qsg_kernel (G tapes + mode-3 columns) + keccak_column_kernel (keccak-f[1600] columns); "
+           "whole-step alg ops / kernel time"),
     "c5": (256, 1_250_000, 5, "C5: 256 deep EVM-shaped paths over 5 txs (-t 5), 5 ABI words per call, 18-24 checks "
            "per tx (~4090 DAG nodes per conjunction before hoisting) x 1.25*10^6 models per GPU (10^7 over 8 GPUs), "
            "seed 5, 10% planted",
-           "mq::qsg_kernel (gfx950 assembly interpreter, variables from HBM) + qs_column_kernel<8> (hoisted columns)"),
+           "mq::qsg_kernel (gfx950 assembly interpreter: tapes, and hoisted columns in mode 3)"),
 }
 
 
@@ -476,6 +476,17 @@ def main():
         bad = np.flatnonzero(got != expected)
         print(f"[rank {rank}] first-hit mismatch on {len(bad)} tapes, e.g. {bad[:5]}", file=sys.stderr)
 
+    # where the batch ran (after a launch): tapes on the P / G assembly interpreters vs the HIP C++
+    # kernels, hoisted columns on G / the keccak column kernel / the C++ column kernel
+    n_p, n_g, asm_live = ct.asm_split()
+    n_cols = int(getattr(ct, "n_columns", 0))
+    cols_g, cols_live = ct.column_asm_split() if n_cols else (0, False)
+    kcols = int(ct.keccak_columns()) if n_cols else 0
+    kernel_split = {"tapes": tb.n_tapes, "tapes_p": n_p, "tapes_g": n_g,
+                    "tapes_cpp": tb.n_tapes - ((n_p + n_g) if asm_live else 0),
+                    "columns": n_cols, "columns_g": cols_g if cols_live else 0, "columns_keccak": kcols,
+                    "columns_cpp": n_cols - kcols - (cols_g if cols_live else 0)}
+
     ev.counters(reset=True)
     # HIP event pair recorded by libmq on `stream` around the evaluation kernel(s) of each launch
     ev.time_kernels(True)
@@ -553,6 +564,7 @@ def main():
                 "hbm_alg_GBps": hbm_gbs, "hbm_frac": hbm_gbs / HBM_PEAK_GBS,
             },
             "planted_first_hits": {"hits": hits, "tapes": tb.n_tapes},
+            "kernel_split": kernel_split,
             "parity_ok": ok,
             "pairs_evaluated": pairs,
             "nominal_node_evals_per_step": float(tb.sizes().sum()) * M * n_gpus,

@@ -361,6 +361,13 @@ double mq_tape_alg_ops(const mq_tape_batch* batch, int32_t t);
 int mq_tape_compile_info(const mq_tape_batch* batch, int32_t t, int32_t* supported, int32_t* limbs,
                          int32_t* depth, int32_t* n_temps, int32_t* prog_words, char* why, int32_t why_len);
 
+/* Host-only: how tape t compiles for the G assembly interpreter, whose operand stack has fewer
+   slots than the other kernels' (kQsaStackG = 4): *depth_g / *n_temps_g / *prog_words_g of the
+   program G runs (subtrees deeper than its stack spilled to LDS temps; the plain program when it
+   already fits).  Returns 0, MQ_ERR_ARG, or MQ_ERR_TAPE when the tape does not compile. */
+int mq_tape_compile_info_g(const mq_tape_batch* batch, int32_t t, int32_t* depth_g, int32_t* n_temps_g,
+                           int32_t* prog_words_g);
+
 /* Host-only: the compiled stack program of tape t (gprog.h instruction words, G_END last) into
    words[cap]; *n_words = its length (also when cap is too small, then nothing is copied).
    Returns 0, MQ_ERR_ARG, or MQ_ERR_TAPE when the tape does not compile. */

@@ -54,7 +54,10 @@ import os
 import re
 import sys
 
-D = 6          # stack slots
+D = 6          # stack slots of the variant being generated (set_layout: P 6, G DG)
+DP = 6         # P: C2's tapes need 5-6 slots
+DG = 4         # G: 4 slots keep the compact layout at 80 VGPRs = 6 waves per SIMD; the tape
+               # compiler spills deeper subtrees of G programs to LDS temps (tape_compiler.cpp)
 NV = 8         # preloaded variables (P)
 NVG = 0        # preloaded variables (G); 0 selects the compact G layout (set_layout): 96 VGPRs,
                # 5 waves / SIMD.  4 = v[8:39] preloaded in a 128-VGPR kernel (4 waves / SIMD)
@@ -1708,10 +1711,12 @@ def set_layout(variant):
     P and G with preloads: the map in the module docstring (G adds the early-exit window v66/v67
     and the decoded program window v68/v69).  Compact G (NVG = 0): UF1 work v[8:31], program
     window v[32:34], staging address v35, next window v36, early-exit window v37/v38 (profile
-    table v39), stack v[40:87], T/W v[88:95] -> 96 VGPRs."""
-    global SBASE, TBASE, UBASE, WIN, WINA, WINI, NWIN, STG, NEXT_G, EEA, EEV, PROF_VGPR
+    table v39), stack v[40:40+8*DG), T/W after it -> 8 * DG + 48 VGPRs (DG = 4: 80, 6 waves
+    per SIMD)."""
+    global SBASE, TBASE, UBASE, WIN, WINA, WINI, NWIN, STG, NEXT_G, EEA, EEV, PROF_VGPR, D
+    D = DG if variant == "g" else DP
     if variant == "g" and NVG == 0:
-        SBASE, TBASE, UBASE = 40, 88, 8
+        SBASE, TBASE, UBASE = 40, 40 + 8 * DG, 8
         WIN, WINA, WINI, STG, NWIN = "v32", "v33", "v34", "v35", "v36"
         EEA, EEV, PROF_VGPR = "v38", "v37", "v39"
     else:
@@ -1722,7 +1727,7 @@ def set_layout(variant):
 
 
 def vgprs(variant):
-    return 96 if (variant == "g" and NVG == 0) else 128
+    return 48 + 8 * DG if (variant == "g" and NVG == 0) else 128
 
 
 def source_stamp() -> str:
@@ -1776,7 +1781,7 @@ def main():
     with open(os.path.join(HERE, "qsa_table.h"), "w") as f:
         f.write(f"// GENERATED by gen_qsa.py (source {stamp}) — handler enumerations of the QSA interpreters\n")
         f.write("#ifndef MQ_QSA_TABLE_H\n#define MQ_QSA_TABLE_H\nnamespace mq {\n")
-        f.write(f"constexpr int kQsaStack = {D};\nconstexpr int kQsaVars = {NV};\nconstexpr int kQsaVarsG = {NVG};\nconstexpr int kQsaSel = {L};\n")
+        f.write(f"constexpr int kQsaStack = {max(DP, DG)};\nconstexpr int kQsaStackP = {DP};\nconstexpr int kQsaStackG = {DG};\nconstexpr int kQsaVars = {NV};\nconstexpr int kQsaVarsG = {NVG};\nconstexpr int kQsaSel = {L};\n")
         f.write("enum QsaKind {\n" + "".join(f"  QK_{n},\n" for n in names) + "  QK_COUNT\n};\n")
         f.write("static const char* const kQsaKindNames[] = {" + ", ".join(f'"{n}"' for n in names) + "};\n")
         idx = {n: i for i, n in enumerate(names)}

@@ -471,6 +471,21 @@ int mq_tape_compile_info(const mq_tape_batch* tb, int32_t t, int32_t* supported,
   return MQ_OK;
 }
 
+int mq_tape_compile_info_g(const mq_tape_batch* tb, int32_t t, int32_t* depth_g, int32_t* n_temps_g,
+                           int32_t* prog_words_g) {
+  if (!tb || t < 0 || t >= tb->n_tapes) return MQ_ERR_ARG;
+  CompileLimits lim;
+  lim.g_depth = kQsaStackG;
+  lim.value_root = true;   // (a hoisted column program reports like a tape)
+  CompiledTape c = compile_tape(tb, t, lim);
+  if (!c.supported) return MQ_ERR_TAPE;
+  const bool alt = !c.prog_g.empty();
+  if (depth_g) *depth_g = alt ? c.depth_g : c.depth;
+  if (n_temps_g) *n_temps_g = alt ? c.n_temps_g : c.n_temps;
+  if (prog_words_g) *prog_words_g = (int32_t)(alt ? c.prog_g.size() : c.prog.size());
+  return MQ_OK;
+}
+
 int mq_tape_program(const mq_tape_batch* tb, int32_t t, uint32_t* words, int32_t cap, int32_t* n_words) {
   if (!tb || t < 0 || t >= tb->n_tapes || !n_words) return MQ_ERR_ARG;
   CompileLimits lim;
@@ -504,6 +519,7 @@ static int qsa_init(mq_ctx* c) {
   bool ok = true;
   for (int k = 0; k < 2; k++) {
     const int nh = k == 0 ? kQsaHandlersP : kQsaHandlersG;
+    static_assert(kQsaStackP <= kQsaStack && kQsaStackG <= kQsaStack, "qsa_index holds both stacks");
     const QsaHandlerKey* keys = k == 0 ? kQsaHandlerKeysP : kQsaHandlerKeysG;
     for (int q = 0; q < QK_COUNT; q++)
       for (int d = 0; d < kQsaStack; d++)
@@ -887,6 +903,14 @@ static void qsa_count(const mq_ctx* c, int k, const std::vector<uint32_t>& tr, s
   }
 }
 
+// The program the assembly interpreter k runs: G's stack has kQsaStackG slots, so a deeper
+// program runs its spilled variant (tape_compiler.cpp CompiledTape::prog_g).
+static inline const std::vector<uint32_t>& qsa_prog(const CompiledTape& x, int k) {
+  return (k == 1 && !x.prog_g.empty()) ? x.prog_g : x.prog;
+}
+static inline int qsa_temps(const CompiledTape& x, int k) { return (k == 1 && !x.prog_g.empty()) ? x.n_temps_g : x.n_temps; }
+static inline int qsa_depth(const CompiledTape& x, int k) { return (k == 1 && !x.prog_g.empty()) ? x.depth_g : x.depth; }
+
 // Translate a compiled stack program into QSA threaded code for kernel k (0 = P, 1 = G).
 // models == false: structural check only (upload time: variable rows and function tables are
 // not known yet, any variable / lookup is assumed expressible).  extra: the tape's derived
@@ -901,8 +925,9 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
   std::vector<uint32_t>& extra = extra_p ? *extra_p : dummy_extra;
   out.clear();
   extra.clear();
-  if (x.L != 8 || x.depth > kQsaStack) return false;
   const bool P = k == 0;
+  if (x.L != 8 || qsa_depth(x, k) > (P ? kQsaStackP : kQsaStackG) || qsa_temps(x, k) > kQsaMaxTemps) return false;
+  const std::vector<uint32_t>& xprog = qsa_prog(x, k);
   const size_t wpi = P ? 3 : 1;   // program words per interpreter instruction
   // every handler word emitted so far (position, key, immediate, inline data words): the
   // fusions below rewrite the last ones while nothing follows them
@@ -1141,14 +1166,14 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
     }
     return word(kind, d, -1, 0);
   };
-  for (size_t pc = 0; pc < x.prog.size(); pc++) {
-    const uint32_t w = x.prog[pc];
+  for (size_t pc = 0; pc < xprog.size(); pc++) {
+    const uint32_t w = xprog[pc];
     const uint32_t op = w & 0xFFu, imm = w >> 12;
     const int d = (int)((w >> 8) & 0xFu);
     uint32_t imm2 = 0;
     if (op == G_EXTRACT || op == G_CONCAT || op == G_SEXT || op == G_UF1 || op == G_UF2) {
-      if (++pc >= x.prog.size()) return false;
-      imm2 = x.prog[pc];
+      if (++pc >= xprog.size()) return false;
+      imm2 = xprog[pc];
     }
     const size_t out_before = out.size();
     const bool after_const = prev_op == G_PUSH_CONST && (int)prev_d == d;
@@ -1548,6 +1573,7 @@ int mq_tapes_upload(mq_ctx* c, const mq_tape_batch* tb, mq_tapes** out, int32_t*
   }
   // compile once (independent per tape), upload to every device of the context
   CompileLimits lim;
+  lim.g_depth = kQsaStackG;
   std::vector<CompiledTape> ct(tb->n_tapes);
   {
     PhaseTimer pt(&c->host_t[0]);
@@ -1699,6 +1725,7 @@ int mq_tapes_upload_dag(mq_ctx* c, const mq_dag_batch* dag, mq_tapes** out, int3
   for (int t = 0; t < dag->n_tapes; t++)
     if (dag->root_offsets[t + 1] < dag->root_offsets[t]) return MQ_ERR_ARG;
   CompileLimits lim;
+  lim.g_depth = kQsaStackG;
   std::vector<CompiledTape> ct;
   {
     PhaseTimer pt(&c->host_t[0]);
@@ -1788,6 +1815,7 @@ static int set_columns_one(mq_tapes* T, const mq_tape_batch* progs, const int32_
   T->col_width.assign(n_columns, 0);
   if (n_columns == 0) return MQ_OK;
   CompileLimits lim;
+  lim.g_depth = kQsaStackG;
   lim.value_root = true;
   std::vector<CompiledTape> ct(n_columns);
   parallel_for(n_columns, 16, [&](int, int64_t b, int64_t e) {
@@ -2091,7 +2119,7 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
   }
   int g_temps = 0;
   for (size_t i = 0; i < T->qct.size(); i++)
-    if (!on_p[i]) g_temps = std::max(g_temps, T->qct[i].n_temps);
+    if (!on_p[i]) g_temps = std::max(g_temps, qsa_temps(T->qct[i], 1));
   int64_t n_g = 0;
   for (size_t i = 0; i < T->qct.size(); i++) n_g += on_p[i] ? 0 : 1;
   const double g_share = n_g ? std::min(1.0, 4.0 * (double)g_tapes_per_group(n_g, c->M) / (double)n_g) : 1.0;
@@ -2127,7 +2155,7 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
     d.prog_len = (uint32_t)t.size();
     words[k].insert(words[k].end(), t.begin(), t.end());
     ds[k].push_back(d);
-    temps[k] = std::max(temps[k], T->qct[i].n_temps);
+    temps[k] = std::max(temps[k], qsa_temps(T->qct[i], k));
   }
   // [P programs | END END | G programs | END END]: the dispatch tail prefetches one word past
   // each program's END
@@ -2192,7 +2220,7 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
     if (n <= 0) continue;
     const std::vector<CompiledTape> lvl(T->cq_ct.begin() + b, T->cq_ct.begin() + b + n);
     int temps = 0;
-    for (const CompiledTape& x : lvl) temps = std::max(temps, x.n_temps);
+    for (const CompiledTape& x : lvl) temps = std::max(temps, qsa_temps(x, 1));
     const double share = std::min(1.0, 4.0 * (double)cq_tapes_per_group(n, c->M) / (double)n);
     std::vector<int> gstage;
     std::vector<uint32_t> rows;

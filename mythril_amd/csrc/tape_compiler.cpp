@@ -317,8 +317,11 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
         }
       }
     }
+    // Phases 3-4 as one function of the spill limit: spill > 0 additionally hoists subtrees into
+    // temps until every unit needs at most `spill` stack slots (Sethi-Ullman order; the G
+    // assembly interpreter has kQsaStackG slots, the P / C++ kernels more).
+    auto build = [&](int spill, std::vector<uint32_t>& prog, int& depth_out, int& temps_out) {
     std::vector<char> hoist(NI, 0);
-    std::vector<int> units;  // hoisted nodes in topological (index) order, then root
     // Rematerialisation: a shared node whose expression is tiny and cheap (a calldata byte
     // `ite(slt(i, size), cd_i, 0)`, a masked extract) is re-evaluated at each use instead of
     // occupying a temp slot: temps cost 2 KB per wave and their count bounds what compiles.
@@ -339,19 +342,17 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
         if (!B.nodes[kid].leaf && !hoist[kid]) c += remat_cost[kid];
       }
       remat_cost[x] = c;
-      if (x != root && uses[x] > 1 && c > lim.remat_max_nodes) {
-        hoist[x] = 1;
-        units.push_back(x);
-      }
+      if (x != root && uses[x] > 1 && c > lim.remat_max_nodes) hoist[x] = 1;
     }
-    units.push_back(root);
 
     // stack need with hoisted nodes as leaves (Sethi-Ullman)
     std::vector<int> need(NI, 1);
     std::vector<char> swap(NI, 0);
+    auto compute_need = [&]() {
     for (int x = 0; x < NI; x++) {
       if (!live[x]) continue;
       const INode& n = B.nodes[x];
+      swap[x] = 0;
       auto nd_of = [&](int c) { return (hoist[c] || B.nodes[c].leaf) ? 1 : need[c]; };
       if (n.leaf || n.nk == 0) need[x] = 1;
       else if (n.nk == 1) need[x] = nd_of(n.kid[0]);
@@ -380,6 +381,33 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
         }
       }
     }
+    };
+    compute_need();
+    if (spill > 0) {
+      // the lowest (first in topological order) unit node needing more than `spill` slots has
+      // kids that each fit: hoist its deepest kid into a temp, recompute, repeat.  (With
+      // spill >= 3 such a node always has a non-leaf kid: all-leaf operands need <= 3 slots.)
+      for (;;) {
+        int bad = -1;
+        for (int x = 0; x < NI && bad < 0; x++)
+          if (live[x] && !B.nodes[x].leaf && need[x] > spill) bad = x;
+        if (bad < 0) break;
+        const INode& n = B.nodes[bad];
+        int best = -1;
+        for (int k = 0; k < n.nk; k++) {
+          const int c = n.kid[k];
+          if (hoist[c] || B.nodes[c].leaf) continue;
+          if (best < 0 || need[c] > need[best]) best = c;
+        }
+        if (best < 0) throw Fail{"cannot spill"};
+        hoist[best] = 1;
+        compute_need();
+      }
+    }
+    std::vector<int> units;  // hoisted nodes in topological (index) order, then root
+    for (int x = 0; x < NI; x++)
+      if (live[x] && hoist[x] && x != root) units.push_back(x);
+    units.push_back(root);
 
     // temp slot allocation with reuse after last use
     std::vector<int> unit_of_last_use(NI, -1);
@@ -387,7 +415,6 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
     for (size_t u = 0; u < units.size(); u++) {
       // temps referenced by unit u: hoisted nodes reachable from units[u] without crossing hoisted nodes
       std::vector<int> st;
-      std::vector<char> seen;
       int top = units[u];
       for (int k = 0; k < B.nodes[top].nk; k++) st.push_back(B.nodes[top].kid[k]);
       std::unordered_map<int, char> vis;
@@ -415,11 +442,11 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
       maxd = std::max(maxd, d + 1);
       const INode& n = B.nodes[x];
       if (hoist[x] && slot[x] >= 0) {
-        out.prog.push_back(gword(n.width == 0 ? G_PUSH_TMP_B : G_PUSH_TMP, d, slot[x]));
+        prog.push_back(gword(n.width == 0 ? G_PUSH_TMP_B : G_PUSH_TMP, d, slot[x]));
         return;
       }
       if (n.leaf) {
-        out.prog.push_back(gword(n.gop, d, n.imm));
+        prog.push_back(gword(n.gop, d, n.imm));
         return;
       }
       uint32_t g = n.gop;
@@ -449,8 +476,8 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
         d += 2;
       }
       if (n.imm > (uint32_t)kMaxImm) throw Fail{"immediate too large"};
-      out.prog.push_back(gword(g, d, n.imm));
-      if (g == G_EXTRACT || g == G_CONCAT || g == G_SEXT || g == G_UF1 || g == G_UF2) out.prog.push_back(n.imm2);
+      prog.push_back(gword(g, d, n.imm));
+      if (g == G_EXTRACT || g == G_CONCAT || g == G_SEXT || g == G_UF1 || g == G_UF2) prog.push_back(n.imm2);
     };
     for (size_t u = 0; u < units.size(); u++) {
       int x = units[u];
@@ -467,18 +494,32 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
           s = n_slots++;
         }
         slot[x] = s;
-        out.prog.push_back(gword(B.nodes[x].width == 0 ? G_STORE_TMP_B : G_STORE_TMP, 0, s));
+        prog.push_back(gword(B.nodes[x].width == 0 ? G_STORE_TMP_B : G_STORE_TMP, 0, s));
       }
     }
     if (n_slots > max_temps) throw Fail{"too many temps"};
-    out.prog.push_back(gword(G_END, 0, 0));
-    out.depth = maxd;
-    out.n_temps = n_slots;
+    prog.push_back(gword(G_END, 0, 0));
+    depth_out = maxd;
+    temps_out = n_slots;
+    };
+    build(0, out.prog, out.depth, out.n_temps);
+    // the G assembly interpreter's stack is shallower: a spilled variant for it (a failure only
+    // leaves the tape to the other kernels)
+    if (lim.g_depth > 0 && out.depth > lim.g_depth) {
+      try {
+        build(lim.g_depth, out.prog_g, out.depth_g, out.n_temps_g);
+      } catch (const Fail&) {
+        out.prog_g.clear();
+        out.depth_g = 0;
+        out.n_temps_g = 0;
+      }
+    }
     out.supported = true;
   } catch (const Fail& f) {
     out.supported = false;
     out.why = f.why;
     out.prog.clear();
+    out.prog_g.clear();
     out.consts.clear();
   }
   out.alg_ops = tape_alg_ops(batch, t);

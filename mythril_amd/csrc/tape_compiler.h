@@ -24,6 +24,11 @@ struct CompiledTape {
   int n_temps = 0;               // LDS temp slots
   std::vector<uint32_t> prog;    // instruction words, terminated by G_END
   std::vector<uint32_t> consts;  // L-limb padded constants (PUSH_CONST imm indexes this)
+  // the program again for the G assembly interpreter (CompileLimits::g_depth slots) when prog
+  // needs more: deeper subtrees spilled to temps; empty when prog fits (or spilling failed)
+  std::vector<uint32_t> prog_g;
+  int depth_g = 0;
+  int n_temps_g = 0;
   uint32_t n_nodes = 0;          // DAG size of the boundary tape (metric)
   double alg_ops = 0;            // SURVEY §8(d) algorithmic cost per model
 };
@@ -42,6 +47,7 @@ struct CompileLimits {
   int max_temps_l32 = 32;
   int max_temps_l64 = 32;
   int remat_max_nodes = 3;    // shared sub-terms up to this many cheap nodes are re-evaluated
+  int g_depth = 0;            // > 0: also build prog_g for a stack of this many slots
   bool value_root = false;    // column program: any BV/Bool root, its value is the result
 };
 

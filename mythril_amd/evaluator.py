@@ -76,6 +76,7 @@ def load_library(path: str = LIB_PATH):
         L.mq_tape_alg_ops.argtypes = [C.POINTER(MqTapeBatch), C.c_int32]
         L.mq_tape_alg_ops.restype = C.c_double
         L.mq_tape_compile_info.argtypes = [C.POINTER(MqTapeBatch), C.c_int32] + [C.POINTER(C.c_int32)] * 5 + [C.c_char_p, C.c_int32]
+        L.mq_tape_compile_info_g.argtypes = [C.POINTER(MqTapeBatch), C.c_int32] + [C.POINTER(C.c_int32)] * 3
         L.mq_tape_program.argtypes = [C.POINTER(MqTapeBatch), C.c_int32, C.POINTER(C.c_uint32), C.c_int32, C.POINTER(C.c_int32)]
         L.mq_tapes_upload_dag.argtypes = [P, C.POINTER(MqDagBatch), C.POINTER(P), C.POINTER(C.c_int32)]
         L.mq_dag_expand.argtypes = [C.POINTER(MqDagBatch), C.c_int32, P, C.c_int64, C.POINTER(C.c_int64)]
@@ -120,6 +121,16 @@ def compile_info(tb: TapeBatch, t: int) -> CompileInfo:
     why = C.create_string_buffer(256)
     _check(L.mq_tape_compile_info(C.byref(s), t, *[C.byref(v) for v in vals], why, 256), "compile_info")
     return CompileInfo(bool(vals[0].value), vals[1].value, vals[2].value, vals[3].value, vals[4].value, why.value.decode())
+
+
+def compile_info_g(tb: TapeBatch, t: int):
+    """Host-only: (depth, LDS temps, program words) of the program the G assembly interpreter
+    runs for tape t (mq_tape_compile_info_g: subtrees deeper than its stack spilled to temps)."""
+    L = load_library()
+    s, keep = as_tape_batch(tb)
+    vals = [C.c_int32() for _ in range(3)]
+    _check(L.mq_tape_compile_info_g(C.byref(s), t, *[C.byref(v) for v in vals]), "compile_info_g")
+    return tuple(v.value for v in vals)
 
 
 def tape_program(tb: TapeBatch, t: int) -> np.ndarray:

@@ -46,7 +46,10 @@ def test_interpreter_registers_stay_inside_the_declared_allocation(variant):
 
 
 def test_product_g_is_the_compact_layout():
-    """The product G kernel fits 96 VGPRs (5 waves per SIMD); P keeps 128."""
+    """The product G kernel fits 80 VGPRs (a 4-slot operand stack: 6 waves per SIMD, DESIGN
+    §3.2); P keeps 128 and its 6-slot stack."""
     t = _texts()
-    assert max(_regs(t["G"][0], "v")) < 96
+    assert max(_regs(t["G"][0], "v")) < 80
     assert max(_regs(t["P"][0], "v")) < 128
+    assert not re.search(r"; \S+ [4-9]\b", "\n".join(ln for ln in t["G"][0].splitlines() if ln.startswith(".Lqsg_h"))), \
+        "G handlers exist only for stack slots 0-3"
