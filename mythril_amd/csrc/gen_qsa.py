@@ -1311,8 +1311,12 @@ def make_handlers(variant, pfx):
 def store_column(pfx):
     """G mode 3 (hoisted column programs, mq_api.cpp cq_prepare): write the program's value into
     the model variable rows of the column, valid lanes only.  Descriptor: s82 = first row of the
-    target variable, s85 = its limbs, s86 = 1 for a Bool root (B(0) stored as 0/1).  A column is
-    not a (tape, model) pair: the pair count the tape end added is taken back."""
+    target variable, s85 = its limbs, s86 = 0 for a BV root, else 1 | (j + 1) << 1 for a Bool
+    root whose packed lane-mask index is j (j + 1 = 0: none).  A Bool root's valid-lane mask
+    B(0) goes straight to the tile's packed masks (s[96:97] + 8 j; one 8-byte vector store by
+    lane 0, so no qs_pack_bool pass reads the rows back); its 0/1 row is written only when
+    QArgs.bool_rows asks for it (a HIP C++ kernel of the launch reads rows).  A column is not a
+    (tape, model) pair: the pair count the tape end added is taken back."""
     out = [f"{pfx}_store_column:",
            "s_sub_u32 s40, s40, s38", "s_subb_u32 s41, s41, 0",
            VMWAIT,
@@ -1320,6 +1324,21 @@ def store_column(pfx):
            "s_add_u32 s38, s38, s90", "s_addc_u32 s39, s39, s91",
            "s_mov_b64 s[60:61], exec", "s_mov_b64 exec, s[62:63]",
            "s_cmp_eq_u32 s86, 0", f"s_cbranch_scc1 {pfx}_col_value",
+           "s_lshr_b32 s36, s86, 1",
+           "s_cmp_eq_u32 s36, 0",
+           f"s_cbranch_scc1 {pfx}_col_row",
+           "s_lshl_b32 s36, s36, 3",
+           "s_sub_u32 s36, s36, 8",
+           f"s_and_b64 s[34:35], {B(0)}, s[62:63]",
+           "s_mov_b64 exec, 1",
+           "v_mov_b32 v6, s36", "v_mov_b32 v4, s34", "v_mov_b32 v5, s35",
+           "global_store_dwordx2 v6, v[4:5], s[96:97]",
+           "s_mov_b64 exec, s[62:63]",
+           "s_load_dword s36, s[10:11], 0x18c",        # QArgs.bool_rows
+           "s_waitcnt lgkmcnt(0)",
+           "s_cmp_eq_u32 s36, 0",
+           f"s_cbranch_scc1 {pfx}_col_done",
+           f"{pfx}_col_row:",
            f"v_cndmask_b32_e64 v5, 0, 1, {B(0)}",
            "global_store_dword v2, v5, s[38:39]",
            f"s_branch {pfx}_col_done",

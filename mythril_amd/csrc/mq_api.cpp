@@ -298,6 +298,10 @@ struct mq_tapes {
   // per column level: mask indices of its Bool columns, repacked after the level ran
   std::vector<std::vector<int32_t>> lvl_bmask_h;
   std::vector<DevBuf> lvl_bmask;
+  // the same for the Bool columns NOT on the G column path (when it runs, G stores its Bool
+  // columns' masks itself: gen_qsa.py store_column)
+  std::vector<std::vector<int32_t>> lvl_bmask_cpp_h;
+  std::vector<DevBuf> lvl_bmask_cpp;
   uint64_t bmask_gen = ~0ull;
   DevBuf cdescs, cprog, cconsts;
   std::vector<CompiledTape> cq_ct;   // the G-eligible columns, level by level
@@ -2030,8 +2034,10 @@ static std::vector<int64_t> count_pushes(const mq_ctx* c, const std::vector<Comp
 
 // G kernel LDS staging plan: the most pushed variables (not preloaded) whose rows fit the
 // workgroup's staging budget get consecutive LDS slots (gen_qsa.py stage_rows); their pushes
-// become LDS reads.  Budget: MQ_G_STAGE_KB (default 40: four workgroups of 4 waves still fit a
-// CU's 160 KB) KB per workgroup minus the temps of its 4 waves.  Every workgroup loads its rows
+// become LDS reads.  Budget: MQ_G_STAGE_KB (default 26: the 80-VGPR G runs 6 waves per SIMD =
+// 6 workgroups of 4 waves per CU, and 6 x 26 KB fit the CU's 160 KB; 40 KB, the budget of the
+// 5-wave layout, capped C5 at 4 workgroups per CU: 70.5 vs 61.6 ms, profiles/r04c) KB per
+// workgroup minus the temps of its 4 waves.  Every workgroup loads its rows
 // once, so a variable is staged only when the workgroup's tapes (wg_share of the batch's
 // programs) push it at least MQ_G_STAGE_MIN (default 1.5) times on average
 // (profiles/r02t_*: 40 KB with no such floor sped C3 up and slowed C5, whose groups cover few
@@ -2041,7 +2047,7 @@ static int64_t cq_tapes_per_group(int64_t n, int64_t M);
 
 static void plan_stage(const mq_ctx* c, const std::vector<int64_t>& pushes, const std::vector<int>* gpre, int temps,
                        double wg_share, std::vector<int>& gstage, std::vector<uint32_t>& rows) {
-  int64_t kb = 40;
+  int64_t kb = 26;
   if (const char* e = std::getenv("MQ_G_STAGE_KB")) kb = std::atol(e);
   double min_pushes = 1.5;
   if (const char* e = std::getenv("MQ_G_STAGE_MIN")) min_pushes = std::atof(e);
@@ -2242,7 +2248,8 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
       d.const_base = (uint32_t)consts.size();
       d.n_nodes = x.n_nodes;
       d.n_temps = c->var_nl_h[v];
-      d.depth = T->cq_bool[i];
+      // Bool root: bit 0, and the packed lane-mask index + 1 above it (store_column)
+      d.depth = T->cq_bool[i] ? 1u | ((uint32_t)(v < (int)c->bmask_of_var.size() ? c->bmask_of_var[v] + 1 : 0) << 1) : 0u;
       d.alg_ops = (uint32_t)std::min(x.alg_ops, 4.0e9);
       prog.insert(prog.end(), tr.begin(), tr.end());
       consts.insert(consts.end(), x.consts.begin(), x.consts.end());
@@ -2373,16 +2380,26 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
   if (T->bmask_gen != c->models_gen) {
     // the mask indices of each level's Bool columns under this model batch
     T->lvl_bmask_h.assign(T->clevels.size(), {});
+    T->lvl_bmask_cpp_h.assign(T->clevels.size(), {});
+    std::vector<char> on_g(c->n_vars, 0);
+    for (int v : T->cq_var)
+      if (v >= 0 && v < c->n_vars) on_g[v] = 1;
     for (size_t i = 0; i < T->col_var.size(); i++) {
       const int v = T->col_var[i];
       if (T->col_width[i] == 0 && v < (int)c->bmask_of_var.size() && c->bmask_of_var[v] >= 0 &&
-          T->col_level[i] < (int)T->clevels.size())
+          T->col_level[i] < (int)T->clevels.size()) {
         T->lvl_bmask_h[T->col_level[i]].push_back(c->bmask_of_var[v]);
+        if (!on_g[v]) T->lvl_bmask_cpp_h[T->col_level[i]].push_back(c->bmask_of_var[v]);
+      }
     }
     T->lvl_bmask.resize(T->clevels.size());
-    for (size_t li = 0; li < T->clevels.size(); li++)
+    T->lvl_bmask_cpp.resize(T->clevels.size());
+    for (size_t li = 0; li < T->clevels.size(); li++) {
       if (!T->lvl_bmask_h[li].empty())
         HIPCHK(T->lvl_bmask[li].upload(T->lvl_bmask_h[li].data(), T->lvl_bmask_h[li].size(), st));
+      if (!T->lvl_bmask_cpp_h[li].empty())
+        HIPCHK(T->lvl_bmask_cpp[li].upload(T->lvl_bmask_cpp_h[li].data(), T->lvl_bmask_cpp_h[li].size(), st));
+    }
     HIPCHK(hipStreamSynchronize(st));
     T->bmask_gen = c->models_gen;
   }
@@ -2417,6 +2434,16 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     HIPCHK(hipStreamSynchronize(st));
     T->kc_gen = c->models_gen;
   }
+  // Bool columns' 0/1 rows are read only by the HIP C++ kernels (the assembly interpreters read
+  // the packed lane masks, which G's column store writes itself): G writes the rows only when a
+  // C++ tape or column kernel, or P (rows of preloaded variables), runs in this launch
+  bool bool_rows = !use_qsa || T->q_count[0] > 0;
+  for (int g = 0; g < kGen && !bool_rows; g++) bool_rows = cpp[g].count > 0;
+  for (size_t li = 0; li < T->clevels.size() && !bool_rows; li++) {
+    const auto& lv = T->clevels[li];
+    for (int g = 0; g < kGen && !bool_rows; g++)
+      bool_rows = (g == 0 ? (use_cq ? lv.v[0].count - lv.v8q : lv.v[0].count) : lv.v[g].count) > 0;
+  }
   for (size_t li = 0; li < T->clevels.size(); li++) {
     const auto& lv = T->clevels[li];
     if (li < T->kc_level.size() && T->kc_level[li].second > 0) {
@@ -2444,6 +2471,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       q.tapes_per_group = (uint32_t)tpg;
       q.early_exit = 0;
       q.mode = 3;
+      q.bool_rows = bool_rows ? 1u : 0u;
       q.lds_wave_bytes = (uint32_t)T->cq_lvl_temps[li] * 2048u;
       q.n_stage = T->cq_lvl_stage_n[li];
       q.stage_base = 4u * q.lds_wave_bytes;
@@ -2486,11 +2514,14 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       HIPCHK(start_timer());
       HIPCHK(launch_columns(a, v->L, v->keccak, st));
     }
-    // the level's Bool columns as lane masks, for the levels and tapes after it
-    if (!T->lvl_bmask_h[li].empty()) {
+    // the level's Bool columns as lane masks, for the levels and tapes after it (those G
+    // computed are stored as masks already)
+    const auto& pk_h = use_cq ? T->lvl_bmask_cpp_h[li] : T->lvl_bmask_h[li];
+    if (!pk_h.empty()) {
       HIPCHK(start_timer());
       HIPCHK(launch_pack_bool(c->vars.as<uint32_t>(), c->bmasks.as<uint64_t>(), c->bmask_rows.as<uint32_t>(),
-                              T->lvl_bmask[li].as<int32_t>(), (int)T->lvl_bmask_h[li].size(), c->n_bmask, c->M, st));
+                              (use_cq ? T->lvl_bmask_cpp[li] : T->lvl_bmask[li]).as<int32_t>(), (int)pk_h.size(),
+                              c->n_bmask, c->M, st));
     }
   }
   for (int k = 0; use_qsa && k < 2; k++) {

@@ -84,7 +84,7 @@ struct QArgs {
   uint32_t n_funcs;              // 0x180
   uint32_t n_stage;              // 0x184 G: model rows staged in LDS per workgroup (multiple of 8)
   uint32_t stage_base;           // 0x188 G: LDS byte offset of the staged rows
-  uint32_t pad2;                 // 0x18c
+  uint32_t bool_rows;            // 0x18c G mode 3: also write Bool columns' 0/1 rows (a C++ kernel reads them)
   const uint32_t* stage_rows;    // 0x190 G: global row of each staged slot
   const uint64_t* bool_masks;    // 0x198 G: packed Bool rows, [tile][n_bool_masks] lane masks
   uint32_t n_bool_masks;         // 0x1a0
@@ -97,6 +97,7 @@ static_assert(__builtin_offsetof(QArgs, var_row) == 0x60, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, funcs) == 0x160, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, n_funcs) == 0x180, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, n_stage) == 0x184, "QArgs layout");
+static_assert(__builtin_offsetof(QArgs, bool_rows) == 0x18c, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, stage_rows) == 0x190, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, bool_masks) == 0x198, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, n_bool_masks) == 0x1a0, "QArgs layout");
