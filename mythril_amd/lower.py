@@ -365,6 +365,8 @@ _LEAVES = frozenset({S.SYM, S.VAL, S.TRUE, S.FALSE, S.ARRAY_SYM})
 # trip each (~12 dispatches of work on the G kernel, profiles/r02s_profile_c3.txt), so a lookup
 # shared by several tapes is worth a column even when its term is small
 _LOOKUP_WEIGHT = 8
+# nested hoisting threshold (nested_shared), in the same weighted nodes
+NESTED_MIN_NODES = 32
 
 
 def shared_subterms(roots: Sequence[S.Term], min_nodes: int = 8, min_tapes: int = 2) -> List[S.Term]:
@@ -408,6 +410,49 @@ def shared_subterms(roots: Sequence[S.Term], min_nodes: int = 8, min_tapes: int 
                     continue
             stack.extend(t.args)
     return list(chosen.values())
+
+
+def nested_shared(cols: Sequence[S.Term], min_nodes: int) -> List[S.Term]:
+    """Sub-terms shared by several hoisted columns, hoisted in turn until none is left.
+    shared_subterms picks the maximal shared sub-term on each path of a TAPE, so a sub-term that
+    several columns contain (C4's calldata word of the transfer amount sits in four storage-chain
+    columns) was evaluated once per column and model.  Counting walks each column's program as
+    lowered, i.e. cut at the other columns it reads, so a term is shared only when two programs
+    would each evaluate it; each round's new columns are strictly inside earlier ones (terms are
+    acyclic), so the rounds end."""
+    chosen: List[S.Term] = list(cols)
+    out: List[S.Term] = []
+    while True:
+        cut = {id(t): t for t in chosen}
+        count: Dict[int, int] = {}
+        terms: Dict[int, S.Term] = {}
+        for r in chosen:
+            for t in _walk_cut(r, cut):
+                if t is r or id(t) in cut or t.kind in _LEAVES or t.sort == "array":
+                    continue
+                count[id(t)] = count.get(id(t), 0) + 1
+                terms[id(t)] = t
+        eligible = {i for i, c in count.items() if c >= 2 and terms[i].width <= 2048}
+
+        def size(t: S.Term) -> int:   # weighted nodes of t's own program (cut at columns)
+            return sum(_LOOKUP_WEIGHT if w.kind in (S.SELECT, S.APP) else 1
+                       for w in _walk_cut(t, cut) if w.kind not in _LEAVES and (w is t or id(w) not in cut))
+        new: Dict[int, S.Term] = {}
+        for r in chosen:   # top-down: the first eligible term on every path is maximal
+            stack, seen = list(r.args), set()
+            while stack:
+                t = stack.pop()
+                if id(t) in seen or t.kind in _LEAVES or id(t) in cut:
+                    continue
+                seen.add(id(t))
+                if id(t) in eligible and id(t) not in new and size(t) >= min_nodes:
+                    new[id(t)] = t
+                    continue
+                stack.extend(t.args)
+        if not new:
+            return out
+        out += new.values()
+        chosen += new.values()
 
 
 def keccak_subterms(terms: Sequence[S.Term], syms, chosen: Sequence[S.Term]) -> List[S.Term]:
@@ -468,8 +513,14 @@ def lower_batch(roots: Sequence[S.Term], syms: Optional[SymbolTable] = None, hoi
     col_terms: List[S.Term] = []
     if hoist and len(roots) > 1:
         # (MQ_HOIST_MIN_NODES / MQ_HOIST_MIN_TAPES: diagnostic overrides of the hoisting threshold)
-        col_terms = shared_subterms(roots, int(os.environ.get("MQ_HOIST_MIN_NODES", hoist_min_nodes)),
-                                    int(os.environ.get("MQ_HOIST_MIN_TAPES", 2)))
+        min_nodes = int(os.environ.get("MQ_HOIST_MIN_NODES", hoist_min_nodes))
+        col_terms = shared_subterms(roots, min_nodes, int(os.environ.get("MQ_HOIST_MIN_TAPES", 2)))
+        # sub-terms shared by several columns: hoisted from NESTED_MIN_NODES weighted nodes (a
+        # column costs a row store and loads, and a deeper level a launch); MQ_HOIST_NESTED
+        # overrides (0 = off)
+        nested_min = int(os.environ.get("MQ_HOIST_NESTED", NESTED_MIN_NODES))
+        if nested_min > 0:
+            col_terms += nested_shared(col_terms, nested_min)
         n_shared = len(col_terms)
         col_terms += keccak_subterms(list(roots), syms, col_terms)
         # every keccak application and Concat piece, also those already chosen as shared terms

@@ -436,10 +436,11 @@ def test_c5_deep_tapes_match_oracle(evaluator, hoist):
 
 
 # ---------------------------------------------------------------- batch-level hoisting (column programs)
-@pytest.mark.parametrize("col_min_nodes", ["0", None])
+@pytest.mark.parametrize("col_min_nodes", ["0", None, "40"])
 def test_c3_hoisted_columns_match_unhoisted_oracle(evaluator, monkeypatch, col_min_nodes):
-    """col_min_nodes "0": every column on the G assembly kernel (mode 3); None: the default split
-    (short columns on the HIP C++ column kernel)."""
+    """col_min_nodes "0": every column on the G assembly kernel (mode 3); None: the default split;
+    "40": columns under 40 nodes on the HIP C++ column kernel, the rest on G, in one launch (G
+    then writes its Bool columns' 0/1 rows too, and only the C++ columns' masks are packed)."""
     from mythril_amd.synth_evm import c3_workload
     if col_min_nodes is not None:
         monkeypatch.setenv("MQ_G_COL_MIN_NODES", col_min_nodes)
@@ -455,6 +456,8 @@ def test_c3_hoisted_columns_match_unhoisted_oracle(evaluator, monkeypatch, col_m
     n_cols_asm, cols_live = ct.column_asm_split()
     if col_min_nodes == "0":
         assert cols_live and n_cols_asm >= 0.5 * tb.columns.n, (n_cols_asm, tb.columns.n)
+    if col_min_nodes == "40":
+        assert cols_live and 0 < n_cols_asm < tb.columns.n, (n_cols_asm, tb.columns.n)
     vref = cref.verdicts(plain[0], plain[1])
     v, _ = evaluator.verdicts(ct)
     assert (v == vref).all()
