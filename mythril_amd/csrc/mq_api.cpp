@@ -13,10 +13,12 @@
 #include <functional>
 #include <mutex>
 #include <thread>
+#include <pthread.h>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <unordered_set>
 #include <memory>
 #include <string>
 #include <vector>
@@ -135,6 +137,10 @@ struct DevBuf {
   }
   hipError_t ensure(size_t n) {
     if (n <= bytes && p) return hipSuccess;
+    // growing: a kernel queued on some stream may still read the old block, and the pool hands
+    // it out again at once (possibly to another stream) -- drain the device first (growth is rare:
+    // size classes double)
+    if (p) (void)hipDeviceSynchronize();
     release();
     int d = 0;
     hipError_t e = hipGetDevice(&d);
@@ -187,6 +193,11 @@ static int gen_kind(const CompiledTape& x) {
 static constexpr int64_t kColAsmMinNodes = 1;    // hoisted columns on qsg_kernel from this size
 
 struct mq_ctx {
+  // compiled batches made on this context, detached (ctx = nullptr) when it is destroyed first:
+  // mq_tapes_free after mq_ctx_destroy must not touch the freed context (a Python finalizer may
+  // run in either order)
+  std::mutex tapes_mu;
+  std::unordered_set<mq_tapes*> live_tapes;
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -336,6 +347,10 @@ struct mq_tapes {
   std::vector<mq_tapes*> peers;
   ~mq_tapes() {
     for (mq_tapes* p : peers) delete p;
+    if (ctx) {
+      std::lock_guard<std::mutex> g(ctx->tapes_mu);
+      ctx->live_tapes.erase(this);
+    }
   }
 };
 
@@ -356,10 +371,18 @@ static void sum_counter_slots(const std::vector<unsigned long long>& raw, unsign
 // torch's own.)
 // The workers are created once and park on a condition variable between calls: a drop-in query
 // compiles a few dozen tapes, and spawning threads per call cost more than the compilation.
+// set in a thread while it runs a pool job (a nested parallel_for runs serially: run() holds
+// call_mu_), and in a forked child (the pool's workers do not exist there)
+static thread_local bool tl_in_pool = false;
+static std::atomic<bool> g_forked_child{false};
+
 class HostPool {
  public:
   static HostPool& get() {
-    static HostPool* p = new HostPool();   // (never destroyed: workers may outlive static dtors)
+    static HostPool* p = [] {
+      pthread_atfork(nullptr, nullptr, [] { g_forked_child.store(true); });
+      return new HostPool();   // (never destroyed: workers may outlive static dtors)
+    }();
     return *p;
   }
   int threads() const { return n_; }
@@ -374,7 +397,9 @@ class HostPool {
       epoch_++;
     }
     cv_.notify_all();
+    tl_in_pool = true;
     job(0);
+    tl_in_pool = false;
     std::unique_lock<std::mutex> g(mu_);
     done_cv_.wait(g, [&] { return done_ == want_; });
     job_ = nullptr;
@@ -403,7 +428,9 @@ class HostPool {
         if (tid > want_) continue;   // not needed this time
         job = job_;
       }
+      tl_in_pool = true;
       (*job)(tid);
+      tl_in_pool = false;
       std::lock_guard<std::mutex> g(mu_);
       if (++done_ == want_) done_cv_.notify_one();
     }
@@ -418,6 +445,10 @@ class HostPool {
 
 template <class F>
 static void parallel_for(int64_t n, int64_t chunk, F&& fn) {
+  if (tl_in_pool || g_forked_child.load(std::memory_order_relaxed)) {   // nested, or no workers
+    fn(0, 0, n);
+    return;
+  }
   HostPool& pool = HostPool::get();
   const int T = (int)std::min<int64_t>(pool.threads(), (n + chunk - 1) / std::max<int64_t>(chunk, 1));
   if (T <= 1) {
@@ -679,6 +710,11 @@ void mq_ctx_destroy(mq_ctx* c) {
     (void)hipEventDestroy(e.second);
   }
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  {
+    std::lock_guard<std::mutex> g(c->tapes_mu);
+    for (mq_tapes* t : c->live_tapes) t->ctx = nullptr;   // their launches were synchronised above
+    c->live_tapes.clear();
+  }
   delete c;
 }
 
@@ -1470,6 +1506,10 @@ static int tapes_upload_one(mq_ctx* c, int32_t n_tapes, const std::vector<Compil
   HIPCHK(hipSetDevice(c->device));
   auto T = std::make_unique<mq_tapes>();
   T->ctx = c;
+  {
+    std::lock_guard<std::mutex> g(c->tapes_mu);
+    c->live_tapes.insert(T.get());
+  }
   T->n_tapes = n_tapes;
   T->unsupported.assign(std::max(n_tapes, 1), 0);
   T->n_nodes.assign(n_tapes, 0);
@@ -1811,6 +1851,7 @@ static bool kc_match(const mq_tape_batch* progs, int32_t k, std::vector<mq_tapes
 static int set_columns_one(mq_tapes* T, const mq_tape_batch* progs, const int32_t* var_index, const int32_t* level,
                            int32_t n_columns) {
   mq_ctx* c = T->ctx;
+  if (!c) return MQ_ERR_STATE;   // the context was destroyed
   HIPCHK(hipSetDevice(c->device));
   T->clevels.clear();
   T->col_var.assign(var_index, var_index + n_columns);
