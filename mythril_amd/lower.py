@@ -367,6 +367,7 @@ _LEAVES = frozenset({S.SYM, S.VAL, S.TRUE, S.FALSE, S.ARRAY_SYM})
 _LOOKUP_WEIGHT = 8
 # nested hoisting threshold (nested_shared), in the same weighted nodes
 NESTED_MIN_NODES = 32
+NESTED_ROUNDS = 1     # rounds of nested_shared: later rounds chain C4's storage balances into ~10 levels
 
 
 def shared_subterms(roots: Sequence[S.Term], min_nodes: int = 8, min_tapes: int = 2) -> List[S.Term]:
@@ -422,6 +423,7 @@ def nested_shared(cols: Sequence[S.Term], min_nodes: int) -> List[S.Term]:
     acyclic), so the rounds end."""
     chosen: List[S.Term] = list(cols)
     out: List[S.Term] = []
+    rounds = 1
     while True:
         cut = {id(t): t for t in chosen}
         count: Dict[int, int] = {}
@@ -453,6 +455,9 @@ def nested_shared(cols: Sequence[S.Term], min_nodes: int) -> List[S.Term]:
             return out
         out += new.values()
         chosen += new.values()
+        if len(out) and int(os.environ.get("MQ_HOIST_NESTED_ROUNDS", NESTED_ROUNDS)) <= rounds:
+            return out
+        rounds += 1
 
 
 def keccak_subterms(terms: Sequence[S.Term], syms, chosen: Sequence[S.Term]) -> List[S.Term]:

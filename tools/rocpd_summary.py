@@ -24,6 +24,15 @@ def kernel_stats(db):
              "vgpr": r[6], "sgpr": r[7], "scratch": r[8], "lds": r[9]} for r in rows]
 
 
+def last_dispatches(db, n=80):
+    """The last n kernel dispatches in start order (name, grid, duration ns, LDS bytes): the launch
+    sequence of the final timed step (column levels, packs, the tape launch)."""
+    c = sqlite3.connect(db)
+    rows = c.execute(
+        "select name, grid_x*grid_y*grid_z, duration, lds_size from kernels order by start desc limit ?", (n,)).fetchall()
+    return [{"kernel": r[0].split("(")[0], "grid": r[1], "ns": r[2], "lds": r[3]} for r in reversed(rows)]
+
+
 def pmc_stats(db):
     c = sqlite3.connect(db)
     rows = c.execute(
@@ -47,6 +56,10 @@ def main():
         kind, db = arg.split("=", 1)
         if kind == "kt":
             res["kernel_trace"] = kernel_stats(db)
+            try:
+                res["last_dispatches"] = last_dispatches(db)
+            except sqlite3.Error:
+                pass
         else:
             for k, d in pmc_stats(db).items():
                 res["pmc"].setdefault(k, {}).update(d)
