@@ -60,13 +60,15 @@ def test_compile_c2_tapes():
         assert evaluator.tape_alg_ops(tb, t) > 0
 
 
-def test_compile_fuzz_tapes_mostly_supported():
-    for seed, mw in ((0, 256), (1, 512)):
+def test_compile_fuzz_tapes_supported():
+    """Every fuzz tape compiles (the fuzz stays inside the named limits of tests/unsupported.py),
+    and the 256-bit ones onto 8 limbs."""
+    from unsupported import expected_unsupported
+    for seed, mw in ((0, 256), (1, 512), (5, 512), (7, 512)):
         tb, mb = fuzz_workload(seed, 60, 4, max_width=mw)
+        assert not expected_unsupported(tb).any()
         infos = [evaluator.compile_info(tb, t) for t in range(tb.n_tapes)]
-        sup = [i for i in infos if i.supported]
-        assert len(sup) >= 0.9 * len(infos), [i.why for i in infos if not i.supported]
-        assert all(i.limbs == (8 if mw == 256 else i.limbs) for i in sup)
+        assert all(i.limbs == 8 for i in infos) if mw == 256 else all(i.limbs in (8, 16) for i in infos)
 
 
 def test_compile_supports_values_up_to_2048_bits():

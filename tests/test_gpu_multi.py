@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 import cref
+from unsupported import supported_exactly
 from mythril_amd import dist
 from mythril_amd.evaluator import Evaluator
 from mythril_amd.models import ModelBatch
@@ -32,7 +33,7 @@ def test_rccl_path_single_rank():
         tb2, mb2 = fuzz_workload(7, 30, 130, max_width=512)
         ev.upload_models(mb2)
         v, fh2 = ev.verdicts(tb2)
-        sup = fh2 != -2
+        sup = supported_exactly(tb2, fh2)
         assert (v[sup] == cref.verdicts(tb2, mb2)[sup]).all()
         assert (ev.first_hit(tb2)[sup] == cref.first_hit(tb2, mb2)[0][sup]).all()
     finally:
@@ -51,7 +52,7 @@ def test_two_devices_one_context(n_models):
         ev.upload_models(mb)
         ref, _ = cref.first_hit(tb, mb)
         fh = ev.first_hit(tb)
-        sup = ref != -2
+        sup = supported_exactly(tb, fh)
         assert (fh[sup] == ref[sup]).all()
         v, fhv = ev.verdicts(tb)
         assert (v[sup] == cref.verdicts(tb, mb)[sup]).all() and (fhv[sup] == ref[sup]).all()
@@ -71,7 +72,7 @@ def test_empty_shards_report_no_hit(evaluator, world):
         evaluator.upload_models(mb.shard(lo, hi))
         parts.append(dist.encode_local(evaluator.first_hit(tb)))
     merged = dist.decode_global(np.minimum.reduce(parts))
-    sup = ref != -2
+    sup = supported_exactly(tb, merged, 256)
     assert (merged[sup] == ref[sup]).all()
 
 

@@ -6,6 +6,7 @@ import pytest
 import cref
 import keccak_ref
 from golden_util import check_tape, load
+from unsupported import supported_exactly
 from mythril_amd.models import FuncSpec, ModelBatch
 from mythril_amd.synth import c2_workload, fuzz_workload
 from mythril_amd.tape import Tape, TapeBatch
@@ -43,15 +44,47 @@ def test_fuzz_verdicts_match_oracle(evaluator, seed, max_width):
     v_gpu, fh_gpu = evaluator.verdicts(tb)
     v_ref = cref.verdicts(tb, mb)
     fh_ref, _ = cref.first_hit(tb, mb)
-    unsup = fh_gpu == -2
-    assert unsup.mean() < 0.1
-    sup = ~unsup
+    sup = supported_exactly(tb, fh_gpu, max_width)
+    unsup = ~sup
     mism = np.argwhere(v_gpu[sup] != v_ref[sup])
     assert len(mism) == 0, f"{len(mism)} mismatches, first {mism[:5]}"
     assert (fh_gpu[sup] == fh_ref[sup]).all()
     fh = evaluator.first_hit(tb)
     assert (fh[sup] == fh_ref[sup]).all()
     assert (fh[unsup] == -2).all()
+
+
+def test_unsupported_tapes_are_exactly_the_named_limits(evaluator):
+    """A batch mixing supported fuzz tapes with tapes past each named limit (a 2056-bit value, a
+    1024-bit multiplication, a 1024-bit overflow predicate): -2 exactly on the latter, every other
+    answer equal to the oracle's."""
+    tb0, mb = fuzz_workload(41, 30, 120, max_width=512, depth=4)
+    extra = []
+    t = Tape()
+    extra.append(t.finish(t.eq(t.zext(1800, t.var(0, 256)), t.const(3, 2056))))
+    t = Tape()
+    a = t.zext(768, t.var(0, 256))
+    extra.append(t.finish(t.eq(t.mul(a, a), t.const(9, 1024))))
+    t = Tape()
+    a = t.zext(768, t.var(1, 256))
+    extra.append(t.finish(t.umul_noovfl(a, a)))
+    tx = TapeBatch(extra)
+    nx = tx.nodes.copy()
+    nx["a"][nx["op"] == 1] += np.uint32(tb0.consts.size)    # CONST nodes index the joined pool
+    both = TapeBatch.from_arrays(np.concatenate([tb0.nodes, nx]),
+                                 np.concatenate([tb0.offsets, tb0.offsets[-1] + tx.offsets[1:]]),
+                                 np.concatenate([tb0.consts, tx.consts]))
+    n0 = tb0.n_tapes
+    order = list(range(5)) + [n0] + list(range(5, 17)) + [n0 + 1] + list(range(17, n0)) + [n0 + 2]
+    tb = both.subset(order)
+    evaluator.upload_models(mb)
+    v, fh = evaluator.verdicts(tb)
+    sup = supported_exactly(tb, fh)
+    assert (~sup).sum() == 3 and not sup[5] and not sup[18] and not sup[-1]
+    assert (v[sup] == cref.verdicts(tb.subset(np.flatnonzero(sup)), mb)).all()
+    fh1 = evaluator.first_hit(tb)
+    assert (fh1[~sup] == -2).all()
+    assert (fh1[sup] == cref.first_hit(tb.subset(np.flatnonzero(sup)), mb)[0]).all()
 
 
 def test_c2_first_hit(evaluator):
