@@ -434,7 +434,9 @@ def nested_shared(cols: Sequence[S.Term], min_nodes: int) -> List[S.Term]:
                     continue
                 count[id(t)] = count.get(id(t), 0) + 1
                 terms[id(t)] = t
-        eligible = {i for i, c in count.items() if c >= 2 and terms[i].width <= 2048}
+        # (at most 256 bits: a wider column would run on the HIP C++ column kernel, e.g. C4's
+        # 512-bit key ++ slot, which took 2.2 ms of a 5.7 ms step)
+        eligible = {i for i, c in count.items() if c >= 2 and terms[i].width <= 256}
 
         def size(t: S.Term) -> int:   # weighted nodes of t's own program (cut at columns)
             return sum(_LOOKUP_WEIGHT if w.kind in (S.SELECT, S.APP) else 1
@@ -458,6 +460,26 @@ def nested_shared(cols: Sequence[S.Term], min_nodes: int) -> List[S.Term]:
         if len(out) and int(os.environ.get("MQ_HOIST_NESTED_ROUNDS", NESTED_ROUNDS)) <= rounds:
             return out
         rounds += 1
+
+
+def _column_levels(cols: Sequence[S.Term]) -> Dict[int, int]:
+    """id(column) -> level: 0 for a column reading no other column, else 1 + the deepest column
+    its program reads (programs cut at the other columns, as lowered)."""
+    cut = {id(t): t for t in cols}
+    inner = {id(t): [h for h in _walk_cut(t, cut) if id(h) in cut and h is not t] for t in cols}
+    level: Dict[int, int] = {}
+    for t0 in cols:
+        stack = [(t0, False)]
+        while stack:
+            t, done = stack.pop()
+            if id(t) in level:
+                continue
+            if done:
+                level[id(t)] = 1 + max((level[id(h)] for h in inner[id(t)]), default=-1)
+                continue
+            stack.append((t, True))
+            stack.extend((h, False) for h in inner[id(t)] if id(h) not in level)
+    return level
 
 
 def keccak_subterms(terms: Sequence[S.Term], syms, chosen: Sequence[S.Term]) -> List[S.Term]:
@@ -520,14 +542,25 @@ def lower_batch(roots: Sequence[S.Term], syms: Optional[SymbolTable] = None, hoi
         # (MQ_HOIST_MIN_NODES / MQ_HOIST_MIN_TAPES: diagnostic overrides of the hoisting threshold)
         min_nodes = int(os.environ.get("MQ_HOIST_MIN_NODES", hoist_min_nodes))
         col_terms = shared_subterms(roots, min_nodes, int(os.environ.get("MQ_HOIST_MIN_TAPES", 2)))
+        kcols = keccak_subterms(list(roots), syms, col_terms)
         # sub-terms shared by several columns: hoisted from NESTED_MIN_NODES weighted nodes (a
-        # column costs a row store and loads, and a deeper level a launch); MQ_HOIST_NESTED
-        # overrides (0 = off)
+        # column costs a row store and loads); MQ_HOIST_NESTED overrides (0 = off).  Each column
+        # level is a launch of its own, so nested columns may not deepen the level structure:
+        # the deepest ones are dropped (inlined again) until the batch has no more levels than
+        # without them (C4's storage balances chain into ~12 levels of tiny programs otherwise)
         nested_min = int(os.environ.get("MQ_HOIST_NESTED", NESTED_MIN_NODES))
         if nested_min > 0:
-            col_terms += nested_shared(col_terms, nested_min)
+            nested = nested_shared(col_terms + kcols, nested_min)
+            if nested:
+                cap = max(_column_levels(col_terms + kcols).values(), default=0)
+                while nested:
+                    lv = _column_levels(col_terms + nested + kcols)
+                    if max(lv.values()) <= cap:
+                        break
+                    nested.remove(max(nested, key=lambda t: lv[id(t)]))
+                col_terms += nested
         n_shared = len(col_terms)
-        col_terms += keccak_subterms(list(roots), syms, col_terms)
+        col_terms += [t for t in kcols if id(t) not in {id(x) for x in col_terms}]
         # every keccak application and Concat piece, also those already chosen as shared terms
         # (an address key x & (2^160 - 1) is both): never narrowed
         kpieces = {id(t) for t in keccak_subterms(list(roots), syms, [])}
