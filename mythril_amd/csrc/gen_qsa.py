@@ -221,6 +221,12 @@ def load_window(first, pfx=None):
 # G: a handler that reads the stack first waits for the pushes in flight — global loads (PUSH_MEM)
 # and LDS reads of staged model rows (PUSH_MEMS)
 VMWAIT = "s_waitcnt vmcnt(0) lgkmcnt(0)"
+# ... and the "_L" variant of every stack reader (and of its fused forms), which waits for LDS /
+# scalar loads only: the translator picks it when no PUSH_MEM (global load) is outstanding
+# (mq_api.cpp qsa_translate, final pass).  Otherwise the first stack reader of every tape also
+# waited for the prefetch of the NEXT program window (load_window's NWIN), an L2 / HBM round trip
+# (C4's tapes: ULTK right after a staged PUSH_MEMS at ~5 800 cycles per dispatch, profiles/r04h)
+LGKMWAIT = "s_waitcnt lgkmcnt(0)"
 
 
 def zero_limbs(d, lo):
@@ -974,10 +980,12 @@ def make_handlers(variant, pfx):
         prof = prof_point(key[0]) if G else []
         if tail:
             hs.append((key, pre + list(body) + prof + (NEXT_G if G else NEXT_P)))
+            if pre:
+                hs.append(((key[0] + "_L",) + tuple(key[1:]), [LGKMWAIT] + list(body) + prof_point(key[0] + "_L") + NEXT_G))
         else:
             hs.append((key, prof + pre + list(body)))
         if key[0] in ACC_KINDS and tail:
-            acc.append((key, pre + list(body)))
+            acc.append((key, list(body), bool(pre)))
 
     H(("END",), [f"s_branch {pfx}_tape_end"], tail=False, reads_stack=False)
     if G:
@@ -1292,7 +1300,7 @@ def make_handlers(variant, pfx):
     # ---- Bool producers fused with the AND / OR that consumes their result (kind_A / kind_O):
     # the translator rewrites "X; AND" into "X_A" when X leaves its result at the AND's right
     # slot, one dispatch instead of two (AND / OR are ~30 % of the dispatches of EVM-shaped tapes)
-    for key, body in acc:
+    for key, body, waits in acc:
         kind, d = key[0], key[1]
         r = d if (kind in ACC_UNARY or kind in ACC_AT_X) else d - 1
         if r < 1:
@@ -1302,7 +1310,10 @@ def make_handlers(variant, pfx):
                 fused = [f"{ins_n} {B(r - 1)}, {B(r - 1)}, {B(r)}"]
             else:
                 fused = list(body) + (["s_nop 3"] if body[-1].startswith("v_") else []) + [f"{ins} {B(r - 1)}, {B(r - 1)}, {B(r)}"]
-            hs.append(((kind + suf,) + tuple(key[1:]), fused + (prof_point(kind + suf) if G else []) + (NEXT_G if G else NEXT_P)))
+            pre = [VMWAIT] if waits else []
+            hs.append(((kind + suf,) + tuple(key[1:]), pre + fused + (prof_point(kind + suf) if G else []) + (NEXT_G if G else NEXT_P)))
+            if waits:
+                hs.append(((kind + suf + "_L",) + tuple(key[1:]), [LGKMWAIT] + fused + prof_point(kind + suf + "_L") + NEXT_G))
     subs = sub_abs_cneg(pfx) + sub_udiv32(pfx) + (sub_uf1(pfx) + sub_udivv(pfx) if G else [])
     return hs, subs
 
@@ -1812,6 +1823,8 @@ def main():
         table("kQsaKindAndForm", lambda n: idx.get(n + "_A", -1))
         table("kQsaKindOrForm", lambda n: idx.get(n + "_O", -1))
         table("kQsaKindBoolRes", lambda n: (0 if (n in ACC_UNARY or n in ACC_AT_X) else 1) if n in ACC_KINDS else -1)
+        # the variant that waits for LDS / scalar loads only (-1: none; G stack readers)
+        table("kQsaKindLForm", lambda n: idx.get(n + "_L", -1))
 
         def inv(n):
             m = re.fullmatch(r"([US])(LT|GT|LE|GE)([VCK]?)", n)

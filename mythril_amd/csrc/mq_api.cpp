@@ -224,6 +224,8 @@ struct mq_ctx {
   bool qsa_ready = false;
   std::vector<uint32_t> qsa_off[2];
   int qsa_index[2][QK_COUNT][kQsaStack][kQsaSel + 1];
+  // G kinds that wait for every vector load themselves (PUSH_MEMB, MEQK*, UF1*)
+  bool qsa_vm_drain[QK_COUNT] = {};
   uint32_t qsa_var_row[64];
   std::vector<uint8_t> qsa_data_words;
   uint32_t qsa_hbase_lo[2] = {0, 0};   // low 32 bits of each interpreter's handler base
@@ -605,6 +607,10 @@ static int qsa_init(mq_ctx* c) {
     else if (base == "MEQK2" || base == "SEQK2") words = 2;
     else if (base == "MEQK8" || base == "SEQK8") words = 8;
     if (words > 0) c->qsa_data_words[hword(1, c->qsa_off[1][h]) & 0xFFFFu] = (uint8_t)words;
+  }
+  for (int q = 0; q < QK_COUNT; q++) {
+    const std::string n = kQsaKindNames[q];
+    c->qsa_vm_drain[q] = n == "PUSH_MEMB" || n.rfind("MEQK", 0) == 0 || n.rfind("UF1", 0) == 0;
   }
   c->qsa_ready = ok && std::getenv("MQ_DISABLE_QSA") == nullptr;
   return MQ_OK;
@@ -1456,6 +1462,27 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
     prev_imm = imm;
     prev_out = out_before;
     prev_pre = op == G_PUSH_VAR ? pushed_pre : -1;
+  }
+  static const bool no_lwait = std::getenv("MQ_NO_LWAIT") != nullptr;   // (diagnostic A/B)
+  if (!P && !no_lwait) {
+    // final pass: a stack reader waits for the vector loads of a PUSH_MEM only when one may be
+    // outstanding; otherwise its "_L" variant waits for LDS / scalar loads alone, and the
+    // prefetch of the next program window (gen_qsa.py load_window) stays in flight
+    bool pending = false;
+    for (const Emit& e : log) {
+      if (e.kind == QK_PUSH_MEM) {
+        pending = true;
+        continue;
+      }
+      const int lk = kQsaKindLForm[e.kind];
+      if (lk >= 0) {
+        const int h = c->qsa_index[k][lk][e.d][e.v + 1];
+        if (!pending && h >= 0) out[e.pos] = hword(k, c->qsa_off[k][h]) | (e.imm << 16);
+        pending = false;   // (the VMWAIT form drained every load)
+        continue;
+      }
+      if (c->qsa_vm_drain[e.kind]) pending = false;
+    }
   }
   if (P) {
     // constant prefetch (gen_qsa.py NEXT_P): a constant handler whose predecessor is not itself
