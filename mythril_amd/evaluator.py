@@ -244,10 +244,25 @@ class CompiledTapes:
         _check(self.ev.lib.mq_tapes_column_keccak(self.handle, C.byref(n)), "mq_tapes_column_keccak")
         return n.value
 
-    def handler_histogram(self, which: int = 1, pairs: bool = False):
+    def handler_histogram(self, which: int = 1, pairs: bool = False, wait_variants: bool = False):
         """After a launch: {handler kind: dispatches per (tape, model) pair, summed over tapes} of
         the assembly translation (which = 0 P tapes, 1 G tapes, 2 G column programs); with
-        pairs, also {(kind, next kind): count} over the G tapes.  Diagnostic."""
+        pairs, also {(kind, next kind): count} over the G tapes.  A G stack reader's "_L" variant
+        (waits for LDS / scalar loads only, gen_qsa.py LGKMWAIT) counts as its kind unless
+        ``wait_variants``.  Diagnostic."""
+        if not wait_variants:
+            fold = lambda k: k[:-2] if k.endswith("_L") else k   # noqa: E731
+            res = self.handler_histogram(which, pairs, True)
+            h = res[0] if pairs else res
+            hf = {}
+            for k, v in h.items():
+                hf[fold(k)] = hf.get(fold(k), 0) + v
+            if not pairs:
+                return hf
+            pf = {}
+            for (a, b), v in res[1].items():
+                pf[(fold(a), fold(b))] = pf.get((fold(a), fold(b)), 0) + v
+            return hf, pf
         lib = self.ev.lib
         n = C.c_int32()
         _check(lib.mq_tapes_qsa_histogram(self.handle, which, None, 0, None, C.byref(n)), "mq_tapes_qsa_histogram")
