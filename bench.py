@@ -292,41 +292,42 @@ def calls_avoided_leg(ev, n_forks: int = 256, n_models: int = 100, seed: int = 2
     (``support.counters``: calls, answers from quick-sat at model.py:101-103, answers from
     generated candidates, calls that reach ``solver_worker`` model.py:28).
 
-    Stream: the per-fork check of svm.py:351-358 on ``n_forks`` JUMPIs.  Each fork's parent path
-    is satisfied by a cached model (fork_workload: 100 models in the LRU, MRU first); its two
-    successors are path + cond (the parent model falsifies cond) and path + Not(cond).  All
-    2 * n_forks states go through ``is_possible_batch`` (one launch, answers sequentially exact),
-    with ``Args.quick_sat_candidates`` off (the reference's behaviour) and on.  There is no z3 on
-    the box: the solver stand-in answers ``unknown`` (what z3 does on a timeout), so a call that
-    reaches it prunes the state (constraints.py:37-38) instead of adding a model."""
-    from mythril_amd import smt as S
+    Stream: the per-fork check of svm.py:351-358 on ``n_forks`` JUMPIs
+    (synth_evm.fork_stream_workload): each fork's parent path is satisfied by a cached model
+    (100 models in the LRU, MRU first); of its two successors one is satisfied by the parent's
+    model, the other needs a different third argument.  All 2 * n_forks states go through
+    ``is_possible_batch`` (one launch, answers sequentially exact), with
+    ``Args.quick_sat_candidates`` off (the reference's behaviour) and on.  There is no z3 on the
+    box: the solver stand-in (support.WitnessSolver) answers every state it is asked with the
+    known satisfying model, which get_model caches in the LRU like z3's (model.py:124-126), so
+    both arms run under the reference's insertion semantics and the LRU evolves alike."""
     from mythril_amd import support as sp
-    from mythril_amd.synth_evm import fork_workload
-    exprs, recs, _ = fork_workload(n_forks, n_models, seed=seed)
-    states = []
-    for e in exprs:
-        path, cond = list(e.args[:-1]), e.args[-1]
-        states += [sp.Constraints(path + [cond]), sp.Constraints(path + [S.Not(cond)])]
+    from mythril_amd.synth_evm import fork_stream_workload
+    states, wits, recs = fork_stream_workload(n_forks, n_models, seed=seed)
     out = {"stream": f"svm.py:351-358 fork checks: {n_forks} forks x 2 successors over {n_models} cached models "
-                     f"(fork_workload seed {seed}); solver stand-in answers unknown (no z3 on the box)"}
+                     f"(fork_stream_workload seed {seed}); solver stand-in returns each state's known witness, "
+                     f"cached like z3's sat model (model.py:124-126)"}
     saved = (sp.model_cache, sp.args.quick_sat_candidates, sp.args.quick_sat_candidate_budget)
     try:
         for cand in (False, True):
             sp.reset_caches()
             sp.model_cache = sp.ModelCache(sp.VerdictEngine(ev))
-            sp.set_solver_backend(sp.NoSolver())
+            solver = sp.WitnessSolver(states, wits)
+            sp.set_solver_backend(solver)
             sp.args.quick_sat_candidates, sp.args.quick_sat_candidate_budget = cand, budget
             for m in reversed(recs):
                 sp.model_cache.put(m, 1)
+            cs = [sp.Constraints(st) for st in states]
             t0 = time.perf_counter()
-            alive = sp.is_possible_batch(states)
+            alive = sp.is_possible_batch(cs)
             dt = time.perf_counter() - t0
             c = dict(sp.counters)
             avoided = c["get_model_calls"] - c["solver_calls"]
             out["candidates_on" if cand else "candidates_off"] = {
                 **c, "states_alive": int(sum(alive)), "solver_calls_avoided": avoided,
-                "fraction_avoided": avoided / max(c["get_model_calls"], 1), "ms_per_state": dt * 1e3 / len(states),
-                "candidate_budget": budget if cand else 0}
+                "fraction_avoided": avoided / max(c["get_model_calls"], 1), "ms_per_state": dt * 1e3 / len(cs),
+                "candidate_budget": budget if cand else 0, "solver_stand_in_calls": solver.calls,
+                "models_inserted_by_solver": solver.calls}
     finally:
         sp.model_cache, sp.args.quick_sat_candidates, sp.args.quick_sat_candidate_budget = saved
         sp.set_solver_backend(None)

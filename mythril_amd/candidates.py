@@ -157,19 +157,25 @@ def _wanted(op: int, const_left: bool, c: int, w: int, positive: Optional[bool])
 
 class CandidateSet:
     """The LRU models followed by the generated candidates, serialized (``batch``), plus what is
-    needed to turn a generated candidate back into a model (:meth:`materialize`)."""
+    needed to turn a generated candidate back into a model (:meth:`materialize`).  Candidates
+    come in blocks: one patch applied to a range of base models."""
 
-    def __init__(self, batch: ModelBatch, n_lru: int, base: np.ndarray, patches: List[Tuple], syms, lru_models):
+    def __init__(self, batch: ModelBatch, n_lru: int, base: np.ndarray, block_of: np.ndarray,
+                 block_patches: List[Tuple], syms, lru_models):
         self.batch = batch
         self.n_lru = n_lru
         self.base = base                  # [K] LRU index each candidate derives from (-1: none)
-        self.patches = patches            # [K] tuple of (var, lo, n_bits, bits)
+        self.block_of = block_of          # [K] its block
+        self.block_patches = block_patches   # per block: tuple of (var, lo, n_bits, bits)
         self.syms = syms
         self.lru_models = list(lru_models)
 
     @property
     def n_generated(self) -> int:
         return self.batch.n_models - self.n_lru
+
+    def patch(self, k: int) -> Tuple:
+        return self.block_patches[int(self.block_of[k])]
 
     def materialize(self, index: int) -> Model:
         """Global candidate ``index`` (>= n_lru) as a model: the base model with the patched
@@ -181,7 +187,7 @@ class CandidateSet:
         funcs = {name: (dict(e), els) for name, (e, els) in rec.functions.items()}
         names = {i: key for key, i in self.syms.vars.items()}
         vals: Dict[int, int] = {}
-        for v, lo, n, bits in sorted(self.patches[k], key=lambda p: p[1] < 0):   # floors last
+        for v, lo, n, bits in sorted(self.patch(k), key=lambda p: p[1] < 0):   # floors last
             if v not in vals:
                 name, w = names[v]
                 if v in self.syms.derived:
@@ -211,10 +217,11 @@ class CandidateSet:
 class CandidateGenerator:
     """Generates up to ``max_candidates`` candidates for a batch of conjunctions (seeded)."""
 
-    def __init__(self, max_candidates: int = 100_000, seed: int = 0, random_frac: float = 0.05):
+    def __init__(self, max_candidates: int = 100_000, seed: int = 0, random_frac: float = 0.05, per_query: int = 16):
         self.max_candidates = int(max_candidates)
         self.rng = np.random.Generator(np.random.PCG64(seed))
         self.random_frac = random_frac
+        self.per_query = int(per_query)   # patches per query (each over every base model)
 
     # ------------------------------------------------------------ targets
     def _targets(self, db, syms):
@@ -262,149 +269,154 @@ class CandidateGenerator:
     # ------------------------------------------------------------ generation
     def generate(self, db, syms, lru_batch: ModelBatch, lru_models: Sequence) -> CandidateSet:
         """``lru_batch`` (the serialized LRU, MRU first, index_base 0) followed by generated
-        candidates; their model rows are patched copies of LRU rows (random fills: fresh)."""
+        candidates; their model rows are patched copies of LRU rows (random fills: fresh).
+
+        Blocks of one patch over every base model, in order: per query all its invertible
+        conditions patched at once (two rounds of options), then single conditions newest first,
+        at most ``per_query`` patches per query; random multi-condition mixes and boundary /
+        random values of plain variables add ``random_frac`` of that.  The budget adapts to the
+        batch: ``per_query`` x bases per query, capped by ``max_candidates``."""
         rng = self.rng
         n_lru = lru_batch.n_models
-        budget = max(0, self.max_candidates - n_lru)
         per_query = self._targets(db, syms)
-        bases: List[int] = []
-        patches: List[Tuple] = []
+        base_ids = np.arange(n_lru, dtype=np.int64) if n_lru else np.full(1, -1, np.int64)
+        nb = len(base_ids)
+        n_q = sum(1 for o in per_query if o)
+        budget = max(0, min(self.max_candidates - n_lru, self.per_query * nb * max(n_q, 1)))
+        blocks: List[Tuple[Tuple, np.ndarray]] = []
+        total = [0]
+        seen = set()
 
-        def add(base: int, patch: Tuple) -> bool:
-            if len(bases) >= budget:
+        def add(patch: Tuple, bases: np.ndarray = base_ids) -> bool:
+            if total[0] + len(bases) > budget:
                 return False
-            bases.append(base)
-            patches.append(patch)
+            if bases is base_ids:
+                if patch in seen:
+                    return True
+                seen.add(patch)
+            blocks.append((patch, bases))
+            total[0] += len(bases)
             return True
 
-        n_base = max(n_lru, 1)
-        # directed: every base with all conditions of a query patched (first option each), then
-        # alternative options in a second round
+        used = [0] * len(per_query)
         for rnd in range(2):
-            for opts in per_query:
+            for q, opts in enumerate(per_query):
                 if not opts:
                     continue
                 patch = tuple(p for o in opts for p in (o[0] if rnd == 0 else o[int(rng.integers(len(o)))]))
-                for bi in range(n_base):
-                    if not add(bi if n_lru else -1, patch):
-                        break
-        # single mutations, every base: a fork is its parent's path plus ONE new branch condition,
-        # appended last (constraints.py append order), so each query's newest conditions go first,
-        # round-robin over the queries
-        singles = [p for opts in per_query for o in opts for p in o]
+                if add(patch):
+                    used[q] += 1
         depth = max((len(o) for o in per_query), default=0)
         for back in range(1, depth + 1):
-            for opts in per_query:
+            for q, opts in enumerate(per_query):
                 if back > len(opts):
                     continue
                 for p in opts[-back]:
-                    for bi in range(n_base):
-                        if not add(bi if n_lru else -1, p):
-                            break
-        # boundary values of single plain variables, random multi-condition mixes, random fills
-        n_rand = int(budget * self.random_frac)
+                    if used[q] >= self.per_query:
+                        break
+                    if add(p):
+                        used[q] += 1
+        singles = [p for opts in per_query for o in opts for p in o]
         plain = [v for v, w in enumerate(syms.var_widths) if w > 0 and v not in syms.derived
                  and v not in syms.hoisted_vars]
-        while len(bases) < budget - n_rand and (singles or plain):
+        n_rand = int(total[0] * self.random_frac)
+        for _ in range(n_rand):
+            bases = base_ids[rng.integers(0, nb, 1)]
             if singles and rng.random() < 0.7:
                 k = int(rng.integers(1, 4))
                 patch = tuple(q for i in rng.integers(0, len(singles), k) for q in singles[int(i)])
             elif plain:
                 v = plain[int(rng.integers(len(plain)))]
                 w = syms.var_widths[v]
-                val = int(rng.choice([0, 1, (1 << w) - 1, 1 << (w - 1), (1 << (w - 1)) - 1])) & ((1 << w) - 1)
+                val = int(rng.choice([0, 1, (1 << w) - 1, 1 << (w - 1), (1 << (w - 1)) - 1,
+                                      int.from_bytes(rng.bytes((w + 7) // 8), "little")])) & ((1 << w) - 1)
                 patch = ((v, 0, w, val),)
             else:
                 break
-            add(int(rng.integers(n_base)) if n_lru else -1, patch)
-        while len(bases) < budget and plain:
-            v = plain[int(rng.integers(len(plain)))]
-            w = syms.var_widths[v]
-            add(int(rng.integers(n_base)) if n_lru else -1,
-                ((v, 0, w, int.from_bytes(rng.bytes((w + 7) // 8), "little") & ((1 << w) - 1)),))
-        return self._serialize(lru_batch, np.asarray(bases, np.int64), patches, syms, lru_models)
+            if not add(patch, bases):
+                break
+        return self._serialize(lru_batch, blocks, syms, lru_models)
 
     # ------------------------------------------------------------ serialization
-    def _serialize(self, lru: ModelBatch, base: np.ndarray, patches: List[Tuple], syms, lru_models) -> CandidateSet:
-        K, n_lru = len(base), lru.n_models
+    def _serialize(self, lru: ModelBatch, blocks: List[Tuple[Tuple, np.ndarray]], syms, lru_models) -> CandidateSet:
+        n_lru = lru.n_models
+        sizes = np.asarray([len(b) for _, b in blocks], np.int64)
+        K = int(sizes.sum())
+        base = np.concatenate([b for _, b in blocks]) if blocks else np.zeros(0, np.int64)
+        block_of = np.repeat(np.arange(len(blocks), dtype=np.int64), sizes)
+        starts = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
         off = lru.var_word_offsets()
         src = np.where(base >= 0, base, 0)
         gen = lru.var_words[:, src].copy() if n_lru else np.zeros((int(off[-1]), K), np.uint32)
-        # apply patches grouped by identical (var, lo, n, bits) assignment
-        groups: Dict[Tuple[int, int, int, int], List[int]] = {}
-        for k, p in enumerate(patches):
-            for asg in p:
-                groups.setdefault(asg, []).append(k)
-        floors = []
-        for (v, lo, n, bits), ks in groups.items():
-            cols = np.asarray(ks, np.int64)
-            if lo < 0:
-                floors.append((v, bits, cols))
-                continue
-            for i in range(limbs(syms.var_widths[v])):
-                blo, bhi = 32 * i, 32 * i + 32
-                a, b2 = max(lo, blo), min(lo + n, bhi)
-                if a >= b2:
+        # each block's patch over its candidate range: value assignments, then size floors
+        for j, (patch, _) in enumerate(blocks):
+            sl = slice(int(starts[j]), int(starts[j + 1]))
+            for v, lo, n, bits in sorted(patch, key=lambda p: p[1] < 0):
+                if lo < 0:   # size >= minimum (values < 2^32 in their low limb)
+                    r0, nl = int(off[v]), limbs(syms.var_widths[v])
+                    small = ~gen[r0 + 1:r0 + nl, sl].any(axis=0) if nl > 1 else np.ones(sl.stop - sl.start, bool)
+                    low = small & (gen[r0, sl] < np.uint32(bits))
+                    gen[r0, sl][low] = np.uint32(bits)
                     continue
-                mask = ((1 << (b2 - a)) - 1) << (a - blo)
-                val = ((bits >> (a - lo)) << (a - blo)) & mask
-                row = int(off[v]) + i
-                gen[row, cols] = (gen[row, cols] & np.uint32(~mask & 0xFFFFFFFF)) | np.uint32(val)
-        for v, mn, cols in floors:   # size >= minimum (values < 2^32 in their low limb)
-            r0, nl = int(off[v]), limbs(syms.var_widths[v])
-            small = ~gen[r0 + 1:r0 + nl, cols].any(axis=0) if nl > 1 else np.ones(len(cols), bool)
-            low = small & (gen[r0, cols] < np.uint32(mn))
-            gen[r0, cols[low]] = np.uint32(mn)
+                for i in range(limbs(syms.var_widths[v])):
+                    blo, bhi = 32 * i, 32 * i + 32
+                    a, b2 = max(lo, blo), min(lo + n, bhi)
+                    if a >= b2:
+                        continue
+                    mask = ((1 << (b2 - a)) - 1) << (a - blo)
+                    val = ((bits >> (a - lo)) << (a - blo)) & mask
+                    row = int(off[v]) + i
+                    gen[row, sl] = (gen[row, sl] & np.uint32(~mask & 0xFFFFFFFF)) | np.uint32(val)
         words = np.concatenate([lru.var_words, gen], axis=1)
         M = n_lru + K
         if not lru.funcs:
-            return CandidateSet(ModelBatch(lru.var_widths, words), n_lru, base, patches, syms, lru_models)
+            return CandidateSet(ModelBatch(lru.var_widths, words), n_lru, base, block_of,
+                                [p for p, _ in blocks], syms, lru_models)
         # function tables: the base model's entries, preceded by an entry for every derived variable
-        # of that function the candidate changed (so table and derived column agree; first match wins)
+        # of that function the candidate's patch changed (so table and derived column agree; first
+        # match wins)
         F = len(lru.funcs)
         func_index = {name: f for f, name in enumerate(syms.func_names)}
+        changed = []   # per block: {f: sorted derived vars of f the patch assigns}
+        for patch, _ in blocks:
+            d: Dict[int, set] = {}
+            for v, lo, n, bits in patch:
+                if lo >= 0 and v in syms.derived and syms.derived[v][0] in func_index:
+                    d.setdefault(func_index[syms.derived[v][0]], set()).add(v)
+            changed.append({f: sorted(vs) for f, vs in d.items()})
         eptr = np.zeros((F, M + 1), np.int64)
         ew_chunks, el_chunks = [], []
         ebase = np.zeros(F, np.int64)
         elb = np.zeros(F, np.int64)
         wpos = epos = 0
-        changed_derived: Dict[int, List[Tuple[int, int]]] = {}   # f -> [(var, cand)]
-        for (v, lo, n, bits), ks in groups.items():
-            if lo >= 0 and v in syms.derived and syms.derived[v][0] in func_index:
-                f = func_index[syms.derived[v][0]]
-                changed_derived.setdefault(f, []).extend((v, k) for k in ks)
         for f, spec in enumerate(lru.funcs):
             s = spec.stride
             base_ptr = lru.entry_ptr[f]
             base_cnt = np.diff(base_ptr)                                   # [n_lru]
             cnt_gen = base_cnt[src] if n_lru else np.zeros(K, np.int64)
-            extra = {}
-            for v, k in changed_derived.get(f, ()):
-                extra.setdefault(k, set()).add(v)
-            add_cnt = np.zeros(K, np.int64)
-            for k, vs in extra.items():
-                add_cnt[k] = len(vs)
+            add_cnt = np.repeat(np.asarray([len(ch.get(f, ())) for ch in changed], np.int64), sizes) \
+                if blocks else np.zeros(0, np.int64)
             counts = np.concatenate([base_cnt, cnt_gen + add_cnt])
             eptr[f, 1:] = np.cumsum(counts)
             ent = lru.entry_words[int(lru.entry_base[f]):int(lru.entry_base[f]) + int(base_ptr[-1]) * s].reshape(-1, s)
             out = np.zeros((int(eptr[f, -1]), s), np.uint32)
             out[:int(base_ptr[-1])] = ent
-            # generated: patch entries, then the base's entries
-            starts = eptr[f, n_lru:n_lru + K]
-            for k, vs in extra.items():
-                pos = int(starts[k])
-                for v in sorted(vs):
-                    fargs = syms.derived[v][1]
-                    w = []
-                    for aw, av in zip(spec.arg_widths, fargs):
-                        w.extend(to_words(int(av), aw))
+            gstarts = eptr[f, n_lru:n_lru + K]
+            for j, ch in enumerate(changed):
+                vs = ch.get(f)
+                if not vs:
+                    continue
+                cols = np.arange(int(starts[j]), int(starts[j + 1]))
+                for i, v in enumerate(vs):
+                    key = []
+                    for aw, av in zip(spec.arg_widths, syms.derived[v][1]):
+                        key.extend(to_words(int(av), aw))
                     nl = limbs(syms.var_widths[v])
-                    w.extend(int(x) for x in words[int(off[v]):int(off[v]) + nl, n_lru + k])
-                    w.extend([0] * (s - len(w)))
-                    out[pos] = np.asarray(w[:s], np.uint32)
-                    pos += 1
+                    rows = gstarts[cols] + i
+                    out[rows, :len(key)] = np.asarray(key, np.uint32)
+                    out[rows, len(key):len(key) + nl] = words[int(off[v]):int(off[v]) + nl, n_lru + cols].T
             if n_lru and K:
-                gstart = starts + add_cnt
+                gstart = gstarts + add_cnt
                 rep = cnt_gen
                 tot = int(rep.sum())
                 if tot:
@@ -426,4 +438,4 @@ class CandidateGenerator:
             epos += el.size
         mb = ModelBatch(lru.var_widths, words, lru.funcs, eptr, np.concatenate(ew_chunks), ebase,
                         np.concatenate(el_chunks), elb, 0)
-        return CandidateSet(mb, n_lru, base, patches, syms, lru_models)
+        return CandidateSet(mb, n_lru, base, block_of, [p for p, _ in blocks], syms, lru_models)

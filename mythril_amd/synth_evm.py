@@ -750,6 +750,64 @@ def fork_workload(n_queries: int, n_models: int, seed: int = 8, n_tx: int = 3,
     return exprs, records, parents
 
 
+def fork_stream_workload(n_forks: int, n_models: int, seed: int = 21, n_tx: int = 3,
+                         checks_per_tx: Tuple[int, int] = (3, 6)):
+    """The per-fork check of svm.py:351-358 with a KNOWN witness for every successor, for the
+    "z3 calls avoided" leg: each fork takes a path a cached model satisfies (evm_path over that
+    model's witness) and branches on the last call's THIRD ABI argument (calldata bytes 68..99, a
+    ``require(arg == c)``, ``if (arg < c)`` or flag-byte test; the path never reads those bytes).
+    One successor is satisfied by the parent model (a quick-sat hit); the other is satisfiable
+    too, by the parent's witness with the argument set and the calldata size raised to 100 (the
+    bytes between the old size and 68 zeroed, so the path's words read the same): the model an
+    SMT solver would return, which get_model then caches (model.py:124-126).
+
+    Returns ``(states, witnesses, records)``: per successor its conjunct list and a satisfying
+    Model (None never occurs: every successor is satisfiable), and the cached models (MRU
+    first)."""
+    import copy
+    rng = np.random.Generator(np.random.PCG64(seed))
+    models = EvmModels(seed, n_models, n_tx)
+    records, wits = [], []
+    for m in range(n_models):
+        w = models.witness(m)
+        w["sender"] = [ACTORS[int(rng.integers(3))] if s not in ACTORS else s for s in w["sender"]]
+        wits.append(w)
+        records.append(evm_model_record(w, n_tx))
+    tx = _Tx(n_tx)
+    arg = tx.word(68)
+    states, witnesses = [], []
+    for f in range(n_forks):
+        p = int(rng.integers(n_models))
+        path = evm_path(rng, dict(wits[p]), n_tx, checks_per_tx)
+        conj = list(path.args) if path.kind == S.AND else [path]
+
+        def witness(value: int):
+            w = copy.deepcopy(wits[p])
+            k = n_tx - 1
+            b = list(w["bytes"][k]) + [0] * max(0, 100 - len(w["bytes"][k]))
+            for i in range(min(w["cds"][k], 68), 68):
+                b[i] = 0
+            for i in range(32):
+                b[68 + i] = (value >> (8 * (31 - i))) & 0xFF
+            w["bytes"][k] = b
+            w["cds"][k] = 100
+            return evm_model_record(w, n_tx)
+
+        kind = int(rng.integers(3))
+        if kind == 0:      # require(arg == c): the parent's argument (0) differs
+            c = int(rng.integers(1, 1 << 32))
+            cond, sat_value = S.Extract(31, 0, arg) == c, c
+        elif kind == 1:    # if (arg < c): the parent (0) takes the branch, the other side needs arg >= c
+            c = int(rng.integers(1, 1 << 16))
+            cond, sat_value = S.Not(S.ULT(arg, S.BitVecVal(c, 256))), c
+        else:              # a flag byte of the argument
+            c = int(rng.integers(1, 256))
+            cond, sat_value = S.Extract(7, 0, arg) == c, c
+        states += [conj + [S.Not(cond)], conj + [cond]]
+        witnesses += [records[p], witness(sat_value)]
+    return states, witnesses, records
+
+
 def fork_children(parents: Sequence[S.Term], n_tx: int = 3, seed: int = 9) -> List[S.Term]:
     """The two successors of a JUMPI after each parent path (svm.py:351-358): ``parent + cond``
     and ``parent + Not(cond)``, with ``cond`` a branch condition on the last transaction's

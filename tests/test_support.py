@@ -468,3 +468,37 @@ def test_resident_models_are_not_reuploaded():
     assert eng.uploads == 1
     eng.rows(q, ms + [Model({"x": 0})])
     assert eng.uploads == 2
+
+
+def test_fork_stream_witnesses_and_both_candidate_arms(fresh):
+    """bench.py's "z3 calls avoided" stream (synth_evm.fork_stream_workload): every successor's
+    known witness satisfies it (checked by the independent term evaluator), the solver stand-in
+    returns it and get_model caches it like z3's model (model.py:124-126) — in BOTH arms — and
+    generated candidates then avoid more solver calls than quick-sat alone, with every state
+    still possible."""
+    import term_eval
+    from mythril_amd.synth_evm import fork_stream_workload
+    states, wits, recs = fork_stream_workload(24, 60, seed=21)
+    assert all(term_eval.is_true(S.And(*st), w) for st, w in zip(states, wits))
+    res = {}
+    for cand in (False, True):
+        sp.reset_caches()
+        sp.model_cache = sp.ModelCache(OracleEngine())
+        solver = sp.WitnessSolver(states, wits)
+        sp.set_solver_backend(solver)
+        saved = sp.args.quick_sat_candidates, sp.args.quick_sat_candidate_budget
+        sp.args.quick_sat_candidates, sp.args.quick_sat_candidate_budget = cand, 20000
+        try:
+            for m in reversed(recs):
+                sp.model_cache.put(m, 1)
+            alive = sp.is_possible_batch([sp.Constraints(st) for st in states])
+        finally:
+            sp.args.quick_sat_candidates, sp.args.quick_sat_candidate_budget = saved
+        assert all(alive)
+        assert solver.calls == sp.counters["solver_calls"]
+        # every solver answer entered the LRU (it holds at most 100 models)
+        lru = list(sp.model_cache.model_cache.lru_cache.keys())
+        assert len(lru) == min(100, len(recs) + solver.calls + sp.counters["candidate_answers"])
+        res[cand] = dict(sp.counters)
+    assert res[True]["solver_calls"] < res[False]["solver_calls"]
+    assert res[True]["get_model_calls"] == res[False]["get_model_calls"] == len(states)
