@@ -235,8 +235,15 @@ class VerdictEngine:
         self.timing = dict.fromkeys(self.STAGES, 0.0)
         self.incremental = IncrementalLowering()
         self.conjuncts = ConjunctRows()
-        self.stats = {"conjuncts_evaluated": 0, "conjuncts_cached": 0, "whole_query_batches": 0}
+        self.stats = {"conjuncts_evaluated": 0, "conjuncts_cached": 0, "whole_query_batches": 0,
+                      "conjunct_batches_reused": 0}
         self._resident = None   # (model key, evaluator upload_seq) of the batch on the device
+        # the last compiled batch of conjunct tapes: (DAG generation, sorted roots, CompiledTapes).
+        # A model inserted mid-batch (a solver answer, model.py:125) needs the still-pending
+        # conjuncts under it alone; they are a subset of what the previous launch compiled, so
+        # that compiled batch is launched again (all of it: the extra rows are cached too) instead
+        # of compiling the subset (~4 ms per fill on the fork stream, profiles/r04k)
+        self._conj_ct = None
 
     @property
     def evaluator(self):
@@ -280,6 +287,16 @@ class VerdictEngine:
             ev.set_option(ev.OPT_LATENCY_WAVES, waves)
         return prev
 
+    def _compile(self, tb):
+        """Device hook: the compiled batch ``_evaluate`` accepts in place of ``tb``."""
+        return self.evaluator.compile(tb)
+
+    @staticmethod
+    def _free(ct) -> None:
+        free = getattr(ct, "free", None)
+        if free is not None:
+            free()
+
     def _evaluate(self, tb, mb, upload: bool = True):
         """Device hook: (verdicts [n_tapes, M], first hits) of ``tb`` over ``mb``; ``upload``
         False when ``mb`` is already the evaluator's resident batch."""
@@ -289,14 +306,17 @@ class VerdictEngine:
         if upload:
             ev.upload_models(mb)
         t1 = clock()
-        ct = ev.compile(tb)
+        from .evaluator import CompiledTapes
+        own = not isinstance(tb, CompiledTapes)   # (a compiled batch the caller keeps)
+        ct = ev.compile(tb) if own else tb
         t2 = clock()
         prev = self._latency_mode(ev, self.latency_waves)
         try:
             v, fh = ev.verdicts(ct)
         finally:
             self._latency_mode(ev, prev)   # (the caller's own setting, not 0)
-            ct.free()
+            if own:
+                ct.free()
         self.timing["upload"] += t1 - t0
         self.timing["compile"] += t2 - t1
         self.timing["evaluate"] += clock() - t2
@@ -401,14 +421,29 @@ class VerdictEngine:
         if n_unk:
             from .lower import DagBatch
             todo = uroots[unk]
-            tb = DagBatch(db.nodes, db.consts, np.arange(n_unk + 1, dtype=np.int64), todo)
-            v, fh = self._evaluate_resident(tb, dev_slots)
-            cache.R[np.ix_(urows[unk], np.asarray(dev_slots, np.int64))] = v.astype(np.int8)
+            prev = self._conj_ct
+            gen = (inc.dag_gen, inc.slot_epoch)
+            if prev is not None and prev[0] == gen and len(prev[1]) <= 4 * n_unk + 64 and \
+                    np.isin(todo, prev[1], assume_unique=True).all():
+                todo, ct = prev[1], prev[2]
+                self.stats["conjunct_batches_reused"] += 1
+            else:
+                if prev is not None:
+                    self._free(prev[2])
+                    self._conj_ct = None
+                tb = DagBatch(db.nodes, db.consts, np.arange(n_unk + 1, dtype=np.int64), todo)
+                t2 = clock()
+                ct = self._compile(tb)
+                self.timing["compile"] += clock() - t2
+                self._conj_ct = (gen, todo, ct)
+            v, fh = self._evaluate_resident(ct, dev_slots)
+            trows = cache.rows_for(todo, int(slots.max()) + 1)
+            cache.R[np.ix_(trows, np.asarray(dev_slots, np.int64))] = v.astype(np.int8)
             for x in todo[fh == -2].tolist():
                 cache.bad.add(int(x))
-            self.stats["conjuncts_evaluated"] += n_unk
+            self.stats["conjuncts_evaluated"] += len(todo)
             self.launches += 1
-            self.pairs += n_unk * len(dev_slots)
+            self.pairs += len(todo) * len(dev_slots)
         # each query: the AND of its conjuncts' rows, in the caller's model order
         occ = cache.R[np.ix_(urows[inv], slots)] > 0
         offs = db.root_offsets
@@ -581,9 +616,18 @@ class ModelCache:
             self._cand[e] = r
 
     def candidate_for(self, expr):
+        """A generated candidate satisfying ``expr`` (a quick-sat miss), or False.  A miss the
+        batch prefetch did not foresee (its LRU hit was evicted by a model inserted meanwhile) is
+        searched together with up to 63 other pending conjunctions not searched yet, whose answers
+        wait in the prefetch table (a candidate is any satisfying model: an older LRU order as its
+        base changes which one is found, never whether it satisfies)."""
         if expr in self._cand:
             return self._cand.pop(expr)
-        return self.candidates([expr])[0]
+        more = [e for e in self._pending if e is not expr and e not in self._cand and isinstance(e, S.Term)][:63]
+        res = self.candidates([expr] + more)
+        for e, r in zip(more, res[1:]):
+            self._cand[e] = r
+        return res[0]
 
     def discard(self, exprs: Iterable) -> None:
         """Forget prefetched rows of conjunctions whose check_quick_sat never ran (their answer
