@@ -217,11 +217,13 @@ class CandidateSet:
 class CandidateGenerator:
     """Generates up to ``max_candidates`` candidates for a batch of conjunctions (seeded)."""
 
-    def __init__(self, max_candidates: int = 100_000, seed: int = 0, random_frac: float = 0.05, per_query: int = 16):
+    def __init__(self, max_candidates: int = 100_000, seed: int = 0, random_frac: float = 0.05, per_query: int = 16,
+                 fill: bool = False):
         self.max_candidates = int(max_candidates)
         self.rng = np.random.Generator(np.random.PCG64(seed))
         self.random_frac = random_frac
         self.per_query = int(per_query)   # patches per query (each over every base model)
+        self.fill = fill                  # fill max_candidates with random mixes (throughput runs)
 
     # ------------------------------------------------------------ targets
     def _targets(self, db, syms):
@@ -282,15 +284,17 @@ class CandidateGenerator:
         base_ids = np.arange(n_lru, dtype=np.int64) if n_lru else np.full(1, -1, np.int64)
         nb = len(base_ids)
         n_q = sum(1 for o in per_query if o)
-        budget = max(0, min(self.max_candidates - n_lru, self.per_query * nb * max(n_q, 1)))
+        budget = max(0, self.max_candidates - n_lru)
+        if not self.fill:
+            budget = min(budget, self.per_query * nb * max(n_q, 1))
         blocks: List[Tuple[Tuple, np.ndarray]] = []
         total = [0]
         seen = set()
 
-        def add(patch: Tuple, bases: np.ndarray = base_ids) -> bool:
+        def add(patch: Tuple, bases: np.ndarray = base_ids, dedupe: bool = True) -> bool:
             if total[0] + len(bases) > budget:
                 return False
-            if bases is base_ids:
+            if dedupe:
                 if patch in seen:
                     return True
                 seen.add(patch)
@@ -319,9 +323,12 @@ class CandidateGenerator:
         singles = [p for opts in per_query for o in opts for p in o]
         plain = [v for v, w in enumerate(syms.var_widths) if w > 0 and v not in syms.derived
                  and v not in syms.hoisted_vars]
-        n_rand = int(total[0] * self.random_frac)
-        for _ in range(n_rand):
-            bases = base_ids[rng.integers(0, nb, 1)]
+        # (each random patch over every base model, like the directed ones)
+        n_rand = budget - total[0] if self.fill else int(total[0] * self.random_frac)
+        for _ in range(-(-n_rand // nb)):
+            bases = base_ids if total[0] + nb <= budget else base_ids[:budget - total[0]]
+            if not len(bases):
+                break
             if singles and rng.random() < 0.7:
                 k = int(rng.integers(1, 4))
                 patch = tuple(q for i in rng.integers(0, len(singles), k) for q in singles[int(i)])
@@ -333,7 +340,7 @@ class CandidateGenerator:
                 patch = ((v, 0, w, val),)
             else:
                 break
-            if not add(patch, bases):
+            if not add(patch, bases, dedupe=False):
                 break
         return self._serialize(lru_batch, blocks, syms, lru_models)
 

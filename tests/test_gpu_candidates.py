@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 def test_candidates_reach_1e5_and_every_hit_rechecks(evaluator):
     exprs, recs, parents = fork_workload(48, 100, seed=11)
     eng = sp.VerdictEngine(evaluator)
-    fh, cs = eng.candidate_first_hits(exprs, recs, CandidateGenerator(100_000, seed=3))
+    fh, cs = eng.candidate_first_hits(exprs, recs, CandidateGenerator(100_000, seed=3, fill=True))
     assert cs.batch.n_models == 100_000 and cs.n_lru == 100
     tb = eng.incremental.lower(exprs)[0].to_tapes()
     lru = fh < cs.n_lru
