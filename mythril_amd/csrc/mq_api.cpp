@@ -1565,7 +1565,7 @@ static int tapes_upload_one(mq_ctx* c, int32_t n_tapes, const std::vector<Compil
   std::vector<std::vector<uint32_t>> qextra(n_tapes);
   std::unique_ptr<PhaseTimer> pt(new PhaseTimer(&c->host_t[1]));
   if (c->qsa_ready)
-    parallel_for(n_tapes, 8, [&](int, int64_t b, int64_t e) {
+    parallel_for(n_tapes, 32, [&](int, int64_t b, int64_t e) {
       for (int64_t t = b; t < e; t++)
         if (ct[t].supported && ct[t].L == 8 && ct[t].n_temps <= kQsaMaxTemps)
           qsa_ok[t] = qsa_translate(c, 1, false, ct[t], nullptr, &qextra[t]) ? 1 : 0;
@@ -2140,7 +2140,7 @@ static void plan_stage(const mq_ctx* c, const std::vector<int64_t>& pushes, cons
 // (Re)translate the QSA-eligible tapes for the current model batch (variable rows, function
 // table): the P kernel when every variable a tape reads is preloaded, the G kernel otherwise.
 // If one tape does not translate, the whole group runs on the HIP C++ kernel for this batch.
-static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
+static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
   if (T->qsa_gen == c->models_gen) return MQ_OK;
   T->qsa_gen = c->models_gen;
   T->qsa_live = false;
@@ -2161,10 +2161,14 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
     }
     return true;
   };
-  parallel_for(nq, 8, [&](int, int64_t b, int64_t e) {
-    for (int64_t i = b; i < e; i++)
-      on_p[i] = p_candidate(T->qct[i]) && qsa_translate(c, 0, true, T->qct[i], nullptr, nullptr) ? 1 : 0;
-  });
+  // (a latency-bound launch runs everything on G, one tape per wave: no P attempt.  Chunks of
+  // 32 tapes: a drop-in batch of a few conjunct tapes is translated on the calling thread, which
+  // is cheaper than waking the pool)
+  if (!latency)
+    parallel_for(nq, 32, [&](int, int64_t b, int64_t e) {
+      for (int64_t i = b; i < e; i++)
+        on_p[i] = p_candidate(T->qct[i]) && qsa_translate(c, 0, true, T->qct[i], nullptr, nullptr) ? 1 : 0;
+    });
   std::vector<int64_t> pushes(c->var_nl_h.size(), 0);
   for (size_t i = 0; i < T->qct.size(); i++) {
     if (on_p[i]) continue;
@@ -2207,7 +2211,7 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T) {
   std::vector<std::vector<uint32_t>> trs(nq);
   std::vector<char> kind_of(nq, 0);
   std::atomic<bool> g_fail{false};
-  parallel_for(nq, 8, [&](int, int64_t b, int64_t e) {
+  parallel_for(nq, 32, [&](int, int64_t b, int64_t e) {
     std::vector<uint32_t> ex;
     for (int64_t i = b; i < e && !g_fail.load(std::memory_order_relaxed); i++) {
       if (on_p[i] && qsa_translate(c, 0, true, T->qct[i], &trs[i], &ex)) continue;
@@ -2395,7 +2399,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     if (nodes > latency_asm_nodes()) use_qsa = false;
   }
   if (use_qsa) {
-    const int rc = qsa_prepare(c, T);
+    const int rc = qsa_prepare(c, T, latency);
     if (rc) return rc;
     use_qsa = T->qsa_live;
   }
