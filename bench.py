@@ -483,10 +483,12 @@ def main():
     n_cols = int(getattr(ct, "n_columns", 0))
     cols_g, cols_live = ct.column_asm_split() if n_cols else (0, False)
     kcols = int(ct.keccak_columns()) if n_cols else 0
+    kpreds = int(ct.keccak_predicate_columns()) if n_cols else 0
     kernel_split = {"tapes": tb.n_tapes, "tapes_p": n_p, "tapes_g": n_g,
                     "tapes_cpp": tb.n_tapes - ((n_p + n_g) if asm_live else 0),
                     "columns": n_cols, "columns_g": cols_g if cols_live else 0, "columns_keccak": kcols,
-                    "columns_cpp": n_cols - kcols - (cols_g if cols_live else 0)}
+                    "columns_keccak_predicates": kpreds,
+                    "columns_cpp": n_cols - kcols - kpreds - (cols_g if cols_live else 0)}
 
     ev.counters(reset=True)
     # HIP event pair recorded by libmq on `stream` around the evaluation kernel(s) of each launch

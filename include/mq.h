@@ -334,6 +334,12 @@ int mq_tapes_column_split(mq_tapes* tapes, int32_t* n_asm, int32_t* live);
    Introspection for tests and the bench (MQ_NO_KECCAK_COLUMNS=1 disables the path). */
 int mq_tapes_column_keccak(mq_tapes* tapes, int32_t* n_keccak_columns);
 
+/* The Bool columns the same kernel evaluates from the digests it computes: a keccak column
+   compared with a constant (h < c, h > c, h <= c, h >= c, h == c, low k bits of h zero — the
+   keccak manager's axioms, keccak_function_manager.py:150-179), their lane masks stored
+   directly (MQ_NO_KECCAK_PREDICATES=1 leaves them to the interpreters). */
+int mq_tapes_column_keccak_predicates(mq_tapes* tapes, int32_t* n_predicate_columns);
+
 /* After a launch: handler-kind histogram of the current assembly translation (which = 0: P
    tapes, 1: G tapes, 2: G column programs) into hist_out[cap]; each tape's program runs once per
    (tape, model) pair, so these are the dispatches per pair summed over tapes.  pairs_out

@@ -84,10 +84,41 @@ __global__ __launch_bounds__(64) void keccak256_kernel(const uint8_t* __restrict
 // Keccak columns: grid.y = column, grid.x = 256-model blocks; the column's message layout is
 // uniform (scalar loads), the variable words are coalesced SoA rows.  The digest read big-endian
 // is the 256-bit value (mq.h MQ_OP_KECCAK), stored into the column's 8 variable rows.
+// h OP c over 8 little-endian limbs (unsigned)
+__device__ __forceinline__ bool kc_pred(const KcPred& p, const uint32_t (&h)[8]) {
+  if (p.kind == KP_LOWZ) {
+    bool z = true;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint32_t b = p.bits > 32u * i ? min(32u, p.bits - 32u * i) : 0u;
+      const uint32_t m = b >= 32 ? 0xFFFFFFFFu : ((1u << b) - 1u);
+      z = z && (h[i] & m) == 0u;
+    }
+    return z;
+  }
+  // lexicographic compare from the top limb: lt = h < c, eq = h == c
+  bool lt = false, eq = true;
+#pragma unroll
+  for (int i = 7; i >= 0; i--) {
+    lt = lt || (eq && h[i] < p.c[i]);
+    eq = eq && h[i] == p.c[i];
+  }
+  switch (p.kind) {
+    case KP_LT: return lt;
+    case KP_GT: return !lt && !eq;
+    case KP_GE: return !lt;
+    case KP_LE: return lt || eq;
+    default: return eq;
+  }
+}
+
 __global__ __launch_bounds__(256) void keccak_column_kernel(const KcCol* __restrict__ cols,
                                                             const KcMapEntry* __restrict__ map,
+                                                            const KcPred* __restrict__ preds,
                                                             uint32_t* __restrict__ vars, int64_t M,
-                                                            unsigned long long* __restrict__ counters) {
+                                                            unsigned long long* __restrict__ counters,
+                                                            uint64_t* __restrict__ bool_masks, int n_bool_masks,
+                                                            int bool_rows) {
   const KcCol col = cols[blockIdx.y];
   const int64_t m0 = (int64_t)blockIdx.x * 256;
   const int64_t m = m0 + threadIdx.x;
@@ -122,18 +153,33 @@ __global__ __launch_bounds__(256) void keccak_column_kernel(const KcCol* __restr
     if ((uint32_t)b == nblocks - 1u) A[16] ^= 0x8000000000000000ull;
     keccak_f(A);
   }
+  uint32_t h[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
     const uint64_t q = A[(7 - i) >> 1];
-    vars[(int64_t)(col.target_row + i) * M + m] = __builtin_bswap32((uint32_t)(((7 - i) & 1) ? (q >> 32) : q));
+    h[i] = __builtin_bswap32((uint32_t)(((7 - i) & 1) ? (q >> 32) : q));
+    vars[(int64_t)(col.target_row + i) * M + m] = h[i];
+  }
+  // the column's predicate columns from the digest in registers: the tile's lane mask (lane 0 of
+  // the wave = one 64-model tile stores it; lanes past M are inactive, so their bits are 0) and,
+  // when a HIP C++ kernel of the launch reads rows, the 0/1 row
+  for (uint32_t j = 0; j < col.n_pred; j++) {
+    const KcPred p = preds[col.pred_off + j];
+    const bool bit = kc_pred(p, h);
+    if (bool_rows) vars[(int64_t)p.row * M + m] = bit ? 1u : 0u;
+    if (p.mask >= 0) {
+      const unsigned long long b = __ballot(bit);
+      if ((threadIdx.x & 63) == 0) bool_masks[(m >> 6) * (int64_t)n_bool_masks + p.mask] = b;
+    }
   }
 }
 
-hipError_t launch_keccak_columns(const KcCol* cols, int n_cols, const KcMapEntry* map, uint32_t* vars, int64_t M,
-                                 unsigned long long* counters, hipStream_t st) {
+hipError_t launch_keccak_columns(const KcCol* cols, int n_cols, const KcMapEntry* map, const KcPred* preds,
+                                 uint32_t* vars, int64_t M, unsigned long long* counters, uint64_t* bool_masks,
+                                 int n_bool_masks, int bool_rows, hipStream_t st) {
   if (n_cols <= 0 || M <= 0) return hipSuccess;
   hipLaunchKernelGGL(keccak_column_kernel, dim3((unsigned)((M + 255) / 256), (unsigned)n_cols), dim3(256), 0, st, cols,
-                     map, vars, M, counters);
+                     map, preds, vars, M, counters, bool_masks, n_bool_masks, bool_rows);
   return hipGetLastError();
 }
 

@@ -335,16 +335,23 @@ struct mq_tapes {
     int32_t var;
     uint32_t nl, coff;
   };
+  struct KcPredHost {   // a Bool column h OP c evaluated from the keccak column's digest
+    int32_t target;
+    uint32_t kind, bits;
+    uint32_t c[8];
+  };
   struct KcHost {
     int32_t target;
-    uint32_t n_nodes, alg_ops;
+    uint32_t n_nodes, alg_ops;   // (its predicate columns' included)
     std::vector<KcPiece> pieces;
+    std::vector<KcPredHost> preds;
   };
   std::vector<KcHost> kc;
   std::vector<uint32_t> kc_consts;
   std::vector<std::pair<int, int>> kc_level;   // (first, count) in kc, per column level
   uint64_t kc_gen = ~0ull;                      // models_gen of the uploaded map
-  DevBuf kc_cols_dev, kc_map_dev;
+  DevBuf kc_cols_dev, kc_map_dev, kc_pred_dev;
+  std::vector<char> col_direct_mask;            // per column: its lane masks are stored by its kernel
   // multi-device context: the same batch compiled on each peer device (ctx->peers order)
   std::vector<mq_tapes*> peers;
   ~mq_tapes() {
@@ -1875,16 +1882,71 @@ static bool kc_match(const mq_tape_batch* progs, int32_t k, std::vector<mq_tapes
   return true;
 }
 
-static int set_columns_one(mq_tapes* T, const mq_tape_batch* progs, const int32_t* var_index, const int32_t* level,
+// A column program comparing a variable with a constant, as lower.py keccak_predicates makes
+// them (root ULT / EQ of a VAR and a CONST, possibly under NOT; or EQ(EXTRACT(k-1, 0, VAR), 0)):
+// the variable and the predicate, for the keccak column kernel.
+static bool kp_match(const mq_tape_batch* progs, int32_t k, int32_t* var, uint32_t* kind, uint32_t* bits,
+                     uint32_t (&c)[8]) {
+  const int64_t base = progs->tape_offsets[k];
+  const int64_t nn = progs->tape_offsets[k + 1] - base;
+  if (nn < 3 || nn > 5) return false;
+  const mq_node* nd = progs->nodes + base;
+  int64_t r = nn - 1;
+  bool neg = false;
+  if (nd[r].op == MQ_OP_NOT) {
+    neg = true;
+    if (nd[r].a >= (uint32_t)r) return false;
+    r = nd[r].a;
+  }
+  const mq_node& p = nd[r];
+  if ((p.op != MQ_OP_ULT && p.op != MQ_OP_EQ) || p.a >= (uint32_t)r || p.b >= (uint32_t)r) return false;
+  const mq_node &x = nd[p.a], &y = nd[p.b];
+  auto konst = [&](const mq_node& n) -> bool {
+    if (n.op != MQ_OP_CONST || n.width == 0 || n.width > 256 || (int64_t)n.a + (n.width + 31) / 32 > progs->n_const_words)
+      return false;
+    for (int i = 0; i < 8; i++) c[i] = i < (int)((n.width + 31) / 32) ? progs->const_words[n.a + i] : 0u;
+    if (n.width % 32) c[(n.width - 1) / 32] &= (1u << (n.width % 32)) - 1u;
+    return true;
+  };
+  *bits = 0;
+  if (p.op == MQ_OP_EQ && x.op == MQ_OP_EXTRACT && !neg && x.c == 0 && x.a < p.a && nd[x.a].op == MQ_OP_VAR &&
+      nd[x.a].width == 256 && konst(y)) {   // EQ(EXTRACT(k-1, 0, h), 0): the low k bits are zero
+    for (int i = 0; i < 8; i++)
+      if (c[i]) return false;
+    *var = (int32_t)nd[x.a].a;
+    *kind = KP_LOWZ;
+    *bits = x.width;
+    return x.width > 0 && x.width <= 256;
+  }
+  bool h_left;
+  if (x.op == MQ_OP_VAR && x.width == 256 && konst(y)) h_left = true;
+  else if (y.op == MQ_OP_VAR && y.width == 256 && konst(x)) h_left = false;
+  else return false;
+  *var = (int32_t)(h_left ? x.a : y.a);
+  if (p.op == MQ_OP_EQ) {
+    if (neg) return false;
+    *kind = KP_EQ;
+  } else if (h_left) {
+    *kind = neg ? KP_GE : KP_LT;   // h < c  /  not (h < c)
+  } else {
+    *kind = neg ? KP_LE : KP_GT;   // c < h  /  not (c < h)
+  }
+  return true;
+}
+
+static int set_columns_one(mq_tapes* T, const mq_tape_batch* progs, const int32_t* var_index, const int32_t* level_in,
                            int32_t n_columns) {
   mq_ctx* c = T->ctx;
   if (!c) return MQ_ERR_STATE;   // the context was destroyed
   HIPCHK(hipSetDevice(c->device));
   T->clevels.clear();
   T->col_var.assign(var_index, var_index + n_columns);
-  T->col_level.assign(level, level + n_columns);
+  T->col_level.assign(level_in, level_in + n_columns);
+  T->col_direct_mask.assign(n_columns, 0);
   T->bmask_gen = ~0ull;
   T->col_width.assign(n_columns, 0);
+  T->kc.clear();
+  T->kc_level.clear();
   if (n_columns == 0) return MQ_OK;
   CompileLimits lim;
   lim.g_depth = kQsaStackG;
@@ -1893,17 +1955,87 @@ static int set_columns_one(mq_tapes* T, const mq_tape_batch* progs, const int32_
   parallel_for(n_columns, 16, [&](int, int64_t b, int64_t e) {
     for (int64_t k = b; k < e; k++) ct[k] = compile_tape(progs, (int32_t)k, lim);
   });
-  int max_level = 0;
   for (int k = 0; k < n_columns; k++) {
     if (!ct[k].supported) {
       g_last_error = "column program " + std::to_string(k) + " unsupported: " + ct[k].why;
       return MQ_ERR_TAPE;
     }
-    if (level[k] < 0) return MQ_ERR_ARG;
-    max_level = std::max(max_level, (int)level[k]);
+    if (level_in[k] < 0) return MQ_ERR_ARG;
     const int64_t last = progs->tape_offsets[k + 1] - 1;
     T->col_width[k] = progs->nodes[last].width;
   }
+  // keccak columns (MQ_NO_KECCAK_COLUMNS=1: leave them to the interpreters), and the predicate
+  // columns over them (lower.py keccak_predicates), which the keccak column kernel evaluates
+  // from the digest it computed (MQ_NO_KECCAK_PREDICATES=1: on the interpreters)
+  std::vector<char> kcm(n_columns, 0), kpm(n_columns, 0);
+  std::vector<mq_tapes::KcPiece> kc_pieces_tmp;
+  std::vector<std::vector<mq_tapes::KcPiece>> kpieces(n_columns);
+  std::unordered_map<int32_t, int> kcol_of_var;   // keccak column target variable -> column
+  T->kc_consts.clear();
+  if (!std::getenv("MQ_NO_KECCAK_COLUMNS")) {
+    for (int k = 0; k < n_columns; k++)
+      if (kc_match(progs, k, kpieces[k], T->kc_consts)) {
+        kcm[k] = 1;
+        kcol_of_var[var_index[k]] = k;
+      }
+  }
+  std::vector<int> kp_of(n_columns, -1);   // predicate column -> its keccak column
+  std::vector<mq_tapes::KcPredHost> kp_host(n_columns);
+  if (!kcol_of_var.empty() && !std::getenv("MQ_NO_KECCAK_PREDICATES")) {
+    for (int k = 0; k < n_columns; k++) {
+      if (kcm[k] || T->col_width[k] != 0) continue;
+      int32_t v;
+      mq_tapes::KcPredHost ph{};
+      if (!kp_match(progs, k, &v, &ph.kind, &ph.bits, ph.c)) continue;
+      auto it = kcol_of_var.find(v);
+      if (it == kcol_of_var.end()) continue;
+      ph.target = var_index[k];
+      kp_of[k] = it->second;
+      kp_host[k] = ph;
+      kpm[k] = 1;
+    }
+  }
+  // levels from the programs: a column is one level past the deepest column it reads, and a
+  // predicate column sits at its keccak column's level (computed in the same launch); otherwise
+  // this is the lowering's own level (lower.py lower_batch), which the C-ABI also passes
+  std::vector<int> level(n_columns, -1);
+  {
+    std::unordered_map<int32_t, int> col_of_var;
+    for (int k = 0; k < n_columns; k++) col_of_var[var_index[k]] = k;
+    std::vector<std::vector<int>> reads(n_columns);
+    for (int k = 0; k < n_columns; k++)
+      for (int64_t i = progs->tape_offsets[k]; i < progs->tape_offsets[k + 1]; i++) {
+        const mq_node& n = progs->nodes[i];
+        if (n.op != MQ_OP_VAR) continue;
+        auto it = col_of_var.find((int32_t)n.a);
+        if (it != col_of_var.end() && it->second != k) reads[k].push_back(it->second);
+      }
+    std::vector<char> state(n_columns, 0);   // 1 = on the DFS stack
+    std::function<int(int)> lv = [&](int k) -> int {
+      if (level[k] >= 0) return level[k];
+      if (state[k]) throw std::runtime_error("cyclic columns");
+      state[k] = 1;
+      int l;
+      if (kp_of[k] >= 0) {
+        l = lv(kp_of[k]);
+      } else {
+        l = 0;
+        for (int j : reads[k]) l = std::max(l, lv(j) + 1);
+      }
+      state[k] = 0;
+      return level[k] = l;
+    };
+    try {
+      for (int k = 0; k < n_columns; k++) lv(k);
+    } catch (const std::exception&) {
+      g_last_error = "hoisted columns read each other in a cycle";
+      return MQ_ERR_ARG;
+    }
+  }
+  int max_level = 0;
+  for (int k = 0; k < n_columns; k++) max_level = std::max(max_level, level[k]);
+  T->col_level.assign(level.begin(), level.end());
+  T->col_direct_mask.assign(kpm.begin(), kpm.end());
   std::vector<uint32_t> prog, consts;
   std::vector<GDesc> descs;
   // G assembly eligibility is structural here, as for tapes (mq_tapes_upload).  Columns shorter
@@ -1913,32 +2045,34 @@ static int set_columns_one(mq_tapes* T, const mq_tape_batch* progs, const int32_
   // MQ_G_COL_MIN_NODES overrides the threshold.
   int64_t min_nodes = kColAsmMinNodes;
   if (const char* e = std::getenv("MQ_G_COL_MIN_NODES")) min_nodes = std::atol(e);
-  // keccak columns, level by level (MQ_NO_KECCAK_COLUMNS=1: leave them to the interpreters)
-  std::vector<char> kcm(n_columns, 0);
+  // keccak columns level by level, each with its predicate columns
   T->kc.clear();
-  T->kc_consts.clear();
   T->kc_gen = ~0ull;
   T->kc_level.assign((size_t)max_level + 1, {0, 0});
-  if (!std::getenv("MQ_NO_KECCAK_COLUMNS")) {
-    for (int lv = 0; lv <= max_level; lv++) {
-      T->kc_level[lv].first = (int)T->kc.size();
-      for (int k = 0; k < n_columns; k++) {
-        if (level[k] != lv) continue;
-        mq_tapes::KcHost h;
-        if (!kc_match(progs, k, h.pieces, T->kc_consts)) continue;
-        h.target = var_index[k];
-        h.n_nodes = ct[k].n_nodes;
-        h.alg_ops = (uint32_t)std::min(ct[k].alg_ops, 4.0e9);
-        T->kc.push_back(std::move(h));
-        kcm[k] = 1;
-      }
-      T->kc_level[lv].second = (int)T->kc.size() - T->kc_level[lv].first;
+  for (int lv = 0; lv <= max_level; lv++) {
+    T->kc_level[lv].first = (int)T->kc.size();
+    for (int k = 0; k < n_columns; k++) {
+      if (level[k] != lv || !kcm[k]) continue;
+      mq_tapes::KcHost h;
+      h.pieces = std::move(kpieces[k]);
+      h.target = var_index[k];
+      double nodes = ct[k].n_nodes, ops = ct[k].alg_ops;
+      for (int j = 0; j < n_columns; j++)
+        if (kp_of[j] == k) {
+          h.preds.push_back(kp_host[j]);
+          nodes += ct[j].n_nodes;
+          ops += ct[j].alg_ops;
+        }
+      h.n_nodes = (uint32_t)std::min(nodes, 4.0e9);
+      h.alg_ops = (uint32_t)std::min(ops, 4.0e9);
+      T->kc.push_back(std::move(h));
     }
+    T->kc_level[lv].second = (int)T->kc.size() - T->kc_level[lv].first;
   }
   std::vector<char> gq(n_columns, 0);
   if (c->qsa_ready)
     for (int k = 0; k < n_columns; k++)
-      gq[k] = !kcm[k] && ct[k].L == 8 && !ct[k].keccak && ct[k].n_temps <= kQsaMaxTemps &&
+      gq[k] = !kcm[k] && !kpm[k] && ct[k].L == 8 && !ct[k].keccak && ct[k].n_temps <= kQsaMaxTemps &&
               (int64_t)ct[k].n_nodes >= min_nodes && qsa_translate(c, 1, false, ct[k], nullptr, nullptr);
   T->cq_ct.clear();
   T->cq_var.clear();
@@ -1956,7 +2090,7 @@ static int set_columns_one(mq_tapes* T, const mq_tape_batch* progs, const int32_
       if (pass != 0) v.begin = (int)descs.size();
       for (int k = 0; k < n_columns; k++) {
         const CompiledTape& x = ct[k];
-        if (level[k] != lv || kcm[k]) continue;
+        if (level[k] != lv || kcm[k] || kpm[k]) continue;
         if (pass == -1 && !gq[k]) continue;
         if (pass >= 0 && (gen_kind(x) != pass || (pass == 0 && gq[k]))) continue;
         GDesc d{};
@@ -2460,8 +2594,9 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       const int v = T->col_var[i];
       if (T->col_width[i] == 0 && v < (int)c->bmask_of_var.size() && c->bmask_of_var[v] >= 0 &&
           T->col_level[i] < (int)T->clevels.size()) {
-        T->lvl_bmask_h[T->col_level[i]].push_back(c->bmask_of_var[v]);
-        if (!on_g[v]) T->lvl_bmask_cpp_h[T->col_level[i]].push_back(c->bmask_of_var[v]);
+        const bool direct = i < T->col_direct_mask.size() && T->col_direct_mask[i];   // the keccak kernel stores it
+        if (!direct) T->lvl_bmask_h[T->col_level[i]].push_back(c->bmask_of_var[v]);
+        if (!on_g[v] && !direct) T->lvl_bmask_cpp_h[T->col_level[i]].push_back(c->bmask_of_var[v]);
       }
     }
     T->lvl_bmask.resize(T->clevels.size());
@@ -2479,6 +2614,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     // the keccak columns' message maps under this model batch's variable rows
     std::vector<KcCol> cols;
     std::vector<KcMapEntry> map;
+    std::vector<KcPred> preds;
     for (const auto& h : T->kc) {
       if (h.target < 0 || h.target >= c->n_vars || c->var_nl_h[h.target] != 8) {
         g_last_error = "keccak column target is not a 256-bit variable of the uploaded model batch";
@@ -2499,10 +2635,27 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
                                    : KcMapEntry{~0u, T->kc_consts[p.coff + (uint32_t)l]});
       }
       kc.nwords = (uint32_t)map.size() - kc.map_off;
+      kc.pred_off = (uint32_t)preds.size();
+      for (const auto& ph : h.preds) {
+        if (ph.target < 0 || ph.target >= c->n_vars || c->var_width[ph.target] != 0) {
+          g_last_error = "keccak predicate column target is not a Bool variable of the uploaded model batch";
+          return MQ_ERR_ARG;
+        }
+        KcPred kp{};
+        kp.kind = ph.kind;
+        kp.bits = ph.bits;
+        kp.row = c->var_off_h[ph.target];
+        kp.mask = ph.target < (int)c->bmask_of_var.size() ? c->bmask_of_var[ph.target] : -1;
+        std::memcpy(kp.c, ph.c, sizeof(kp.c));
+        preds.push_back(kp);
+      }
+      kc.n_pred = (uint32_t)h.preds.size();
       cols.push_back(kc);
     }
     HIPCHK(T->kc_cols_dev.upload(cols.data(), cols.size(), st));
     HIPCHK(T->kc_map_dev.upload(map.data(), map.size(), st));
+    if (preds.empty()) HIPCHK(T->kc_pred_dev.ensure(sizeof(KcPred)));
+    else HIPCHK(T->kc_pred_dev.upload(preds.data(), preds.size(), st));
     HIPCHK(hipStreamSynchronize(st));
     T->kc_gen = c->models_gen;
   }
@@ -2521,8 +2674,10 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     if (li < T->kc_level.size() && T->kc_level[li].second > 0) {
       HIPCHK(start_timer());
       HIPCHK(launch_keccak_columns(T->kc_cols_dev.as<KcCol>() + T->kc_level[li].first, T->kc_level[li].second,
-                                   T->kc_map_dev.as<KcMapEntry>(), const_cast<uint32_t*>(c->vars.as<uint32_t>()), c->M,
-                                   c->counters.as<unsigned long long>(), st));
+                                   T->kc_map_dev.as<KcMapEntry>(), T->kc_pred_dev.as<KcPred>(),
+                                   const_cast<uint32_t*>(c->vars.as<uint32_t>()), c->M,
+                                   c->counters.as<unsigned long long>(), c->bmasks.as<uint64_t>(), c->n_bmask,
+                                   bool_rows ? 1 : 0, st));
     }
     const mq_tapes::Variant v8 = use_cq ? cut_front(lv.v[0], lv.v8q) : lv.v[0];
     if (use_cq && lv.v8q > 0) {
@@ -2985,6 +3140,14 @@ int mq_tapes_column_split(mq_tapes* T, int32_t* n_asm, int32_t* live) {
 int mq_tapes_column_keccak(mq_tapes* T, int32_t* n_keccak_columns) {
   if (!T || !n_keccak_columns) return MQ_ERR_ARG;
   *n_keccak_columns = (int32_t)T->kc.size();
+  return MQ_OK;
+}
+
+int mq_tapes_column_keccak_predicates(mq_tapes* T, int32_t* n_predicate_columns) {
+  if (!T || !n_predicate_columns) return MQ_ERR_ARG;
+  size_t n = 0;
+  for (const auto& h : T->kc) n += h.preds.size();
+  *n_predicate_columns = (int32_t)n;
   return MQ_OK;
 }
 

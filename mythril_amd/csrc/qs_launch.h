@@ -128,12 +128,25 @@ struct KcCol {
   uint32_t map_off;     // first map entry of the column
   uint32_t nwords;      // message words (<= 64: at most 2048 bits, two 136-byte blocks)
   uint32_t target_row;  // first of the 8 rows of the column's variable
-  uint32_t n_nodes;     // DAG nodes of the column program (metric)
-  uint32_t alg_ops;     // SURVEY §8(d) algorithmic ops of the program (metric)
-  uint32_t pad[3];
+  uint32_t n_nodes;     // DAG nodes of the column program (metric; + its predicates')
+  uint32_t alg_ops;     // SURVEY §8(d) algorithmic ops of the program (metric; + its predicates')
+  uint32_t pred_off;    // its predicate columns (KcPred) evaluated from the digest in registers
+  uint32_t n_pred;
+  uint32_t pad;
 };
-hipError_t launch_keccak_columns(const KcCol* cols, int n_cols, const KcMapEntry* map, uint32_t* vars, int64_t M,
-                                 unsigned long long* counters, hipStream_t st);
+// A Bool column comparing a keccak column h with a constant (lower.py keccak_predicates,
+// mq_api.cpp kp_match): evaluated by the keccak column kernel right after h
+enum KcPredKind : uint32_t { KP_LT = 0, KP_GT = 1, KP_GE = 2, KP_LE = 3, KP_EQ = 4, KP_LOWZ = 5 };
+struct KcPred {
+  uint32_t kind;        // h < c, h > c, h >= c, h <= c, h == c, low `bits` bits of h zero
+  uint32_t bits;        // KP_LOWZ: number of low bits
+  uint32_t row;         // the Bool column's variable row (0/1 per model)
+  int32_t mask;         // its packed lane-mask index (-1: none)
+  uint32_t c[8];        // the constant, limbs little-endian
+};
+hipError_t launch_keccak_columns(const KcCol* cols, int n_cols, const KcMapEntry* map, const KcPred* preds,
+                                 uint32_t* vars, int64_t M, unsigned long long* counters, uint64_t* bool_masks,
+                                 int n_bool_masks, int bool_rows, hipStream_t st);
 
 }  // namespace mq
 #endif

@@ -76,6 +76,7 @@ def load_library(path: str = LIB_PATH):
         L.mq_tape_alg_ops.argtypes = [C.POINTER(MqTapeBatch), C.c_int32]
         L.mq_tape_alg_ops.restype = C.c_double
         L.mq_tape_compile_info.argtypes = [C.POINTER(MqTapeBatch), C.c_int32] + [C.POINTER(C.c_int32)] * 5 + [C.c_char_p, C.c_int32]
+        L.mq_tapes_column_keccak_predicates.argtypes = [P, C.POINTER(C.c_int32)]
         L.mq_tape_compile_info_g.argtypes = [C.POINTER(MqTapeBatch), C.c_int32] + [C.POINTER(C.c_int32)] * 3
         L.mq_tape_program.argtypes = [C.POINTER(MqTapeBatch), C.c_int32, C.POINTER(C.c_uint32), C.c_int32, C.POINTER(C.c_int32)]
         L.mq_tapes_upload_dag.argtypes = [P, C.POINTER(MqDagBatch), C.POINTER(P), C.POINTER(C.c_int32)]
@@ -237,6 +238,13 @@ class CompiledTapes:
         a, b = C.c_int32(), C.c_int32()
         _check(self.ev.lib.mq_tapes_column_split(self.handle, C.byref(a), C.byref(b)), "mq_tapes_column_split")
         return a.value, bool(b.value)
+
+    def keccak_predicate_columns(self) -> int:
+        """Bool columns over keccak columns evaluated by the keccak column kernel
+        (mq_tapes_column_keccak_predicates)."""
+        n = C.c_int32()
+        _check(self.ev.lib.mq_tapes_column_keccak_predicates(self.handle, C.byref(n)), "mq_tapes_column_keccak_predicates")
+        return n.value
 
     def keccak_columns(self) -> int:
         """Hoisted columns computed by the keccak-f[1600] column kernel (mq_tapes_column_keccak)."""

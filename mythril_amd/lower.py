@@ -512,6 +512,54 @@ def keccak_subterms(terms: Sequence[S.Term], syms, chosen: Sequence[S.Term]) -> 
     return out
 
 
+def keccak_predicates(terms: Sequence[S.Term], kcols: Sequence[S.Term]) -> List[Tuple[S.Term, S.Term]]:
+    """Predicates comparing a keccak column with a constant — the keccak manager's axioms
+    ``lo <= h``, ``h < hi``, ``h urem 64 == 0`` and ``h == h_c`` (keccak_function_manager.py:
+    150-179) — as ``(term, canonical form)``: each becomes a Bool column of its own, which the
+    keccak column kernel evaluates from the digest in registers (mq_api.cpp kp_match), so no
+    interpreter re-reads the digest row for it.  Canonical forms (h the keccak column, c a
+    constant): ``ULT(h, c)``, ``ULT(c, h)``, ``Not`` of either (Mythril's ``ULE`` / ``UGE`` are
+    ``Or(ULT, ==)``, bitvec_helper.py:85-112), ``h == c``, ``Extract(k-1, 0, h) == 0`` for
+    ``h urem 2^k == 0``."""
+    kc = {id(t) for t in kcols if t.kind == S.KECCAK or t.kind == S.APP}
+    out: List[Tuple[S.Term, S.Term]] = []
+    seen = set()
+
+    def const(t):
+        return t.kind == S.VAL
+
+    def canon(t: S.Term):
+        k, a = t.kind, t.args
+        if k == S.BVULT and ((id(a[0]) in kc and const(a[1])) or (const(a[0]) and id(a[1]) in kc)):
+            return t
+        if k == S.EQ and len(a) == 2 and a[0].sort == "bv":
+            x, y = a
+            if const(x) and id(y) in kc:
+                x, y = y, x
+            if id(x) in kc and const(y):
+                return t if x is a[0] else (x == y)
+            if x.kind == S.UREM and id(x.args[0]) in kc and const(x.args[1]) and const(y) and y.params[0] == 0:
+                p = x.args[1].params[0]
+                if p > 0 and p & (p - 1) == 0:
+                    kb = p.bit_length() - 1
+                    return S.Extract(kb - 1, 0, x.args[0]) == 0 if kb > 0 else S.BoolVal(True)
+        if k == S.OR and len(a) == 2 and a[0].kind == S.BVULT and a[1].kind == S.EQ:
+            u, e = a
+            if {id(u.args[0]), id(u.args[1])} == {id(e.args[0]), id(e.args[1])} and canon(u) is not None:
+                return S.Not(S.ULT(u.args[1], u.args[0]))   # a < b or a == b  <=>  not (b < a)
+        return None
+
+    for r in terms:
+        for t in S.walk(r):
+            if id(t) in seen or t.sort != "bool":
+                continue
+            seen.add(id(t))
+            c = canon(t)
+            if c is not None and c.kind != S.TRUE:
+                out.append((t, c))
+    return out
+
+
 def _is_keccak_uf(name: str) -> bool:
     """``keccak256_<n>`` (keccak_function_manager.py:77), not its inverse ``keccak256_<n>-1``."""
     return name.startswith("keccak256_") and name[10:].isdigit()
@@ -538,6 +586,7 @@ def lower_batch(roots: Sequence[S.Term], syms: Optional[SymbolTable] = None, hoi
     hoisted: Dict[int, int] = {}
     narrow: Dict[int, int] = {}
     col_terms: List[S.Term] = []
+    program: Dict[int, S.Term] = {}   # id(column term) -> the (equivalent) term its program lowers
     if hoist and len(roots) > 1:
         # (MQ_HOIST_MIN_NODES / MQ_HOIST_MIN_TAPES: diagnostic overrides of the hoisting threshold)
         min_nodes = int(os.environ.get("MQ_HOIST_MIN_NODES", hoist_min_nodes))
@@ -561,6 +610,15 @@ def lower_batch(roots: Sequence[S.Term], syms: Optional[SymbolTable] = None, hoi
                 col_terms += nested
         n_shared = len(col_terms)
         col_terms += [t for t in kcols if id(t) not in {id(x) for x in col_terms}]
+        # predicates over keccak columns, evaluated by the keccak column kernel (interpreted keccak)
+        if syms.interpret_keccak and os.environ.get("MQ_NO_KECCAK_PREDICATES") is None:
+            have = {id(t) for t in col_terms}
+            kterms = [t for t in col_terms if t.kind == S.KECCAK or (t.kind == S.APP and _is_keccak_uf(t.params[0]))]
+            for t, c in keccak_predicates(list(roots) + col_terms, kterms):
+                if id(t) not in have:
+                    have.add(id(t))
+                    col_terms.append(t)
+                    program[id(t)] = c
         # every keccak application and Concat piece, also those already chosen as shared terms
         # (an address key x & (2^160 - 1) is both): never narrowed
         kpieces = {id(t) for t in keccak_subterms(list(roots), syms, [])}
@@ -586,15 +644,15 @@ def lower_batch(roots: Sequence[S.Term], syms: Optional[SymbolTable] = None, hoi
         progs, levels = [], []
         lvl: Dict[int, int] = {}
         for t in col_terms:   # column programs; a column may read columns nested inside it
-            inner = [h for h in _walk_cut(t, hoisted) if id(h) in hoisted and h is not t]
             lvl[id(t)] = 0
-            progs.append(lower_term(t, syms, hoisted, value_root=True, narrow=narrow))
+            progs.append(lower_term(program.get(id(t), t), syms, hoisted, value_root=True, narrow=narrow))
         # levels: longest chain of nested columns (terms are acyclic)
         changed = True
         while changed:
             changed = False
             for t in col_terms:
-                inner = [h for h in _walk_cut(t, hoisted) if id(h) in hoisted and h is not t]
+                pt = program.get(id(t), t)
+                inner = [h for h in _walk_cut(pt, hoisted) if id(h) in hoisted and h is not t and h is not pt]
                 want = 1 + max((lvl[id(h)] for h in inner), default=-1)
                 if want > lvl[id(t)]:
                     lvl[id(t)] = want

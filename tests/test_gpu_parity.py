@@ -544,6 +544,41 @@ def test_c4_hoisted_in_kernel_keccak(evaluator):
     assert (ref == exp).all() and (fh == ref).all()
 
 
+@pytest.mark.parametrize("variant", ["fused", "no_predicates", "no_keccak_columns", "cpp_columns"])
+def test_c4_keccak_predicates_in_the_keccak_column_kernel(evaluator, monkeypatch, variant):
+    """The keccak manager's predicates over keccak columns (lo <= h, h < hi, h urem 64 == 0,
+    h == h_c; keccak_function_manager.py:150-179) evaluated by the keccak column kernel from the
+    digest in registers, their lane masks stored directly: full verdict matrix and first hits
+    against the oracle on the UNhoisted lowering.  Variants: predicates on the interpreters, keccak
+    columns on the interpreters (predicate columns then run one level later), and the G column
+    path off (the kernel then also writes the 0/1 rows the HIP C++ kernels read)."""
+    from mythril_amd.synth_evm import c4_workload
+    if variant == "no_predicates":
+        monkeypatch.setenv("MQ_NO_KECCAK_PREDICATES", "1")
+    if variant == "no_keccak_columns":
+        monkeypatch.setenv("MQ_NO_KECCAK_COLUMNS", "1")
+    plain = c4_workload(40, 1500, seed=24, planted_frac=0.4, hasher_many=evaluator.keccak256_array)
+    tb, mb, exp, _ = c4_workload(40, 1500, seed=24, planted_frac=0.4, hasher_many=evaluator.keccak256_array,
+                                 interpret_keccak=True, hoist=True)
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    if variant == "cpp_columns":
+        evaluator.use_asm(False)
+    try:
+        fh = evaluator.first_hit(ct)
+        v, _ = evaluator.verdicts(ct)
+    finally:
+        evaluator.use_asm(True)
+    kp = ct.keccak_predicate_columns()
+    if variant in ("fused", "cpp_columns"):
+        assert kp >= 8 and ct.keccak_columns() >= 4, (kp, ct.keccak_columns())
+    else:
+        assert kp == 0
+    ref, _ = cref.first_hit(plain[0], plain[1])
+    assert (ref == exp).all() and (fh == ref).all(), np.flatnonzero(fh != ref)[:10]
+    assert (v == cref.verdicts(plain[0], plain[1])).all()
+
+
 # ---------------------------------------------------------------- assembly interpreters: P and G kernels
 @pytest.mark.parametrize("seed", range(4))
 def test_asm_const_ops_and_lookups_match_oracle(evaluator, seed):

@@ -12,6 +12,7 @@ from mythril_amd import smt as S
 from mythril_amd.exceptions import LoweringError
 from mythril_amd.lower import SymbolTable, lower_batch, lower_term, serialize_models
 from mythril_amd.smt_model import Model
+from mythril_amd.tape import Op
 
 M256 = (1 << 256) - 1
 
@@ -323,3 +324,49 @@ def test_wide_equality_of_opaque_terms_stays_wide():
     e = S.If(S.ULT(x, y), x, y) == S.Concat(S.BitVecSym("a", 256), S.BitVecSym("b", 256))
     tb, syms, ok = lower_batch([e])
     assert ok.all() and int(tb.tape_nodes(0)["width"].max()) == 512
+
+
+def _cref_hasher(msgs):
+    return np.stack([np.frombuffer(cref.keccak256(bytes(m)), np.uint8) for m in msgs])
+
+
+def test_c4_hoisting_with_keccak_predicates_and_nested_columns_preserves_verdicts():
+    """C4 with interpreted keccak, hoisted: the keccak manager's interval / urem / concrete-hash
+    predicates (keccak_function_manager.py:150-179) become Bool columns over the keccak columns
+    (lower.keccak_predicates, canonical forms), sub-terms several columns share become columns of
+    their own (lower.nested_shared) — and the oracle's verdicts, columns applied level by level,
+    equal the unhoisted lowering's."""
+    from mythril_amd.lower import keccak_predicates
+    from mythril_amd.synth_evm import c4_workload
+    from oracle_engine import apply_columns
+    plain = c4_workload(24, 80, seed=14, planted_frac=0.4, hasher_many=_cref_hasher)
+    tb, mb, exp, _ = c4_workload(24, 80, seed=14, planted_frac=0.4, hasher_many=_cref_hasher,
+                                 interpret_keccak=True, hoist=True)
+    cols = tb.columns
+    ops = [set(Op(int(o)).name for o in cols.programs.tape_nodes(k)["op"]) for k in range(cols.n)]
+    # predicate columns: a ULT / EQ of one variable and a constant (or an EXTRACT of it == 0)
+    preds = [k for k in range(cols.n) if ops[k] <= {"VAR", "CONST", "ULT", "EQ", "NOT", "EXTRACT"}
+             and "VAR" in ops[k] and cols.programs.tape_nodes(k)["width"][-1] == 0]
+    assert len(preds) >= 8, preds
+    assert any("EXTRACT" in ops[k] for k in preds)          # h urem 64 == 0
+    mb_full = apply_columns(tb, mb)
+    v = cref.verdicts(tb, mb_full)
+    assert (v == cref.verdicts(plain[0], plain[1])).all()
+    fh, _ = cref.first_hit(tb, mb_full)
+    assert (fh == exp).all()
+
+
+def test_keccak_predicate_canonical_forms():
+    from mythril_amd.lower import keccak_predicates
+    x = S.BitVecSym("x", 512)
+    h = S.Function("keccak256_512", [512], 256)(x)
+    c = S.BitVecVal(12345, 256)
+    terms = [S.ULE(c, h), S.ULT(h, c), S.URem(h, S.BitVecVal(64, 256)) == 0, h == c, S.UGE(h, c),
+             S.URem(h, S.BitVecVal(48, 256)) == 0]
+    got = dict((id(t), k) for t, k in keccak_predicates([S.And(*terms)], [h]))
+    assert got[id(terms[0])] is S.Not(S.ULT(h, c))           # c <= h  <=>  not (h < c)
+    assert got[id(terms[1])] is terms[1]
+    assert got[id(terms[2])] is (S.Extract(5, 0, h) == 0)
+    assert got[id(terms[3])] is terms[3]
+    assert got[id(terms[4])] is S.Not(S.ULT(h, c))           # UGE(h, c) = Or(UGT(h, c), h == c)
+    assert id(terms[5]) not in got                            # 48 is not a power of two
