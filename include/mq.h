@@ -109,6 +109,18 @@ typedef enum mq_op {
   MQ_OP_CONST_ARRAY = 62, /* a = value node (K(sort, v))            (array sort) */
   MQ_OP_ARRAY_VAR = 63,   /* a = function id of the model table     (array sort) */
   MQ_OP_UF = 64,          /* a = function id, b = arg0, c = arg1 (MQ_NONE if arity 1) */
+  /* An arity-1 lookup whose key is wider than 2048 bits (keccak256_<n> of a > 256-byte SHA3
+     input, instructions.py:1018-1055), matched 256 bits at a time so that no value is wider:
+     MQ_OP_UF_CHUNK: width 64, a = function id, b = key chunk k (bits [256k, 256k + width(b))),
+       c = the UF_CHUNK of chunk k - 1, MQ_NONE for k = 0 (k = the length of that chain).  Its
+       value is the set of the model's table entries (bit e = entry e, e < 64) whose key chunks
+       0..k all equal the given ones.
+     MQ_OP_UF_WIDE: a = function id, b = the last UF_CHUNK; the value of the first entry in the
+       set, or the table's else value when it is empty — exactly the lookup of the whole key.
+     A tape with these ops is unsupported (-2) under a model batch in which some model's table
+     of that function holds more than 64 entries. */
+  MQ_OP_UF_CHUNK = 65,
+  MQ_OP_UF_WIDE = 66,
   /* interpreted keccak256 (Ethereum padding) of the big-endian bytes of a; width 256.
      NOT z3 semantics: only for keccak-consistent synthetic models and constant folding
      (keccak_function_manager.py:56-69). */

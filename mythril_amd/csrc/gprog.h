@@ -79,8 +79,26 @@ enum GOp : uint32_t {
   // ite(k == i, v, <rest of the chain>)), so the chain costs O(1) stack slots, not 2 per store.
   G_ITE_EF = 63,
   G_BITE_EF = 9,
+  // arity-1 lookup of a key wider than any value, 256 bits at a time (mq.h MQ_OP_UF_CHUNK /
+  // MQ_OP_UF_WIDE); imm = function id.  The running value is the set of the model's table
+  // entries still matching (a 64-bit mask in limbs 0-1)
+  G_UFK0 = 32,       // S[d] = entries whose key chunk 0 equals S[d]; next word = chunk index (0)
+  G_UFK = 33,        // S[d-1] = S[d-1] & entries whose key chunk k equals S[d]; next word = k
+  G_UFKV = 34,       // S[d] = value of the first entry in the set S[d], else the else value;
+                     // next word = result width
   G_NUM_OPS = 64
 };
+
+#ifdef __HIPCC__
+#define GPROG_HD __host__ __device__
+#else
+#define GPROG_HD
+#endif
+
+// ops followed by a second instruction word (imm2)
+GPROG_HD static inline bool has_imm2(uint32_t op) {
+  return op == 56 || op == 57 || op == 58 || op == 60 || op == 61 || op == 32 || op == 33 || op == 34;
+}
 
 static inline uint32_t gword(uint32_t op, uint32_t d, uint32_t imm) { return op | (d << 8) | (imm << 12); }
 

@@ -198,6 +198,10 @@ struct mq_ctx {
   // run in either order)
   std::mutex tapes_mu;
   std::unordered_set<mq_tapes*> live_tapes;
+  // per model function: the most table entries any model of the WHOLE batch holds (all shards):
+  // a wide-key lookup (MQ_OP_UF_WIDE) tracks at most 64 entries per model
+  std::vector<int64_t> func_max_entries;
+  uint64_t batch_gen = 0;   // bumped by every mq_models_upload (all devices of a context alike)
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -262,6 +266,13 @@ struct mq_tapes {
   std::vector<double> alg_ops;
   double total_nodes = 0, total_alg_ops = 0;
   DevBuf descs, prog, consts, unsup_dev;
+  // wide-key lookups (MQ_OP_UF_WIDE): per tape the functions, the compile-time unsupported flags,
+  // and the batch the flags were last re-derived for (a function with more than kWideMaxEntries
+  // entries in some model makes its tapes unsupported under that batch)
+  std::vector<std::vector<uint32_t>> wide_funcs;
+  std::vector<uint8_t> unsupported_base;
+  bool wide_any = false;
+  uint64_t wide_gen = ~0ull;
   struct Variant {
     int L = 0;
     int begin = 0, count = 0;  // range in descs
@@ -901,9 +912,23 @@ int mq_models_shard(const mq_model_batch* mb, int64_t lo, int64_t hi, mq_model_b
 
 void mq_models_shard_free(void* handle) { delete static_cast<ShardBuffers*>(handle); }
 
+static constexpr int64_t kWideMaxEntries = 64;
+
 int mq_models_upload(mq_ctx* c, const mq_model_batch* mb) {
   if (!c || !mb || mb->n_models < 0) return MQ_ERR_ARG;
   PhaseTimer pt(&c->host_t[8]);
+  {
+    std::vector<int64_t> mx((size_t)std::max(mb->n_funcs, 0), 0);
+    if (mb->entry_ptr)
+      for (int f = 0; f < mb->n_funcs; f++) {
+        const int64_t* p = mb->entry_ptr + (int64_t)f * (mb->n_models + 1);
+        for (int64_t m = 0; m < mb->n_models; m++) mx[f] = std::max(mx[f], p[m + 1] - p[m]);
+      }
+    for (mq_ctx* d : devices_of(c)) {
+      d->func_max_entries = mx;
+      d->batch_gen++;
+    }
+  }
   if (c->peers.empty()) {
     c->shard_lo.assign(1, 0);
     c->M_total = mb->n_models;
@@ -1224,7 +1249,7 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
     const uint32_t op = w & 0xFFu, imm = w >> 12;
     const int d = (int)((w >> 8) & 0xFu);
     uint32_t imm2 = 0;
-    if (op == G_EXTRACT || op == G_CONCAT || op == G_SEXT || op == G_UF1 || op == G_UF2) {
+    if (has_imm2(op)) {
       if (++pc >= xprog.size()) return false;
       imm2 = xprog[pc];
     }
@@ -1605,6 +1630,11 @@ static int tapes_upload_one(mq_ctx* c, int32_t n_tapes, const std::vector<Compil
   T->l8_all.max_depth = std::max(T->qsa.max_depth, T->gen[0].max_depth);
   consts.resize(consts.size() + 16, 0);
   prog.push_back(gword(G_END, 0, 0));
+  T->wide_funcs.assign(n_tapes, {});
+  for (int t = 0; t < n_tapes; t++) {
+    T->wide_funcs[t] = ct[t].wide_funcs;
+    T->wide_any = T->wide_any || !ct[t].wide_funcs.empty();
+  }
   for (int t = 0; t < n_tapes; t++) {
     T->unsupported[t] = ct[t].supported ? 0 : 1;
     T->n_unsupported += ct[t].supported ? 0 : 1;
@@ -1621,6 +1651,7 @@ static int tapes_upload_one(mq_ctx* c, int32_t n_tapes, const std::vector<Compil
   HIPCHK(T->consts.upload(consts.data(), consts.size(), c->stream));
   HIPCHK(T->unsup_dev.upload(T->unsupported.data(), T->unsupported.size(), c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  T->unsupported_base = T->unsupported;
   *out = T.release();
   return MQ_OK;
 }
@@ -1676,10 +1707,14 @@ static int node_refs(const mq_node& n, uint32_t r[3]) {
       r[0] = n.a; r[1] = n.b; r[2] = n.c;
       return 3;
     case MQ_OP_UF:
+    case MQ_OP_UF_CHUNK:
       r[0] = n.b;
       if (n.c == MQ_NONE) return 1;
       r[1] = n.c;
       return 2;
+    case MQ_OP_UF_WIDE:
+      r[0] = n.b;
+      return 1;
     default:
       r[0] = n.a; r[1] = n.b;
       return 2;
@@ -1736,8 +1771,12 @@ static bool expand_dag_tape(const mq_dag_batch* dag, int32_t t, std::vector<int3
         for (int k = 0; k < 3; k++) *f[k] = (uint32_t)(-mark[*f[k]] - 2);
         break;
       case MQ_OP_UF:
+      case MQ_OP_UF_CHUNK:
         n.b = (uint32_t)(-mark[n.b] - 2);
         if (n.c != MQ_NONE) n.c = (uint32_t)(-mark[n.c] - 2);
+        break;
+      case MQ_OP_UF_WIDE:
+        n.b = (uint32_t)(-mark[n.b] - 2);
         break;
       default:
         n.a = (uint32_t)(-mark[n.a] - 2);
@@ -2228,7 +2267,7 @@ static std::vector<int64_t> count_pushes(const mq_ctx* c, const std::vector<Comp
       if ((op == G_PUSH_VAR || (op == G_PUSH_VAR_B && !(imm < c->bmask_of_var.size() && c->bmask_of_var[imm] >= 0))) &&
           imm < pushes.size() && c->var_nl_h[imm] <= 8)
         pushes[imm]++;
-      if (op == G_EXTRACT || op == G_CONCAT || op == G_SEXT || op == G_UF1 || op == G_UF2) pc++;
+      if (has_imm2(op)) pc++;
     }
   }
   return pushes;
@@ -2291,7 +2330,7 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
     for (size_t pc = 0; pc < x.prog.size(); pc++) {
       const uint32_t op = x.prog[pc] & 0xFFu;
       if ((op == G_PUSH_VAR || op == G_PUSH_VAR_B) && (x.prog[pc] >> 12) >= (uint32_t)kQsaVars) return false;
-      if (op == G_EXTRACT || op == G_CONCAT || op == G_SEXT || op == G_UF1 || op == G_UF2) pc++;
+      if (has_imm2(op)) pc++;
     }
     return true;
   };
@@ -2313,7 +2352,7 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
       if ((op == G_PUSH_VAR || (op == G_PUSH_VAR_B && !(imm < c->bmask_of_var.size() && c->bmask_of_var[imm] >= 0))) &&
           imm < pushes.size() && c->var_nl_h[imm] <= 8)
         pushes[imm]++;
-      if (op == G_EXTRACT || op == G_CONCAT || op == G_SEXT || op == G_UF1 || op == G_UF2) pc++;
+      if (has_imm2(op)) pc++;
     }
   }
   std::vector<int> order;
@@ -2520,7 +2559,26 @@ static int64_t latency_asm_nodes() {
   return v;
 }
 
+// Tapes with a wide-key lookup of a function that some model of the current batch holds more
+// than kWideMaxEntries entries of are unsupported (-2) under that batch (mq.h MQ_OP_UF_WIDE).
+static int refresh_wide_unsupported(mq_ctx* c, mq_tapes* T, hipStream_t st) {
+  if (!T->wide_any || T->wide_gen == c->batch_gen) return MQ_OK;
+  T->wide_gen = c->batch_gen;
+  T->unsupported = T->unsupported_base;
+  int n = 0;
+  for (int t = 0; t < T->n_tapes; t++) {
+    for (uint32_t f : T->wide_funcs[t])
+      if (f < c->func_max_entries.size() && c->func_max_entries[f] > kWideMaxEntries) T->unsupported[t] = 1;
+    n += T->unsupported[t];
+  }
+  T->n_unsupported = n;
+  HIPCHK(T->unsup_dev.upload(T->unsupported.data(), T->unsupported.size(), st));
+  HIPCHK(hipStreamSynchronize(st));
+  return MQ_OK;
+}
+
 static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, hipStream_t st) {
+  if (const int rc = refresh_wide_unsupported(c, T, st)) return rc;
   bool use_qsa = c->qsa_ready && c->use_asm && T->qsa.count > 0;
   // latency-bound launch (a few tapes over a few models): G runs one tape per wave instead of
   // batching tapes per wave for throughput -- unless the batch is large enough that translating

@@ -593,6 +593,85 @@ MQ_DEV void func_lookup(const Ctx& cx, uint32_t f, uint32_t W, const uint32_t (&
   mask_w<L>(out, W == 0 ? 1u : W);  // Bool range: limb 0 holds 0/1
 }
 
+// the function descriptor of f (qs_launch.h FuncDev); false if f is out of range
+MQ_DEV bool load_func(const Ctx& cx, uint32_t f, FuncDev& fd) {
+  if (f >= (uint32_t)cx.n_funcs) return false;
+  cu32p w = CONSTP(cu32p, cx.funcs) + (size_t)f * (sizeof(FuncDev) / 4);
+  fd.arity = w[0];
+  fd.nl_a0 = w[1];
+  fd.nl_a1 = w[2];
+  fd.nl_res = w[3];
+  fd.stride = w[4];
+  fd.entry_base = (int64_t)((uint64_t)w[6] | ((uint64_t)w[7] << 32));
+  fd.ptr_base = (int64_t)((uint64_t)w[8] | ((uint64_t)w[9] << 32));
+  fd.else_base = (int64_t)((uint64_t)w[10] | ((uint64_t)w[11] << 32));
+  return true;
+}
+
+// wide-key lookup, one 256-bit key chunk k at a time (mq.h MQ_OP_UF_CHUNK): the set of this
+// model's entries of f (bit e = entry e; the host guarantees at most 64 entries per model) whose
+// key limbs [8k, 8k + 8) equal the chunk, within the set so far (G_UFK) or all entries (G_UFK0)
+template <int L>
+MQ_DEV void h_ufk(const Ctx& cx, int d, uint32_t op, uint32_t f, uint32_t k) {
+  uint32_t X[L];
+  sld<L>(cx, d, X);
+  const int out = op == G_UFK0 ? d : d - 1;
+  uint64_t mask = 0;
+  FuncDev fd;
+  if (load_func(cx, f, fd) && fd.arity == 1) {
+    const int64_t lo = cx.entry_ptr[fd.ptr_base + cx.m], hi = cx.entry_ptr[fd.ptr_base + cx.m + 1];
+    const int64_t E = min<int64_t>(hi - lo, 64);
+    if (op == G_UFK0) {
+      mask = E >= 64 ? ~0ull : ((1ull << E) - 1ull);
+    } else {
+      uint32_t P[L];
+      sld<L>(cx, d - 1, P);
+      mask = (uint64_t)P[0] | ((uint64_t)P[1] << 32);
+    }
+    const int nk = (int)fd.nl_a0 - 8 * (int)k;   // key limbs in this chunk (the last may be short)
+    if (nk <= 0) mask = 0;
+    for (int64_t e = 0; e < E && mask; e++) {
+      if (!((mask >> e) & 1ull)) continue;
+      const uint32_t* ent = cx.entry_words + fd.entry_base + (lo + e) * (int64_t)fd.stride + 8 * k;
+      bool eq = true;
+#pragma unroll
+      for (int i = 0; i < 8 && i < L; i++)
+        if (i < nk) eq = eq && ent[i] == X[i];
+      if (!eq) mask &= ~(1ull << e);
+    }
+  }
+  uint32_t R[L];
+#pragma unroll
+  for (int i = 0; i < L; i++) R[i] = i == 0 ? (uint32_t)mask : i == 1 ? (uint32_t)(mask >> 32) : 0u;
+  sst<L>(cx, out, R);
+}
+
+// the value of the first entry of the set S[d] (mq.h MQ_OP_UF_WIDE), or f's else value
+template <int L>
+MQ_DEV void h_ufkv(const Ctx& cx, int d, uint32_t f, uint32_t W) {
+  uint32_t P[L], R[L];
+  sld<L>(cx, d, P);
+  const uint64_t mask = (uint64_t)P[0] | ((uint64_t)P[1] << 32);
+#pragma unroll
+  for (int i = 0; i < L; i++) R[i] = 0;
+  FuncDev fd;
+  if (load_func(cx, f, fd)) {
+    const int64_t M = cx.M;
+    const uint32_t* ev = cx.else_words + fd.else_base + cx.m;
+#pragma unroll
+    for (int i = 0; i < L; i++) R[i] = ((uint32_t)i < fd.nl_res) ? ev[(int64_t)i * M] : 0u;
+    if (mask) {
+      const int64_t lo = cx.entry_ptr[fd.ptr_base + cx.m];
+      const int e = __builtin_ctzll(mask);
+      const uint32_t* v = cx.entry_words + fd.entry_base + (lo + e) * (int64_t)fd.stride + fd.nl_a0;
+#pragma unroll
+      for (int i = 0; i < L; i++) R[i] = ((uint32_t)i < fd.nl_res) ? v[i] : 0u;
+    }
+  }
+  mask_w<L>(R, W == 0 ? 1u : W);
+  sst<L>(cx, d, R);
+}
+
 template <int L>
 MQ_DEV void h_uf(const Ctx& cx, int d, uint32_t op, uint32_t f, uint32_t W) {
   uint32_t X[L], Y[L], R[L];
@@ -709,7 +788,7 @@ MQ_DEV bool run_tape(cu32p prog, const Ctx& cx) {
     const uint32_t imm = ins >> 12;
     if (op == G_END) break;
     uint32_t imm2 = 0;
-    if (op == G_EXTRACT || op == G_CONCAT || op == G_SEXT || op == G_UF1 || op == G_UF2) imm2 = prog[pc++];
+    if (has_imm2(op)) imm2 = prog[pc++];
     switch (op) {
       case G_PUSH_VAR:
       case G_PUSH_VAR_B: h_push_var<L>(cx, d, imm); break;
@@ -771,6 +850,9 @@ MQ_DEV bool run_tape(cu32p prog, const Ctx& cx) {
       case G_SMUL_NOUDFL: h_mul_ovfl<L>(cx, d, op, imm); break;
       case G_UF1:
       case G_UF2: h_uf<L>(cx, d, op, imm, imm2); break;
+      case G_UFK0:
+      case G_UFK: h_ufk<L>(cx, d, op, imm, imm2); break;
+      case G_UFKV: h_ufkv<L>(cx, d, imm, imm2); break;
       case G_KECCAK:
         if constexpr (K) h_keccak<L>(cx, d, imm);
         break;

@@ -88,6 +88,7 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
   try {
     // ---------------------------------------------------------------- 1. validate, kinds, widths
     std::vector<Kind> kind(nn);
+    std::vector<uint32_t> chunk_k(nn, 0);   // MQ_OP_UF_CHUNK: the key chunk's index
     int maxw = 1;
     auto ref = [&](int64_t i, uint32_t r) -> int {
       if (r >= (uint32_t)i) throw Fail{"operand does not precede its user"};
@@ -104,6 +105,7 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
           break;
         case MQ_OP_SELECT:
         case MQ_OP_UF:
+        case MQ_OP_UF_WIDE:
         case MQ_OP_VAR:
           kind[i] = n.width == 0 ? K_BOOL : K_BV;
           break;
@@ -133,6 +135,21 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
         case MQ_OP_UF:
           ref(i, n.b);
           if (n.c != MQ_NONE) ref(i, n.c);
+          break;
+        case MQ_OP_UF_CHUNK:
+          ref(i, n.b);
+          if (n.width != 64 || nd[n.b].width == 0 || nd[n.b].width > 256) throw Fail{"bad UF key chunk"};
+          if (n.c != MQ_NONE) {
+            ref(i, n.c);
+            if (nd[n.c].op != MQ_OP_UF_CHUNK || nd[n.c].a != n.a) throw Fail{"bad UF key chunk chain"};
+            chunk_k[i] = chunk_k[n.c] + 1;
+          }
+          break;
+        case MQ_OP_UF_WIDE:
+          ref(i, n.b);
+          if (nd[n.b].op != MQ_OP_UF_CHUNK || nd[n.b].a != n.a) throw Fail{"UF_WIDE without its key chunks"};
+          if (std::find(out.wide_funcs.begin(), out.wide_funcs.end(), n.a) == out.wide_funcs.end())
+            out.wide_funcs.push_back(n.a);
           break;
         default:
           if (n.op > 100) throw Fail{"unknown opcode"};
@@ -217,7 +234,8 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
         return B.add(x);
       };
       int aw = (n.op != MQ_OP_VAR && n.op != MQ_OP_CONST && n.op != MQ_OP_TRUE && n.op != MQ_OP_FALSE &&
-                n.op != MQ_OP_ARRAY_VAR && n.op != MQ_OP_UF && n.a < (uint32_t)i)
+                n.op != MQ_OP_ARRAY_VAR && n.op != MQ_OP_UF && n.op != MQ_OP_UF_CHUNK && n.op != MQ_OP_UF_WIDE &&
+                n.a < (uint32_t)i)
                    ? nd[n.a].width : 0;
       int r = -1;
       switch (n.op) {
@@ -289,6 +307,17 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
           else r = B.add(mk(G_UF2, w, {Bk(), Ck()}, n.a, (uint32_t)w));
           break;
         }
+        case MQ_OP_UF_CHUNK: {
+          if (n.a > (uint32_t)kMaxImm) throw Fail{"function id too large"};
+          if (n.c == MQ_NONE) r = B.add(mk(G_UFK0, 64, {Bk()}, n.a, 0u));
+          else r = B.add(mk(G_UFK, 64, {Ck(), Bk()}, n.a, chunk_k[i]));
+          break;
+        }
+        case MQ_OP_UF_WIDE: {
+          if (n.a > (uint32_t)kMaxImm) throw Fail{"function id too large"};
+          r = B.add(mk(G_UFKV, w, {Bk()}, n.a, (uint32_t)w));
+          break;
+        }
         default:
           throw Fail{"unsupported opcode"};
       }
@@ -329,7 +358,8 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
     std::vector<int> remat_cost(NI, 0);
     auto expensive = [&](uint32_t g) {
       return g == G_MUL || g == G_UDIV || g == G_UREM || g == G_SDIV || g == G_SREM || g == G_SMOD ||
-             g == G_UF1 || g == G_UF2 || g == G_KECCAK || g == G_UMUL_NOOVFL || g == G_SMUL_NOOVFL ||
+             g == G_UF1 || g == G_UF2 || g == G_UFK0 || g == G_UFK || g == G_UFKV || g == G_KECCAK ||
+             g == G_UMUL_NOOVFL || g == G_SMUL_NOOVFL ||
              g == G_SMUL_NOUDFL || g == G_SHL || g == G_LSHR || g == G_ASHR;
     };
     for (int x = 0; x < NI; x++) {
@@ -477,7 +507,7 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
       }
       if (n.imm > (uint32_t)kMaxImm) throw Fail{"immediate too large"};
       prog.push_back(gword(g, d, n.imm));
-      if (g == G_EXTRACT || g == G_CONCAT || g == G_SEXT || g == G_UF1 || g == G_UF2) prog.push_back(n.imm2);
+      if (has_imm2(g)) prog.push_back(n.imm2);
     };
     for (size_t u = 0; u < units.size(); u++) {
       int x = units[u];
@@ -520,6 +550,7 @@ CompiledTape compile_tape(const mq_tape_batch* batch, int32_t t, const CompileLi
     out.why = f.why;
     out.prog.clear();
     out.prog_g.clear();
+    out.wide_funcs.clear();
     out.consts.clear();
   }
   out.alg_ops = tape_alg_ops(batch, t);
@@ -584,6 +615,12 @@ double tape_alg_ops(const mq_tape_batch* batch, int32_t t) {
         ops += Larg + L;  // one-entry table (model-dependent; SURVEY §8(d) e*L_arg + L_val, e = 1)
         break;
       }
+      case MQ_OP_UF_CHUNK:   // the key's share of the lookup, chunk by chunk (e = 1, as MQ_OP_UF)
+        ops += n.b < (uint32_t)i ? nl_of(nd[n.b].width) : 8;
+        break;
+      case MQ_OP_UF_WIDE:
+        ops += L;
+        break;
       case MQ_OP_KECCAK:
         // keccak-f[1600] permutations: one per started 136-byte block (padding included)
         ops += kKeccakOpsPerBlock * std::floor((La * 4 + 1 + 135) / 136);

@@ -30,6 +30,7 @@ struct CompiledTape {
   int depth_g = 0;
   int n_temps_g = 0;
   uint32_t n_nodes = 0;          // DAG size of the boundary tape (metric)
+  std::vector<uint32_t> wide_funcs;   // functions looked up by a chunked wide key (MQ_OP_UF_WIDE)
   double alg_ops = 0;            // SURVEY §8(d) algorithmic cost per model
 };
 

@@ -30,6 +30,8 @@ from .smt_model import as_record
 from .tape import BOOL, NODE_DTYPE, NONE, ColumnSet, Op, Tape, TapeBatch, limbs, to_words
 
 MAX_WIDTH = 0xFFFF
+# keys wider than this are looked up chunk by chunk (the evaluator holds values of <= 2048 bits)
+WIDE_KEY_BITS = 2048
 
 
 class SymbolTable:
@@ -276,16 +278,34 @@ def _lower_one(t: S.Term, a: List[int], tp: Tape, syms: SymbolTable, node: Dict[
         name, dom = t.params
         fid = syms.func(name, dom, t.width)
         if syms.derive and all(x.kind == S.VAL for x in t.args):
+            if any(x.width > WIDE_KEY_BITS for x in t.args):
+                tp.has_dead = True   # the wide constant key is dead: finish() prunes it
             return tp.var(syms.derived_var(name, tuple(x.params[0] for x in t.args), _w(t)), _w(t))
+        if len(t.args) == 1 and t.args[0].width > WIDE_KEY_BITS:
+            # a key wider than any value may be (keccak256_<n> of a > 256-byte SHA3 input,
+            # instructions.py:1018-1055): matched 256 bits at a time (mq.h MQ_OP_UF_CHUNK /
+            # MQ_OP_UF_WIDE), its chunks cut out of the key's concatenation like _wide_eq's
+            x = t.args[0]
+            chunks = []
+            for lo in range(0, x.width, 256):
+                ch = _chunk(x, lo, min(x.width, lo + 256), tp, syms, node, cut_any=True)
+                if ch is None:
+                    raise LoweringError(f"UF key of {x.width} bits that does not split into 256-bit chunks")
+                chunks.append(ch)
+            tp.has_dead = True   # the wide key itself is dead now: finish() prunes it
+            return tp.uf_wide(fid, t.width, chunks)
         return tp.uf(fid, t.width, *a)
     raise LoweringError(f"term kind {k!r} not in the tape vocabulary")
 
 
-def _chunk(t: S.Term, lo: int, hi: int, tp: Tape, syms: SymbolTable, node: Dict[int, int]) -> Optional[int]:
+def _chunk(t: S.Term, lo: int, hi: int, tp: Tape, syms: SymbolTable, node: Dict[int, int],
+           cut_any: bool = False) -> Optional[int]:
     """Tape node of bits [lo, hi) (<= 256 bits) of the BV term ``t`` built without its full
     width, or None: constants are cut, concatenations split, a UF result is read through the
-    slice function of its bits.  ``t`` must be a term whose lowering kept its structure (a term
-    cut by hoisting is a variable node: None)."""
+    slice function of its bits, a variable is extracted from.  ``t`` must be a term whose lowering
+    kept its structure (a term cut by hoisting is a variable node: None).  ``cut_any``: any
+    other operand within the value limit is extracted from too (a wide UF key has no wide
+    fallback)."""
     n = node.get(id(t))
     if n is None:
         return None
@@ -297,10 +317,10 @@ def _chunk(t: S.Term, lo: int, hi: int, tp: Tape, syms: SymbolTable, node: Dict[
         x, y = t.args                       # value = x ++ y (x high)
         wy = y.width
         if hi <= wy:
-            return _chunk(y, lo, hi, tp, syms, node)
+            return _chunk(y, lo, hi, tp, syms, node, cut_any)
         if lo >= wy:
-            return _chunk(x, lo - wy, hi - wy, tp, syms, node)
-        hx, ly = _chunk(x, 0, hi - wy, tp, syms, node), _chunk(y, lo, wy, tp, syms, node)
+            return _chunk(x, lo - wy, hi - wy, tp, syms, node, cut_any)
+        hx, ly = _chunk(x, 0, hi - wy, tp, syms, node, cut_any), _chunk(y, lo, wy, tp, syms, node, cut_any)
         return None if hx is None or ly is None else tp.concat(hx, ly)
     const_args = all(x.kind == S.VAL for x in t.args)
     if k == S.APP and t.width > 256 and (op == Op.UF.value or (op == Op.VAR.value and syms.derive and const_args)):
@@ -316,6 +336,8 @@ def _chunk(t: S.Term, lo: int, hi: int, tp: Tape, syms: SymbolTable, node: Dict[
         return tp.uf(fid, hi - lo, *args)
     if t.width <= 256:   # a narrow operand of a split concatenation: itself, or a cut of it
         return n if hi - lo == t.width else tp.extract(hi - 1, lo, n)
+    if op == Op.VAR.value or (cut_any and t.width <= WIDE_KEY_BITS):
+        return tp.extract(hi - 1, lo, n)
     return None
 
 

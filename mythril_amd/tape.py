@@ -69,6 +69,8 @@ class Op(enum.IntEnum):
     CONST_ARRAY = 62
     ARRAY_VAR = 63
     UF = 64
+    UF_CHUNK = 65
+    UF_WIDE = 66
     KECCAK = 70
 
 
@@ -205,8 +207,10 @@ class Tape:
             return (0,)
         if op in (Op.BITE, Op.ITE, Op.STORE):
             return (0, 1, 2)
-        if op == Op.UF:
+        if op in (Op.UF, Op.UF_CHUNK):
             return (1, 2)
+        if op == Op.UF_WIDE:
+            return (1,)
         return (0, 1)
 
     def children(self, n: int) -> List[int]:
@@ -407,6 +411,18 @@ class Tape:
         b = args[0]
         c = args[1] if len(args) > 1 else NONE
         return self._add(Op.UF, result_width, func, b, c, kind="bool" if result_width == BOOL else "bv")
+
+    def uf_wide(self, func: int, result_width: int, chunks: Sequence[int]) -> int:
+        """Arity-1 lookup of a key given as 256-bit chunks, lowest first (mq.h MQ_OP_UF_CHUNK /
+        MQ_OP_UF_WIDE): a key wider than any value may be."""
+        prev = NONE
+        for ch in chunks:
+            if self.kind[ch] != "bv" or self.width(ch) > 256:
+                raise SortError("UF key chunks are BV values of at most 256 bits")
+            prev = self._add(Op.UF_CHUNK, 64, func, ch, prev)
+        if prev == NONE:
+            raise SortError("UF key without chunks")
+        return self._add(Op.UF_WIDE, result_width, func, prev, NONE, kind="bool" if result_width == BOOL else "bv")
 
     # ------------------------------------------------------------ packing
     def packed(self) -> Tuple[np.ndarray, np.ndarray]:

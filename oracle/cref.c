@@ -511,6 +511,48 @@ static int eval_tape(const cref_env* env, int32_t t, int64_t m, uint32_t* vals) 
         }
         break;
       }
+      case MQ_OP_UF_CHUNK: {
+        /* wide-key lookup, key chunk k (mq.h): the entries of the model's table of f (bit e,
+           at most 64 of them, else unsupported) whose key limbs [8k, 8k + 8) equal the chunk,
+           within the previous chunk's set (or all entries for k = 0) */
+        const mq_func_desc* fd = (int32_t)nd->a < mb->n_funcs ? &mb->funcs[nd->a] : NULL;
+        int k = 0;
+        for (uint32_t q = nd->c; q != MQ_NONE && q < (uint32_t)i; q = nodes[q].c) k++;
+        uint64_t mask = 0;
+        if (fd && fd->arity == 1) {
+          int64_t lo = mb->entry_ptr[nd->a * (M + 1) + m], hi = mb->entry_ptr[nd->a * (M + 1) + m + 1];
+          int64_t E = hi - lo, stride = func_stride(fd);
+          int nk = nlimbs(fd->arg_width[0]) - 8 * k;
+          if (E > 64) return -2;
+          mask = nd->c == MQ_NONE ? (E == 64 ? ~0ull : ((1ull << E) - 1)) : ((uint64_t)Cv[0] | ((uint64_t)Cv[1] << 32));
+          for (int64_t e = 0; e < E; e++) {
+            const uint32_t* ent = mb->entry_words + mb->entry_base[nd->a] + (lo + e) * stride + 8 * k;
+            int eq = nk > 0;
+            for (int l = 0; l < 8 && l < nk && eq; l++) eq = ent[l] == Bv[l];
+            if (!eq) mask &= ~(1ull << e);
+          }
+        }
+        r[0] = (uint32_t)mask;
+        r[1] = (uint32_t)(mask >> 32);
+        break;
+      }
+      case MQ_OP_UF_WIDE: {
+        /* the first entry of the set, else the else value (the lookup of the whole key) */
+        uint64_t mask = (uint64_t)Bv[0] | ((uint64_t)Bv[1] << 32);
+        const mq_func_desc* fd = (int32_t)nd->a < mb->n_funcs ? &mb->funcs[nd->a] : NULL;
+        if (!fd) break;
+        int nv = nlimbs(fd->result_width);
+        if (mask) {
+          int e = __builtin_ctzll(mask);
+          int64_t lo = mb->entry_ptr[nd->a * (M + 1) + m];
+          const uint32_t* ent = mb->entry_words + mb->entry_base[nd->a] + (lo + e) * func_stride(fd);
+          memcpy(r, ent + nlimbs(fd->arg_width[0]), 4 * nv);
+        } else {
+          memcpy(r, mb->else_words + mb->else_base[nd->a] + m * nv, 4 * nv);
+        }
+        mask_top(r, w ? w : 1);
+        break;
+      }
       case MQ_OP_UF: {
         const uint32_t* args[2] = {Bv, Cv};
         func_lookup(env, nd->a, m, args, r);
@@ -561,6 +603,20 @@ int cref_eval_tape(const mq_tape_batch* tb, int32_t t, const mq_model_batch* mb,
   return r;
 }
 
+/* A wide-key lookup (MQ_OP_UF_CHUNK) of a function that some model of the batch holds more than
+   64 entries of: the tape is unsupported under the whole batch (mq.h; the evaluator's rule). */
+static int wide_unsupported(const mq_tape_batch* tb, const mq_model_batch* mb, int32_t t) {
+  int64_t base = tb->tape_offsets[t], nn = tb->tape_offsets[t + 1] - base, M = mb->n_models;
+  for (int64_t i = 0; i < nn; i++) {
+    const mq_node* nd = &tb->nodes[base + i];
+    if (nd->op != MQ_OP_UF_CHUNK || (int32_t)nd->a >= mb->n_funcs) continue;
+    const int64_t* p = mb->entry_ptr + (int64_t)nd->a * (M + 1);
+    for (int64_t m = 0; m < M; m++)
+      if (p[m + 1] - p[m] > 64) return 1;
+  }
+  return 0;
+}
+
 /* check_quick_sat for every tape; out[t] = global index (index_base + m) | -1 | -2.
    Parallel over tapes with OpenMP (nthreads <= 0: runtime default). Returns evaluated pairs. */
 int64_t cref_first_hit(const mq_tape_batch* tb, const mq_model_batch* mb, int32_t* out, int nthreads) {
@@ -575,8 +631,8 @@ int64_t cref_first_hit(const mq_tape_batch* tb, const mq_model_batch* mb, int32_
     uint32_t* vals = (uint32_t*)malloc(sizeof(uint32_t) * MAXL * (mx + 1));
 #pragma omp for schedule(dynamic, 4)
     for (int t = 0; t < tb->n_tapes; t++) {
-      int32_t hit = -1;
-      for (int64_t m = 0; m < mb->n_models; m++) {
+      int32_t hit = wide_unsupported(tb, mb, t) ? -2 : -1;
+      for (int64_t m = 0; m < mb->n_models && hit == -1; m++) {
         int r = eval_tape(&env, t, m, vals);
         pairs++;
         if (r == -2) { hit = -2; break; }
@@ -605,6 +661,7 @@ int cref_verdicts(const mq_tape_batch* tb, const mq_model_batch* mb, uint8_t* bi
     uint32_t* vals = (uint32_t*)malloc(sizeof(uint32_t) * MAXL * (mx + 1));
 #pragma omp for schedule(dynamic, 4)
     for (int t = 0; t < tb->n_tapes; t++) {
+      if (wide_unsupported(tb, mb, t)) { bad = 1; continue; }
       for (int64_t m = 0; m < M; m++) {
         int r = eval_tape(&env, t, m, vals);
         if (r == -2) { bad = 1; break; }

@@ -109,6 +109,18 @@ def _func_lookup(models: ModelBatch, f: int, m: int, args) -> int:
     return table.get(tuple(args), els)
 
 
+def _entries(models: ModelBatch, f: int, m: int):
+    """The model's table of arity-1 function f in entry order: [(key, value)] (duplicates kept)."""
+    spec = models.funcs[f]
+    lo, hi = int(models.entry_ptr[f, m]), int(models.entry_ptr[f, m + 1])
+    base, nk, nv = int(models.entry_base[f]), limbs(spec.arg_widths[0]), limbs(spec.result_width)
+    out = []
+    for e in range(lo, hi):
+        w0 = base + e * spec.stride
+        out.append((from_words(models.entry_words[w0:w0 + nk]), from_words(models.entry_words[w0 + nk:w0 + nk + nv])))
+    return out
+
+
 def _select(models: ModelBatch, m: int, arr: _Arr, idx: int) -> int:
     # select(store(A,k,v), i) = i==k ? v : select(A, i); select(K(d), i) = d;
     # select(as-array f, i) = f's FuncInterp entry or else (SURVEY Appendix A "Arrays").
@@ -224,6 +236,20 @@ def eval_nodes(nodes, consts, models: ModelBatch, m: int) -> list:
         elif op == Op.UF:
             args = [V[b]] if c == NONE else [V[b], V[c]]
             r = _func_lookup(models, a, m, args)
+        elif op == Op.UF_CHUNK:
+            # wide-key lookup, key chunk k (mq.h): the ordered entries of the model's table whose
+            # key bits [256k, 256k + 256) equal the chunk, within the previous chunk's set
+            k, q = 0, c
+            while q != NONE:
+                k, q = k + 1, int(nodes[q]["c"])
+            ents = _entries(models, a, m)
+            if len(ents) > 64:
+                raise ValueError("unsupported: more than 64 entries under a wide-key lookup")
+            prev = set(range(len(ents))) if c == NONE else V[c]
+            r = {e for e in prev if (ents[e][0] >> (256 * k)) & _mask(256) == V[b]}
+        elif op == Op.UF_WIDE:
+            ents = _entries(models, a, m)
+            r = ents[min(V[b])][1] if V[b] else models.func_table(a, m)[1]
         elif op == Op.KECCAK:
             aw = int(nodes[a]["width"])
             r = int.from_bytes(keccak256(V[a].to_bytes(aw // 8, "big")), "big")

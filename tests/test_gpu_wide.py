@@ -147,3 +147,78 @@ def test_address_key_mapping_uses_keccak_columns(evaluator):
     ct = evaluator.compile(tb)
     assert ct.keccak_columns() == len(hs)
     assert (evaluator.first_hit(ct) == ref).all() and (ref >= 0).any()
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_wide_key_chunk_lookups_match_oracle(evaluator, seed):
+    """keccak256_4096 / _2560 keys matched 256 bits at a time (G_UFK0 / G_UFK / G_UFKV on the
+    assembly interpreter, h_ufk / h_ufkv on the C++ one): verdicts equal the oracle's and the
+    independent term evaluator's (tests/test_wide_keys.py)."""
+    import random
+    import term_eval
+    from test_wide_keys import _wide_cases
+    from mythril_amd.lower import lower_batch, serialize_models
+    exprs, models = _wide_cases(random.Random(40 + seed))
+    tb, syms, ok = lower_batch(exprs)
+    assert ok.all()
+    mb = serialize_models(models, syms)
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    assert ct.n_unsupported == 0
+    v, fh = evaluator.verdicts(ct)
+    want = np.array([[term_eval.is_true(e, m) for m in models] for e in exprs])
+    assert (v == want).all(), np.argwhere(v != want)[:5]
+    assert (v == cref.verdicts(tb, mb)).all()
+    assert (fh == cref.first_hit(tb, mb)[0]).all() and (fh != -2).all()
+
+
+def test_wide_key_over_64_entries_is_unsupported_only_where_looked_up(evaluator):
+    import random
+    from test_wide_keys import _wide_cases
+    from mythril_amd import smt as S
+    from mythril_amd.lower import lower_batch, serialize_models
+    from mythril_amd.smt_model import Model
+    rng = random.Random(9)
+    exprs, models = _wide_cases(rng)
+    exprs = exprs + [S.BitVecSym("w0", 256) == 1]
+    big = dict(models[3].functions["keccak256_4096"][0])
+    while len(big) <= 64:
+        big[(rng.getrandbits(4096),)] = rng.getrandbits(256)
+    models[3] = Model(models[3].assignment, {**models[3].functions, "keccak256_4096": (big, 0)})
+    tb, syms, _ = lower_batch(exprs)
+    mb = serialize_models(models, syms)
+    evaluator.upload_models(mb)
+    ref, _ = cref.first_hit(tb, mb)
+    assert (ref == -2).any() and (ref != -2).any()
+    assert (evaluator.first_hit(tb) == ref).all()
+
+
+def test_gpu_engine_answers_states_after_a_long_sha3_input():
+    """The product VerdictEngine: states carrying keccak256_4096 axioms are answered on the
+    device (hits equal to the reference loop's), none unsupported."""
+    import random
+    import term_eval
+    from oracle_engine import ReferenceLoopCache
+    from mythril_amd import smt as S
+    from mythril_amd import support as sp
+    from mythril_amd.function_managers import KeccakFunctionManager
+    from mythril_amd.smt_model import Model
+    km = KeccakFunctionManager(hasher=keccak_ref.keccak256)
+    w = [S.BitVecSym(f"w{i}", 256) for i in range(16)]
+    msg = S.Concat(*w)
+    km.create_keccak(msg)
+    cond = km.create_conditions()
+    lo = (km.interval(4096)[0] + 63) // 64 * 64
+    rng = random.Random(3)
+    gpu, ref = sp.ModelCache(sp.VerdictEngine()), ReferenceLoopCache()
+    for i in range(20):
+        vals = {f"w{j}": rng.getrandbits(8) for j in range(16)}
+        key = term_eval.evaluate(msg, Model(vals))
+        v = lo + 64 * rng.randrange(1, 100) + (0 if i % 3 else 1)
+        m = Model(vals, {"keccak256_4096": ({(key,): v}, 0), "keccak256_4096-1": ({(v,): key}, 0)})
+        gpu.put(m, 1)
+        ref.put(m, 1)
+    qs = [S.And(cond, S.ULT(w[i], w[i + 1])) for i in range(8)] + [S.And(cond, w[2] == 300 % 256)]
+    for q in qs:
+        assert gpu.check_quick_sat(q) is ref.check_quick_sat(q)
+    assert gpu.stats["unsupported"] == 0 and gpu.stats["hits"] > 0
