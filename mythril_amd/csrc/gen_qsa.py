@@ -974,8 +974,6 @@ def make_handlers(variant, pfx):
     acc = []   # (key, body without the dispatch tail) of the Bool producers that get _A/_O forms
 
     def H(key, body, tail=True, reads_stack=True):
-        if PROF and G:
-            body = long_calls(body)
         pre = [VMWAIT] if (G and reads_stack) else []
         prof = prof_point(key[0]) if G else []
         if tail:
@@ -1776,6 +1774,8 @@ def main():
     for variant, pfx, macro, suffix in VARIANTS:
         set_layout(variant)
         hs, subs = make_handlers(variant, pfx)
+        if PROF and variant == "g":
+            hs = [(k, long_calls(b)) for k, b in hs]   # per emitted copy: unique labels
         gen[variant] = (hs, frame(variant, pfx, hs, subs), macro, suffix)
     # (kinds the translator names exist in the enum even when a layout generates no handler)
     names = sorted({k[0] for hs, *_ in gen.values() for k, _ in hs} | {"EQVK", "PUSH_VAR", "PUSH_VARB"})
@@ -1792,8 +1792,9 @@ def main():
         if ln == "@PROFFLUSH@":
             out = []
             for j in range(prof_bytes // 512):
+                # (global offsets are 13-bit signed: the address advances instead)
                 out += [f"ds_read_b64 v[4:5], v7 offset:{512 * j}", "s_waitcnt lgkmcnt(0)",
-                        f"global_atomic_add_x2 v6, v[4:5], s[64:65] offset:{512 * j}"]
+                        "global_atomic_add_x2 v6, v[4:5], s[64:65]", "v_add_u32 v6, 0x200, v6"]
             return out
         return [ln.replace("@PROFBYTES@", str(prof_bytes))]
     for v in gen:

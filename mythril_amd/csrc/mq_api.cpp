@@ -222,6 +222,7 @@ struct mq_ctx {
   int32_t n_bmask = 0;
   DevBuf bmasks, bmask_rows;
   DevBuf prof;   // G profile build (kQsaProfBytes > 0): per-kind (cycles, count), mq_qsa_profile
+  DevBuf prof_sink;   // ... the launches MQ_PROF_LEVEL leaves out write here
   DevBuf verdict_buf;
   // assembly interpreters (qsa.hip): handler byte offsets read back at context creation;
   // k = 0 the P kernel (preloaded variables), k = 1 the G kernel (general)
@@ -952,12 +953,19 @@ int mq_models_upload(mq_ctx* c, const mq_model_batch* mb) {
   return MQ_OK;
 }
 
-// G profile build: the zeroed per-kind (cycles, count) accumulator, nullptr in product builds
-static unsigned long long* prof_buffer(mq_ctx* c) {
+// G profile build: the zeroed per-kind (cycles, count) accumulator, nullptr in product builds.
+// level: the launch's column level, -1 for the tape launch; MQ_PROF_LEVEL=k (diagnostic) keeps
+// only column level k's launch ("t": the tape launch), the others accumulate into a sink.
+static unsigned long long* prof_buffer(mq_ctx* c, int level) {
   if (kQsaProfBytes <= 0) return nullptr;
   if (!c->prof.p) {
     if (c->prof.ensure((size_t)kQsaProfBytes) != hipSuccess) return nullptr;
     if (hipMemset(c->prof.p, 0, (size_t)kQsaProfBytes) != hipSuccess) return nullptr;
+  }
+  static const char* only = std::getenv("MQ_PROF_LEVEL");
+  if (only && *only && (only[0] == 't' ? level != -1 : std::atoi(only) != level)) {
+    if (!c->prof_sink.p && c->prof_sink.ensure((size_t)kQsaProfBytes) != hipSuccess) return nullptr;
+    return c->prof_sink.as<unsigned long long>();
   }
   return c->prof.as<unsigned long long>();
 }
@@ -2769,7 +2777,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       q.n_funcs = (uint32_t)c->n_funcs;
       q.bool_masks = c->bmasks.as<uint64_t>();
       q.n_bool_masks = (uint32_t)c->n_bmask;
-      q.prof_out = prof_buffer(c);
+      q.prof_out = prof_buffer(c, (int)li);
       QArgs* dq = T->cqargs.as<QArgs>() + li;
       if (std::memcmp(&T->cqargs_host[li], &q, sizeof(QArgs)) != 0) {
         PhaseTimer pq(&c->host_t[6]);
@@ -2848,7 +2856,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     q.n_funcs = (uint32_t)c->n_funcs;
     q.bool_masks = c->bmasks.as<uint64_t>();
     q.n_bool_masks = (uint32_t)c->n_bmask;
-    if (k == 1) q.prof_out = prof_buffer(c);
+    if (k == 1) q.prof_out = prof_buffer(c, -1);
     // the argument block only changes with the output buffer / mode / models: re-upload then
     if (!T->qargs_valid[k] || std::memcmp(&T->qargs_dev_copy[k], &q, sizeof(QArgs)) != 0) {
       PhaseTimer pq(&c->host_t[6]);

@@ -41,7 +41,8 @@ class SymbolTable:
     sorts are different declarations.  A symbolic array ``Array(name, dom, rng)`` is read through
     the model's interpretation of ``name`` (its ``as-array`` function, arity 1)."""
 
-    def __init__(self, derive_constant_lookups: bool = True, interpret_keccak: bool = False) -> None:
+    def __init__(self, derive_constant_lookups: bool = True, interpret_keccak: bool = False,
+                 keccak_of_constant=None) -> None:
         self.vars: Dict[Tuple[str, int], int] = {}
         self.var_widths: List[int] = []
         self.funcs: Dict[str, int] = {}
@@ -51,6 +52,10 @@ class SymbolTable:
         # lower keccak256_<n>(x) to in-kernel keccak-f[1600] instead of the model's UF table:
         # exact only for keccak-consistent candidate sets (C4), never for z3 models in general
         self.interpret_keccak = interpret_keccak
+        # bytes -> 32-byte digest (the GPU keccak service in the product): an interpreted keccak
+        # of a constant is folded at lowering time (keccak_function_manager.py:56-64 hashes
+        # concrete inputs concretely) instead of being one keccak-f[1600] column per model
+        self.keccak_of_constant = keccak_of_constant
         self.derived: Dict[int, Tuple[str, Tuple[int, ...]]] = {}  # var index -> (function, const args)
         self.hoisted_vars = set()   # variables computed on the device from column programs
 
@@ -270,9 +275,12 @@ def _lower_one(t: S.Term, a: List[int], tp: Tape, syms: SymbolTable, node: Dict[
         if syms.derive and arr.kind == S.ARRAY_SYM and idx.kind == S.VAL:
             return tp.var(syms.derived_var(arr.params[0], (idx.params[0],), _w(t)), _w(t))
         return tp.select(arr_node(arr, a[0]), a[1])
-    if k == S.KECCAK:
-        return tp.keccak(a[0])
-    if k == S.APP and syms.interpret_keccak and _is_keccak_uf(t.params[0]):
+    if k == S.KECCAK or (k == S.APP and syms.interpret_keccak and _is_keccak_uf(t.params[0])):
+        x = t.args[0]
+        if x.kind == S.VAL and syms.keccak_of_constant is not None and x.width % 8 == 0:
+            dig = syms.keccak_of_constant(x.params[0].to_bytes(x.width // 8, "big"))
+            tp.has_dead = True   # the constant argument is dead: finish() prunes it
+            return tp.const(int.from_bytes(bytes(dig), "big"), 256)
         return tp.keccak(a[0])
     if k == S.APP:
         name, dom = t.params
@@ -582,6 +590,52 @@ def keccak_predicates(terms: Sequence[S.Term], kcols: Sequence[S.Term]) -> List[
     return out
 
 
+def fold_constant_keccaks(roots: Sequence[S.Term], syms: SymbolTable) -> List[S.Term]:
+    """Interpreted keccak (C4) with a host hasher: every keccak of a constant becomes its digest
+    (keccak_function_manager.py:56-64 hashes concrete inputs concretely), and the equalities /
+    connectives that turn constant by it are folded (``keccak(c) == h_c`` of the manager's
+    concrete-hash axioms is TRUE), so no keccak-f[1600] column or tape node is spent on a value
+    every model shares.  Other terms are returned as they are (interned: same objects)."""
+    hasher = syms.keccak_of_constant
+    memo: Dict[int, S.Term] = {}
+
+    def fold(t: S.Term, args: Tuple[S.Term, ...]) -> S.Term:
+        k = t.kind
+        if (k == S.KECCAK or (k == S.APP and _is_keccak_uf(t.params[0]))) and args[0].kind == S.VAL \
+                and args[0].width % 8 == 0:
+            x = args[0]
+            return S.BitVecVal(int.from_bytes(bytes(hasher(x.params[0].to_bytes(x.width // 8, "big"))), "big"), 256)
+        if k == S.EQ and args[0].kind == S.VAL and args[1].kind == S.VAL:
+            return S.BoolVal(args[0].params[0] == args[1].params[0])
+        if k in (S.AND, S.OR):
+            absorb, unit = (S.FALSE, S.TRUE) if k == S.AND else (S.TRUE, S.FALSE)
+            if any(a.kind == absorb for a in args):
+                return S.BoolVal(k == S.OR)
+            rest = tuple(a for a in args if a.kind != unit)
+            if len(rest) != len(args):
+                return (S.And if k == S.AND else S.Or)(*rest) if len(rest) != 1 else rest[0]
+        if k == S.NOT and args[0].kind in (S.TRUE, S.FALSE):
+            return S.BoolVal(args[0].kind == S.FALSE)
+        if all(a is b for a, b in zip(args, t.args)):
+            return t
+        return S.Term(t.kind, t.sort, t.width, args, t.params, t.domain)
+
+    out = []
+    for r in roots:
+        stack = [(r, False)]
+        while stack:
+            t, done = stack.pop()
+            if id(t) in memo:
+                continue
+            if done or not t.args:
+                memo[id(t)] = fold(t, tuple(memo[id(a)] for a in t.args)) if t.args else t
+                continue
+            stack.append((t, True))
+            stack.extend((a, False) for a in t.args if id(a) not in memo)
+        out.append(memo[id(r)])
+    return out
+
+
 def _is_keccak_uf(name: str) -> bool:
     """``keccak256_<n>`` (keccak_function_manager.py:77), not its inverse ``keccak256_<n>-1``."""
     return name.startswith("keccak256_") and name[10:].isdigit()
@@ -605,6 +659,8 @@ def lower_batch(roots: Sequence[S.Term], syms: Optional[SymbolTable] = None, hoi
     even a two-node sub-term in each tape (C3 46.2 -> 36.1 ms, C5 61.6 -> 51.4 ms, C4 11.5 ->
     10.2 ms against the earlier threshold of 8; profiles/r02hm*)."""
     syms = syms or SymbolTable()
+    if syms.interpret_keccak and syms.keccak_of_constant is not None:
+        roots = fold_constant_keccaks(roots, syms)
     hoisted: Dict[int, int] = {}
     narrow: Dict[int, int] = {}
     col_terms: List[S.Term] = []
@@ -641,6 +697,13 @@ def lower_batch(roots: Sequence[S.Term], syms: Optional[SymbolTable] = None, hoi
                     have.add(id(t))
                     col_terms.append(t)
                     program[id(t)] = c
+        # the Not of another column is one NOT in its readers (G fuses it into the packed-Bool
+        # push), not a column of its own a level deeper (C4: a whole launch of NOT columns)
+        ids = {id(t) for t in col_terms}
+        drop = {k for k, t in enumerate(col_terms[:n_shared]) if t.kind == S.NOT and id(t.args[0]) in ids}
+        if drop:
+            col_terms = [t for k, t in enumerate(col_terms) if k not in drop]
+            n_shared -= len(drop)
         # every keccak application and Concat piece, also those already chosen as shared terms
         # (an address key x & (2^160 - 1) is both): never narrowed
         kpieces = {id(t) for t in keccak_subterms(list(roots), syms, [])}

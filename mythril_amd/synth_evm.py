@@ -539,7 +539,8 @@ def c4_workload(n_tapes: int = 200, n_models: int = 1_000_000, seed: int = 4, pl
     lo, hi = shard if shard else (0, n_models)
     models = KeccakModels(seed, n_models, n_tx, lo, hi, hasher_many)
     ghost = EvmModels(seed + 1_000_003, max(1, n_tapes), n_tx, 0, 0, address_args=True)
-    syms = SymbolTable(interpret_keccak=interpret_keccak)
+    syms = SymbolTable(interpret_keccak=interpret_keccak,
+                       keccak_of_constant=lambda b: bytes(hasher_many(np.frombuffer(b, np.uint8)[None, :])[0]))
     roots, expected = [], np.full(n_tapes, -1, np.int32)
     planted = rng.random(n_tapes) < planted_frac
     def hashed_keys_are_concrete(w) -> bool:

@@ -370,3 +370,35 @@ def test_keccak_predicate_canonical_forms():
     assert got[id(terms[3])] is terms[3]
     assert got[id(terms[4])] is S.Not(S.ULT(h, c))           # UGE(h, c) = Or(UGT(h, c), h == c)
     assert id(terms[5]) not in got                            # 48 is not a power of two
+
+
+def test_constant_keccaks_fold_at_lowering():
+    """Interpreted keccak with a host hasher: keccak of a constant is its digest, the manager's
+    concrete-hash equalities fold to TRUE, and no keccak node or column is left for them; the
+    verdicts equal the unfolded lowering's."""
+    import keccak_ref
+    from mythril_amd.lower import fold_constant_keccaks
+    f = S.Function("keccak256_512", [512], 256)
+    c = S.BitVecVal(0x1234 << 256 | 7, 512)
+    hc = S.BitVecVal(int.from_bytes(keccak_ref.keccak256(c.params[0].to_bytes(64, "big")), "big"), 256)
+    x = S.BitVecSym("x", 256)
+    roots = [S.And(f(c) == hc, S.ULT(x, f(c))), S.Or(f(c) == x, x == 3), S.Not(f(c) == hc),
+             S.And(f(S.Concat(x, S.BitVecVal(1, 256))) == x, f(c) == hc)]
+    syms = SymbolTable(interpret_keccak=True, keccak_of_constant=keccak_ref.keccak256)
+    folded = fold_constant_keccaks(roots, syms)
+    assert folded[0] is S.And(S.ULT(x, hc)) or folded[0] is S.ULT(x, hc)
+    assert folded[2].kind == S.FALSE
+    tb, syms1, ok = lower_batch(roots, syms, hoist=True)
+    tb0, syms0, ok0 = lower_batch(roots, SymbolTable(interpret_keccak=True))
+    assert ok.all() and ok0.all()
+    n_kec = sum(int((tb.tape_nodes(t)["op"] == Op.KECCAK).sum()) for t in range(tb.n_tapes))
+    n_kec += 0 if tb.columns is None else sum(int((tb.columns.programs.tape_nodes(k)["op"] == Op.KECCAK).sum())
+                                              for k in range(tb.columns.n))
+    assert n_kec == 1                      # only the symbolic message is hashed
+    from mythril_amd.smt_model import Model
+    rnd = random.Random(4)
+    models = [Model({"x": rnd.choice([3, hc.params[0] + 1, rnd.getrandbits(256)])}) for _ in range(30)]
+    from oracle_engine import apply_columns
+    mb = serialize_models(models, syms1)
+    v = cref.verdicts(tb, apply_columns(tb, mb) if tb.columns is not None else mb)
+    assert (v == cref.verdicts(tb0, serialize_models(models, syms0))).all()
