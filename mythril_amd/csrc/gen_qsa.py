@@ -190,13 +190,35 @@ NEXT_P = [
 ]
 
 
+_WIN_LABELS = [0]
+
+
 def load_window(first, pfx=None):
     """Make the program's next 64-word block the window (decoded, s16 = 0) and prefetch the one
     after it into NWIN (mq_api.cpp qsa_window_layout: blocks are aligned and contiguous).
     first (tape start, s[36:37] = the program's address): the block is NWIN when the previous
     window's successor is this program (consecutive descriptors), else it is loaded.  Otherwise
-    (REFILL): the block is NWIN, 256 bytes on."""
-    out = ["v_mbcnt_lo_u32_b32 v5, -1, 0", "v_mbcnt_hi_u32_b32 v5, -1, v5", "v_lshlrev_b32 v5, 2, v5"]
+    (REFILL): the block is NWIN, 256 bytes on.
+    Programs in LDS (QArgs.prog_lds bit 0, s57 = its LDS offset | 1; the workgroup's programs
+    were copied there by the prologue, stage_programs, from word s56 on): the block is one LDS
+    read, s14 = its LDS address — no global round trip at a tape start, where a short tape (C4)
+    could not cover the prefetch's latency."""
+    k = _WIN_LABELS[0]
+    _WIN_LABELS[0] += 1
+    glob, dec = f"{pfx}_wg{k}", f"{pfx}_wd{k}"
+    out = ["v_mbcnt_lo_u32_b32 v5, -1, 0", "v_mbcnt_hi_u32_b32 v5, -1, v5", "v_lshlrev_b32 v5, 2, v5",
+           "s_bitcmp1_b32 s57, 0",
+           f"s_cbranch_scc0 {glob}"]
+    if first:
+        out += ["s_sub_u32 s34, s80, s56", "s_lshl_b32 s34, s34, 2", "s_add_u32 s14, s57, s34",
+                "s_sub_u32 s14, s14, 1"] + (["s_mov_b32 s39, 1"] if PROF else [])
+    else:
+        out += ["s_add_u32 s14, s14, 256"]
+    out += ["v_add_u32 v5, s14, v5",
+            f"ds_read_b32 {WIN}, v5",
+            "s_waitcnt lgkmcnt(0)",
+            f"s_branch {dec}",
+            f"{glob}:"]
     if first:
         out += ["s_add_u32 s34, s14, 256", "s_addc_u32 s35, s15, 0",
                 "s_cmp_eq_u64 s[34:35], s[36:37]",
@@ -210,6 +232,7 @@ def load_window(first, pfx=None):
         out += ["s_add_u32 s14, s14, 256", "s_addc_u32 s15, s15, 0", "s_waitcnt vmcnt(0)"]
     out += [f"v_mov_b32 {WIN}, {NWIN}",
             f"global_load_dword {NWIN}, v5, s[14:15] offset:256",
+            f"{dec}:",
             "s_mov_b32 s16, 0",
             f"v_and_b32 v5, 0xffff, {WIN}",
             f"v_lshl_add_u32 {WINA}, v5, {3 if PROF else 2}, s12",
@@ -967,6 +990,14 @@ def long_calls(body):
     return out
 
 
+def handler_data_words(body):
+    """Inline program words a G handler body reads past its own word: every window read
+    advances s16, and the dispatch tail's advance is the next handler word."""
+    adv = sum(1 for ln in body if ln == "s_add_u32 s16, s16, 1")
+    tail = sum(1 for ln in body if ln.startswith("s_setpc_b64 s[18:19]"))
+    return adv - tail
+
+
 def make_handlers(variant, pfx):
     """(key, body lines) for the variant; key = (kind, d, v)."""
     G = variant == "g"
@@ -987,7 +1018,7 @@ def make_handlers(variant, pfx):
 
     H(("END",), [f"s_branch {pfx}_tape_end"], tail=False, reads_stack=False)
     if G:
-        H(("REFILL",), load_window(False), reads_stack=False)
+        H(("REFILL",), load_window(False, pfx), reads_stack=False)
     # ---- leaves
     for d in range(D):
         # preloaded variables (P: the batch's first 8; G: the 8 its tapes push most)
@@ -1022,21 +1053,31 @@ def make_handlers(variant, pfx):
             # tile's masks): one scalar load straight into the Bool stack
             H(("PUSH_PKB", d), ["s_lshl_b32 s34, s17, 3", f"s_load_dwordx2 {B(d)}, s[96:97], s34", "s_waitcnt lgkmcnt(0)"],
               reads_stack=False)
-        if G and d >= 1:
-            # a run of n + 1 packed Bool masks AND-ed into B(d - 1) (the translator merges
-            # consecutive PUSH_PKB_A at slot d): imm = the first mask, n inline data words the
-            # others; all n + 1 scalar loads are in flight behind one wait
-            for n in range(1, 4):
-                body = ["s_lshl_b32 s34, s17, 3", "s_load_dwordx2 s[64:65], s[96:97], s34"]
+        if G:
+            # a run of n + 1 packed Bool masks (the translator merges consecutive PUSH_PKB_A at
+            # slot d, after a PUSH_PKB at d - 1 or not): PKBN_A AND-s them into B(d - 1), PKBP
+            # pushes their AND as B(d) (at most six masks a word).  imm = the first mask, n inline
+            # data words the others;
+            # all n + 1 scalar loads are in flight behind one wait.  (lowering puts the Bool
+            # columns of a conjunction first, so C4's ~11 column conjuncts are one or two words)
+            # (mask pairs: never s[72:75] — &best[tape], M * 4 — nor s[80:87], live across handlers)
+            idx = ["s35", "s36", "s37", "s38", "s39"]
+            mr = ["s[64:65]", "s[66:67]", "s[68:69]", "s[70:71]", "s[76:77]", "s[78:79]"]
+            for n in range(1, len(mr)):
+                body = ["s_lshl_b32 s34, s17, 3", f"s_load_dwordx2 {mr[0]}, s[96:97], s34"]
                 for i in range(n):
-                    body += [f"v_readlane_b32 s{35 + i}, {WIN}, s16", "s_add_u32 s16, s16, 1"]
+                    body += [f"v_readlane_b32 {idx[i]}, {WIN}, s16", "s_add_u32 s16, s16, 1"]
                 body += ["s_nop 3"]
                 for i in range(n):
-                    body += [f"s_lshl_b32 s{35 + i}, s{35 + i}, 3",
-                             f"s_load_dwordx2 s[{66 + 2 * i}:{67 + 2 * i}], s[96:97], s{35 + i}"]
+                    body += [f"s_lshl_b32 {idx[i]}, {idx[i]}, 3",
+                             f"s_load_dwordx2 {mr[i + 1]}, s[96:97], {idx[i]}"]
                 body += ["s_waitcnt lgkmcnt(0)"]
-                body += [f"s_and_b64 {B(d - 1)}, {B(d - 1)}, s[{64 + 2 * i}:{65 + 2 * i}]" for i in range(n + 1)]
-                H(("PKBN_A", d, n), body, reads_stack=False)
+                if d >= 1:
+                    H(("PKBN_A", d, n), body + [f"s_and_b64 {B(d - 1)}, {B(d - 1)}, {mr[i]}" for i in range(n + 1)],
+                      reads_stack=False)
+                H(("PKBP", d, n), body + [f"s_and_b64 {B(d)}, {mr[0]}, {mr[1]}"]
+                  + [f"s_and_b64 {B(d)}, {B(d)}, {mr[i]}" for i in range(2, n + 1)],
+                  reads_stack=False)
         H(("PUSH_CONST", d), ["s_lshl_b32 s34, s17, 2", "s_load_dwordx8 s[64:71], s[20:21], s34", "s_waitcnt lgkmcnt(0)"]
           + [f"v_mov_b64 {S2(d, l)}, s[{64 + l}:{65 + l}]" for l in range(0, L, 2)], reads_stack=False)
         if G:
@@ -1390,9 +1431,88 @@ def stage_rows(pfx):
     out += ["s_lshl_b32 s70, s61, 8", f"v_add_u32 v5, s70, {STG}", "s_waitcnt vmcnt(0)"]
     out += [f"ds_write_b32 v5, {T(j)} offset:{256 * j}" for j in range(8)]
     out += ["s_add_u32 s61, s61, 32", f"s_branch {pfx}_stage_loop",
-            f"{pfx}_stage_done:",
-            "s_waitcnt lgkmcnt(0)",
+            f"{pfx}_stage_done:"]
+    out += stage_programs(pfx)
+    out += ["s_waitcnt lgkmcnt(0)",
             "s_barrier"]
+    return out
+
+
+DESC_LDS = 2048   # G: LDS bytes of the workgroup's descriptors (<= 64 of 32 B), just below its programs
+
+
+def stage_descs(pfx):
+    """stage_programs, first: the workgroup's descriptors [s58, s59) (at most 64) into LDS at
+    (s57 - 1) - DESC_LDS, descriptor i of the run at 32 * i; wave w copies words 64w .. and
+    256 + 64w .. (lanes past the run's end masked off: no read past the descriptor array).
+    Wants s68 = wave, v6 = 4 * lane."""
+    out = ["s_sub_u32 s64, s59, s58", "s_lshl_b32 s64, s64, 3",                      # words
+           "s_lshl_b32 s66, s58, 5", "s_add_u32 s66, s22, s66", "s_addc_u32 s67, s23, 0",
+           f"s_sub_u32 s69, s57, {DESC_LDS + 1}",
+           "v_lshrrev_b32 v7, 2, v6"]
+    for j in range(2):
+        out += [f"s_lshl_b32 s70, s68, 6", f"s_add_u32 s70, s70, {256 * j}",
+                "v_add_u32 v5, s70, v7",
+                "v_cmp_gt_u32_e64 s[60:61], s64, v5",
+                "s_nop 3",
+                "s_and_saveexec_b64 s[36:37], s[60:61]",
+                "v_lshlrev_b32 v5, 2, v5",
+                f"global_load_dword {T(j)}, v5, s[66:67]",
+                "s_waitcnt vmcnt(0)",
+                "v_add_u32 v5, s69, v5",
+                f"ds_write_b32 v5, {T(j)}",
+                "s_mov_b64 exec, s[36:37]"]
+    return out
+
+
+def stage_programs(pfx):
+    """G, QArgs.prog_lds on (s57 = its LDS offset | 1, else 0): copy the programs of the
+    workgroup's descriptors [s58, s59) — one contiguous run of 64-word blocks, from word s56 on
+    (mq_api.cpp: descriptors in order, programs contiguous) — into LDS, block b at offset
+    256 * b; wave w copies blocks w, w + 4, ..., 8 loads in flight.  The host turns it on only
+    when the largest workgroup's run fits beside the temps and staged rows."""
+    out = ["s_load_dword s57, s[10:11], 0x1a4",
+           "s_waitcnt lgkmcnt(0)",
+           "s_bitcmp1_b32 s57, 0",
+           f"s_cbranch_scc0 {pfx}_pst_done",
+           "s_cmp_ge_u32 s58, s59",
+           f"s_cbranch_scc1 {pfx}_pst_done",
+           "v_lshrrev_b32 v4, 6, v3",
+           "v_mbcnt_lo_u32_b32 v6, -1, 0", "v_mbcnt_hi_u32_b32 v6, -1, v6", "v_lshlrev_b32 v6, 2, v6",
+           "s_nop 1",
+           "v_readfirstlane_b32 s68, v4",                      # wave
+           "s_nop 3"]                                          # VALU SGPR write -> SALU read
+    out += stage_descs(pfx)
+    out += ["s_lshl_b32 s34, s58, 5", "s_add_u32 s34, s22, s34", "s_addc_u32 s35, s23, 0",
+            "s_load_dword s56, s[34:35], 0x0",                 # prog_off of the first descriptor
+            "s_lshl_b32 s36, s59, 5", "s_sub_u32 s36, s36, 32", "s_add_u32 s36, s22, s36", "s_addc_u32 s37, s23, 0",
+            "s_load_dwordx2 s[64:65], s[36:37], 0x0",          # prog_off, prog_len of the last
+            "s_waitcnt lgkmcnt(0)",
+            "s_add_u32 s64, s64, s65",
+            "s_sub_u32 s64, s64, s56",
+            "s_add_u32 s64, s64, 63",
+            "s_lshr_b32 s64, s64, 6",                          # blocks
+            "s_lshl_b32 s66, s56, 2", "s_add_u32 s66, s46, s66", "s_addc_u32 s67, s47, 0",   # first block
+            "s_sub_u32 s69, s57, 1",                            # LDS offset
+            "s_mov_b32 s65, s68"]                               # this wave's next block
+    out += [f"{pfx}_pst_loop:",
+           "s_cmp_ge_u32 s65, s64",
+           f"s_cbranch_scc1 {pfx}_pst_done"]
+    for j in range(8):
+        out += [f"s_add_u32 s70, s65, {4 * j}", "s_cmp_ge_u32 s70, s64", f"s_cbranch_scc1 {pfx}_pst_l{j}",
+                "s_lshl_b32 s70, s70, 8", "s_add_u32 s36, s66, s70", "s_addc_u32 s37, s67, 0",
+                f"global_load_dword {T(j)}, v6, s[36:37]"]
+    out += [f"{pfx}_pst_l8:"] + [f"{pfx}_pst_l{j}:" for j in range(8)]
+    out += ["s_waitcnt vmcnt(0)"]
+    for j in range(8):
+        out += [f"s_add_u32 s70, s65, {4 * j}", "s_cmp_ge_u32 s70, s64", f"s_cbranch_scc1 {pfx}_pst_w",
+                "s_lshl_b32 s70, s70, 8", "s_add_u32 s70, s69, s70",
+                "v_add_u32 v7, s70, v6",
+                f"ds_write_b32 v7, {T(j)}"]
+    out += [f"{pfx}_pst_w:",
+            "s_add_u32 s65, s65, 32",
+            f"s_branch {pfx}_pst_loop",
+            f"{pfx}_pst_done:"]
     return out
 
 
@@ -1513,6 +1633,14 @@ def frame(variant, pfx, handlers, subs):
         "s_add_u32 s25, s24, s83",
         "s_min_u32 s25, s25, s82",
     ] + ([
+        # G: the workgroup's descriptors [s58, s59) (its 4 waves' tape groups), for stage_programs
+        "s_andn2_b32 s58, s97, 3",
+        "s_mul_i32 s58, s58, s83",
+        "s_or_b32 s59, s97, 3",
+        "s_add_u32 s59, s59, 1",
+        "s_mul_i32 s59, s59, s83",
+        "s_min_u32 s59, s59, s82",
+    ] if G else []) + ([
         # G: s[96:97] = this tile's packed Bool masks, bool_masks + 8 * tile * n_bool_masks
         "s_load_dwordx2 s[64:65], s[10:11], 0x198",
         "s_load_dword s66, s[10:11], 0x1a0",
@@ -1575,12 +1703,29 @@ def frame(variant, pfx, handlers, subs):
         f"{pfx}_tape_loop:",
         "s_cmp_ge_u32 s24, s25",
         f"s_cbranch_scc1 {pfx}_tapes_done",
+    ] + ([
+        # programs in LDS: the descriptors too (stage_descs), 8 words read into s[80:87]
+        "s_bitcmp1_b32 s57, 0",
+        f"s_cbranch_scc0 {pfx}_hdr_mem",
+        "s_sub_u32 s34, s24, s58",
+        "s_lshl_b32 s34, s34, 5",
+        "s_add_u32 s34, s34, s57",
+        f"s_sub_u32 s34, s34, {DESC_LDS + 1}",
+        "v_mbcnt_lo_u32_b32 v4, -1, 0", "v_mbcnt_hi_u32_b32 v4, -1, v4", "v_lshlrev_b32 v4, 2, v4",
+        "v_add_u32 v4, s34, v4",
+        "ds_read_b32 v4, v4",
+        "s_waitcnt lgkmcnt(0)",
+    ] + [f"v_readlane_b32 s{80 + i}, v4, {i}" for i in range(8)] + [
+        "s_nop 3",                          # VALU SGPR write -> SALU read
+        f"s_branch {pfx}_hdr_done",
+        f"{pfx}_hdr_mem:",
+    ] if G else []) + [
         "s_lshl_b32 s34, s24, 5",
         "s_add_u32 s34, s22, s34",
         "s_addc_u32 s35, s23, 0",
         "s_load_dwordx8 s[80:87], s[34:35], 0x0",
         "s_waitcnt lgkmcnt(0)",
-    ] + (prof_point("F_HDR") if G else []) + [
+    ] + ([f"{pfx}_hdr_done:"] if G else []) + (prof_point("F_HDR") if G else []) + [
         "s_lshl_b32 s34, s82, 2",
         "s_add_u32 s72, s26, s34",           # s[72:73] = &best[tape] (handlers never touch s72-s73, s80-s87)
         "s_addc_u32 s73, s27, 0",
@@ -1848,6 +1993,12 @@ def main():
                 v = key[2] if len(key) > 2 else -1
                 f.write(f"  {{QK_{kind}, {d}, {v}}},\n")
             f.write("};\n")
+        # G: inline data words each handler consumes from the program window (its reads of the
+        # window advance s16; NEXT_G's one is the next handler word) — qsa_window_layout keeps a
+        # handler and its data in one window, the translator's passes step over the data
+        hs_g = gen["g"][0]
+        f.write("static const unsigned char kQsaHandlerDataWordsG[] = {"
+                + ", ".join(str(handler_data_words(b)) for _, b in hs_g) + "};\n")
         f.write("}  // namespace mq\n#endif\n")
     for variant, (hs, lines, *_ ) in gen.items():
         nins = sum(1 for ln in lines if ln and not ln.startswith(".L"))

@@ -336,6 +336,7 @@ struct mq_tapes {
   bool cq_live = false;
   DevBuf cqdescs, cqprog, cqconsts, cqargs;
   std::vector<QArgs> cqargs_host;   // what cqargs holds on the device, per level
+  std::vector<GDesc> qdescs_h, cqdescs_h;   // host copies (program runs for QArgs.prog_lds)
   std::vector<uint32_t> cq_stage_rows;                   // staged rows of every level, level by level
   std::vector<uint32_t> cq_lvl_stage_off, cq_lvl_stage_n;  // per level: its rows in cq_stage_rows
   std::vector<int> cq_lvl_temps;                         // per level: LDS temp slots
@@ -607,26 +608,11 @@ static int qsa_init(mq_ctx* c) {
     ok = ok && (uint64_t)c->qsa_hbase_lo[k] + max_off < (1ull << 32);
     c->qsa_off[k].resize(nh);
   }
-  // G handler word index -> inline data words that follow it (PUSH_CONSTW)
+  // G handler word index -> inline data words that follow it (generated: the window words the
+  // handler body reads, gen_qsa.py handler_data_words)
   c->qsa_data_words.assign(1 << 16, 0);
-  for (int d = 0; ok && d < kQsaStack; d++)
-    for (int n = 0; n < 8; n++) {
-      const int h = c->qsa_index[1][QK_PUSH_CONSTW][d][n + 1];
-      if (h >= 0) c->qsa_data_words[hword(1, c->qsa_off[1][h]) & 0xFFFFu] = (uint8_t)(n + 1);
-    }
-  // compare-with-inline-constant handlers (and their fused forms): kQsaKClassWords[class]
-  for (int h = 0; ok && h < kQsaHandlersG; h++) {
-    const std::string name = kQsaKindNames[kQsaHandlerKeysG[h].kind];
-    const std::string base = name.substr(0, name.find('_'));
-    const int v = kQsaHandlerKeysG[h].v;
-    int words = -1;
-    if (base == "EQVK") words = kQsaKClassWords[1 + (v & 1)];
-    else if (base == "EQK" || base == "ULTK" || base == "UGTK" || base == "ULEK" || base == "UGEK") words = kQsaKClassWords[v];
-    else if (base == "PKBN") words = v;   // the run's other mask indices
-    else if (base == "MEQK2" || base == "SEQK2") words = 2;
-    else if (base == "MEQK8" || base == "SEQK8") words = 8;
-    if (words > 0) c->qsa_data_words[hword(1, c->qsa_off[1][h]) & 0xFFFFu] = (uint8_t)words;
-  }
+  for (int h = 0; ok && h < kQsaHandlersG; h++)
+    if (kQsaHandlerDataWordsG[h] > 0) c->qsa_data_words[hword(1, c->qsa_off[1][h]) & 0xFFFFu] = kQsaHandlerDataWordsG[h];
   for (int q = 0; q < QK_COUNT; q++) {
     const std::string n = kQsaKindNames[q];
     c->qsa_vm_drain[q] = n == "PUSH_MEMB" || n.rfind("MEQK", 0) == 0 || n.rfind("UF1", 0) == 0;
@@ -1142,22 +1128,26 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
   };
   // G: consecutive "B(d - 1) &= packed mask" words (PUSH_PKB_A at slot d) as one PKBN_A word
   // with up to four masks: their scalar loads share one wait
+  // ... and a PUSH_PKB at slot d - 1 followed by such words as one PKBP word at d - 1 (their AND
+  // pushed); up to six masks a word
   auto merge_pkb = [&](int d) {
     if (log.size() < 2) return;
     const Emit e1 = log.back();
     if (e1.kind != QK_PUSH_PKB_A || e1.d != d || out.size() != ends_at(e1)) return;
     const Emit e0 = log[log.size() - 2];
-    if (ends_at(e0) != e1.pos || e0.d != d) return;
-    int n0;   // masks after the first one in e0
-    if (e0.kind == QK_PUSH_PKB_A) n0 = 0;
-    else if (e0.kind == QK_PKBN_A) n0 = e0.v;
+    if (ends_at(e0) != e1.pos) return;
+    int n0, kind, x;   // masks after the first one in e0; merged kind and slot
+    if (e0.d == d && e0.kind == QK_PUSH_PKB_A) n0 = 0, kind = QK_PKBN_A, x = d;
+    else if (e0.d == d && e0.kind == QK_PKBN_A) n0 = e0.v, kind = QK_PKBN_A, x = d;
+    else if (e0.d == d - 1 && e0.kind == QK_PUSH_PKB) n0 = 0, kind = QK_PKBP, x = d - 1;
+    else if (e0.d == d - 1 && e0.kind == QK_PKBP) n0 = e0.v, kind = QK_PKBP, x = d - 1;
     else return;
-    if (n0 + 1 > 3 || c->qsa_index[k][QK_PKBN_A][d][n0 + 2] < 0) return;
+    if (n0 + 1 > 5 || c->qsa_index[k][kind][x][n0 + 2] < 0) return;
     std::vector<uint32_t> data(out.begin() + (long)(e0.pos + 1), out.begin() + (long)ends_at(e0));
     data.push_back(e1.imm);
     const uint32_t imm0 = e0.imm;
     drop_last(2);
-    emit_k(QK_PKBN_A, d, n0 + 1, imm0, data);
+    emit_k(kind, x, n0 + 1, imm0, data);
   };
   // G: "PUSH_MEM / PUSH_MEMS x (n limbs); EQK_A x" (a model variable compared with an inline
   // constant, AND-ed into the conjunction) as one M/SEQK{2,8}_A word: row / slot in the
@@ -2294,6 +2284,36 @@ static std::vector<int64_t> count_pushes(const mq_ctx* c, const std::vector<Comp
 static int64_t g_tapes_per_group(int64_t n, int64_t M);
 static int64_t cq_tapes_per_group(int64_t n, int64_t M);
 
+// QArgs.prog_lds of a G launch over descriptors d[0, n) with tpg tapes per wave: the largest run
+// of program blocks one workgroup (4 tape groups) reads, copied into LDS by its prologue
+// (gen_qsa.py stage_programs) when it fits beside the temps, staged rows and profile tables in
+// the G workgroup budget (MQ_G_STAGE_KB, 26 KB: 6 workgroups per CU).  Sets q.prog_lds and
+// returns the LDS bytes it adds (0: programs stay in memory; MQ_NO_PROG_LDS=1 forces that).
+static size_t plan_prog_lds(QArgs& q, const GDesc* d, int64_t n, int64_t tpg, size_t lds_other, size_t lds_prof) {
+  static const bool off = std::getenv("MQ_NO_PROG_LDS") != nullptr;
+  q.prog_lds = 0;
+  // (the workgroup's descriptors go to LDS too: kDescLds bytes, at most 64 of them)
+  constexpr size_t kDescLds = 2048;
+  if (off || n <= 0 || 4 * tpg * (int64_t)sizeof(GDesc) > (int64_t)kDescLds) return 0;
+  int64_t kb = 26;
+  if (const char* e = std::getenv("MQ_G_STAGE_KB")) kb = std::atol(e);
+  uint64_t run = 0;
+  for (int64_t f = 0; f < n; f += 4 * tpg) {
+    const int64_t l = std::min<int64_t>(n, f + 4 * tpg) - 1;
+    run = std::max<uint64_t>(run, (uint64_t)d[l].prog_off + d[l].prog_len - d[f].prog_off);
+  }
+  const size_t bytes = kDescLds + (size_t)((run + 63) / 64) * 256;
+  // (the profile build's per-wave tables, lds_prof of lds_other, are not charged to the budget)
+  const bool fits = lds_other - lds_prof + bytes <= (size_t)kb * 1024;
+  static const bool dbg = std::getenv("MQ_PROG_LDS_DEBUG") != nullptr;
+  if (dbg)
+    std::fprintf(stderr, "prog_lds: %lld descs, tpg %lld, run %llu words (%zu B) + %zu B other: %s\n", (long long)n,
+                 (long long)tpg, (unsigned long long)run, bytes, lds_other - lds_prof, fits ? "LDS" : "memory");
+  if (!fits) return 0;
+  q.prog_lds = (uint32_t)(lds_other + kDescLds) | 1u;
+  return bytes;
+}
+
 static void plan_stage(const mq_ctx* c, const std::vector<int64_t>& pushes, const std::vector<int>* gpre, int temps,
                        double wg_share, std::vector<int>& gstage, std::vector<uint32_t>& rows) {
   int64_t kb = 26;
@@ -2447,6 +2467,7 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
     T->q_temps[k] = temps[k];
   }
   if (descs.empty()) descs.push_back(GDesc{});
+  T->qdescs_h = descs;
   HIPCHK(T->qdescs.upload(descs.data(), descs.size(), c->stream));
   HIPCHK(T->qprog.upload(prog.data(), prog.size(), c->stream));
   if (T->stage_rows.empty()) HIPCHK(T->stage_dev.ensure(sizeof(uint32_t)));
@@ -2513,6 +2534,7 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
   const uint32_t endw = hword(1, c->qsa_off[1][c->qsa_index[1][QK_END][0][0]]);
   prog.insert(prog.end(), 130, endw);   // the window + next-window prefetch read up to 127 words past the last END
   consts.resize(consts.size() + 16, 0);
+  T->cqdescs_h = descs;
   HIPCHK(T->cqdescs.upload(descs.data(), descs.size(), c->stream));
   HIPCHK(T->cqprog.upload(prog.data(), prog.size(), c->stream));
   HIPCHK(T->cqconsts.upload(consts.data(), consts.size(), c->stream));
@@ -2778,6 +2800,9 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       q.bool_masks = c->bmasks.as<uint64_t>();
       q.n_bool_masks = (uint32_t)c->n_bmask;
       q.prof_out = prof_buffer(c, (int)li);
+      const size_t lds_other = (size_t)q.lds_wave_bytes * 4 + (size_t)q.n_stage * 256 + 4 * (size_t)kQsaProfBytes;
+      const size_t lds = lds_other + plan_prog_lds(q, T->cqdescs_h.data() + lv.cq_begin, n, tpg, lds_other,
+                                                   4 * (size_t)kQsaProfBytes);
       QArgs* dq = T->cqargs.as<QArgs>() + li;
       if (std::memcmp(&T->cqargs_host[li], &q, sizeof(QArgs)) != 0) {
         PhaseTimer pq(&c->host_t[6]);
@@ -2792,8 +2817,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
         return MQ_ERR_ARG;
       }
       HIPCHK(start_timer());
-      HIPCHK(launch_qsa(1, dq, 8u * (unsigned)((groups + 3) / 4), (unsigned)rows,
-                        (size_t)q.lds_wave_bytes * 4 + (size_t)q.n_stage * 256 + 4 * (size_t)kQsaProfBytes, st));
+      HIPCHK(launch_qsa(1, dq, 8u * (unsigned)((groups + 3) / 4), (unsigned)rows, lds, st));
     }
     for (int g = 0; g < kGen; g++) {
       const mq_tapes::Variant* v = g == 0 ? &v8 : &lv.v[g];
@@ -2857,6 +2881,8 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     q.bool_masks = c->bmasks.as<uint64_t>();
     q.n_bool_masks = (uint32_t)c->n_bmask;
     if (k == 1) q.prof_out = prof_buffer(c, -1);
+    size_t lds = (size_t)q.lds_wave_bytes * 4 + (size_t)q.n_stage * 256 + (k == 1 ? 4 * (size_t)kQsaProfBytes : 0);
+    if (k == 1) lds += plan_prog_lds(q, T->qdescs_h.data() + T->q_count[0], n, tpg, lds, 4 * (size_t)kQsaProfBytes);
     // the argument block only changes with the output buffer / mode / models: re-upload then
     if (!T->qargs_valid[k] || std::memcmp(&T->qargs_dev_copy[k], &q, sizeof(QArgs)) != 0) {
       PhaseTimer pq(&c->host_t[6]);
@@ -2877,8 +2903,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       }
     }
     HIPCHK(start_timer());
-    HIPCHK(launch_qsa(k, T->qargs[k].as<QArgs>(), gx, gy,
-                      (size_t)q.lds_wave_bytes * 4 + (size_t)q.n_stage * 256 + (k == 1 ? 4 * (size_t)kQsaProfBytes : 0), st));
+    HIPCHK(launch_qsa(k, T->qargs[k].as<QArgs>(), gx, gy, lds, st));
   }
   for (const auto& v : cpp) {
     if (v.count <= 0) continue;

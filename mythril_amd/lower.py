@@ -213,7 +213,10 @@ def _lower_one(t: S.Term, a: List[int], tp: Tape, syms: SymbolTable, node: Dict[
     if k == S.NOT:
         return tp.not_(a[0])
     if k == S.AND:
-        return tp.and_(*a)
+        # Bool variables (hoisted Bool columns: packed lane masks) first — the G interpreter
+        # ANDs a run of up to eight in one dispatch (gen_qsa.py PKBP / PKBN_A); a conjunction's
+        # value does not depend on its order
+        return tp.and_(*sorted(a, key=lambda n: 0 if tp.nodes[n][0] == Op.VAR.value and tp.kind[n] == "bool" else 1))
     if k == S.OR:
         return tp.or_(*a)
     if k == S.XOR:
@@ -512,6 +515,45 @@ def _column_levels(cols: Sequence[S.Term]) -> Dict[int, int]:
     return level
 
 
+# a column conjunction doing at least this many model-table lookups (UF / array reads, one memory
+# round trip per entry scanned) is evaluated as its lookup-carrying conjuncts, each a column of
+# its own (MQ_SPLIT_AND_LOOKUPS overrides, 0 = off)
+SPLIT_AND_LOOKUPS = 4
+
+
+def split_lookup_conjunctions(cols: Sequence[S.Term], min_lookups: int) -> List[S.Term]:
+    """C4's keccak-axiom conjunction (keccak_function_manager.py:116-130: inv(f(x)) == x for
+    every hashed input, two 256-bit inverse lookups each) is one column of ~140 nodes and 14
+    lookups: one wave per 64-model tile walks all 14 lookups in sequence (~15 000 cycles of
+    latency each) while the workgroup's other waves, done with their small columns, wait — the
+    level ran 1.6 ms.  Its conjuncts that do lookups become columns of their own (spread over the
+    waves of the level's launch); the conjunction then ANDs their Bool lane masks, a level later.
+    Returns the new columns."""
+    cut = {id(t) for t in cols}
+    out: List[S.Term] = []
+
+    def lookups(t: S.Term) -> int:
+        return sum(1 for h in _walk_cut(t, cut) if h.kind in (S.APP, S.SELECT) and (h is t or id(h) not in cut))
+
+    for t in list(cols):
+        if t.kind != S.AND or lookups(t) < min_lookups:
+            continue
+        stack, parts = list(t.args), []
+        while stack:   # conjuncts of the AND tree, through ANDs that are not columns themselves
+            a = stack.pop()
+            if a.kind == S.AND and id(a) not in cut:
+                stack.extend(a.args)
+            elif a.kind not in _LEAVES and id(a) not in cut and lookups(a) > 0:
+                parts.append(a)
+        if len(parts) < 2:
+            continue
+        for a in parts:
+            if id(a) not in cut:
+                cut.add(id(a))
+                out.append(a)
+    return out
+
+
 def keccak_subterms(terms: Sequence[S.Term], syms, chosen: Sequence[S.Term]) -> List[S.Term]:
     """Hoisting companion for interpreted keccak (C4): every keccak application under ``terms``
     becomes a column of its own — its argument's Concat pieces too, unless they are leaves — so
@@ -686,6 +728,9 @@ def lower_batch(roots: Sequence[S.Term], syms: Optional[SymbolTable] = None, hoi
                         break
                     nested.remove(max(nested, key=lambda t: lv[id(t)]))
                 col_terms += nested
+        split_min = int(os.environ.get("MQ_SPLIT_AND_LOOKUPS", SPLIT_AND_LOOKUPS))
+        if split_min > 0:
+            col_terms += split_lookup_conjunctions(col_terms + kcols, split_min)
         n_shared = len(col_terms)
         col_terms += [t for t in kcols if id(t) not in {id(x) for x in col_terms}]
         # predicates over keccak columns, evaluated by the keccak column kernel (interpreted keccak)
@@ -697,10 +742,21 @@ def lower_batch(roots: Sequence[S.Term], syms: Optional[SymbolTable] = None, hoi
                     have.add(id(t))
                     col_terms.append(t)
                     program[id(t)] = c
-        # the Not of another column is one NOT in its readers (G fuses it into the packed-Bool
-        # push), not a column of its own a level deeper (C4: a whole launch of NOT columns)
+        # deepest levels holding only Nots of other columns (C4: a whole launch of them) are
+        # folded into their readers — one NOT per reader instead of a launch, a row store and a
+        # row read per model; elsewhere such a column stays (C3: inlining them cost 2 %)
         ids = {id(t) for t in col_terms}
-        drop = {k for k, t in enumerate(col_terms[:n_shared]) if t.kind == S.NOT and id(t.args[0]) in ids}
+        lv = _column_levels([t for t in col_terms if id(t) not in program])   # predicates: inlined
+        by_level: Dict[int, List[int]] = {}
+        for k, t in enumerate(col_terms):
+            if id(t) not in program:   # (keccak predicates run in their keccak column's launch)
+                by_level.setdefault(lv[id(t)], []).append(k)
+        drop = set()
+        for level_ks in (by_level[x] for x in sorted(by_level, reverse=True)):
+            if not all(k < n_shared and col_terms[k].kind == S.NOT and id(col_terms[k].args[0]) in ids
+                       for k in level_ks):
+                break
+            drop.update(level_ks)
         if drop:
             col_terms = [t for k, t in enumerate(col_terms) if k not in drop]
             n_shared -= len(drop)
