@@ -53,8 +53,9 @@ def _generated_current() -> bool:
     """qsa_gen.inc / qsa_table.h (generated, not tracked) carry the sha256 of gen_qsa.py."""
     import hashlib
     with open(os.path.join(CSRC, "gen_qsa.py"), "rb") as f:
-        # (the diagnostic profile build, QSA_PROF=1, stamps differently: switching regenerates)
-        stamp = hashlib.sha256(f.read() + (b"PROF" if os.environ.get("QSA_PROF") == "1" else b"")).hexdigest()[:16]
+        # (the diagnostic profile build, QSA_PROF=1, and QSA_PROG_LDS=1 stamp differently: switching regenerates)
+        stamp = hashlib.sha256(f.read() + (b"PROF" if os.environ.get("QSA_PROF") == "1" else b"")
+                               + (b"LDS" if os.environ.get("QSA_PROG_LDS") == "1" else b"")).hexdigest()[:16]
     for name in ("qsa_gen.inc", "qsa_table.h"):
         path = os.path.join(CSRC, name)
         if not os.path.exists(path):

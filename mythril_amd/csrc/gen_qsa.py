@@ -206,32 +206,34 @@ def load_window(first, pfx=None):
     k = _WIN_LABELS[0]
     _WIN_LABELS[0] += 1
     glob, dec = f"{pfx}_wg{k}", f"{pfx}_wd{k}"
-    out = ["v_mbcnt_lo_u32_b32 v5, -1, 0", "v_mbcnt_hi_u32_b32 v5, -1, v5", "v_lshlrev_b32 v5, 2, v5",
-           "s_bitcmp1_b32 s57, 0",
-           f"s_cbranch_scc0 {glob}"]
-    if first:
-        out += ["s_sub_u32 s34, s80, s56", "s_lshl_b32 s34, s34, 2", "s_add_u32 s14, s57, s34",
-                "s_sub_u32 s14, s14, 1"] + (["s_mov_b32 s39, 1"] if PROF else [])
-    else:
-        out += ["s_add_u32 s14, s14, 256"]
-    out += ["v_add_u32 v5, s14, v5",
-            f"ds_read_b32 {WIN}, v5",
-            "s_waitcnt lgkmcnt(0)",
-            f"s_branch {dec}",
-            f"{glob}:"]
+    lane4 = LANE4 or "v5"
+    out = [] if LANE4 else ["v_mbcnt_lo_u32_b32 v5, -1, 0", "v_mbcnt_hi_u32_b32 v5, -1, v5", "v_lshlrev_b32 v5, 2, v5"]
+    if PROG_LDS:
+        out += ["s_bitcmp1_b32 s57, 0",
+                f"s_cbranch_scc0 {glob}"]
+        if first:
+            out += ["s_sub_u32 s34, s80, s56", "s_lshl_b32 s34, s34, 2", "s_add_u32 s14, s57, s34",
+                    "s_sub_u32 s14, s14, 1"] + (["s_mov_b32 s39, 1"] if PROF else [])
+        else:
+            out += ["s_add_u32 s14, s14, 256"]
+        out += [f"v_add_u32 v5, s14, {lane4}",
+                f"ds_read_b32 {WIN}, v5",
+                "s_waitcnt lgkmcnt(0)",
+                f"s_branch {dec}",
+                f"{glob}:"]
     if first:
         out += ["s_add_u32 s34, s14, 256", "s_addc_u32 s35, s15, 0",
                 "s_cmp_eq_u64 s[34:35], s[36:37]",
                 "s_mov_b64 s[14:15], s[36:37]"] + (["s_cselect_b32 s39, 1, 0"] if PROF else []) + [
                 "s_waitcnt vmcnt(0)",
                 f"s_cbranch_scc1 {pfx}_win_pref",
-                f"global_load_dword {NWIN}, v5, s[14:15]",
+                f"global_load_dword {NWIN}, {lane4}, s[14:15]",
                 "s_waitcnt vmcnt(0)",
                 f"{pfx}_win_pref:"]
     else:
         out += ["s_add_u32 s14, s14, 256", "s_addc_u32 s15, s15, 0", "s_waitcnt vmcnt(0)"]
     out += [f"v_mov_b32 {WIN}, {NWIN}",
-            f"global_load_dword {NWIN}, v5, s[14:15] offset:256",
+            f"global_load_dword {NWIN}, {lane4}, s[14:15] offset:256",
             f"{dec}:",
             "s_mov_b32 s16, 0",
             f"v_and_b32 v5, 0xffff, {WIN}",
@@ -1368,7 +1370,7 @@ def store_column(pfx):
     QArgs.bool_rows asks for it (a HIP C++ kernel of the launch reads rows).  A column is not a
     (tape, model) pair: the pair count the tape end added is taken back."""
     out = [f"{pfx}_store_column:",
-           "s_sub_u32 s40, s40, s38", "s_subb_u32 s41, s41, 0",
+           "s_sub_u32 s40, s40, 1",
            VMWAIT,
            "s_mul_i32 s38, s82, s29", "s_mul_hi_u32 s39, s82, s29", "s_lshl_b64 s[38:39], s[38:39], 2",
            "s_add_u32 s38, s38, s90", "s_addc_u32 s39, s39, s91",
@@ -1432,13 +1434,21 @@ def stage_rows(pfx):
     out += [f"ds_write_b32 v5, {T(j)} offset:{256 * j}" for j in range(8)]
     out += ["s_add_u32 s61, s61, 32", f"s_branch {pfx}_stage_loop",
             f"{pfx}_stage_done:"]
-    out += stage_programs(pfx)
+    if PROG_LDS:
+        out += stage_programs(pfx)
     out += ["s_waitcnt lgkmcnt(0)",
             "s_barrier"]
     return out
 
 
 DESC_LDS = 2048   # G: LDS bytes of the workgroup's descriptors (<= 64 of 32 B), just below its programs
+# G programs and descriptors staged in LDS per workgroup (QArgs.prog_lds; QSA_PROG_LDS=1 at
+# generation).  Off by default: it removes the tape start's memory waits (FRAME 5 200 -> 430,
+# F_HDR 1 200 -> 510 cycles per dispatch on C4, profiles/r04z3) but G is issue-bound there, and
+# the extra VALU of the LDS header read made C4 3.43 -> 3.53 ms (profiles/r04z6)
+PROG_LDS = os.environ.get("QSA_PROG_LDS") == "1"
+# G (product build): 4 * lane, kept in v39 (the profile build's table register)
+LANE4 = None
 
 
 def stage_descs(pfx):
@@ -1564,6 +1574,9 @@ def frame(variant, pfx, handlers, subs):
         "s_mov_b32 s30, s84",
         "s_mov_b32 s31, s85",
         "s_mov_b32 s99, s86",
+        # s30 = early exit on AND first-hit mode: the tape loop's one test
+        "s_cmp_lg_u32 s31, 0",
+        "s_cselect_b32 s30, 0, s30",
         # handler base
         "s_getpc_b64 s[12:13]",
         f"{pfx}_pc:",
@@ -1595,6 +1608,9 @@ def frame(variant, pfx, handlers, subs):
         "s_mov_b64 exec, s[36:37]",
         f"s_branch {pfx}_exit",
         f"{pfx}_main:",
+    ] + ([
+        "v_mbcnt_lo_u32_b32 v39, -1, 0", "v_mbcnt_hi_u32_b32 v39, -1, v39", "v_lshlrev_b32 v39, 2, v39",
+    ] if G and LANE4 else []) + [
         # wave / lane / model index
         "v_and_b32 v4, 63, v3",
         "v_lshrrev_b32 v5, 6, v3",
@@ -1690,9 +1706,7 @@ def frame(variant, pfx, handlers, subs):
         P += ["s_mov_b64 s[14:15], 0"]   # no window yet (load_window's successor test fails)
     ee = G and EEV is not None
     if ee:
-        P += ["s_cmp_lg_u32 s31, 0",
-              f"s_cbranch_scc1 {pfx}_ee_init_done",
-              "s_cmp_eq_u32 s30, 0",
+        P += ["s_cmp_eq_u32 s30, 0",
               f"s_cbranch_scc1 {pfx}_ee_init_done",
               "s_cmp_ge_u32 s24, s25",
               f"s_cbranch_scc1 {pfx}_ee_init_done",
@@ -1719,17 +1733,17 @@ def frame(variant, pfx, handlers, subs):
         "s_nop 3",                          # VALU SGPR write -> SALU read
         f"s_branch {pfx}_hdr_done",
         f"{pfx}_hdr_mem:",
-    ] if G else []) + [
+    ] if G and PROG_LDS else []) + [
         "s_lshl_b32 s34, s24, 5",
         "s_add_u32 s34, s22, s34",
         "s_addc_u32 s35, s23, 0",
         "s_load_dwordx8 s[80:87], s[34:35], 0x0",
         "s_waitcnt lgkmcnt(0)",
-    ] + ([f"{pfx}_hdr_done:"] if G else []) + (prof_point("F_HDR") if G else []) + [
+    ] + ([f"{pfx}_hdr_done:"] if G and PROG_LDS else []) + (prof_point("F_HDR") if G else []) + ([] if G else [
+        # P: &best[tape] (G computes it on a hit only; handlers never touch s72-s73, s80-s87)
         "s_lshl_b32 s34, s82, 2",
-        "s_add_u32 s72, s26, s34",           # s[72:73] = &best[tape] (handlers never touch s72-s73, s80-s87)
+        "s_add_u32 s72, s26, s34",
         "s_addc_u32 s73, s27, 0",
-    ] + ([] if G else [
         # P: the first program entry is requested together with best[tape] (one round trip for
         # both; a skipped tape wasted a scalar load)
         "s_lshl_b32 s34, s80, 2",
@@ -1737,8 +1751,7 @@ def frame(variant, pfx, handlers, subs):
         "s_addc_u32 s15, s47, 0",
         "s_load_dwordx4 s[96:99], s[14:15], 0x0",
     ]) + [
-        "s_cmp_eq_u32 s31, 1",
-        f"s_cbranch_scc1 {pfx}_run",
+        # s30: early exit on and the mode first-hit (set at the prologue)
         "s_cmp_eq_u32 s30, 0",
         f"s_cbranch_scc1 {pfx}_run",
     ] + ([
@@ -1785,17 +1798,13 @@ def frame(variant, pfx, handlers, subs):
         f"{pfx}_tape_end:",
         "s_waitcnt lgkmcnt(0)",
         "s_and_b64 s[34:35], s[48:49], s[62:63]",
-        "s_bcnt1_i32_b64 s38, s[62:63]",
-        "s_add_u32 s40, s40, s38",
-        "s_addc_u32 s41, s41, 0",
-        f"s_mul_i32 s60, s38, {DN}",
-        f"s_mul_hi_u32 s61, s38, {DN}",
-        "s_add_u32 s42, s42, s60",
-        "s_addc_u32 s43, s43, s61",
-        f"s_mul_i32 s60, s38, {DA}",
-        f"s_mul_hi_u32 s61, s38, {DA}",
-        "s_add_u32 s44, s44, s60",
-        "s_addc_u32 s45, s45, s61",
+        # counters per wave: tapes run, their node counts and algorithmic ops; multiplied by the
+        # tile's valid lanes once, when the wave's tapes are done
+        "s_add_u32 s40, s40, 1",
+        f"s_add_u32 s42, s42, {DN}",
+        "s_addc_u32 s43, s43, 0",
+        f"s_add_u32 s44, s44, {DA}",
+        "s_addc_u32 s45, s45, 0",
     ] + ([
         "s_cmp_eq_u32 s31, 3",
         f"s_cbranch_scc1 {pfx}_store_column",
@@ -1806,6 +1815,11 @@ def frame(variant, pfx, handlers, subs):
         f"s_cbranch_scc1 {pfx}_next_tape",
         "s_ff1_i32_b64 s38, s[34:35]",
         "s_add_u32 s38, s38, s28",
+    ] + ([
+        "s_lshl_b32 s39, s82, 2",            # G: &best[tape]
+        "s_add_u32 s72, s26, s39",
+        "s_addc_u32 s73, s27, 0",
+    ] if G else []) + [
         "s_mov_b64 s[60:61], exec",
         "s_mov_b64 exec, 1",
         "v_mov_b32 v5, s38",
@@ -1838,6 +1852,18 @@ def frame(variant, pfx, handlers, subs):
         "@PROFFLUSH@",
         "s_waitcnt vmcnt(0)",
     ] if (G and PROF) else []) + [
+        # counters x the tile's valid lanes: pairs = tapes run x valid, nodes and ops likewise
+        "s_bcnt1_i32_b64 s38, s[62:63]",
+        "s_mul_hi_u32 s41, s40, s38",
+        "s_mul_i32 s40, s40, s38",
+        "s_mul_i32 s43, s43, s38",
+        "s_mul_hi_u32 s34, s42, s38",
+        "s_add_u32 s43, s43, s34",
+        "s_mul_i32 s42, s42, s38",
+        "s_mul_i32 s45, s45, s38",
+        "s_mul_hi_u32 s34, s44, s38",
+        "s_add_u32 s45, s45, s34",
+        "s_mul_i32 s44, s44, s38",
         # the wave's counters go to slot (tile ^ last tape) mod 256 of the slotted counter array
         # (qs_launch.h kCounterSlots): 10^6 waves adding into one cache line serialise in L2
         "s_lshr_b32 s34, s28, 6",
@@ -1886,8 +1912,9 @@ def set_layout(variant):
     window v[32:34], staging address v35, next window v36, early-exit window v37/v38 (profile
     table v39), stack v[40:40+8*DG), T/W after it -> 8 * DG + 48 VGPRs (DG = 4: 80, 6 waves
     per SIMD)."""
-    global SBASE, TBASE, UBASE, WIN, WINA, WINI, NWIN, STG, NEXT_G, EEA, EEV, PROF_VGPR, D
+    global SBASE, TBASE, UBASE, WIN, WINA, WINI, NWIN, STG, NEXT_G, EEA, EEV, PROF_VGPR, D, LANE4
     D = DG if variant == "g" else DP
+    LANE4 = "v39" if (variant == "g" and NVG == 0 and not PROF) else None
     if variant == "g" and NVG == 0:
         SBASE, TBASE, UBASE = 40, 40 + 8 * DG, 8
         WIN, WINA, WINI, STG, NWIN = "v32", "v33", "v34", "v35", "v36"
@@ -1908,7 +1935,7 @@ def source_stamp() -> str:
     any change of the generator, independent of file times)."""
     import hashlib
     with open(os.path.abspath(__file__), "rb") as f:
-        return hashlib.sha256(f.read() + (b"PROF" if PROF else b"")).hexdigest()[:16]
+        return hashlib.sha256(f.read() + (b"PROF" if PROF else b"") + (b"LDS" if PROG_LDS else b"")).hexdigest()[:16]
 
 
 def main():
@@ -1980,6 +2007,7 @@ def main():
         # diagnostic profile build (QSA_PROF=1): per-wave LDS table bytes; entry i = (cycles,
         # count) of kind i, entry QK_COUNT = the tape frame
         f.write(f"constexpr int kQsaProfBytes = {prof_bytes};\n")
+        f.write(f"constexpr int kQsaProgLds = {1 if PROG_LDS else 0};   // G stages programs in LDS (QSA_PROG_LDS=1)\n")
         f.write(f"constexpr int kQsaProfExtra = {len(PROF_EXTRA)};\n")
         f.write("static const char* const kQsaProfExtraNames[] = {" + ", ".join(f'"{n}"' for n in PROF_EXTRA) + "};\n")
         f.write(f"constexpr int kQsaHandlerShiftG = {3 if PROF else 2};\n")

@@ -2294,7 +2294,7 @@ static size_t plan_prog_lds(QArgs& q, const GDesc* d, int64_t n, int64_t tpg, si
   q.prog_lds = 0;
   // (the workgroup's descriptors go to LDS too: kDescLds bytes, at most 64 of them)
   constexpr size_t kDescLds = 2048;
-  if (off || n <= 0 || 4 * tpg * (int64_t)sizeof(GDesc) > (int64_t)kDescLds) return 0;
+  if (!kQsaProgLds || off || n <= 0 || 4 * tpg * (int64_t)sizeof(GDesc) > (int64_t)kDescLds) return 0;
   int64_t kb = 26;
   if (const char* e = std::getenv("MQ_G_STAGE_KB")) kb = std::atol(e);
   uint64_t run = 0;
