@@ -891,61 +891,85 @@ def sub_uf1(pfx):
             "s_add_u32 s68, s68, s64",
             "s_addc_u32 s69, s69, s65",                       # entry 0 of the function
             "s_lshl_b32 s39, s38, 2",                         # stride bytes
-            "s_lshl_b32 s98, s36, 2",                        # value offset in an entry
-            # else value: nl_res SoA rows
+            "s_lshl_b32 s98, s36, 2"]                        # value offset in an entry
+    # The scan: eight entries per memory round trip by their first key limb (keys are hashes or
+    # small integers: a limb-0 match is nearly always the entry), a full key compare for the
+    # candidates only; then one round trip for the value (matched lanes) or the else value.
+    # Entry offsets are 32-bit, relative to the function's entry 0 (mq_api.cpp keeps
+    # entry_words under 4 GB for G and pads it: limb-0 reads run up to 7 entries past a lane's
+    # last one).  U[0:8] hold the eight limb-0 words during the scan, the result after it.
+    # SGPRs: s36 nl_a0, s37 nl_res, s39 stride bytes, s98 value offset, s[68:69] entry 0,
+    # s[70:71] else rows, s[60:61] exec at entry, s[64:65] matched lanes, s[66:67] lanes still
+    # scanning, s[34:35] / s[78:79] / s99 scratch.
+    out += ["v_lshlrev_b32 v4, 1, v2",                        # m*8
+            "global_load_dword v5, v4, s[66:67]",             # first entry of (f, m)
+            "global_load_dword v6, v4, s[66:67] offset:8",    # end
+            "s_waitcnt vmcnt(0)",
+            "v_mul_lo_u32 v136, v5, s39",                      # byte offset of entry lo
+            "s_mov_b64 s[60:61], exec",
+            "s_mov_b64 s[64:65], 0",
+            f"{P}_uf_loop:",
+            "v_cmp_lt_u32_e64 s[66:67], v5, v6",
+            "s_nop 3",
+            "s_and_b64 exec, exec, s[66:67]",
+            f"s_cbranch_execz {P}_uf_done"]
+    for j in range(8):
+        out += [f"s_mul_i32 s99, s39, {j}", "v_add_u32 v137, s99, v136",
+                f"global_load_dword v{UBASE + j}, v137, s[68:69]"]
+    out += ["s_mov_b64 s[66:67], exec", "s_waitcnt vmcnt(0)"]
+    for j in range(8):
+        nj = f"{P}_uf_nj{j}"
+        out += [f"v_cmp_eq_u32_e64 s[34:35], v{UBASE + j}, {W(0)}",
+                f"v_add_u32 v139, {j}, v5",
+                "v_cmp_lt_u32_e64 s[78:79], v139, v6",
+                "s_nop 3",
+                "s_and_b64 s[34:35], s[34:35], s[78:79]",
+                "s_and_b64 s[34:35], s[34:35], s[66:67]",      # (scc: any candidate)
+                f"s_cbranch_scc0 {nj}",
+                "s_mov_b64 exec, s[34:35]",
+                f"s_mul_i32 s99, s39, {j}", "v_add_u32 v137, s99, v136"]
+        for l in range(1, L):
+            out += [f"s_cmp_le_u32 s36, {l}", f"s_cbranch_scc1 {P}_uf_kl{j}",
+                    f"global_load_dword v{UBASE + 12 + l}, v137, s[68:69] offset:{4 * l}"]
+        out += [f"{P}_uf_kl{j}:", "s_waitcnt vmcnt(0)", "v_mov_b32 v148, 0"]
+        for l in range(1, L):
+            out += [f"s_cmp_le_u32 s36, {l}", f"s_cbranch_scc1 {P}_uf_kc{j}",
+                    f"v_xor_b32 v149, v{UBASE + 12 + l}, {W(l)}", "v_or_b32 v148, v148, v149"]
+        out += [f"{P}_uf_kc{j}:",
+                "v_cmp_eq_u32_e64 s[34:35], 0, v148",
+                "s_nop 3",
+                "s_and_b64 s[34:35], s[34:35], exec",
+                "s_or_b64 s[64:65], s[64:65], s[34:35]",
+                "s_mov_b64 exec, s[34:35]",
+                "v_mov_b32 v138, v137",                          # matched entry's offset
+                "s_andn2_b64 s[66:67], s[66:67], s[34:35]",     # matched lanes are done
+                "s_mov_b64 exec, s[66:67]",
+                f"{nj}:"]
+    out += ["s_mov_b64 exec, s[66:67]",
+            "v_add_u32 v5, 8, v5",
+            "s_lshl_b32 s99, s39, 3",
+            "v_add_u32 v136, s99, v136",
+            f"s_branch {P}_uf_loop",
+            f"{P}_uf_done:",
+            "s_mov_b64 exec, s[60:61]"]
+    out += [f"v_mov_b64 v[{UBASE + l}:{UBASE + 1 + l}], 0" for l in range(0, 8, 2)]
+    # matched lanes: the value after the key; the others: the else value (SoA rows)
+    out += ["s_and_b64 exec, s[60:61], s[64:65]",
+            f"s_cbranch_execz {P}_uf_vl_issued",
+            "v_add_u32 v150, s98, v138"]
+    for l in range(L):
+        out += [f"s_cmp_le_u32 s37, {l}", f"s_cbranch_scc1 {P}_uf_vl_issued",
+                f"global_load_dword v{UBASE + l}, v150, s[68:69] offset:{4 * l}"]
+    out += [f"{P}_uf_vl_issued:",
+            "s_andn2_b64 exec, s[60:61], s[64:65]",
+            f"s_cbranch_execz {P}_uf_else_done",
             "s_mov_b64 s[34:35], s[70:71]"]
     for l in range(L):
         out += [f"s_cmp_le_u32 s37, {l}", f"s_cbranch_scc1 {P}_uf_else_done",
                 f"global_load_dword v{UBASE + l}, v2, s[34:35]",
                 "s_add_u32 s34, s34, s74", "s_addc_u32 s35, s35, s75"]
     out += [f"{P}_uf_else_done:",
-            "v_lshlrev_b32 v4, 1, v2",                        # m*8
-            "global_load_dword v5, v4, s[66:67]",             # first entry of (f, m)
-            "global_load_dword v6, v4, s[66:67] offset:8",    # end
-            "v_mov_b32 v7, s39",
             "s_waitcnt vmcnt(0)",
-            "v_mad_u64_u32 v[136:137], s[34:35], v5, v7, s[68:69]",   # &entry[lo]
-            "s_mov_b64 s[60:61], exec",
-            "s_mov_b64 s[64:65], 0",                          # lanes that matched
-            f"{P}_uf_loop:",
-            "v_cmp_lt_u32_e64 s[34:35], v5, v6",
-            "s_nop 3",
-            "s_and_b64 exec, exec, s[34:35]",
-            f"s_cbranch_execz {P}_uf_done"]
-    # one memory round trip per entry (its key); the value of the first matching entry is read
-    # once after the scan from the remembered entry pointer v[138:139]
-    for l in range(L):
-        out += [f"s_cmp_le_u32 s36, {l}", f"s_cbranch_scc1 {P}_uf_kl_done",
-                f"global_load_dword v{UBASE + 12 + l}, v[136:137], off offset:{4 * l}"]
-    out += [f"{P}_uf_kl_done:", "s_waitcnt vmcnt(0)", "v_mov_b32 v148, 0"]
-    for l in range(L):
-        out += [f"s_cmp_le_u32 s36, {l}", f"s_cbranch_scc1 {P}_uf_kc_done",
-                f"v_xor_b32 v149, v{UBASE + 12 + l}, {W(l)}", "v_or_b32 v148, v148, v149"]
-    out += [f"{P}_uf_kc_done:",
-            "v_cmp_eq_u32_e64 s[34:35], 0, v148",
-            "s_nop 3",
-            "s_and_b64 s[34:35], s[34:35], exec",
-            "s_or_b64 s[64:65], s[64:65], s[34:35]",
-            "s_nop 1",
-            "v_cndmask_b32_e64 v138, v138, v136, s[34:35]",
-            "v_cndmask_b32_e64 v139, v139, v137, s[34:35]",
-            "s_andn2_b64 exec, exec, s[34:35]",               # matched lanes are done
-            "v_add_u32 v5, 1, v5",
-            "v_add_co_u32 v136, vcc, v136, v7",
-            "s_nop 1",
-            "v_addc_co_u32 v137, vcc, 0, v137, vcc",
-            f"s_branch {P}_uf_loop",
-            f"{P}_uf_done:",
-            "s_mov_b64 exec, s[64:65]",
-            f"s_cbranch_execz {P}_uf_vl_done",
-            "v_add_co_u32 v150, vcc, s98, v138",
-            "s_nop 1",
-            "v_addc_co_u32 v151, vcc, 0, v139, vcc"]
-    for l in range(L):
-        out += [f"s_cmp_le_u32 s37, {l}", f"s_cbranch_scc1 {P}_uf_vl_issued",
-                f"global_load_dword v{UBASE + l}, v[150:151], off offset:{4 * l}"]
-    out += [f"{P}_uf_vl_issued:", "s_waitcnt vmcnt(0)",
-            f"{P}_uf_vl_done:",
             "s_mov_b64 exec, s[60:61]",
             f"{P}_uf_ret:",
             "s_setpc_b64 s[76:77]"]
@@ -1251,6 +1275,20 @@ def make_handlers(variant, pfx):
                     for nw in (2, 8):
                         H((f"{src}EQK{nw}_A", x, n - 1),
                           load + zero + const_words(nw) + [wait] + eq_const_body(tl, nw, B(x))
+                          + [f"s_and_b64 {B(x - 1)}, {B(x - 1)}, {B(x)}"], reads_stack=False)
+        # "push staged variable row imm (n limbs) at x; unsigned-compare it with an inline
+        # constant; AND into B(x - 1)" (PUSH_MEMS + ULTK_A / UGTK_A: C4's balance checks): the
+        # value goes to the free slot x, the constant to T (a borrow chain reads one SGPR only)
+        for x in range(1, D):
+            for n in (1, 2, 8):
+                lds = ["s_lshl_b32 s34, s17, 8", f"v_add_u32 v5, s34, {STG}"] + \
+                      [f"ds_read_b32 {S(x, l)}, v5 offset:{256 * l}" for l in range(n)]
+                for nw in (2, 8):
+                    pre = lds + zero_limbs(x, n) + const_words(nw) + \
+                        [f"v_mov_b32 {T(l)}, {kconst(l, nw)}" for l in range(L)] + ["s_waitcnt lgkmcnt(0)"]
+                    xs = (lambda l, _x=x: S(_x, l))
+                    for nm, a_, b_ in (("ULTK", xs, T), ("UGTK", T, xs)):
+                        H((f"S{nm}{nw}_A", x, n - 1), pre + lt_chain(a_, b_, B(x))
                           + [f"s_and_b64 {B(x - 1)}, {B(x - 1)}, {B(x)}"], reads_stack=False)
     # ---- (last: these handlers never branch, so the subroutine calls above stay in s_call range)
     # ---- binary ops whose right operand is a preloaded variable (the translator fuses

@@ -175,6 +175,9 @@ struct DevBuf {
 
 }  // namespace
 
+// words past the function entries that reads may touch (8 entries of the widest G table)
+static constexpr size_t kEntryPadWords = 512;
+
 // the assembly interpreter keeps temps in LDS (2 KB per temp per wave, 4 waves per workgroup)
 static constexpr int kQsaMaxTemps = 16;
 
@@ -211,6 +214,7 @@ struct mq_ctx {
   int n_vars = 0, n_funcs = 0;
   std::vector<uint16_t> var_width;
   DevBuf vars, var_off, var_nl, funcs, entry_ptr, entry_words, else_words;
+  int64_t entry_words_n = 0;   // words of function entries (G scans them with 32-bit offsets)
   DevBuf counters;
   DevBuf best_tmp;  // scratch first-hit buffer for the synchronous API
   DevBuf scratch;   // per-wave temp slots of the HIP C++ interpreter (persistent grid)
@@ -821,17 +825,22 @@ static int upload_one(mq_ctx* c, const mq_model_batch* mb) {
   c->var_off_h.assign(voff.begin(), voff.begin() + mb->n_vars);
   c->var_nl_h.assign(vnl.begin(), vnl.begin() + mb->n_vars);
   c->funcs_h.assign(mb->funcs, mb->funcs + F);
+  c->entry_words_n = F > 0 ? ew_total : 0;
   c->models_gen++;
   HIPCHK(c->var_off.upload(voff.data(), voff.size(), c->stream));
   HIPCHK(c->var_nl.upload(vnl.data(), vnl.size(), c->stream));
   HIPCHK(c->funcs.upload(fd.data(), fd.size(), c->stream));
   if (F > 0) {
     HIPCHK(c->entry_ptr.upload(mb->entry_ptr, (size_t)F * (M + 1), c->stream));
+    // (padded: G's table scan reads the first word of up to 7 entries past a model's last one,
+    // gen_qsa.py sub_uf1)
+    HIPCHK(c->entry_words.ensure(sizeof(uint32_t) * ((size_t)std::max<int64_t>(ew_total, 1) + kEntryPadWords)));
     HIPCHK(c->entry_words.upload(mb->entry_words, (size_t)std::max<int64_t>(ew_total, 1), c->stream));
   } else {
     int64_t z = 0;
     uint32_t zw = 0;
     HIPCHK(c->entry_ptr.upload(&z, 1, c->stream));
+    HIPCHK(c->entry_words.ensure(sizeof(uint32_t) * (1 + kEntryPadWords)));
     HIPCHK(c->entry_words.upload(&zw, 1, c->stream));
   }
   HIPCHK(c->else_words.upload(else_soa.data(), else_soa.size(), c->stream));
@@ -1153,15 +1162,22 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
   // constant, AND-ed into the conjunction) as one M/SEQK{2,8}_A word: row / slot in the
   // immediate, the constant in 2 or 8 inline data words (a 16-bit immediate constant travels
   // as two)
+  // (and "PUSH_MEMS x; ULTK_A / UGTK_A x" as one S{ULT,UGT}K{2,8}_A word, same layout)
   auto merge_memk = [&]() {
     if (log.size() < 2) return;
     const Emit e1 = log.back();
-    if (e1.kind != QK_EQK_A || out.size() != ends_at(e1)) return;
+    if ((e1.kind != QK_EQK_A && e1.kind != QK_ULTK_A && e1.kind != QK_UGTK_A) || out.size() != ends_at(e1)) return;
     const Emit e0 = log[log.size() - 2];
     if (ends_at(e0) != e1.pos || e0.d != e1.d || e0.nd != 0 || e0.v < 0) return;
     const bool wide = e1.v == 2;
     int fk;
-    if (e0.kind == QK_PUSH_MEM) fk = wide ? QK_MEQK8_A : QK_MEQK2_A;
+    if (e1.kind == QK_ULTK_A) {
+      if (e0.kind != QK_PUSH_MEMS) return;
+      fk = wide ? QK_SULTK8_A : QK_SULTK2_A;
+    } else if (e1.kind == QK_UGTK_A) {
+      if (e0.kind != QK_PUSH_MEMS) return;
+      fk = wide ? QK_SUGTK8_A : QK_SUGTK2_A;
+    } else if (e0.kind == QK_PUSH_MEM) fk = wide ? QK_MEQK8_A : QK_MEQK2_A;
     else if (e0.kind == QK_PUSH_MEMS) fk = wide ? QK_SEQK8_A : QK_SEQK2_A;
     else return;
     if (c->qsa_index[k][fk][e1.d][e0.v + 1] < 0) return;
@@ -1468,7 +1484,8 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
         break;
       }
       case G_UF1: {  // imm = function id, imm2 = result width (0 = Bool)
-        ok = !P && imm2 <= 256;
+        // (G scans the entries with 32-bit byte offsets)
+        ok = !P && imm2 <= 256 && (uint64_t)(c->entry_words_n + (int64_t)kEntryPadWords) * 4 < (1ull << 32);
         if (ok && models) {
           // a function absent from the model batch evaluates to 0 (as in the C++ kernel)
           ok = imm >= c->funcs_h.size() || (c->funcs_h[imm].arity == 1 && c->funcs_h[imm].arg_width[0] <= 256 &&

@@ -72,9 +72,9 @@ def test_g_handler_data_words_match_their_kinds():
             want = v
         elif kind.startswith("PUSH_CONSTW"):
             want = v + 1
-        elif base in ("MEQK2", "SEQK2"):
+        elif base in ("MEQK2", "SEQK2", "SULTK2", "SUGTK2"):
             want = 2
-        elif base in ("MEQK8", "SEQK8"):
+        elif base in ("MEQK8", "SEQK8", "SULTK8", "SUGTK8"):
             want = 8
         elif base in ("EQK", "ULTK", "UGTK", "ULEK", "UGEK"):
             want = kcls[v]
