@@ -1021,13 +1021,16 @@ class IncrementalLowering:
             self._names_n = nv
         return nv
 
-    def slots(self, models: Sequence) -> List[int]:
+    def slots(self, models: Sequence, live: int = 0) -> List[int]:
         """Slot of each model (new models get one, with the rows of every serialized variable);
-        then the rows of variables the symbol table gained since the last call, for every slot."""
+        then the rows of variables the symbol table gained since the last call, for every slot.
+        ``live``: how many models can still be candidates (the caller's LRU capacity; a batch
+        often names only the one model not yet evaluated) — the slots start over only when far
+        more models than that piled up (every reset drops the cached conjunct verdicts)."""
         if not hasattr(self, "_slot"):
             self._reset_models()
         nv = self._sync_names()
-        if len(self._slot_model) > 4 * len(models) + 256:
+        if len(self._slot_model) > 4 * max(len(models), live) + 256:
             self._reset_models()   # models that left the candidate set piled up: start over
         out, new = [], []
         for mod in models:

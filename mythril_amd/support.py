@@ -405,7 +405,7 @@ class VerdictEngine:
         t0 = clock()
         db, ok = inc.lower(exprs)
         t1 = clock()
-        slots = np.asarray(inc.slots(models), np.int64)
+        slots = np.asarray(inc.slots(models, live=getattr(self, "live_models", 0)), np.int64)
         dev_slots = sorted(set(slots.tolist()))
         self.timing["lower"] += t1 - t0
         self.timing["serialize"] += clock() - t1
@@ -648,6 +648,9 @@ class ModelCache:
         return np.full(max(len(self._slot_model), 16), -1, np.int8)
 
     def _fill(self, exprs: List, models: List, slots: np.ndarray) -> None:
+        # the engine's model slots outlive a batch: tell it how many models stay candidates (the
+        # LRU's capacity), so it does not start its slots over every few hundred solver models
+        self.engine.live_models = max(getattr(self.engine, "live_models", 0), self.model_cache.size)
         rows = self.engine.rows(exprs, models)
         n = len(self._slot_model)
         for e, r in zip(exprs, rows):

@@ -502,3 +502,24 @@ def test_fork_stream_witnesses_and_both_candidate_arms(fresh):
         res[cand] = dict(sp.counters)
     assert res[True]["solver_calls"] < res[False]["solver_calls"]
     assert res[True]["get_model_calls"] == res[False]["get_model_calls"] == len(states)
+
+
+def test_model_slots_survive_solver_model_churn():
+    """A long run's solver answers churn through the 100-entry LRU; batches then name only the
+    few models not evaluated yet.  The engine's model slots (and with them the cached conjunct
+    verdicts) start over only past ~4x the LRU's capacity, not every ~260 models."""
+    eng = OracleEngine()
+    cache = sp.ModelCache(eng)
+    for i in range(100):
+        cache.put(Model({"x": i}), 1)
+    cache.check_quick_sat(x == 5)
+    epoch = eng.incremental.slot_epoch
+    n = 100
+    for b in range(6):                  # prefetched batches; a solver model arrives before each
+        exprs = [x == 10_000 + 50 * b + k for k in range(50)]
+        cache.prefetch(exprs)
+        for e in exprs:
+            cache.put(Model({"x": n}), 1)   # (the pending rows need this one model only)
+            n += 1
+            assert cache.check_quick_sat(e) is False
+    assert n == 400 and eng.incremental.slot_epoch == epoch
