@@ -20,12 +20,28 @@ __constant__ uint64_t kRC[24] = {
 
 __device__ __forceinline__ uint64_t rol(uint64_t v, int n) { return n ? (v << n) | (v >> (64 - n)) : v; }
 
+// gfx950 v_bitop3_b32: any function of three 32-bit operands, the truth table as an 8-bit
+// immediate indexed by (a << 2) | (b << 1) | c.  A three-way XOR (0x96) halves theta's column
+// parities, and chi's a ^ (~b & c) (0xD2) is one instruction instead of two.
+template <int LUT>
+__device__ __forceinline__ uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(r) : "v"(a), "v"(b), "v"(c), "i"(LUT));
+  return r;
+}
+template <int LUT>
+__device__ __forceinline__ uint64_t bitop3_64(uint64_t a, uint64_t b, uint64_t c) {
+  return (uint64_t)bitop3<LUT>((uint32_t)a, (uint32_t)b, (uint32_t)c) |
+         ((uint64_t)bitop3<LUT>((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)) << 32);
+}
+
 __device__ __forceinline__ void keccak_f(uint64_t (&A)[25]) {
   constexpr int R[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
   for (int r = 0; r < 24; r++) {
     uint64_t C[5], Dd[5], B[25];
 #pragma unroll
-    for (int x = 0; x < 5; x++) C[x] = A[x] ^ A[x + 5] ^ A[x + 10] ^ A[x + 15] ^ A[x + 20];
+    for (int x = 0; x < 5; x++)
+      C[x] = bitop3_64<0x96>(bitop3_64<0x96>(A[x], A[x + 5], A[x + 10]), A[x + 15], A[x + 20]);
 #pragma unroll
     for (int x = 0; x < 5; x++) Dd[x] = C[(x + 4) % 5] ^ rol(C[(x + 1) % 5], 1);
 #pragma unroll
@@ -37,7 +53,8 @@ __device__ __forceinline__ void keccak_f(uint64_t (&A)[25]) {
 #pragma unroll
     for (int y = 0; y < 5; y++)
 #pragma unroll
-      for (int x = 0; x < 5; x++) A[x + 5 * y] = B[x + 5 * y] ^ ((~B[(x + 1) % 5 + 5 * y]) & B[(x + 2) % 5 + 5 * y]);
+      for (int x = 0; x < 5; x++)
+        A[x + 5 * y] = bitop3_64<0xD2>(B[x + 5 * y], B[(x + 1) % 5 + 5 * y], B[(x + 2) % 5 + 5 * y]);
     A[0] ^= kRC[r];
   }
 }
