@@ -222,10 +222,23 @@ def load_window(first, pfx=None):
                 f"s_branch {dec}",
                 f"{glob}:"]
     if first:
+        # the prefetched window was issued before the previous tape's stores (s59 of them, column
+        # rows / a verdict byte / a hit's atomic): wait for it, not for them (vector memory
+        # operations complete in order)
+        w = f"{pfx}_ws{k}"
+        out += ["s_cmp_eq_u32 s59, 0", f"s_cbranch_scc1 {w}0",
+                "s_cmp_eq_u32 s59, 1", f"s_cbranch_scc1 {w}1",
+                "s_cmp_lt_u32 s59, 4", f"s_cbranch_scc1 {w}2",
+                "s_cmp_lt_u32 s59, 8", f"s_cbranch_scc1 {w}4",
+                "s_waitcnt vmcnt(8)", f"s_branch {w}d",
+                f"{w}4:", "s_waitcnt vmcnt(4)", f"s_branch {w}d",
+                f"{w}2:", "s_waitcnt vmcnt(2)", f"s_branch {w}d",
+                f"{w}1:", "s_waitcnt vmcnt(1)", f"s_branch {w}d",
+                f"{w}0:", "s_waitcnt vmcnt(0)",
+                f"{w}d:", "s_mov_b32 s59, 0"]
         out += ["s_add_u32 s34, s14, 256", "s_addc_u32 s35, s15, 0",
                 "s_cmp_eq_u64 s[34:35], s[36:37]",
                 "s_mov_b64 s[14:15], s[36:37]"] + (["s_cselect_b32 s39, 1, 0"] if PROF else []) + [
-                "s_waitcnt vmcnt(0)",
                 f"s_cbranch_scc1 {pfx}_win_pref",
                 f"global_load_dword {NWIN}, {lane4}, s[14:15]",
                 "s_waitcnt vmcnt(0)",
@@ -1044,6 +1057,9 @@ def make_handlers(variant, pfx):
 
     H(("END",), [f"s_branch {pfx}_tape_end"], tail=False, reads_stack=False)
     if G:
+        # a program whose last push (PUSH_MEM) may still be in flight (mq_api.cpp final pass):
+        # the tape end waits for it here, so the column store needs no vector wait of its own
+        H(("END_V",), ["s_waitcnt vmcnt(0)", f"s_branch {pfx}_tape_end"], tail=False, reads_stack=False)
         H(("REFILL",), load_window(False, pfx), reads_stack=False)
     # ---- leaves
     for d in range(D):
@@ -1409,7 +1425,8 @@ def store_column(pfx):
     (tape, model) pair: the pair count the tape end added is taken back."""
     out = [f"{pfx}_store_column:",
            "s_sub_u32 s40, s40, 1",
-           VMWAIT,
+           LGKMWAIT,                                    # (a vector push in flight: END_V waited)
+           "s_mov_b32 s59, 0",                          # stores issued (load_window's wait)
            "s_mul_i32 s38, s82, s29", "s_mul_hi_u32 s39, s82, s29", "s_lshl_b64 s[38:39], s[38:39], 2",
            "s_add_u32 s38, s38, s90", "s_addc_u32 s39, s39, s91",
            "s_mov_b64 s[60:61], exec", "s_mov_b64 exec, s[62:63]",
@@ -1423,6 +1440,7 @@ def store_column(pfx):
            "s_mov_b64 exec, 1",
            "v_mov_b32 v6, s36", "v_mov_b32 v4, s34", "v_mov_b32 v5, s35",
            "global_store_dwordx2 v6, v[4:5], s[96:97]",
+           "s_add_u32 s59, s59, 1",
            "s_mov_b64 exec, s[62:63]",
            "s_load_dword s36, s[10:11], 0x18c",        # QArgs.bool_rows
            "s_waitcnt lgkmcnt(0)",
@@ -1431,11 +1449,12 @@ def store_column(pfx):
            f"{pfx}_col_row:",
            f"v_cndmask_b32_e64 v5, 0, 1, {B(0)}",
            "global_store_dword v2, v5, s[38:39]",
+           "s_add_u32 s59, s59, 1",
            f"s_branch {pfx}_col_done",
            f"{pfx}_col_value:"]
     for l in range(L):
         out += [f"s_cmp_le_u32 s85, {l}", f"s_cbranch_scc1 {pfx}_col_done",
-                f"global_store_dword v2, {S(0, l)}, s[38:39]"]
+                f"global_store_dword v2, {S(0, l)}, s[38:39]", "s_add_u32 s59, s59, 1"]
         if l < L - 1:
             out += ["s_add_u32 s38, s38, s74", "s_addc_u32 s39, s39, s75"]
     out += [f"{pfx}_col_done:", "s_mov_b64 exec, s[60:61]", f"s_branch {pfx}_next_tape"]
@@ -1741,7 +1760,8 @@ def frame(variant, pfx, handlers, subs):
         P += stage_rows(pfx)
         P += prof_point("STAGE")
     if G:
-        P += ["s_mov_b64 s[14:15], 0"]   # no window yet (load_window's successor test fails)
+        P += ["s_mov_b64 s[14:15], 0",   # no window yet (load_window's successor test fails)
+              "s_mov_b32 s59, 0"]        # vector stores issued by the previous tape (none)
     ee = G and EEV is not None
     if ee:
         P += ["s_cmp_eq_u32 s30, 0",
@@ -1863,6 +1883,7 @@ def frame(variant, pfx, handlers, subs):
         "v_mov_b32 v5, s38",
         "v_mov_b32 v6, 0",
         "global_atomic_smin v6, v5, s[72:73]",
+    ] + (["s_mov_b32 s59, 1"] if G else []) + [
         "s_mov_b64 exec, s[60:61]",
         f"s_branch {pfx}_next_tape",
         f"{pfx}_store_verdict:",
@@ -1875,6 +1896,7 @@ def frame(variant, pfx, handlers, subs):
         "s_mov_b64 s[60:61], exec",
         "s_mov_b64 exec, s[62:63]",
         "global_store_byte v6, v5, s[38:39]",
+    ] + (["s_mov_b32 s59, 1"] if G else []) + [
         "s_mov_b64 exec, s[60:61]",
     ] + ([f"s_branch {pfx}_next_tape"] + store_column(pfx) if G else []) + [
         f"{pfx}_next_tape:",

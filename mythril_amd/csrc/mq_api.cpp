@@ -1511,20 +1511,28 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
     prev_pre = op == G_PUSH_VAR ? pushed_pre : -1;
   }
   static const bool no_lwait = std::getenv("MQ_NO_LWAIT") != nullptr;   // (diagnostic A/B)
-  if (!P && !no_lwait) {
+  if (!P) {
     // final pass: a stack reader waits for the vector loads of a PUSH_MEM only when one may be
     // outstanding; otherwise its "_L" variant waits for LDS / scalar loads alone, and the
     // prefetch of the next program window (gen_qsa.py load_window) stays in flight
+    // (MQ_NO_LWAIT: no _L variants; END_V is needed either way)
     bool pending = false;
     for (const Emit& e : log) {
       if (e.kind == QK_PUSH_MEM) {
         pending = true;
         continue;
       }
+      if (e.kind == QK_END) {
+        // the value a column stores may still be a load in flight: END_V waits for it (the
+        // tape end's column store waits for LDS / scalar loads only)
+        const int h = c->qsa_index[k][QK_END_V][0][0];
+        if (pending && h >= 0) out[e.pos] = hword(k, c->qsa_off[k][h]);
+        continue;
+      }
       const int lk = kQsaKindLForm[e.kind];
       if (lk >= 0) {
         const int h = c->qsa_index[k][lk][e.d][e.v + 1];
-        if (!pending && h >= 0) out[e.pos] = hword(k, c->qsa_off[k][h]) | (e.imm << 16);
+        if (!pending && h >= 0 && !no_lwait) out[e.pos] = hword(k, c->qsa_off[k][h]) | (e.imm << 16);
         pending = false;   // (the VMWAIT form drained every load)
         continue;
       }
