@@ -884,15 +884,17 @@ def sub_uf1(pfx):
             "s_waitcnt lgkmcnt(0)",
             "s_cmp_ge_u32 s98, s99",
             f"s_cbranch_scc1 {P}_uf_ret",
-            "s_mul_i32 s34, s98, 48",
+            "s_mul_i32 s34, s98, 56",                         # sizeof(FuncDev)
             "s_add_u32 s78, s64, s34",
             "s_addc_u32 s79, s65, 0",
             "s_load_dword s36, s[78:79], 0x4",                # nl_a0
             "s_load_dword s37, s[78:79], 0xc",                # nl_res
             "s_load_dword s38, s[78:79], 0x10",               # stride (words)
+            "s_load_dword s99, s[78:79], 0x14",               # dense_e
             "s_load_dwordx2 s[64:65], s[78:79], 0x18",        # entry_base
             "s_load_dwordx2 s[60:61], s[78:79], 0x20",        # ptr_base
             "s_load_dwordx2 s[34:35], s[78:79], 0x28",        # else_base
+            "s_load_dwordx2 s[78:79], s[78:79], 0x30",        # dense_base
             "s_waitcnt lgkmcnt(0)",
             "s_lshl_b64 s[34:35], s[34:35], 2",
             "s_add_u32 s70, s70, s34",
@@ -904,7 +906,9 @@ def sub_uf1(pfx):
             "s_add_u32 s68, s68, s64",
             "s_addc_u32 s69, s69, s65",                       # entry 0 of the function
             "s_lshl_b32 s39, s38, 2",                         # stride bytes
-            "s_lshl_b32 s98, s36, 2"]                        # value offset in an entry
+            "s_lshl_b32 s98, s36, 2",                        # value offset in an entry
+            "s_cmp_lg_u32 s99, 0",
+            f"s_cbranch_scc1 {P}_uf_dense"]
     # The scan: eight entries per memory round trip by their first key limb (keys are hashes or
     # small integers: a limb-0 match is nearly always the entry), a full key compare for the
     # candidates only; then one round trip for the value (matched lanes) or the else value.
@@ -986,6 +990,93 @@ def sub_uf1(pfx):
             "s_mov_b64 exec, s[60:61]",
             f"{P}_uf_ret:",
             "s_setpc_b64 s[76:77]"]
+    # Dense slots (FuncDev dense_e > 0, mq_api.cpp mq_models_upload): key limb l of entry slot e
+    # of every model is one SoA row, so the wave's probe of slot e is one coalesced 256-byte read
+    # per limb.  Same scan as above (first key limb of eight slots per round trip, full compare
+    # of candidates); a lane stops at its model's entry count.  SGPRs: s38 dense_e, s98 slot,
+    # s[68:69] the keys block, s39 / s[78:79] / s[34:35] scratch.
+    out += [f"{P}_uf_dense:",
+            "s_mov_b32 s38, s99",
+            "s_load_dwordx2 s[68:69], s[10:11], 0x1b0",      # dense_words
+            "s_waitcnt lgkmcnt(0)",
+            "s_lshl_b64 s[78:79], s[78:79], 2",
+            "s_add_u32 s68, s68, s78",
+            "s_addc_u32 s69, s69, s79",
+            "v_lshlrev_b32 v4, 1, v2",
+            "global_load_dword v5, v4, s[66:67]",
+            "global_load_dword v6, v4, s[66:67] offset:8",
+            "s_waitcnt vmcnt(0)",
+            "v_sub_u32 v6, v6, v5",                          # this model's entries
+            "s_mov_b64 s[60:61], exec",
+            "s_mov_b64 s[64:65], 0",
+            "s_mov_b32 s98, 0",
+            f"{P}_ufd_loop:",
+            "v_cmp_lt_u32_e64 s[66:67], s98, v6",
+            "s_nop 3",
+            "s_and_b64 exec, exec, s[66:67]",
+            f"s_cbranch_execz {P}_ufd_done"]
+    for j in range(8):
+        out += [f"s_add_u32 s39, s98, {j}", "s_cmp_ge_u32 s39, s38", f"s_cbranch_scc1 {P}_ufd_ld",
+                "s_mul_i32 s39, s39, s36",
+                "s_mul_i32 s78, s39, s74", "s_mul_hi_u32 s79, s39, s74",
+                "s_add_u32 s78, s78, s68", "s_addc_u32 s79, s79, s69",
+                f"global_load_dword v{UBASE + j}, v2, s[78:79]"]
+    out += [f"{P}_ufd_ld:", "s_mov_b64 s[66:67], exec", "s_waitcnt vmcnt(0)"]
+    for j in range(8):
+        nj = f"{P}_ufd_nj{j}"
+        out += [f"s_add_u32 s39, s98, {j}", "s_cmp_ge_u32 s39, s38", f"s_cbranch_scc1 {P}_ufd_next",
+                f"v_cmp_eq_u32_e64 s[34:35], v{UBASE + j}, {W(0)}",
+                "v_cmp_lt_u32_e64 s[78:79], s39, v6",
+                "s_nop 3",
+                "s_and_b64 s[34:35], s[34:35], s[78:79]",
+                "s_and_b64 s[34:35], s[34:35], s[66:67]",
+                f"s_cbranch_scc0 {nj}",
+                "s_mov_b64 exec, s[34:35]",
+                "s_mul_i32 s99, s39, s36",
+                "s_mul_i32 s78, s99, s74", "s_mul_hi_u32 s79, s99, s74",
+                "s_add_u32 s78, s78, s68", "s_addc_u32 s79, s79, s69"]
+        for l in range(1, L):
+            out += [f"s_cmp_le_u32 s36, {l}", f"s_cbranch_scc1 {P}_ufd_kl{j}",
+                    "s_add_u32 s78, s78, s74", "s_addc_u32 s79, s79, 0",
+                    f"global_load_dword v{UBASE + 12 + l}, v2, s[78:79]"]
+        out += [f"{P}_ufd_kl{j}:", "s_waitcnt vmcnt(0)", "v_mov_b32 v148, 0"]
+        for l in range(1, L):
+            out += [f"s_cmp_le_u32 s36, {l}", f"s_cbranch_scc1 {P}_ufd_kc{j}",
+                    f"v_xor_b32 v149, v{UBASE + 12 + l}, {W(l)}", "v_or_b32 v148, v148, v149"]
+        out += [f"{P}_ufd_kc{j}:",
+                "v_cmp_eq_u32_e64 s[34:35], 0, v148",
+                "s_nop 3",
+                "s_and_b64 s[34:35], s[34:35], exec",
+                "s_or_b64 s[64:65], s[64:65], s[34:35]",
+                "s_mov_b64 exec, s[34:35]",
+                "v_mov_b32 v138, s39",                           # matched slot
+                "s_andn2_b64 s[66:67], s[66:67], s[34:35]",
+                "s_mov_b64 exec, s[66:67]",
+                f"{nj}:"]
+    out += [f"{P}_ufd_next:",
+            "s_mov_b64 exec, s[66:67]",
+            "s_add_u32 s98, s98, 8",
+            f"s_branch {P}_ufd_loop",
+            f"{P}_ufd_done:",
+            "s_mov_b64 exec, s[60:61]"]
+    out += [f"v_mov_b64 v[{UBASE + l}:{UBASE + 1 + l}], 0" for l in range(0, 8, 2)]
+    # matched lanes: value limb l of slot e at keys + (dense_e * nl_a0 + e * nl_res + l) * M * 4
+    out += ["s_and_b64 exec, s[60:61], s[64:65]",
+            f"s_cbranch_execz {P}_uf_vl_issued",
+            "s_mul_i32 s99, s38, s36",                      # dense_e * nl_a0
+            "s_mul_i32 s78, s99, s74", "s_mul_hi_u32 s79, s99, s74",
+            "s_add_u32 s78, s78, s68", "s_addc_u32 s79, s79, s69",
+            "s_mul_i32 s39, s37, s74",                      # nl_res * M * 4
+            "v_mov_b32 v149, s39",                          # (one SGPR operand per VALU)
+            "v_mad_u64_u32 v[150:151], s[34:35], v138, v149, s[78:79]",
+            "v_add_co_u32 v150, vcc, v150, v2",
+            "v_addc_co_u32 v151, vcc, 0, v151, vcc"]
+    for l in range(L):
+        out += [f"s_cmp_le_u32 s37, {l}", f"s_cbranch_scc1 {P}_uf_vl_issued",
+                f"global_load_dword v{UBASE + l}, v[150:151], off"]
+        if l < L - 1:
+            out += ["v_add_co_u32 v150, vcc, s74, v150", "v_addc_co_u32 v151, vcc, 0, v151, vcc"]
+    out += [f"s_branch {P}_uf_vl_issued"]
     # the lookup's pointer / match registers were written as v128..v151: move them to UBASE + k
     def remap(line):
         line = re.sub(r"v\[(\d+):(\d+)\]", lambda m: f"v[{fix(int(m.group(1)))}:{fix(int(m.group(2)))}]", line)

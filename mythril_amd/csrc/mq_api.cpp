@@ -177,6 +177,8 @@ struct DevBuf {
 
 // words past the function entries that reads may touch (8 entries of the widest G table)
 static constexpr size_t kEntryPadWords = 512;
+// most entry slots per model a function may have to get dense lookup slots (FuncDev dense_e)
+static constexpr int64_t kDenseMaxE = 16;
 
 // the assembly interpreter keeps temps in LDS (2 KB per temp per wave, 4 waves per workgroup)
 static constexpr int kQsaMaxTemps = 16;
@@ -213,7 +215,7 @@ struct mq_ctx {
   int64_t M = 0, index_base = 0;
   int n_vars = 0, n_funcs = 0;
   std::vector<uint16_t> var_width;
-  DevBuf vars, var_off, var_nl, funcs, entry_ptr, entry_words, else_words;
+  DevBuf vars, var_off, var_nl, funcs, entry_ptr, entry_words, else_words, dense_words;
   int64_t entry_words_n = 0;   // words of function entries (G scans them with 32-bit offsets)
   DevBuf counters;
   DevBuf best_tmp;  // scratch first-hit buffer for the synchronous API
@@ -774,6 +776,38 @@ static int upload_one(mq_ctx* c, const mq_model_batch* mb) {
     ew_total = std::max(ew_total, last);
   }
   if (else_soa.empty()) else_soa.push_back(0);
+  // dense lookup slots for the G interpreter's table scan (gen_qsa.py sub_uf1): functions of one
+  // argument whose per-model entry count is small (keccak inverse tables, C4) get every model's
+  // entries as slot-major SoA rows as well, so the 64 lanes of a wave probing slot e read one
+  // coalesced row per key limb instead of 64 scattered entries.  MQ_NO_DENSE_TABLES=1: off.
+  std::vector<uint32_t> dense;
+  {
+    static const bool no_dense = std::getenv("MQ_NO_DENSE_TABLES") != nullptr;
+    for (int f = 0; f < F && !no_dense && M > 0; f++) {
+      FuncDev& x = fd[f];
+      if (x.arity != 1 || x.nl_a0 > 8 || x.nl_res > 8) continue;
+      const int64_t* ep = mb->entry_ptr + (int64_t)f * (M + 1);
+      int64_t emax = 0;
+      for (int64_t m = 0; m < M; m++) emax = std::max(emax, ep[m + 1] - ep[m]);
+      const int64_t total = ep[M] - ep[0];
+      const int64_t words = emax * (int64_t)(x.nl_a0 + x.nl_res) * M;
+      // bounded: at most kDenseMaxE slots, and not much more memory than the CSR entries
+      if (emax == 0 || emax > kDenseMaxE || words > 2 * total * (int64_t)x.stride + 16 * M) continue;
+      x.dense_e = (uint32_t)emax;
+      x.dense_base = (int64_t)dense.size();
+      dense.resize(dense.size() + (size_t)words, 0);
+      uint32_t* kd = dense.data() + x.dense_base;
+      uint32_t* vd = kd + (size_t)emax * x.nl_a0 * M;
+      const uint32_t* base = mb->entry_words + mb->entry_base[f];
+      for (int64_t m = 0; m < M; m++)
+        for (int64_t e = 0; e < ep[m + 1] - ep[m]; e++) {
+          const uint32_t* ent = base + (ep[m] + e) * (int64_t)x.stride;
+          for (uint32_t l = 0; l < x.nl_a0; l++) kd[((size_t)e * x.nl_a0 + l) * M + m] = ent[l];
+          for (uint32_t l = 0; l < x.nl_res; l++) vd[((size_t)e * x.nl_res + l) * M + m] = ent[x.nl_a0 + l];
+        }
+    }
+  }
+  if (dense.empty()) dense.push_back(0);
   c->have_models = false;
   // variable rows followed by one all-zero row (the QSA preload points absent limbs at it)
   HIPCHK(c->vars.ensure(sizeof(uint32_t) * (size_t)(rows + 1) * M));
@@ -844,6 +878,7 @@ static int upload_one(mq_ctx* c, const mq_model_batch* mb) {
     HIPCHK(c->entry_words.upload(&zw, 1, c->stream));
   }
   HIPCHK(c->else_words.upload(else_soa.data(), else_soa.size(), c->stream));
+  HIPCHK(c->dense_words.upload(dense.data(), dense.size(), c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   c->M = M;
   c->index_base = mb->index_base;
@@ -2822,6 +2857,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       q.entry_words = c->entry_words.p;
       q.else_words = c->else_words.p;
       q.n_funcs = (uint32_t)c->n_funcs;
+      q.dense_words = c->dense_words.as<uint32_t>();
       q.bool_masks = c->bmasks.as<uint64_t>();
       q.n_bool_masks = (uint32_t)c->n_bmask;
       q.prof_out = prof_buffer(c, (int)li);
@@ -2903,6 +2939,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     q.entry_words = c->entry_words.p;
     q.else_words = c->else_words.p;
     q.n_funcs = (uint32_t)c->n_funcs;
+    q.dense_words = c->dense_words.as<uint32_t>();
     q.bool_masks = c->bmasks.as<uint64_t>();
     q.n_bool_masks = (uint32_t)c->n_bmask;
     if (k == 1) q.prof_out = prof_buffer(c, -1);

@@ -18,11 +18,17 @@ struct FuncDev {
   uint32_t arity;
   uint32_t nl_a0, nl_a1, nl_res;
   uint32_t stride;      // words per entry
-  uint32_t pad;
+  uint32_t dense_e;     // > 0: also held as dense slots (G lookups): entry slots per model
   int64_t entry_base;   // word offset of entry 0 in entry_words
   int64_t ptr_base;     // offset of row pointers [M+1] in entry_ptr
   int64_t else_base;    // word offset of the SoA else block: else_words[else_base + limb*M + m]
+  // dense slots (dense_e > 0): key limb l of entry slot e of model m at
+  // dense_words[dense_base + (e * nl_a0 + l) * M + m], value limb l at
+  // dense_words[dense_base + (dense_e * nl_a0 + e * nl_res + l) * M + m]; a model's entries keep
+  // their order, slots past its count are never read (the count is entry_ptr's)
+  int64_t dense_base;
 };
+static_assert(sizeof(FuncDev) == 56, "FuncDev layout (gen_qsa.py sub_uf1 reads it)");
 
 struct KArgs {
   // tapes
@@ -90,6 +96,7 @@ struct QArgs {
   uint32_t n_bool_masks;         // 0x1a0
   uint32_t prog_lds;             // 0x1a4 G: LDS offset | 1 of the workgroup's programs (0: read from memory)
   unsigned long long* prof_out;  // 0x1a8 G profile build only: (cycles, count) per handler kind
+  const uint32_t* dense_words;   // 0x1b0 G: dense lookup slots (FuncDev dense_base / dense_e)
 };
 static_assert(sizeof(void*) == 8, "64-bit");
 static_assert(__builtin_offsetof(QArgs, M) == 0x40, "QArgs layout");
@@ -103,6 +110,7 @@ static_assert(__builtin_offsetof(QArgs, bool_masks) == 0x198, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, n_bool_masks) == 0x1a0, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, prog_lds) == 0x1a4, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, prof_out) == 0x1a8, "QArgs layout");
+static_assert(__builtin_offsetof(QArgs, dense_words) == 0x1b0, "QArgs layout");
 
 // variant 0 = P (preloaded variables, qsa_kernel), 1 = G (general, qsg_kernel)
 hipError_t launch_qsa(int variant, const QArgs* d_args, unsigned gx, unsigned gy, size_t lds, hipStream_t st);
