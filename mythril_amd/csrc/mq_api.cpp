@@ -782,7 +782,7 @@ static int upload_one(mq_ctx* c, const mq_model_batch* mb) {
   // coalesced row per key limb instead of 64 scattered entries.  MQ_NO_DENSE_TABLES=1: off.
   std::vector<uint32_t> dense;
   {
-    static const bool no_dense = std::getenv("MQ_NO_DENSE_TABLES") != nullptr;
+    const bool no_dense = std::getenv("MQ_NO_DENSE_TABLES") != nullptr;
     for (int f = 0; f < F && !no_dense && M > 0; f++) {
       FuncDev& x = fd[f];
       if (x.arity != 1 || x.nl_a0 > 8 || x.nl_res > 8) continue;

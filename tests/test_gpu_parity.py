@@ -1002,3 +1002,41 @@ def test_g_kernel_variable_shifts_match_oracle(evaluator, M):
     assert len(mism) == 0, f"{len(mism)} mismatches, first {mism[:5]}"
     fh_ref, _ = cref.first_hit(tb, mb)
     assert (evaluator.first_hit(ct) == fh_ref).all()
+
+
+@pytest.mark.parametrize("dense", [True, False])
+@pytest.mark.parametrize("max_entries", [3, 9, 20])
+def test_table_lookups_dense_and_csr_match_oracle(evaluator, monkeypatch, dense, max_entries):
+    """UF / array lookups on G through both table layouts: dense slot-major rows (functions with
+    at most 16 entries per model, mq_models_upload) and the CSR entry lists (more entries, or
+    MQ_NO_DENSE_TABLES=1); keys found at every slot, absent keys (else value), empty tables."""
+    import random
+    from mythril_amd import smt as S
+    from mythril_amd.lower import lower_batch, serialize_models
+    from mythril_amd.smt_model import Model
+    if not dense:
+        monkeypatch.setenv("MQ_NO_DENSE_TABLES", "1")
+    rng = random.Random(max_entries)
+    f = S.Function("inv", [256], 256)
+    g = S.Function("bal", [160], 64)
+    x, y = S.BitVecSym("x", 256), S.BitVecSym("y", 160)
+    exprs = [f(x) == S.BitVecVal(7, 256), S.ULT(f(x), S.BitVecVal(1 << 200, 256)),
+             g(y) == S.BitVecVal(5, 64), S.And(f(x) == S.ZeroExt(192, g(y)), S.ULT(x, S.BitVecVal(1 << 255, 256)))]
+    models = []
+    for m in range(300):
+        n = rng.randrange(max_entries + 1)
+        keys = [rng.getrandbits(256) for _ in range(n)]
+        xv = rng.choice(keys) if keys and rng.random() < 0.7 else rng.getrandbits(256)
+        ft = {(k,): rng.choice([7, rng.getrandbits(256), rng.getrandbits(64)]) for k in keys}
+        gk = [rng.getrandbits(160) for _ in range(rng.randrange(max_entries + 1))]
+        yv = rng.choice(gk) if gk and rng.random() < 0.7 else rng.getrandbits(160)
+        gt = {(k,): rng.choice([5, rng.getrandbits(64)]) for k in gk}
+        models.append(Model({"x": xv, "y": yv}, {"inv": (ft, rng.choice([0, 7])), "bal": (gt, rng.choice([0, 5]))}))
+    tb, syms, ok = lower_batch(exprs)
+    assert ok.all()
+    mb = serialize_models(models, syms)
+    evaluator.upload_models(mb)
+    v, fh = evaluator.verdicts(tb)
+    assert (v == cref.verdicts(tb, mb)).all()
+    assert (fh == cref.first_hit(tb, mb)[0]).all()
+    assert 0 < v.mean() < 1
