@@ -371,6 +371,18 @@ def lt_chain(x, y, dst):
     return out
 
 
+def tl_signed(nw):
+    """T = the inline constant of class nw with its sign bit (255) flipped."""
+    out = [f"v_mov_b32 {T(l)}, {kconst(l, nw)}" for l in range(L - 1)]
+    if nw < L:
+        return out + [f"v_mov_b32 {T(L - 1)}, 0x80000000"]
+    return out + [f"v_mov_b32 {T(L - 1)}, {kconst(L - 1, nw)}", f"v_xor_b32 {T(L - 1)}, 0x80000000, {T(L - 1)}"]
+
+
+def flip_top(x):
+    return [f"v_xor_b32 {S(x, L - 1)}, 0x80000000, {S(x, L - 1)}"]
+
+
 def flip_signs(d):
     return [f"v_xor_b32 {S(d - 1, 7)}, 0x80000000, {S(d - 1, 7)}", f"v_xor_b32 {S(d, 7)}, 0x80000000, {S(d, 7)}"]
 
@@ -1359,6 +1371,10 @@ def make_handlers(variant, pfx):
                 H(("UGTK", x, cls), kread + tl + lt_chain(T, xa, B(x)))
                 H(("ULEK", x, cls), kread + tl + lt_chain(T, xa, "s[38:39]") + ["s_nop 3", f"s_not_b64 {B(x)}, s[38:39]"])
                 H(("UGEK", x, cls), kread + tl + lt_chain(xa, T, "s[38:39]") + ["s_nop 3", f"s_not_b64 {B(x)}, s[38:39]"])
+                # signed at 256 bits (SLT / SGT with a constant operand): both sign bits flipped,
+                # then the unsigned borrow chain (calldata bytes: ite(k <s size, cd_k, 0))
+                H(("SLTK", x, cls), kread + tl_signed(nw) + flip_top(x) + lt_chain(xa, T, B(x)))
+                H(("SGTK", x, cls), kread + tl_signed(nw) + flip_top(x) + lt_chain(T, xa, B(x)))
             for v in range(NVG):
                 for c, nw in enumerate(KCLS[1:]):
                     H(("EQVK", x, 2 * v + c), const_words(nw) + eq_const_body(lambda l, _v=v: f"v{VBASE + 8 * _v + l}", nw, B(x)),
@@ -1397,6 +1413,26 @@ def make_handlers(variant, pfx):
                     for nm, a_, b_ in (("ULTK", xs, T), ("UGTK", T, xs)):
                         H((f"S{nm}{nw}_A", x, n - 1), pre + lt_chain(a_, b_, B(x))
                           + [f"s_and_b64 {B(x - 1)}, {B(x - 1)}, {B(x)}"], reads_stack=False)
+        # "push staged variable row imm (n limbs) at x; signed-compare it (256 bits) with an
+        # inline constant" (PUSH_MEMS + SLTK / SGTK; the Bool stays at B(x))
+        for x in range(D - 1):
+            for n in (1, 2, 8):
+                lds = ["s_lshl_b32 s34, s17, 8", f"v_add_u32 v5, s34, {STG}"] + \
+                      [f"ds_read_b32 {S(x, l)}, v5 offset:{256 * l}" for l in range(n)]
+                for nw in (2, 8):
+                    pre = lds + zero_limbs(x, n) + const_words(nw) + tl_signed(nw) + ["s_waitcnt lgkmcnt(0)"] + flip_top(x)
+                    xs = (lambda l, _x=x: S(_x, l))
+                    for nm, a_, b_ in (("SLTK", xs, T), ("SGTK", T, xs)):
+                        H((f"S{nm}{nw}", x, n - 1), pre + lt_chain(a_, b_, B(x)), reads_stack=False)
+        # ite(c, x, 0) (the translator drops the zero's push): then-value at t, condition B(t - 1)
+        for t in range(1, D - 1):
+            H(("ITEZ", t), [f"v_cndmask_b32_e64 {S(t - 1, l)}, 0, {S(t, l)}, {B(t - 1)}" for l in range(L)])
+        # concat: S[d-1] = S[d-1] << (32q + s) | S[d] (s != 0, imm = 32 - s; SHLI + BOR in one):
+        # the low operand is narrower than 32q + s bits, so only limbs 0..q take it
+        for d in range(1, D):
+            for q in range(L):
+                H(("SHLOR", d, q), shl_body(d - 1, q, True) + [f"v_or_b32 {S(d - 1, l)}, {S(d - 1, l)}, {S(d, l)}"
+                                                              for l in range(q + 1)])
     # ---- (last: these handlers never branch, so the subroutine calls above stay in s_call range)
     # ---- binary ops whose right operand is a preloaded variable (the translator fuses
     # PUSH_VAR v at slot d with the consuming op at d: no stack copy, one dispatch less)
@@ -1552,10 +1588,13 @@ def store_column(pfx):
     return out
 
 
+STAGE_CHUNKS = 4   # G: 8-row chunks per wave per staging round (4 waves: 128 rows a round)
+
+
 def stage_rows(pfx):
     """G: copy the model rows the batch's tapes push most (QArgs stage_rows[0..n_stage), a
     multiple of 8, padded with the zero row) for this workgroup's 64-model tile into LDS at
-    stage_base + 256 * slot, 8 rows per wave per round (8 loads in flight), then s_barrier: the
+    stage_base + 256 * slot, 32 rows per wave per round (32 loads in flight), then s_barrier: the
     4 waves of the workgroup share the tile, so each row is fetched once per workgroup and every
     PUSH_MEMS of its tapes is an LDS read."""
     out = ["s_load_dwordx2 s[64:65], s[10:11], 0x184",     # n_stage, stage_base
@@ -1570,17 +1609,27 @@ def stage_rows(pfx):
            "s_lshl_b32 s61, s60, 3",                        # first row of this wave's rounds
            f"{pfx}_stage_loop:",
            "s_cmp_ge_u32 s61, s64",
-           f"s_cbranch_scc1 {pfx}_stage_done",
-           "s_lshl_b32 s70, s61, 2",
-           "s_load_dwordx8 s[80:87], s[66:67], s70",
-           "s_waitcnt lgkmcnt(0)"]
-    for j in range(8):
-        out += [f"s_mul_i32 s68, s{80 + j}, s29", f"s_mul_hi_u32 s69, s{80 + j}, s29", "s_lshl_b64 s[68:69], s[68:69], 2",
-                "s_add_u32 s68, s68, s90", "s_addc_u32 s69, s69, s91",
-                f"global_load_dword {T(j)}, v2, s[68:69]"]
-    out += ["s_lshl_b32 s70, s61, 8", f"v_add_u32 v5, s70, {STG}", "s_waitcnt vmcnt(0)"]
-    out += [f"ds_write_b32 v5, {T(j)} offset:{256 * j}" for j in range(8)]
-    out += ["s_add_u32 s61, s61, 32", f"s_branch {pfx}_stage_loop",
+           f"s_cbranch_scc1 {pfx}_stage_done"]
+    # a round: up to STAGE_CHUNKS chunks of 8 rows per wave (rows s61 + 32 c ..), every load
+    # issued before the one wait (the UF1 work registers are free before the first tape)
+    regs = [[T(j) for j in range(8)]] + [[f"v{UBASE + 8 * (c - 1) + j}" for j in range(8)] for c in range(1, STAGE_CHUNKS)]
+    for c in range(STAGE_CHUNKS):
+        if c:
+            out += [f"s_add_u32 s70, s61, {32 * c}", "s_cmp_ge_u32 s70, s64", f"s_cbranch_scc1 {pfx}_stage_wait",
+                    "s_lshl_b32 s70, s70, 2"]
+        else:
+            out += ["s_lshl_b32 s70, s61, 2"]
+        out += ["s_load_dwordx8 s[80:87], s[66:67], s70", "s_waitcnt lgkmcnt(0)"]
+        for j in range(8):
+            out += [f"s_mul_i32 s68, s{80 + j}, s29", f"s_mul_hi_u32 s69, s{80 + j}, s29", "s_lshl_b64 s[68:69], s[68:69], 2",
+                    "s_add_u32 s68, s68, s90", "s_addc_u32 s69, s69, s91",
+                    f"global_load_dword {regs[c][j]}, v2, s[68:69]"]
+    out += [f"{pfx}_stage_wait:", "s_lshl_b32 s70, s61, 8", f"v_add_u32 v5, s70, {STG}", "s_waitcnt vmcnt(0)"]
+    for c in range(STAGE_CHUNKS):
+        if c:
+            out += [f"s_add_u32 s71, s61, {32 * c}", "s_cmp_ge_u32 s71, s64", f"s_cbranch_scc1 {pfx}_stage_next"]
+        out += [f"ds_write_b32 v5, {regs[c][j]} offset:{8192 * c + 256 * j}" for j in range(8)]
+    out += [f"{pfx}_stage_next:", f"s_add_u32 s61, s61, {32 * STAGE_CHUNKS}", f"s_branch {pfx}_stage_loop",
             f"{pfx}_stage_done:"]
     if PROG_LDS:
         out += stage_programs(pfx)

@@ -1224,6 +1224,24 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
     drop_last(2);
     emit_k(fk, x, nsel, imm0, data);
   };
+  // G: "PUSH_MEMS x (n limbs); SLTK / SGTK x" as one S{SLT,SGT}K{2,8} word (layout as merge_memk's)
+  auto merge_mems_k = [&]() {
+    if (P || log.size() < 2) return;
+    const Emit e1 = log.back();
+    if ((e1.kind != QK_SLTK && e1.kind != QK_SGTK) || out.size() != ends_at(e1)) return;
+    const Emit e0 = log[log.size() - 2];
+    if (e0.kind != QK_PUSH_MEMS || ends_at(e0) != e1.pos || e0.d != e1.d || e0.nd != 0 || e0.v < 0) return;
+    const bool wide = e1.v == 2;
+    const int fk = e1.kind == QK_SLTK ? (wide ? QK_SSLTK8 : QK_SSLTK2) : (wide ? QK_SSGTK8 : QK_SSGTK2);
+    if (c->qsa_index[k][fk][e1.d][e0.v + 1] < 0) return;
+    std::vector<uint32_t> data;
+    if (e1.v == 0) data = {e1.imm, 0u};
+    else data.assign(out.begin() + (long)(e1.pos + 1), out.begin() + (long)ends_at(e1));
+    const int x = e1.d, nsel = e0.v;
+    const uint32_t imm0 = e0.imm;
+    drop_last(2);
+    emit_k(fk, x, nsel, imm0, data);
+  };
   uint32_t prev_op = G_END, prev_d = 0, prev_imm = 0;
   size_t prev_out = 0;
   int prev_pre = -1;   // preload slot of the variable the previous instruction pushed
@@ -1380,14 +1398,29 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
       case G_BAND: ok = binop(d, QK_BAND, QK_BANDV, QK_BANDC); break;
       case G_BOR: ok = binop(d, QK_BOR, QK_BORV, QK_BORC); break;
       case G_BXOR: ok = binop(d, QK_BXOR, QK_BXORV, QK_BXORC); break;
-      case G_ITE: ok = word(QK_ITE, d, -1, 0); break;
+      case G_ITE: {
+        // G: ite(c, x, 0) with the zero pushed last -> ITEZ at the then-slot (the push dropped)
+        const Emit* e = log.empty() ? nullptr : &log.back();
+        if (!P && d >= 2 && e && e->kind == QK_PUSH_CONSTI && e->imm == 0 && e->d == d && out.size() == ends_at(*e) &&
+            c->qsa_index[k][QK_ITEZ][d - 1][0] >= 0) {
+          drop_last(1);
+          ok = word(QK_ITEZ, d - 1, -1, 0);
+        } else ok = word(QK_ITE, d, -1, 0);
+        break;
+      }
       case G_ITE_EF: ok = word(QK_ITE_EF, d, -1, 0); break;
       // signed predicates: at 256 bits the handler flips bit 255; below, flip bit W-1 of both
       // operands (FLIP2) and compare unsigned
       case G_SLT: case G_SLE: case G_SGT: case G_SGE: {
         const int su = op == G_SLT ? QK_SLT : op == G_SLE ? QK_SLE : op == G_SGT ? QK_SGT : QK_SGE;
         const int uu = op == G_SLT ? QK_ULT : op == G_SLE ? QK_ULE : op == G_SGT ? QK_UGT : QK_UGE;
-        if (imm == 256) ok = word(su, d, -1, 0);
+        if (imm == 256 && (op == G_SLT || op == G_SGT) &&
+            fuse_const(d, op == G_SLT ? QK_SLTK : QK_SGTK, op == G_SLT ? QK_SGTK : QK_SLTK)) {
+          // G: a compare with a constant operand; a staged variable pushed right before it is
+          // read by the compare itself (S{SLT,SGT}K{2,8})
+          merge_mems_k();
+          ok = true;
+        } else if (imm == 256) ok = word(su, d, -1, 0);
         else ok = imm >= 1 && imm < 256 && word(QK_FLIP2, d, (int)((imm - 1) >> 5), (imm - 1) & 31) && word(uu, d, -1, 0);
         break;
       }
@@ -1506,7 +1539,10 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
         ok = imm < 256 && imm2 >= 1 && imm2 <= 256 && lshr(d, imm, false) && mask(d, imm2);
         break;
       case G_CONCAT:  // imm = width of the low operand (slot d), imm2 = result width
-        ok = imm >= 1 && imm < 256 && imm2 <= 256 && shl(d - 1, imm) && word(QK_BOR, d, -1, 0);
+        ok = imm >= 1 && imm < 256 && imm2 <= 256;
+        if (ok && !P && (imm & 31) && c->qsa_index[k][QK_SHLOR][d][(imm >> 5) + 1] >= 0)
+          ok = word(QK_SHLOR, d, (int)(imm >> 5), 32 - (imm & 31));   // G: shift and OR in one
+        else ok = ok && shl(d - 1, imm) && word(QK_BOR, d, -1, 0);
         break;
       case G_SEXT: {  // imm = source width, imm2 = result width
         ok = imm >= 1 && imm <= 256 && imm2 <= 256;

@@ -72,11 +72,11 @@ def test_g_handler_data_words_match_their_kinds():
             want = v
         elif kind.startswith("PUSH_CONSTW"):
             want = v + 1
-        elif base in ("MEQK2", "SEQK2", "SULTK2", "SUGTK2"):
+        elif base in ("MEQK2", "SEQK2", "SULTK2", "SUGTK2", "SSLTK2", "SSGTK2"):
             want = 2
-        elif base in ("MEQK8", "SEQK8", "SULTK8", "SUGTK8"):
+        elif base in ("MEQK8", "SEQK8", "SULTK8", "SUGTK8", "SSLTK8", "SSGTK8"):
             want = 8
-        elif base in ("EQK", "ULTK", "UGTK", "ULEK", "UGEK"):
+        elif base in ("EQK", "ULTK", "UGTK", "ULEK", "UGEK", "SLTK", "SGTK"):
             want = kcls[v]
         else:
             want = 0

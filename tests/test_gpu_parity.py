@@ -1040,3 +1040,105 @@ def test_table_lookups_dense_and_csr_match_oracle(evaluator, monkeypatch, dense,
     assert (v == cref.verdicts(tb, mb)).all()
     assert (fh == cref.first_hit(tb, mb)[0]).all()
     assert 0 < v.mean() < 1
+
+
+# ---------------------------------------------------------------- G kernel: calldata words, signed compares with constants
+def _calldata_word_workload(n_tapes, M, seed):
+    """Mythril's symbolic calldata words (laser/ethereum/state/calldata.py: a word is the Concat
+    of 32 ``If(i < size, cd[i], 0)`` bytes, ``<`` signed) and their neighbours: signed compares
+    of a variable with a constant in both operand orders (16-bit, two-word and eight-word
+    constants, negative ones), ite with a zero else, concatenations whose low operand is 8, 31,
+    40, 72 or 100 bits wide.  Sizes include 0, values around the byte offsets, huge positive
+    and negative (bit 255 set) ones."""
+    from mythril_amd.models import ModelBatch
+    from mythril_amd.tape import Tape, TapeBatch
+    rng = np.random.default_rng(seed)
+    NB = 48
+    widths = [256] + [8] * NB + [256] * 4 + [40, 72, 100, 31]
+    rows = []
+    size = np.zeros((8, M), dtype=np.uint32)
+    kind = rng.integers(0, 10, M)
+    size[0] = np.where(kind < 6, rng.integers(0, NB + 8, M), rng.integers(0, 1 << 32, M, dtype=np.uint64)).astype(np.uint32)
+    size[7] = np.where(kind == 8, rng.integers(1 << 31, 1 << 32, M, dtype=np.uint64),
+                       np.where(kind == 9, rng.integers(0, 1 << 31, M), 0)).astype(np.uint32)
+    rows.append(size)
+    rows.append(rng.integers(0, 256, (NB, M)).astype(np.uint32))
+    w256 = rng.integers(0, 1 << 32, (4 * 8, M), dtype=np.uint64).astype(np.uint32)
+    w256[7::8][:, : M // 3] |= np.uint32(1 << 31)          # negative words
+    rows.append(w256)
+    for w in (40, 72, 100, 31):
+        nl = (w + 31) // 32
+        r = rng.integers(0, 1 << 32, (nl, M), dtype=np.uint64).astype(np.uint32)
+        if w % 32:
+            r[nl - 1] &= np.uint32((1 << (w % 32)) - 1)
+        rows.append(r)
+    mb = ModelBatch(widths, np.concatenate(rows))
+    W0, N0 = 1 + NB, 1 + NB + 4
+
+    def kconst():
+        c = int(rng.integers(0, 4))
+        if c == 0:
+            return int(rng.integers(0, 1 << 16))
+        if c == 1:
+            return int(rng.integers(0, 1 << 62))
+        if c == 2:
+            return (1 << 256) - int(rng.integers(1, 1 << 40))     # negative
+        return int.from_bytes(rng.bytes(32), "little")
+
+    tapes = []
+    for t in range(n_tapes):
+        tp = Tape()
+        preds = []
+        for _ in range(int(rng.integers(1, 4))):
+            k = int(rng.integers(0, 5))
+            if k <= 1:   # a calldata word at a random offset
+                off = int(rng.integers(0, NB - 31))
+                sz = tp.var(0, 256)
+                word = tp.concat(*[tp.ite(tp.slt(tp.const(off + i, 256), sz), tp.var(1 + off + i, 8), tp.const(0, 8))
+                                   for i in range(32)])
+                thr = int.from_bytes(rng.bytes(32), "little")
+                preds.append(tp.ult(word, tp.const(thr, 256)) if k == 0 else
+                             tp.not_(tp.eq(tp.extract(255, 224, word), tp.const(0, 32))))
+            elif k == 2:  # signed compares with a constant, either side
+                x = tp.var(int(rng.integers(0, 1)) if rng.random() < 0.3 else W0 + int(rng.integers(0, 4)), 256)
+                c = tp.const(kconst(), 256)
+                preds.append([tp.slt(x, c), tp.slt(c, x), tp.sgt(x, c), tp.sge(c, x)][int(rng.integers(0, 4))])
+            elif k == 3:  # concatenations of wider low operands
+                a = tp.var(W0 + int(rng.integers(0, 4)), 256)
+                lo = N0 + int(rng.integers(0, 4))
+                lw = widths[lo]
+                hi = tp.extract(255 - lw, 0, a)
+                cat = tp.concat(hi, tp.var(lo, lw))
+                preds.append(tp.ult(cat, tp.const(int.from_bytes(rng.bytes(32), "little"), 256)))
+            else:         # ite with a zero else
+                a, b = tp.var(W0 + int(rng.integers(0, 4)), 256), tp.var(W0 + int(rng.integers(0, 4)), 256)
+                c = tp.ult(b, tp.const(int.from_bytes(rng.bytes(32), "little"), 256))
+                preds.append(tp.ult(tp.ite(c, a, tp.const(0, 256)), tp.const(int.from_bytes(rng.bytes(32), "little"), 256)))
+        tapes.append(tp.finish(tp.and_(*preds)))
+    return TapeBatch(tapes), mb
+
+
+@pytest.mark.parametrize("stage_kb", ["0", "26"])
+def test_g_kernel_calldata_words_and_signed_constant_compares(evaluator, monkeypatch, stage_kb):
+    """SLTK / SGTK, their staged-variable forms S{SLT,SGT}K{2,8}, ITEZ and SHLOR on the G
+    kernel (rows read from global memory with MQ_G_STAGE_KB=0, from LDS otherwise): verdicts and
+    first hits identical to the oracle's."""
+    monkeypatch.setenv("MQ_G_STAGE_KB", stage_kb)
+    tb, mb = _calldata_word_workload(160, 3000, seed=int(stage_kb) + 5)
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    v, _ = evaluator.verdicts(ct)
+    n_p, n_g, live = ct.asm_split()
+    assert live and n_g >= 0.9 * tb.n_tapes, (n_p, n_g, ct.split())
+    hist = ct.handler_histogram(1)
+    base = {k.split("_")[0] for k in hist}
+    assert {"SHLOR", "ITEZ"} <= base, hist
+    assert {"SLTK", "SGTK"} & base, hist
+    if stage_kb != "0":
+        assert {"SSLTK2", "SSGTK2", "SSLTK8", "SSGTK8"} & base, hist
+    ref = cref.verdicts(tb, mb)
+    mism = np.argwhere(v != ref)
+    assert len(mism) == 0, f"{len(mism)} mismatches, first {mism[:5]}"
+    assert 0.02 < v.mean() < 0.98
+    fh_ref, _ = cref.first_hit(tb, mb)
+    assert (evaluator.first_hit(ct) == fh_ref).all()
