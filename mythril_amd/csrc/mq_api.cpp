@@ -1404,6 +1404,19 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
         if (!P && d >= 2 && e && e->kind == QK_PUSH_CONSTI && e->imm == 0 && e->d == d && out.size() == ends_at(*e) &&
             c->qsa_index[k][QK_ITEZ][d - 1][0] >= 0) {
           drop_last(1);
+          // "SS{LT,GT}K x; PUSH_MEM x + 1": the load goes first, so it is in flight while the
+          // compare reads LDS (the compare touches slot x, T and B(x) only)
+          if (log.size() >= 2) {
+            const Emit ep = log.back(), ec = log[log.size() - 2];
+            const bool cmp = ec.kind == QK_SSLTK2 || ec.kind == QK_SSGTK2 || ec.kind == QK_SSLTK8 || ec.kind == QK_SSGTK8;
+            if (cmp && ep.kind == QK_PUSH_MEM && ep.nd == 0 && ep.d == d - 1 && ec.d == d - 2 &&
+                ends_at(ec) == ep.pos && out.size() == ends_at(ep)) {
+              std::vector<uint32_t> data(out.begin() + (long)(ec.pos + 1), out.begin() + (long)ends_at(ec));
+              drop_last(2);
+              ok = word(ep.kind, ep.d, ep.v, ep.imm) && emit_k(ec.kind, ec.d, ec.v, ec.imm, data);
+              if (!ok) break;
+            }
+          }
           ok = word(QK_ITEZ, d - 1, -1, 0);
         } else ok = word(QK_ITE, d, -1, 0);
         break;

@@ -131,3 +131,24 @@ def test_g_handlers_write_only_scratch_sgprs():
         if w:
             bad.setdefault(cur, set()).update(w)
     assert not bad, {k: sorted(v) for k, v in list(bad.items())[:10]}
+
+
+def test_g_staging_round_keeps_the_frame_registers():
+    """The G staging round (gen_qsa.py stage_rows: 32 row loads per wave in flight) loads into
+    T and the UF1 work registers only — never the program window, the staging address, the
+    early-exit window or 4 * lane, which are live from the kernel prologue on."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen_qsa", os.path.join(os.path.dirname(INC), "gen_qsa.py"))
+    g = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(g)
+    g.set_layout("g")
+    live = {g.WIN, g.WINA, g.WINI, g.STG, g.NWIN, g.EEA, g.EEV, g.LANE4, "v2", "v3"}
+    body = g.stage_rows("t")
+    dsts = set()
+    for ln in body:
+        m = re.match(r"global_load_dword (v\d+),", ln)
+        if m:
+            dsts.add(m.group(1))
+    assert len(dsts) == 8 * g.STAGE_CHUNKS
+    assert not (dsts & live), sorted(dsts & live)
+    assert all(int(r[1:]) < 80 for r in dsts)
