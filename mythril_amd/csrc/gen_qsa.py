@@ -1427,6 +1427,14 @@ def make_handlers(variant, pfx):
         # ite(c, x, 0) (the translator drops the zero's push): then-value at t, condition B(t - 1)
         for t in range(1, D - 1):
             H(("ITEZ", t), [f"v_cndmask_b32_e64 {S(t - 1, l)}, 0, {S(t, l)}, {B(t - 1)}" for l in range(L)])
+            # ... its then-value a staged row (n limbs) pushed right before: read into the
+            # result slot (its own value is the dead condition's) and masked there
+            for n in range(1, L + 1):
+                H(("ITEZS", t, n - 1), ["s_lshl_b32 s34, s17, 8", f"v_add_u32 v5, s34, {STG}"]
+                  + [f"ds_read_b32 {S(t - 1, l)}, v5 offset:{256 * l}" for l in range(n)] + zero_limbs(t - 1, n)
+                  + ["s_waitcnt lgkmcnt(0)"]
+                  + [f"v_cndmask_b32_e64 {S(t - 1, l)}, 0, {S(t - 1, l)}, {B(t - 1)}" for l in range(n)],
+                  reads_stack=False)
         # concat: S[d-1] = S[d-1] << (32q + s) | S[d] (s != 0, imm = 32 - s; SHLI + BOR in one):
         # the low operand is narrower than 32q + s bits, so only limbs 0..q take it
         for d in range(1, D):

@@ -1417,6 +1417,16 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
               if (!ok) break;
             }
           }
+          // a staged then-value pushed right before: ITEZS reads the row itself
+          const Emit ev = log.empty() ? Emit{} : log.back();
+          if (!log.empty() && ev.kind == QK_PUSH_MEMS && ev.nd == 0 && ev.d == d - 1 && ev.v >= 0 && out.size() == ends_at(ev) &&
+              c->qsa_index[k][QK_ITEZS][d - 1][ev.v + 1] >= 0) {
+            const int nsel = ev.v;
+            const uint32_t row = ev.imm;
+            drop_last(1);
+            ok = word(QK_ITEZS, d - 1, nsel, row);
+            break;
+          }
           ok = word(QK_ITEZ, d - 1, -1, 0);
         } else ok = word(QK_ITE, d, -1, 0);
         break;
