@@ -327,37 +327,51 @@ def calls_avoided_leg(ev, n_forks: int = 256, n_models: int = 100, seed: int = 2
                 **c, "states_alive": int(sum(alive)), "solver_calls_avoided": avoided,
                 "fraction_avoided": avoided / max(c["get_model_calls"], 1), "ms_per_state": dt * 1e3 / len(cs),
                 "candidate_budget": budget if cand else 0, "solver_stand_in_calls": solver.calls,
-                "models_inserted_by_solver": solver.calls}
+                "models_inserted_by_solver": solver.sat_calls}
     finally:
         sp.model_cache, sp.args.quick_sat_candidates, sp.args.quick_sat_candidate_budget = saved
         sp.set_solver_backend(None)
     return out
 
 
-def keccak_leg(ev, sizes=(1, 64, 4096, 262144), msg_bytes: int = 64):
-    """Concrete keccak service (mythril_amd.keccak_service): GPU mq_keccak256 per-call latency by
-    batch size vs the per-call CPU keccak the reference uses (eth_hash from Python, here the
-    oracle's C keccak called from Python per message: oracle/cref.c, one core)."""
+def keccak_leg(ev, sizes=(1, 4, 16, 64, 256, 4096, 262144), msg_bytes: int = 64):
+    """Concrete keccak service (mythril_amd.keccak_service): mq_keccak256 per-call latency by
+    batch size — as shipped (batches of <= MQ_OPT_KECCAK_HOST_BLOCKS blocks hashed by the library's
+    host keccak, larger ones by the GPU kernel) and with every batch forced onto the GPU — vs the
+    per-call CPU keccak the reference uses (eth_hash from Python, here the oracle's C keccak called
+    from Python per message: oracle/cref.c, one core)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import cref  # oracle: CPU comparison only
     rng = np.random.default_rng(5)
     out = []
-    for n in sizes:
-        msgs = rng.integers(0, 256, (n, msg_bytes), dtype=np.uint8)
+    default_blocks = 128
+
+    def per_call(msgs, reps):
         ev.keccak256_array(msgs)   # the first call at a size grows the device buffers
-        reps = max(3, min(50, 20000 // n))
         t0 = time.perf_counter()
         for _ in range(reps):
             dg = ev.keccak256_array(msgs)
-        gpu = (time.perf_counter() - t0) / reps
+        return (time.perf_counter() - t0) / reps, dg
+
+    for n in sizes:
+        msgs = rng.integers(0, 256, (n, msg_bytes), dtype=np.uint8)
+        reps = max(3, min(200, 20000 // n))
+        service, dg = per_call(msgs, reps)
+        ev.set_option(ev.OPT_KECCAK_HOST_BLOCKS, 0)
+        try:
+            gpu, dg2 = per_call(msgs, reps)
+        finally:
+            ev.set_option(ev.OPT_KECCAK_HOST_BLOCKS, default_blocks)
         k = min(n, 20000)
         t0 = time.perf_counter()
         ref = [cref.keccak256(bytes(m)) for m in msgs[:k]]
         cpu = (time.perf_counter() - t0) / k * n
-        ok = all(bytes(dg[i]) == ref[i] for i in range(min(k, 256)))
-        out.append({"messages": n, "bytes_each": msg_bytes, "gpu_ms_per_call": gpu * 1e3,
-                    "gpu_us_per_hash": gpu / n * 1e6, "cpu_us_per_hash_1core": cpu / n * 1e6,
-                    "gpu_over_cpu": cpu / gpu, "digests_match": bool(ok)})
+        ok = all(bytes(dg[i]) == ref[i] and bytes(dg2[i]) == ref[i] for i in range(min(k, 256)))
+        out.append({"messages": n, "bytes_each": msg_bytes,
+                    "path": "host" if n * (msg_bytes // 136 + 1) <= default_blocks else "gpu",
+                    "service_ms_per_call": service * 1e3, "gpu_kernel_path_ms_per_call": gpu * 1e3,
+                    "service_us_per_hash": service / n * 1e6, "cpu_us_per_hash_1core": cpu / n * 1e6,
+                    "service_over_cpu": cpu / service, "gpu_path_over_cpu": cpu / gpu, "digests_match": bool(ok)})
     return out
 
 

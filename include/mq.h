@@ -284,9 +284,13 @@ int mq_eval_verdicts(mq_ctx* ctx, const mq_tape_batch* batch, uint8_t* bits_out,
 int mq_eval_tapes_verdicts(mq_ctx* ctx, mq_tapes* tapes, uint8_t* bits_out, int32_t* first_hit_out);
 
 /* Concrete keccak256 (Ethereum padding 0x01) of n messages on the GPU (keccak-f[1600] kernel);
-   message i = data[offsets[i] .. offsets[i+1]), digests_out = 32*n bytes.
+   message i = data[offsets[i] .. offsets[i+1]), digests_out = 32*n bytes.  A batch of at most
+   MQ_OPT_KECCAK_HOST_BLOCKS 136-byte blocks in total is hashed on the host instead (one launch
+   plus two copies cost more than that); 0 sends every batch to the GPU.
    Replaces eth_hash in sha3 (support_utils.py:92-100) / find_concrete_keccak (kfm.py:56-69). */
 int mq_keccak256(mq_ctx* ctx, const uint8_t* data, const int64_t* offsets, int32_t n, uint8_t* digests_out);
+/* The same on the host only (no context, no GPU): what mq_keccak256 runs below its threshold. */
+int mq_keccak256_host(const uint8_t* data, const int64_t* offsets, int32_t n, uint8_t* digests_out);
 
 /* Context options.  MQ_OPT_USE_ASM (default 1): run eligible 256-bit tapes on the gfx950
    assembly interpreter, the rest on the HIP C++ interpreter (0: HIP C++ for all — the A/B and
@@ -301,7 +305,9 @@ int mq_keccak256(mq_ctx* ctx, const uint8_t* data, const int64_t* offsets, int32
    tiles) runs the general assembly kernel with one tape per wave instead of several tapes per
    wave: a few tapes over a few models are latency-bound (the drop-in path at the reference's
    shape sets it).  Such a launch with more than 131 072 tape nodes (MQ_LATENCY_ASM_NODES)
-   skips the assembly translation (host time) and runs on the HIP C++ kernel. */
+   skips the assembly translation (host time) and runs on the HIP C++ kernel.
+   MQ_OPT_KECCAK_HOST_BLOCKS (default 128): mq_keccak256 batches of at most this many blocks are
+   hashed on the host (0: always on the GPU). */
 enum mq_option {
   MQ_OPT_USE_ASM = 1,
   MQ_OPT_EARLY_EXIT = 2,
@@ -309,7 +315,8 @@ enum mq_option {
   MQ_OPT_TIME_KERNELS = 4,
   MQ_OPT_USE_RCCL = 5,
   MQ_OPT_RCCL_ACTIVE = 6,
-  MQ_OPT_LATENCY_WAVES = 7
+  MQ_OPT_LATENCY_WAVES = 7,
+  MQ_OPT_KECCAK_HOST_BLOCKS = 8
 };
 int mq_ctx_set_option(mq_ctx* ctx, int option, int value);
 

@@ -17,8 +17,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libmq.so")
 OBJDIR = os.path.join(HERE, "csrc", "_obj")
-SOURCES = ["mq_api.cpp", "tape_compiler.cpp", "qs_kernels.hip", "keccak.hip", "qsa.hip"]
-HEADERS = ["gprog.h", "bvops.h", "qs_launch.h", "tape_compiler.h", "qsa_table.h", "qsa_gen.inc"]
+SOURCES = ["mq_api.cpp", "host_keccak.cpp", "tape_compiler.cpp", "qs_kernels.hip", "keccak.hip", "qsa.hip"]
+HEADERS = ["host_keccak.h", "gprog.h", "bvops.h", "qs_launch.h", "tape_compiler.h", "qsa_table.h", "qsa_gen.inc"]
 ARCH = os.environ.get("MQ_OFFLOAD_ARCH", "gfx950")
 
 
@@ -53,9 +53,8 @@ def _generated_current() -> bool:
     """qsa_gen.inc / qsa_table.h (generated, not tracked) carry the sha256 of gen_qsa.py."""
     import hashlib
     with open(os.path.join(CSRC, "gen_qsa.py"), "rb") as f:
-        # (the diagnostic profile build, QSA_PROF=1, and QSA_PROG_LDS=1 stamp differently: switching regenerates)
-        stamp = hashlib.sha256(f.read() + (b"PROF" if os.environ.get("QSA_PROF") == "1" else b"")
-                               + (b"LDS" if os.environ.get("QSA_PROG_LDS") == "1" else b"")).hexdigest()[:16]
+        # (the diagnostic profile build, QSA_PROF=1, stamps differently: switching regenerates)
+        stamp = hashlib.sha256(f.read() + (b"PROF" if os.environ.get("QSA_PROF") == "1" else b"")).hexdigest()[:16]
     for name in ("qsa_gen.inc", "qsa_table.h"):
         path = os.path.join(CSRC, name)
         if not os.path.exists(path):

@@ -198,29 +198,11 @@ def load_window(first, pfx=None):
     after it into NWIN (mq_api.cpp qsa_window_layout: blocks are aligned and contiguous).
     first (tape start, s[36:37] = the program's address): the block is NWIN when the previous
     window's successor is this program (consecutive descriptors), else it is loaded.  Otherwise
-    (REFILL): the block is NWIN, 256 bytes on.
-    Programs in LDS (QArgs.prog_lds bit 0, s57 = its LDS offset | 1; the workgroup's programs
-    were copied there by the prologue, stage_programs, from word s56 on): the block is one LDS
-    read, s14 = its LDS address — no global round trip at a tape start, where a short tape (C4)
-    could not cover the prefetch's latency."""
+    (REFILL): the block is NWIN, 256 bytes on."""
     k = _WIN_LABELS[0]
     _WIN_LABELS[0] += 1
-    glob, dec = f"{pfx}_wg{k}", f"{pfx}_wd{k}"
     lane4 = LANE4 or "v5"
     out = [] if LANE4 else ["v_mbcnt_lo_u32_b32 v5, -1, 0", "v_mbcnt_hi_u32_b32 v5, -1, v5", "v_lshlrev_b32 v5, 2, v5"]
-    if PROG_LDS:
-        out += ["s_bitcmp1_b32 s57, 0",
-                f"s_cbranch_scc0 {glob}"]
-        if first:
-            out += ["s_sub_u32 s34, s80, s56", "s_lshl_b32 s34, s34, 2", "s_add_u32 s14, s57, s34",
-                    "s_sub_u32 s14, s14, 1"] + (["s_mov_b32 s39, 1"] if PROF else [])
-        else:
-            out += ["s_add_u32 s14, s14, 256"]
-        out += [f"v_add_u32 v5, s14, {lane4}",
-                f"ds_read_b32 {WIN}, v5",
-                "s_waitcnt lgkmcnt(0)",
-                f"s_branch {dec}",
-                f"{glob}:"]
     if first:
         # the prefetched window was issued before the previous tape's stores (s59 of them, column
         # rows / a verdict byte / a hit's atomic): wait for it, not for them (vector memory
@@ -247,7 +229,6 @@ def load_window(first, pfx=None):
         out += ["s_add_u32 s14, s14, 256", "s_addc_u32 s15, s15, 0", "s_waitcnt vmcnt(0)"]
     out += [f"v_mov_b32 {WIN}, {NWIN}",
             f"global_load_dword {NWIN}, {lane4}, s[14:15] offset:256",
-            f"{dec}:",
             "s_mov_b32 s16, 0",
             f"v_and_b32 v5, 0xffff, {WIN}",
             f"v_lshl_add_u32 {WINA}, v5, {3 if PROF else 2}, s12",
@@ -1639,96 +1620,13 @@ def stage_rows(pfx):
         out += [f"ds_write_b32 v5, {regs[c][j]} offset:{8192 * c + 256 * j}" for j in range(8)]
     out += [f"{pfx}_stage_next:", f"s_add_u32 s61, s61, {32 * STAGE_CHUNKS}", f"s_branch {pfx}_stage_loop",
             f"{pfx}_stage_done:"]
-    if PROG_LDS:
-        out += stage_programs(pfx)
     out += ["s_waitcnt lgkmcnt(0)",
             "s_barrier"]
     return out
 
 
-DESC_LDS = 2048   # G: LDS bytes of the workgroup's descriptors (<= 64 of 32 B), just below its programs
-# G programs and descriptors staged in LDS per workgroup (QArgs.prog_lds; QSA_PROG_LDS=1 at
-# generation).  Off by default: it removes the tape start's memory waits (FRAME 5 200 -> 430,
-# F_HDR 1 200 -> 510 cycles per dispatch on C4, profiles/r04z3) but G is issue-bound there, and
-# the extra VALU of the LDS header read made C4 3.43 -> 3.53 ms (profiles/r04z6)
-PROG_LDS = os.environ.get("QSA_PROG_LDS") == "1"
 # G (product build): 4 * lane, kept in v39 (the profile build's table register)
 LANE4 = None
-
-
-def stage_descs(pfx):
-    """stage_programs, first: the workgroup's descriptors [s58, s59) (at most 64) into LDS at
-    (s57 - 1) - DESC_LDS, descriptor i of the run at 32 * i; wave w copies words 64w .. and
-    256 + 64w .. (lanes past the run's end masked off: no read past the descriptor array).
-    Wants s68 = wave, v6 = 4 * lane."""
-    out = ["s_sub_u32 s64, s59, s58", "s_lshl_b32 s64, s64, 3",                      # words
-           "s_lshl_b32 s66, s58, 5", "s_add_u32 s66, s22, s66", "s_addc_u32 s67, s23, 0",
-           f"s_sub_u32 s69, s57, {DESC_LDS + 1}",
-           "v_lshrrev_b32 v7, 2, v6"]
-    for j in range(2):
-        out += [f"s_lshl_b32 s70, s68, 6", f"s_add_u32 s70, s70, {256 * j}",
-                "v_add_u32 v5, s70, v7",
-                "v_cmp_gt_u32_e64 s[60:61], s64, v5",
-                "s_nop 3",
-                "s_and_saveexec_b64 s[36:37], s[60:61]",
-                "v_lshlrev_b32 v5, 2, v5",
-                f"global_load_dword {T(j)}, v5, s[66:67]",
-                "s_waitcnt vmcnt(0)",
-                "v_add_u32 v5, s69, v5",
-                f"ds_write_b32 v5, {T(j)}",
-                "s_mov_b64 exec, s[36:37]"]
-    return out
-
-
-def stage_programs(pfx):
-    """G, QArgs.prog_lds on (s57 = its LDS offset | 1, else 0): copy the programs of the
-    workgroup's descriptors [s58, s59) — one contiguous run of 64-word blocks, from word s56 on
-    (mq_api.cpp: descriptors in order, programs contiguous) — into LDS, block b at offset
-    256 * b; wave w copies blocks w, w + 4, ..., 8 loads in flight.  The host turns it on only
-    when the largest workgroup's run fits beside the temps and staged rows."""
-    out = ["s_load_dword s57, s[10:11], 0x1a4",
-           "s_waitcnt lgkmcnt(0)",
-           "s_bitcmp1_b32 s57, 0",
-           f"s_cbranch_scc0 {pfx}_pst_done",
-           "s_cmp_ge_u32 s58, s59",
-           f"s_cbranch_scc1 {pfx}_pst_done",
-           "v_lshrrev_b32 v4, 6, v3",
-           "v_mbcnt_lo_u32_b32 v6, -1, 0", "v_mbcnt_hi_u32_b32 v6, -1, v6", "v_lshlrev_b32 v6, 2, v6",
-           "s_nop 1",
-           "v_readfirstlane_b32 s68, v4",                      # wave
-           "s_nop 3"]                                          # VALU SGPR write -> SALU read
-    out += stage_descs(pfx)
-    out += ["s_lshl_b32 s34, s58, 5", "s_add_u32 s34, s22, s34", "s_addc_u32 s35, s23, 0",
-            "s_load_dword s56, s[34:35], 0x0",                 # prog_off of the first descriptor
-            "s_lshl_b32 s36, s59, 5", "s_sub_u32 s36, s36, 32", "s_add_u32 s36, s22, s36", "s_addc_u32 s37, s23, 0",
-            "s_load_dwordx2 s[64:65], s[36:37], 0x0",          # prog_off, prog_len of the last
-            "s_waitcnt lgkmcnt(0)",
-            "s_add_u32 s64, s64, s65",
-            "s_sub_u32 s64, s64, s56",
-            "s_add_u32 s64, s64, 63",
-            "s_lshr_b32 s64, s64, 6",                          # blocks
-            "s_lshl_b32 s66, s56, 2", "s_add_u32 s66, s46, s66", "s_addc_u32 s67, s47, 0",   # first block
-            "s_sub_u32 s69, s57, 1",                            # LDS offset
-            "s_mov_b32 s65, s68"]                               # this wave's next block
-    out += [f"{pfx}_pst_loop:",
-           "s_cmp_ge_u32 s65, s64",
-           f"s_cbranch_scc1 {pfx}_pst_done"]
-    for j in range(8):
-        out += [f"s_add_u32 s70, s65, {4 * j}", "s_cmp_ge_u32 s70, s64", f"s_cbranch_scc1 {pfx}_pst_l{j}",
-                "s_lshl_b32 s70, s70, 8", "s_add_u32 s36, s66, s70", "s_addc_u32 s37, s67, 0",
-                f"global_load_dword {T(j)}, v6, s[36:37]"]
-    out += [f"{pfx}_pst_l8:"] + [f"{pfx}_pst_l{j}:" for j in range(8)]
-    out += ["s_waitcnt vmcnt(0)"]
-    for j in range(8):
-        out += [f"s_add_u32 s70, s65, {4 * j}", "s_cmp_ge_u32 s70, s64", f"s_cbranch_scc1 {pfx}_pst_w",
-                "s_lshl_b32 s70, s70, 8", "s_add_u32 s70, s69, s70",
-                "v_add_u32 v7, s70, v6",
-                f"ds_write_b32 v7, {T(j)}"]
-    out += [f"{pfx}_pst_w:",
-            "s_add_u32 s65, s65, 32",
-            f"s_branch {pfx}_pst_loop",
-            f"{pfx}_pst_done:"]
-    return out
 
 
 def ee_window():
@@ -1854,14 +1752,6 @@ def frame(variant, pfx, handlers, subs):
         "s_add_u32 s25, s24, s83",
         "s_min_u32 s25, s25, s82",
     ] + ([
-        # G: the workgroup's descriptors [s58, s59) (its 4 waves' tape groups), for stage_programs
-        "s_andn2_b32 s58, s97, 3",
-        "s_mul_i32 s58, s58, s83",
-        "s_or_b32 s59, s97, 3",
-        "s_add_u32 s59, s59, 1",
-        "s_mul_i32 s59, s59, s83",
-        "s_min_u32 s59, s59, s82",
-    ] if G else []) + ([
         # G: s[96:97] = this tile's packed Bool masks, bool_masks + 8 * tile * n_bool_masks
         "s_load_dwordx2 s[64:65], s[10:11], 0x198",
         "s_load_dword s66, s[10:11], 0x1a0",
@@ -1923,29 +1813,13 @@ def frame(variant, pfx, handlers, subs):
         f"{pfx}_tape_loop:",
         "s_cmp_ge_u32 s24, s25",
         f"s_cbranch_scc1 {pfx}_tapes_done",
-    ] + ([
-        # programs in LDS: the descriptors too (stage_descs), 8 words read into s[80:87]
-        "s_bitcmp1_b32 s57, 0",
-        f"s_cbranch_scc0 {pfx}_hdr_mem",
-        "s_sub_u32 s34, s24, s58",
-        "s_lshl_b32 s34, s34, 5",
-        "s_add_u32 s34, s34, s57",
-        f"s_sub_u32 s34, s34, {DESC_LDS + 1}",
-        "v_mbcnt_lo_u32_b32 v4, -1, 0", "v_mbcnt_hi_u32_b32 v4, -1, v4", "v_lshlrev_b32 v4, 2, v4",
-        "v_add_u32 v4, s34, v4",
-        "ds_read_b32 v4, v4",
-        "s_waitcnt lgkmcnt(0)",
-    ] + [f"v_readlane_b32 s{80 + i}, v4, {i}" for i in range(8)] + [
-        "s_nop 3",                          # VALU SGPR write -> SALU read
-        f"s_branch {pfx}_hdr_done",
-        f"{pfx}_hdr_mem:",
-    ] if G and PROG_LDS else []) + [
+    ] + [
         "s_lshl_b32 s34, s24, 5",
         "s_add_u32 s34, s22, s34",
         "s_addc_u32 s35, s23, 0",
         "s_load_dwordx8 s[80:87], s[34:35], 0x0",
         "s_waitcnt lgkmcnt(0)",
-    ] + ([f"{pfx}_hdr_done:"] if G and PROG_LDS else []) + (prof_point("F_HDR") if G else []) + ([] if G else [
+    ] + (prof_point("F_HDR") if G else []) + ([] if G else [
         # P: &best[tape] (G computes it on a hit only; handlers never touch s72-s73, s80-s87)
         "s_lshl_b32 s34, s82, 2",
         "s_add_u32 s72, s26, s34",
@@ -2143,7 +2017,7 @@ def source_stamp() -> str:
     any change of the generator, independent of file times)."""
     import hashlib
     with open(os.path.abspath(__file__), "rb") as f:
-        return hashlib.sha256(f.read() + (b"PROF" if PROF else b"") + (b"LDS" if PROG_LDS else b"")).hexdigest()[:16]
+        return hashlib.sha256(f.read() + (b"PROF" if PROF else b"")).hexdigest()[:16]
 
 
 def main():
@@ -2215,7 +2089,6 @@ def main():
         # diagnostic profile build (QSA_PROF=1): per-wave LDS table bytes; entry i = (cycles,
         # count) of kind i, entry QK_COUNT = the tape frame
         f.write(f"constexpr int kQsaProfBytes = {prof_bytes};\n")
-        f.write(f"constexpr int kQsaProgLds = {1 if PROG_LDS else 0};   // G stages programs in LDS (QSA_PROG_LDS=1)\n")
         f.write(f"constexpr int kQsaProfExtra = {len(PROF_EXTRA)};\n")
         f.write("static const char* const kQsaProfExtraNames[] = {" + ", ".join(f'"{n}"' for n in PROF_EXTRA) + "};\n")
         f.write(f"constexpr int kQsaHandlerShiftG = {3 if PROF else 2};\n")

@@ -178,12 +178,13 @@ __global__ __launch_bounds__(256) void keccak_column_kernel(const KcCol* __restr
     vars[(int64_t)(col.target_row + i) * M + m] = h[i];
   }
   // the column's predicate columns from the digest in registers: the tile's lane mask (lane 0 of
-  // the wave = one 64-model tile stores it; lanes past M are inactive, so their bits are 0) and,
-  // when a HIP C++ kernel of the launch reads rows, the 0/1 row
+  // the wave = one 64-model tile stores it; lanes past M are inactive, so their bits are 0) and
+  // the 0/1 row when a HIP C++ kernel of the launch reads rows or the column has no mask index
+  // (past the mask cap: readers then read the row, as G's column store does)
   for (uint32_t j = 0; j < col.n_pred; j++) {
     const KcPred p = preds[col.pred_off + j];
     const bool bit = kc_pred(p, h);
-    if (bool_rows) vars[(int64_t)p.row * M + m] = bit ? 1u : 0u;
+    if (bool_rows || p.mask < 0) vars[(int64_t)p.row * M + m] = bit ? 1u : 0u;
     if (p.mask >= 0) {
       const unsigned long long b = __ballot(bit);
       if ((threadIdx.x & 63) == 0) bool_masks[(m >> 6) * (int64_t)n_bool_masks + p.mask] = b;

@@ -28,6 +28,7 @@
 #include "qs_launch.h"
 #include "qsa_table.h"
 #include "tape_compiler.h"
+#include "host_keccak.h"
 
 using namespace mq;
 
@@ -71,6 +72,31 @@ class DevPool {
   // device may still be read there, so the next release synchronises the device first (what
   // hipFree would have done)
   void mark_foreign(int dev) { foreign_[dev & 15].store(true); }
+  // the library's own streams per device (each context's), so a growing buffer drains those
+  // instead of the whole device
+  void register_stream(int dev, hipStream_t s) {
+    std::lock_guard<std::mutex> g(mu_);
+    streams_[dev & 15].push_back(s);
+  }
+  void unregister_stream(int dev, hipStream_t s) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto& v = streams_[dev & 15];
+    v.erase(std::remove(v.begin(), v.end(), s), v.end());
+  }
+  // before a block is handed out again: the library's streams on dev are drained, and the device
+  // when a caller's stream may hold a reader (mark_foreign)
+  void drain(int dev) {
+    if (foreign_[dev & 15].load()) {
+      (void)hipDeviceSynchronize();
+      return;
+    }
+    std::vector<hipStream_t> v;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      v = streams_[dev & 15];
+    }
+    for (hipStream_t s : v) (void)hipStreamSynchronize(s);
+  }
   void put(int dev, void* p, size_t cls) {
     if (foreign_[dev & 15].exchange(false)) {
       int cur = 0;
@@ -105,6 +131,7 @@ class DevPool {
   std::multimap<size_t, void*> free_[16];
   size_t cached_[16] = {};
   std::atomic<bool> foreign_[16] = {};
+  std::vector<hipStream_t> streams_[16];
 };
 
 struct DevBuf {
@@ -137,10 +164,10 @@ struct DevBuf {
   }
   hipError_t ensure(size_t n) {
     if (n <= bytes && p) return hipSuccess;
-    // growing: a kernel queued on some stream may still read the old block, and the pool hands
-    // it out again at once (possibly to another stream) -- drain the device first (growth is rare:
+    // growing: a kernel queued on one of the library's streams (or a caller's) may still read the
+    // old block, and the pool hands it out again at once -- drain those first (growth is rare:
     // size classes double)
-    if (p) (void)hipDeviceSynchronize();
+    if (p) DevPool::get().drain(dev);
     release();
     int d = 0;
     hipError_t e = hipGetDevice(&d);
@@ -197,11 +224,18 @@ static int gen_kind(const CompiledTape& x) {
 }
 static constexpr int64_t kColAsmMinNodes = 1;    // hoisted columns on qsg_kernel from this size
 
+// Guards every context's live_tapes and every mq_tapes::ctx: a batch freed on one thread while
+// its context is destroyed on another must not read the context after it is deleted.
+static std::mutex g_live_mu;
+
+// mq_keccak256 hashes a batch of at most this many 136-byte blocks on the host (measured crossover
+// against one launch + two copies: profiles/r05*/bench_c2.json keccak_service)
+static constexpr int64_t kKeccakHostBlocks = 128;
+
 struct mq_ctx {
   // compiled batches made on this context, detached (ctx = nullptr) when it is destroyed first:
   // mq_tapes_free after mq_ctx_destroy must not touch the freed context (a Python finalizer may
-  // run in either order)
-  std::mutex tapes_mu;
+  // run in either order); both under g_live_mu
   std::unordered_set<mq_tapes*> live_tapes;
   // per model function: the most table entries any model of the WHOLE batch holds (all shards):
   // a wide-key lookup (MQ_OP_UF_WIDE) tracks at most 64 entries per model
@@ -249,6 +283,7 @@ struct mq_ctx {
   int use_asm = 1;      // MQ_OPT_USE_ASM
   int early_exit = 1;   // MQ_OPT_EARLY_EXIT
   int64_t latency_waves = 0;   // MQ_OPT_LATENCY_WAVES
+  int64_t keccak_host_blocks = kKeccakHostBlocks;   // MQ_OPT_KECCAK_HOST_BLOCKS
   // MQ_OPT_TIME_KERNELS: one HIP event pair bracketing the evaluation kernels of each launch
   int time_kernels = 0;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> kev;
@@ -342,7 +377,6 @@ struct mq_tapes {
   bool cq_live = false;
   DevBuf cqdescs, cqprog, cqconsts, cqargs;
   std::vector<QArgs> cqargs_host;   // what cqargs holds on the device, per level
-  std::vector<GDesc> qdescs_h, cqdescs_h;   // host copies (program runs for QArgs.prog_lds)
   std::vector<uint32_t> cq_stage_rows;                   // staged rows of every level, level by level
   std::vector<uint32_t> cq_lvl_stage_off, cq_lvl_stage_n;  // per level: its rows in cq_stage_rows
   std::vector<int> cq_lvl_temps;                         // per level: LDS temp slots
@@ -375,10 +409,8 @@ struct mq_tapes {
   std::vector<mq_tapes*> peers;
   ~mq_tapes() {
     for (mq_tapes* p : peers) delete p;
-    if (ctx) {
-      std::lock_guard<std::mutex> g(ctx->tapes_mu);
-      ctx->live_tapes.erase(this);
-    }
+    std::lock_guard<std::mutex> g(g_live_mu);
+    if (ctx) ctx->live_tapes.erase(this);
   }
 };
 
@@ -403,6 +435,10 @@ static void sum_counter_slots(const std::vector<unsigned long long>& raw, unsign
 // call_mu_), and in a forked child (the pool's workers do not exist there)
 static thread_local bool tl_in_pool = false;
 static std::atomic<bool> g_forked_child{false};
+struct InPool {   // tl_in_pool for a job's extent, cleared when the job throws too
+  InPool() { tl_in_pool = true; }
+  ~InPool() { tl_in_pool = false; }
+};
 
 class HostPool {
  public:
@@ -425,9 +461,10 @@ class HostPool {
       epoch_++;
     }
     cv_.notify_all();
-    tl_in_pool = true;
-    job(0);
-    tl_in_pool = false;
+    {
+      InPool in;
+      job(0);
+    }
     std::unique_lock<std::mutex> g(mu_);
     done_cv_.wait(g, [&] { return done_ == want_; });
     job_ = nullptr;
@@ -456,9 +493,10 @@ class HostPool {
         if (tid > want_) continue;   // not needed this time
         job = job_;
       }
-      tl_in_pool = true;
-      (*job)(tid);
-      tl_in_pool = false;
+      {
+        InPool in;
+        (*job)(tid);
+      }
       std::lock_guard<std::mutex> g(mu_);
       if (++done_ == want_) done_cv_.notify_one();
     }
@@ -646,6 +684,7 @@ static int create_one(int dev, mq_ctx** out) {
     mq_ctx_destroy(c);
     return MQ_ERR_HIP;
   }
+  DevPool::get().register_stream(dev, c->stream);
   if (c->counters.ensure(kCounterBytes) != hipSuccess) {
     mq_ctx_destroy(c);
     return MQ_ERR_NOMEM;
@@ -727,12 +766,13 @@ void mq_ctx_destroy(mq_ctx* c) {
     (void)hipEventDestroy(e.second);
   }
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  DevPool::get().unregister_stream(c->device, c->stream);
   {
-    std::lock_guard<std::mutex> g(c->tapes_mu);
+    std::lock_guard<std::mutex> g(g_live_mu);
     for (mq_tapes* t : c->live_tapes) t->ctx = nullptr;   // their launches were synchronised above
     c->live_tapes.clear();
+    delete c;
   }
-  delete c;
 }
 
 // Upload a model batch to ONE device (n_models may be 0: an empty shard evaluates to "no hit").
@@ -839,11 +879,14 @@ static int upload_one(mq_ctx* c, const mq_model_batch* mb) {
       if (v < mb->n_vars && mb->var_width[v] <= 256 && (uint32_t)l < vnl[v]) row = voff[v] + l;
       c->qsa_var_row[8 * v + l] = row;
     }
-  // Bool variables as lane masks (at most 65535 of them; the others are read as rows)
+  // Bool variables as lane masks (at most 65535 of them; the others are read as rows;
+  // MQ_BMASK_CAP lowers the cap so tests reach the row path)
   {
     std::vector<uint32_t> brows;
     c->bmask_of_var.assign(mb->n_vars, -1);
-    for (int v = 0; v < mb->n_vars && brows.size() < 65535; v++)
+    size_t cap = 65535;
+    if (const char* e = std::getenv("MQ_BMASK_CAP")) cap = std::min<size_t>(cap, (size_t)std::atol(e));
+    for (int v = 0; v < mb->n_vars && brows.size() < cap; v++)
       if (mb->var_width[v] == 0) {
         c->bmask_of_var[v] = (int32_t)brows.size();
         brows.push_back(voff[v]);
@@ -1683,7 +1726,7 @@ static int tapes_upload_one(mq_ctx* c, int32_t n_tapes, const std::vector<Compil
   auto T = std::make_unique<mq_tapes>();
   T->ctx = c;
   {
-    std::lock_guard<std::mutex> g(c->tapes_mu);
+    std::lock_guard<std::mutex> g(g_live_mu);
     c->live_tapes.insert(T.get());
   }
   T->n_tapes = n_tapes;
@@ -2403,35 +2446,6 @@ static std::vector<int64_t> count_pushes(const mq_ctx* c, const std::vector<Comp
 static int64_t g_tapes_per_group(int64_t n, int64_t M);
 static int64_t cq_tapes_per_group(int64_t n, int64_t M);
 
-// QArgs.prog_lds of a G launch over descriptors d[0, n) with tpg tapes per wave: the largest run
-// of program blocks one workgroup (4 tape groups) reads, copied into LDS by its prologue
-// (gen_qsa.py stage_programs) when it fits beside the temps, staged rows and profile tables in
-// the G workgroup budget (MQ_G_STAGE_KB, 26 KB: 6 workgroups per CU).  Sets q.prog_lds and
-// returns the LDS bytes it adds (0: programs stay in memory; MQ_NO_PROG_LDS=1 forces that).
-static size_t plan_prog_lds(QArgs& q, const GDesc* d, int64_t n, int64_t tpg, size_t lds_other, size_t lds_prof) {
-  static const bool off = std::getenv("MQ_NO_PROG_LDS") != nullptr;
-  q.prog_lds = 0;
-  // (the workgroup's descriptors go to LDS too: kDescLds bytes, at most 64 of them)
-  constexpr size_t kDescLds = 2048;
-  if (!kQsaProgLds || off || n <= 0 || 4 * tpg * (int64_t)sizeof(GDesc) > (int64_t)kDescLds) return 0;
-  int64_t kb = 26;
-  if (const char* e = std::getenv("MQ_G_STAGE_KB")) kb = std::atol(e);
-  uint64_t run = 0;
-  for (int64_t f = 0; f < n; f += 4 * tpg) {
-    const int64_t l = std::min<int64_t>(n, f + 4 * tpg) - 1;
-    run = std::max<uint64_t>(run, (uint64_t)d[l].prog_off + d[l].prog_len - d[f].prog_off);
-  }
-  const size_t bytes = kDescLds + (size_t)((run + 63) / 64) * 256;
-  // (the profile build's per-wave tables, lds_prof of lds_other, are not charged to the budget)
-  const bool fits = lds_other - lds_prof + bytes <= (size_t)kb * 1024;
-  static const bool dbg = std::getenv("MQ_PROG_LDS_DEBUG") != nullptr;
-  if (dbg)
-    std::fprintf(stderr, "prog_lds: %lld descs, tpg %lld, run %llu words (%zu B) + %zu B other: %s\n", (long long)n,
-                 (long long)tpg, (unsigned long long)run, bytes, lds_other - lds_prof, fits ? "LDS" : "memory");
-  if (!fits) return 0;
-  q.prog_lds = (uint32_t)(lds_other + kDescLds) | 1u;
-  return bytes;
-}
 
 static void plan_stage(const mq_ctx* c, const std::vector<int64_t>& pushes, const std::vector<int>* gpre, int temps,
                        double wg_share, std::vector<int>& gstage, std::vector<uint32_t>& rows) {
@@ -2586,7 +2600,6 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
     T->q_temps[k] = temps[k];
   }
   if (descs.empty()) descs.push_back(GDesc{});
-  T->qdescs_h = descs;
   HIPCHK(T->qdescs.upload(descs.data(), descs.size(), c->stream));
   HIPCHK(T->qprog.upload(prog.data(), prog.size(), c->stream));
   if (T->stage_rows.empty()) HIPCHK(T->stage_dev.ensure(sizeof(uint32_t)));
@@ -2653,7 +2666,6 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
   const uint32_t endw = hword(1, c->qsa_off[1][c->qsa_index[1][QK_END][0][0]]);
   prog.insert(prog.end(), 130, endw);   // the window + next-window prefetch read up to 127 words past the last END
   consts.resize(consts.size() + 16, 0);
-  T->cqdescs_h = descs;
   HIPCHK(T->cqdescs.upload(descs.data(), descs.size(), c->stream));
   HIPCHK(T->cqprog.upload(prog.data(), prog.size(), c->stream));
   HIPCHK(T->cqconsts.upload(consts.data(), consts.size(), c->stream));
@@ -2921,8 +2933,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       q.n_bool_masks = (uint32_t)c->n_bmask;
       q.prof_out = prof_buffer(c, (int)li);
       const size_t lds_other = (size_t)q.lds_wave_bytes * 4 + (size_t)q.n_stage * 256 + 4 * (size_t)kQsaProfBytes;
-      const size_t lds = lds_other + plan_prog_lds(q, T->cqdescs_h.data() + lv.cq_begin, n, tpg, lds_other,
-                                                   4 * (size_t)kQsaProfBytes);
+      const size_t lds = lds_other;
       QArgs* dq = T->cqargs.as<QArgs>() + li;
       if (std::memcmp(&T->cqargs_host[li], &q, sizeof(QArgs)) != 0) {
         PhaseTimer pq(&c->host_t[6]);
@@ -3003,7 +3014,6 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     q.n_bool_masks = (uint32_t)c->n_bmask;
     if (k == 1) q.prof_out = prof_buffer(c, -1);
     size_t lds = (size_t)q.lds_wave_bytes * 4 + (size_t)q.n_stage * 256 + (k == 1 ? 4 * (size_t)kQsaProfBytes : 0);
-    if (k == 1) lds += plan_prog_lds(q, T->qdescs_h.data() + T->q_count[0], n, tpg, lds, 4 * (size_t)kQsaProfBytes);
     // the argument block only changes with the output buffer / mode / models: re-upload then
     if (!T->qargs_valid[k] || std::memcmp(&T->qargs_dev_copy[k], &q, sizeof(QArgs)) != 0) {
       PhaseTimer pq(&c->host_t[6]);
@@ -3286,6 +3296,7 @@ int mq_ctx_set_option(mq_ctx* c, int option, int value) {
     case MQ_OPT_USE_ASM: c->use_asm = value ? 1 : 0; return MQ_OK;
     case MQ_OPT_EARLY_EXIT: c->early_exit = value ? 1 : 0; return MQ_OK;
     case MQ_OPT_LATENCY_WAVES: c->latency_waves = value > 0 ? value : 0; return MQ_OK;
+    case MQ_OPT_KECCAK_HOST_BLOCKS: c->keccak_host_blocks = value > 0 ? value : 0; return MQ_OK;
     case MQ_OPT_ASM_READY: return c->qsa_ready ? 1 : 0;
     case MQ_OPT_TIME_KERNELS:
       c->time_kernels = value ? 1 : 0;
@@ -3378,9 +3389,24 @@ double mq_tape_alg_ops(const mq_tape_batch* tb, int32_t t) {
   return tape_alg_ops(tb, t);
 }
 
+int mq_keccak256_host(const uint8_t* data, const int64_t* offsets, int32_t n, uint8_t* out) {
+  if ((n > 0 && (!data || !offsets || !out)) || n < 0) return MQ_ERR_ARG;
+  for (int32_t i = 0; i < n; i++)
+    if (offsets[i + 1] < offsets[i]) return MQ_ERR_ARG;
+  for (int32_t i = 0; i < n; i++) host_keccak256(data + offsets[i], offsets[i + 1] - offsets[i], out + 32 * (int64_t)i);
+  return MQ_OK;
+}
+
 int mq_keccak256(mq_ctx* c, const uint8_t* data, const int64_t* offsets, int32_t n, uint8_t* out) {
   if (!c || (n > 0 && (!data || !offsets || !out)) || n < 0) return MQ_ERR_ARG;
   if (n == 0) return MQ_OK;
+  // a small batch (the reference's call size: one to a few messages) is hashed on the host
+  int64_t blocks = 0;
+  for (int32_t i = 0; i < n && blocks <= c->keccak_host_blocks; i++) {
+    if (offsets[i + 1] < offsets[i]) return MQ_ERR_ARG;
+    blocks += (offsets[i + 1] - offsets[i]) / 136 + 1;
+  }
+  if (blocks <= c->keccak_host_blocks) return mq_keccak256_host(data, offsets, n, out);
   HIPCHK(hipSetDevice(c->device));
   const int64_t total = offsets[n];
   // (kept in the context: a hipMalloc / hipFree pair per call cost more than the hashing)

@@ -94,7 +94,7 @@ struct QArgs {
   const uint32_t* stage_rows;    // 0x190 G: global row of each staged slot
   const uint64_t* bool_masks;    // 0x198 G: packed Bool rows, [tile][n_bool_masks] lane masks
   uint32_t n_bool_masks;         // 0x1a0
-  uint32_t prog_lds;             // 0x1a4 G: LDS offset | 1 of the workgroup's programs (0: read from memory)
+  uint32_t reserved_1a4;         // 0x1a4 (unused; keeps the layout the generated code addresses)
   unsigned long long* prof_out;  // 0x1a8 G profile build only: (cycles, count) per handler kind
   const uint32_t* dense_words;   // 0x1b0 G: dense lookup slots (FuncDev dense_base / dense_e)
 };
@@ -108,7 +108,7 @@ static_assert(__builtin_offsetof(QArgs, bool_rows) == 0x18c, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, stage_rows) == 0x190, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, bool_masks) == 0x198, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, n_bool_masks) == 0x1a0, "QArgs layout");
-static_assert(__builtin_offsetof(QArgs, prog_lds) == 0x1a4, "QArgs layout");
+static_assert(__builtin_offsetof(QArgs, reserved_1a4) == 0x1a4, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, prof_out) == 0x1a8, "QArgs layout");
 static_assert(__builtin_offsetof(QArgs, dense_words) == 0x1b0, "QArgs layout");
 

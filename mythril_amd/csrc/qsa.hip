@@ -4,8 +4,9 @@
 // G: one workgroup = 4 waves on the same 64 models, each wave its own tape group.  See gen_qsa.py for
 // the register maps and the program encoding.
 //   qsa_kernel (P): the first 8 model variables preloaded in VGPRs (C2-shaped batches)
-//   qsg_kernel (G): the 8 variables its tapes push most preloaded, the rest pushed from HBM,
-//                   model-function lookups (EVM-shaped batches)
+//   qsg_kernel (G): no preloaded variables (a 4-slot stack, 80 VGPRs, 6 waves per SIMD): rows
+//                   pushed from HBM or from the workgroup's LDS-staged rows, model-function
+//                   lookups (EVM-shaped batches)
 #include <hip/hip_runtime.h>
 
 #include "qs_launch.h"

@@ -73,6 +73,7 @@ def load_library(path: str = LIB_PATH):
         L.mq_eval_tapes_verdicts.argtypes = [P, P, C.POINTER(C.c_uint8), C.POINTER(C.c_int32)]
         L.mq_tapes_set_columns.argtypes = [P, C.POINTER(MqTapeBatch), C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_int32]
         L.mq_keccak256.argtypes = [P, C.POINTER(C.c_uint8), C.POINTER(C.c_int64), C.c_int32, C.POINTER(C.c_uint8)]
+        L.mq_keccak256_host.argtypes = [C.POINTER(C.c_uint8), C.POINTER(C.c_int64), C.c_int32, C.POINTER(C.c_uint8)]
         L.mq_tape_alg_ops.argtypes = [C.POINTER(MqTapeBatch), C.c_int32]
         L.mq_tape_alg_ops.restype = C.c_double
         L.mq_tape_compile_info.argtypes = [C.POINTER(MqTapeBatch), C.c_int32] + [C.POINTER(C.c_int32)] * 5 + [C.c_char_p, C.c_int32]
@@ -112,6 +113,19 @@ class CompileInfo:
     n_temps: int
     prog_words: int
     why: str
+
+
+def keccak256_host(messages: Sequence[bytes]) -> List[bytes]:
+    """keccak256 of each message through the library's host path (``mq_keccak256_host``: what
+    ``Evaluator.keccak256`` runs for small batches); no GPU needed."""
+    msgs = [bytes(m) for m in messages]
+    offs = np.zeros(len(msgs) + 1, np.int64)
+    offs[1:] = np.cumsum([len(m) for m in msgs])
+    data = np.frombuffer(b"".join(msgs) or b"\0", dtype=np.uint8).copy()
+    out = np.zeros(32 * len(msgs), np.uint8)
+    _check(load_library().mq_keccak256_host(data.ctypes.data_as(C.POINTER(C.c_uint8)), offs.ctypes.data_as(C.POINTER(C.c_int64)),
+                                            len(msgs), out.ctypes.data_as(C.POINTER(C.c_uint8))), "mq_keccak256_host")
+    return [bytes(out[32 * i:32 * i + 32]) for i in range(len(msgs))]
 
 
 def compile_info(tb: TapeBatch, t: int) -> CompileInfo:
@@ -322,7 +336,7 @@ class Evaluator:
             self.set_option(self.OPT_USE_RCCL, 1)
 
     OPT_USE_ASM, OPT_EARLY_EXIT, OPT_ASM_READY, OPT_TIME_KERNELS = 1, 2, 3, 4
-    OPT_USE_RCCL, OPT_RCCL_ACTIVE, OPT_LATENCY_WAVES = 5, 6, 7
+    OPT_USE_RCCL, OPT_RCCL_ACTIVE, OPT_LATENCY_WAVES, OPT_KECCAK_HOST_BLOCKS = 5, 6, 7, 8
 
     @property
     def rccl_active(self) -> bool:

@@ -23,7 +23,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import smt as S
-from .exceptions import LoweringError
+from .exceptions import LoweringError, note_fail_closed
 from .models import FuncSpec, ModelBatch
 from .smt_model import Model
 from .smt_model import as_record
@@ -776,7 +776,8 @@ def lower_batch(roots: Sequence[S.Term], syms: Optional[SymbolTable] = None, hoi
     for i, r in enumerate(roots):
         try:
             tapes.append(lower_term(r, syms, hoisted, narrow=narrow))
-        except (LoweringError, TypeError):
+        except (LoweringError, TypeError) as e:
+            note_fail_closed(e)
             ok[i] = False
             t = Tape()
             tapes.append(t.finish(t.false()))
@@ -888,7 +889,7 @@ class IncrementalLowering:
         self.tape = Tape()
         self._node: Dict[int, int] = {}       # id(term) -> DAG node
         self._keep: Dict[int, S.Term] = {}    # keeps those terms (and their ids) alive
-        self._bad: Dict[int, S.Term] = {}     # terms that failed to lower
+        self._bad: Dict[int, Tuple[S.Term, str]] = {}   # terms that failed to lower (+ why)
         self._np_nodes = np.zeros(1024, NODE_DTYPE)
         self._np_n = 0
         self._np_consts = np.zeros(1024, np.uint32)
@@ -901,7 +902,7 @@ class IncrementalLowering:
         if hit is not None:
             return hit
         if id(root) in self._bad:
-            raise LoweringError("conjunct not in the tape vocabulary")
+            raise LoweringError(self._bad[id(root)][1])
         node, tp, syms = self._node, self.tape, self.syms
         order: List[S.Term] = []
         seen = set()
@@ -928,8 +929,8 @@ class IncrementalLowering:
                 node[id(t)] = _lower_one(t, [get(id(x), -1) for x in t.args], tp, syms, node)
                 keep[id(t)] = t
         except (LoweringError, TypeError) as e:
-            self._bad[id(root)] = root
-            raise LoweringError(str(e))
+            self._bad[id(root)] = (root, str(e) or "conjunct not in the tape vocabulary")
+            raise LoweringError(self._bad[id(root)][1])
         return node[id(root)]
 
     def _sync(self) -> Tuple[np.ndarray, np.ndarray]:
@@ -968,7 +969,8 @@ class IncrementalLowering:
             conj = r.args if r.kind == S.AND else (r,)
             try:
                 ids = [self._lower(c) for c in conj]
-            except LoweringError:
+            except LoweringError as e:
+                note_fail_closed(e)
                 ok[i] = False
                 if false_node is None:
                     false_node = self.tape.false()

@@ -24,7 +24,7 @@ import numpy as np
 import z3  # noqa: F401  (ImportError here means: no z3 host)
 from z3 import z3consts as C
 
-from .exceptions import LoweringError
+from .exceptions import LoweringError, note_fail_closed
 from .lower import SymbolTable, serialize_models
 from .smt_model import Model
 from .tape import Tape, TapeBatch
@@ -224,7 +224,8 @@ def lower_batch_z3(exprs: Sequence, models: Sequence):
     for i, e in enumerate(exprs):
         try:
             tapes.append(lower_z3_term(e, syms))
-        except (LoweringError, TypeError):
+        except (LoweringError, TypeError) as err:
+            note_fail_closed(err)
             ok[i] = False
             t = Tape()
             tapes.append(t.finish(t.false()))

@@ -47,7 +47,8 @@ from typing import Callable, Dict, Iterable, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import smt as S
-from .exceptions import SolverTimeOutException, UnsatError
+from .exceptions import SolverTimeOutException, UnsatError, fail_closed  # noqa: F401 (fail_closed: queries
+#   routed to z3 because a conjunct did not lower, by reason -- array-valued ite, array equality, ...)
 from .lower import DagBatch
 from .smt_model import Model, as_record
 
@@ -297,6 +298,18 @@ class VerdictEngine:
         if free is not None:
             free()
 
+    def close(self) -> None:
+        """Free the device buffers this engine keeps across calls (the reused conjunct batch)."""
+        prev, self._conj_ct = self._conj_ct, None
+        if prev is not None:
+            self._free(prev[2])
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:   # (interpreter shutdown: the library may be gone)
+            pass
+
     def _evaluate(self, tb, mb, upload: bool = True):
         """Device hook: (verdicts [n_tapes, M], first hits) of ``tb`` over ``mb``; ``upload``
         False when ``mb`` is already the evaluator's resident batch."""
@@ -422,7 +435,8 @@ class VerdictEngine:
             from .lower import DagBatch
             todo = uroots[unk]
             prev = self._conj_ct
-            gen = (inc.dag_gen, inc.slot_epoch)
+            # (the evaluator that compiled it is part of the key: a batch is bound to its context)
+            gen = (inc.dag_gen, inc.slot_epoch, id(self._ev))
             if prev is not None and prev[0] == gen and len(prev[1]) <= 4 * n_unk + 64 and \
                     np.isin(todo, prev[1], assume_unique=True).all():
                 todo, ct = prev[1], prev[2]
@@ -722,11 +736,15 @@ class WitnessSolver(SolverBackend):
     def __init__(self, states: Sequence, witnesses: Sequence):
         self.known = {frozenset(c for c in st if c.kind != S.TRUE): w for st, w in zip(states, witnesses) if w is not None}
         self.calls = 0
+        self.sat_calls = 0   # calls answered sat: each inserts its model into the LRU
 
     def solve(self, constraints, minimize, maximize, timeout_ms):
         self.calls += 1
         w = self.known.get(frozenset(c for c in constraints if c.kind != S.TRUE))
-        return ("sat", lambda: w) if w is not None else ("unknown", None)
+        if w is None:
+            return "unknown", None
+        self.sat_calls += 1
+        return "sat", lambda: w
 
 
 def _default_backend() -> SolverBackend:
@@ -923,6 +941,7 @@ def reset_caches() -> None:
     global model_cache
     get_model.cache_clear()
     engine = model_cache.engine
+    engine.close()
     model_cache = ModelCache(engine)
     for k in counters:
         counters[k] = 0

@@ -149,3 +149,17 @@ def test_models_shard_matches_python_shard_and_covers_the_batch(world):
                 assert a.func_table(f, m) == b.func_table(f, m) == mb.func_table(f, lo + m)
         parts.append(dist.encode_local(cref.first_hit(tb, a)[0]))
     assert (dist.decode_global(np.minimum.reduce(parts)) == ref).all()
+
+
+def test_host_keccak_path_matches_the_kats_and_the_oracle():
+    """mq_keccak256's host path (small batches, no GPU) against the keccak KATs and the oracle at
+    every length around the 136-byte block boundary."""
+    import keccak_ref
+    from golden_util import load
+    from mythril_amd.evaluator import keccak256_host
+    kats = load("keccak_kats.json")
+    out = keccak256_host([bytes.fromhex(k["data"]) for k in kats])
+    assert [d.hex() for d in out] == [k["digest"] for k in kats]
+    msgs = [bytes((i * 13 + n) & 0xFF for i in range(n)) for n in list(range(0, 300)) + [1000, 4096]]
+    assert keccak256_host(msgs) == [keccak_ref.keccak256(m) for m in msgs]
+    assert keccak256_host([]) == []

@@ -169,12 +169,20 @@ def test_uf_and_arrays(evaluator):
     assert list(fh) == [0, 0, 151]
 
 
-def test_keccak_kernel(evaluator):
+@pytest.mark.parametrize("host_blocks", [0, None])
+def test_keccak_kernel(evaluator, host_blocks):
+    """host_blocks 0: every batch on the GPU kernel; None: the default threshold (this small batch
+    is hashed on the host path of mq_keccak256)."""
     kats = load("keccak_kats.json")
     msgs = [bytes.fromhex(k["data"]) for k in kats]
     rng = np.random.default_rng(3)
     extra = [bytes(rng.integers(0, 256, n, dtype=np.uint8)) for n in (1, 31, 32, 64, 135, 136, 137, 300)]
-    out = evaluator.keccak256(msgs + extra)
+    if host_blocks is not None:
+        evaluator.set_option(evaluator.OPT_KECCAK_HOST_BLOCKS, host_blocks)
+    try:
+        out = evaluator.keccak256(msgs + extra)
+    finally:
+        evaluator.set_option(evaluator.OPT_KECCAK_HOST_BLOCKS, 128)
     for k, d in zip(kats, out):
         assert d.hex() == k["digest"], k["name"]
     for m, d in zip(extra, out[len(msgs):]):
@@ -544,15 +552,19 @@ def test_c4_hoisted_in_kernel_keccak(evaluator):
     assert (ref == exp).all() and (fh == ref).all()
 
 
-@pytest.mark.parametrize("variant", ["fused", "no_predicates", "no_keccak_columns", "cpp_columns"])
+@pytest.mark.parametrize("variant", ["fused", "no_predicates", "no_keccak_columns", "cpp_columns", "no_mask_index"])
 def test_c4_keccak_predicates_in_the_keccak_column_kernel(evaluator, monkeypatch, variant):
     """The keccak manager's predicates over keccak columns (lo <= h, h < hi, h urem 64 == 0,
     h == h_c; keccak_function_manager.py:150-179) evaluated by the keccak column kernel from the
     digest in registers, their lane masks stored directly: full verdict matrix and first hits
     against the oracle on the UNhoisted lowering.  Variants: predicates on the interpreters, keccak
     columns on the interpreters (predicate columns then run one level later), and the G column
-    path off (the kernel then also writes the 0/1 rows the HIP C++ kernels read)."""
+    path off (the kernel then also writes the 0/1 rows the HIP C++ kernels read); no Bool
+    variable with a lane-mask index (MQ_BMASK_CAP=0, as past the 65 535-mask cap): G-only launches
+    read the predicate columns' 0/1 rows, which the keccak kernel must then write."""
     from mythril_amd.synth_evm import c4_workload
+    if variant == "no_mask_index":
+        monkeypatch.setenv("MQ_BMASK_CAP", "0")
     if variant == "no_predicates":
         monkeypatch.setenv("MQ_NO_KECCAK_PREDICATES", "1")
     if variant == "no_keccak_columns":
@@ -570,7 +582,7 @@ def test_c4_keccak_predicates_in_the_keccak_column_kernel(evaluator, monkeypatch
     finally:
         evaluator.use_asm(True)
     kp = ct.keccak_predicate_columns()
-    if variant in ("fused", "cpp_columns"):
+    if variant in ("fused", "cpp_columns", "no_mask_index"):
         assert kp >= 8 and ct.keccak_columns() >= 4, (kp, ct.keccak_columns())
     else:
         assert kp == 0

@@ -294,8 +294,14 @@ def exercise_fail_closed(lz3):
     exprs = [good] + rej + [good]
     m = Z.ModelRef()
     m.set(x.decl(), Z.BitVecVal(3, 256))
+    from mythril_amd.exceptions import fail_closed
+    before = dict(fail_closed)
     tb, mb, ok = lz3.lower_batch_z3(exprs, [wrap(m)])
     assert ok.tolist() == [True] + [False] * len(rej) + [True]
+    # each rejected query is counted under its reason (the state-merge shapes by name)
+    new = {k: fail_closed[k] - before.get(k, 0) for k in fail_closed if fail_closed[k] != before.get(k, 0)}
+    assert sum(new.values()) == len(rej), new
+    assert new.get("array equality") == 1 and new.get("array-valued ite") == 1, new
     v = cref.verdicts(tb, mb)
     assert v[0, 0] and v[-1, 0]
     # a model whose interpretation cannot be read routes the whole batch to the z3 loop
