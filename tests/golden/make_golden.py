@@ -14,6 +14,21 @@ Outputs
                         (tests/laser/evm_testsuite/VMTests, harness evm_test.py:178-189) for the
                         straight-line programs, each stored word lowered to a tape with
                         mythril's EVM->BV mapping (instructions.py:360-767).
+                        EXP (0x0a) goes through the product's own
+                        ``function_managers.exponent_function_manager.create_condition``
+                        (exponent_function_manager.py:32-60, called at instructions.py:629-642):
+                        concrete operands give pow(b, e, 2^256) and the constraint
+                        ``c == Power(b, e)``; the conjunction of a program's constraints is lowered
+                        by the product lowering (lower.py, Power a 2-argument model table looked up
+                        on the GPU) into the entry's "constraint" tape, true under a model whose
+                        Power table holds the entries listed in "power".  CALLDATALOAD (0x35) reads
+                        the test's concrete calldata as Mythril's ConcreteCalldata does
+                        (state/calldata.py:119-147: select over a store chain on K(0), the 32
+                        bytes concatenated, get_word_at :48-55); CALLDATASIZE is its length.
+                        Where Mythril needs a concrete value (EXP operands, BYTE index, SSTORE /
+                        MSTORE keys) the operand expression is folded as z3's simplify folds it
+                        (util.get_concrete_int): evaluated by the oracle (oracle/pyoracle.py);
+                        the expected values stay the VMTests' own.
   keccak_kats.json    — VMTests vmSha3Test digests (keccak of zero/constant memory) plus
                         keccak("") = get_empty_keccak_hash() (keccak_function_manager.py:86-93).
 """
@@ -27,8 +42,18 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
+import numpy as np  # noqa: E402
+
+import pyoracle  # noqa: E402  (test infrastructure: folds constant operands)
+from mythril_amd import smt as S  # noqa: E402
+from mythril_amd.function_managers import exponent_function_manager  # noqa: E402
+from mythril_amd.lower import SymbolTable, lower_term  # noqa: E402
+from mythril_amd.models import ModelBatch  # noqa: E402
 from mythril_amd.tape import Tape, TapeBatch  # noqa: E402
+
+_NO_MODELS = ModelBatch([], np.zeros((0, 1), np.uint32))
 
 REF = os.environ.get("MYTHRIL_REFERENCE", "/root/reference")
 VMT = os.path.join(REF, "tests", "laser", "evm_testsuite", "VMTests")
@@ -64,9 +89,10 @@ class Skip(Exception):
     pass
 
 
-def lower_program(code: bytes, t: Tape):
+def lower_program(code: bytes, t: Tape, calldata: bytes = b"", exp_conditions=None):
     """Symbolically run straight-line EVM code building tape terms with mythril's mapping.
-    Returns {storage_key_int: node}.  Raises Skip for control flow / unsupported opcodes."""
+    Returns {storage_key_int: node}.  Raises Skip for control flow / unsupported opcodes.
+    ``exp_conditions`` (a list) collects (base, exponent, result, condition term) per EXP."""
     stack = []
     store = {}
     mem = {}  # byte offset -> constant byte (sha3 tests only use constant memory)
@@ -88,13 +114,15 @@ def lower_program(code: bytes, t: Tape):
         return x
 
     def const_value(x):
+        """The concrete value of a constant expression (z3's simplify folds it; util.get_concrete_int)."""
         if isinstance(x, tuple):
             raise Skip("sha3 result used as a concrete value")
         op, w, a, b, c = t.nodes[x]
-        if op != 1:
-            raise Skip("non-constant where mythril needs a concrete value")
-        words = t.consts[a:a + (w + 31) // 32]
-        return sum(int(v) << (32 * i) for i, v in enumerate(words))
+        if op == 1:
+            words = t.consts[a:a + (w + 31) // 32]
+            return sum(int(v) << (32 * i) for i, v in enumerate(words))
+        arr, consts = t.packed()
+        return int(pyoracle.eval_nodes(arr[:x + 1], np.asarray(consts, np.uint32), _NO_MODELS, 0)[x])
 
     while pc < len(code):
         op = code[pc]
@@ -164,6 +192,31 @@ def lower_program(code: bytes, t: Tape):
         if op == 0x19:  # NOT = TT256M1 - x (instructions.py:427)
             stack.append(t.sub(t.const(M256, 256), as_bv(pop())))
             continue
+        if op == 0x0A:  # EXP (instructions.py:629-642 -> exponent_function_manager.create_condition)
+            base, expo = as_bv(pop()), as_bv(pop())
+            b_val, e_val = const_value(base), const_value(expo)
+            res, cond = exponent_function_manager.create_condition(S.BitVecVal(b_val, 256), S.BitVecVal(e_val, 256))
+            if res.symbolic:
+                raise Skip("EXP result not concrete")
+            if exp_conditions is None:
+                raise Skip("EXP without a constraint sink")
+            exp_conditions.append((b_val, e_val, res.value, cond))
+            stack.append(t.const(res.value, 256))
+            continue
+        if op == 0x35:  # CALLDATALOAD over ConcreteCalldata (state/calldata.py:119-147, :48-55)
+            off = const_value(pop())
+            arr = t.const_array(t.const(0, 8))
+            for i, byte in enumerate(calldata):
+                arr = t.store(arr, t.const(i, 256), t.const(byte, 8))
+            word = None
+            for k in range(32):
+                part = t.select(arr, t.const((off + k) & M256, 256))
+                word = part if word is None else t.concat(word, part)
+            stack.append(word)
+            continue
+        if op == 0x36:  # CALLDATASIZE (concrete calldata: its length)
+            stack.append(t.const(len(calldata), 256))
+            continue
         if op == 0x1A:  # BYTE with concrete index (instructions.py:431-458)
             i, x = pop(), as_bv(pop())
             idx = const_value(i)
@@ -204,6 +257,7 @@ def lower_program(code: bytes, t: Tape):
 
 def vmtests():
     kats, sha = [], []
+    skipped = {}
     for sub in ("vmArithmeticTest", "vmBitwiseLogicOperation", "vmSha3Test"):
         d = os.path.join(VMT, sub)
         for fn in sorted(os.listdir(d)):
@@ -217,11 +271,25 @@ def vmtests():
                 if not expected:
                     continue
                 code = bytes.fromhex(case["exec"]["code"][2:])
+                calldata = bytes.fromhex(case["exec"].get("data", "0x")[2:])
                 t = Tape()
+                conds = []
                 try:
-                    store = lower_program(code, t)
-                except Skip:
+                    store = lower_program(code, t, calldata, conds)
+                except Skip as e:
+                    skipped[str(e)] = skipped.get(str(e), 0) + 1
                     continue
+                extra = {}
+                if conds:
+                    # the program's EXP constraints, lowered by the product lowering with Power as
+                    # a 2-argument model table (no host-side derivation of constant lookups)
+                    syms = SymbolTable(derive_constant_lookups=False)
+                    ct = lower_term(S.And(*[c for _, _, _, c in conds]), syms)
+                    assert syms.func_names == ["Power"], syms.func_names
+                    arr, consts = ct.packed()
+                    extra = dict(constraint=dict(nodes=[[int(x) for x in row] for row in arr.tolist()],
+                                                 consts=[int(c) for c in consts]),
+                                 power=sorted({(f"{b:#x}", f"{e:#x}", f"{r:#x}") for b, e, r, _ in conds}))
                 for key, exp in sorted(expected.items()):
                     node = store.get(key)
                     if node is None:
@@ -233,10 +301,11 @@ def vmtests():
                     if t.kind[node] == "bool":
                         node = t.ite(node, t.const(1, 256), t.const(0, 256))
                     kats.append(dump_tape(t, node, name=f"{sub}/{name}[{key}]", expected=f"0x{exp:064x}",
-                                          source=f"tests/laser/evm_testsuite/VMTests/{sub}/{fn}"))
+                                          source=f"tests/laser/evm_testsuite/VMTests/{sub}/{fn}", **extra))
     sha.append(dict(name="keccak_function_manager.get_empty_keccak_hash", data="",
                     digest=f"{89477152217924674838424037953991966239322087453347756267410168184682657981552:064x}",
                     source="mythril/laser/ethereum/function_managers/keccak_function_manager.py:86-93"))
+    print("skipped programs:", skipped)
     return kats, sha
 
 

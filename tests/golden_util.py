@@ -17,6 +17,7 @@ def load(name: str):
 
 
 def fixture_tape(entry) -> Tape:
+    """The entry's tape (its nodes and consts; finish() picks the root)."""
     t = Tape()
     for row in entry["nodes"]:
         op, w, a, b, c = row
@@ -34,3 +35,22 @@ def check_tape(entry, expected: int, negate: bool = False) -> Tape:
     c = t.const(expected ^ (1 if negate else 0), w)
     root = t.eq(v, c)
     return t.finish(root)
+
+
+def constraint_tape(entry) -> Tape:
+    """The entry's EXP constraint tape (the product lowering of the conjunction of
+    ``c == Power(b, e)``, tests/golden/make_golden.py), Power = model function 0."""
+    t = fixture_tape(entry["constraint"])
+    return t.finish(len(t.nodes) - 1)
+
+
+def power_models(entries) -> "ModelBatch":
+    """Two models over one 8-bit variable and the 2-argument ``Power`` table (function 0): model
+    0 holds every (b, e) -> pow(b, e, 2^256) entry the entries list, model 1 none (z3's
+    completion: else 0)."""
+    from mythril_amd.models import FuncSpec, ModelBatch
+    table = {}
+    for e in entries:
+        for b, x, r in e.get("power", ()):
+            table[(int(b, 16), int(x, 16))] = int(r, 16)
+    return ModelBatch.from_python([8], [{"funcs": {0: (table, 0)}}, {}], [FuncSpec(2, 256, (256, 256))])

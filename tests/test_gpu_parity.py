@@ -5,7 +5,7 @@ import pytest
 
 import cref
 import keccak_ref
-from golden_util import check_tape, load
+from golden_util import check_tape, constraint_tape, load, power_models
 from unsupported import supported_exactly
 from mythril_amd.models import FuncSpec, ModelBatch
 from mythril_amd.synth import c2_workload, fuzz_workload
@@ -16,6 +16,21 @@ pytestmark = pytest.mark.gpu
 
 def _one_model():
     return ModelBatch([8], np.zeros((1, 1), np.uint32))
+
+
+def test_golden_exp_constraints_on_gpu(evaluator):
+    """The VMTests EXP programs' Power constraints (product create_condition + lowering): verdicts
+    under the model with the Power table and under the empty one, against the oracle."""
+    kats = [e for e in load("vmtests_kats.json") if "constraint" in e]
+    tb = TapeBatch([constraint_tape(e) for e in kats])
+    mb = power_models(kats)
+    evaluator.upload_models(mb)
+    v, fh = evaluator.verdicts(tb)
+    assert (fh != -2).all()
+    assert v[:, 0].all()
+    assert (v == cref.verdicts(tb, mb)).all()
+    want_empty = np.array([all(int(r, 16) == 0 for _, _, r in e["power"]) for e in kats])
+    assert (v[:, 1] == want_empty).all()
 
 
 def test_golden_vectors_on_gpu(evaluator):

@@ -7,7 +7,7 @@ import pytest
 import cref
 import keccak_ref
 import pyoracle
-from golden_util import check_tape, fixture_tape, load
+from golden_util import check_tape, constraint_tape, fixture_tape, load, power_models
 from mythril_amd.models import ModelBatch
 from mythril_amd.synth import c2_workload, fuzz_workload
 from mythril_amd.tape import NODE_DTYPE, Tape, TapeBatch
@@ -36,6 +36,35 @@ def test_shift_vectors_count():
 @pytest.mark.parametrize("entry", load("vmtests_kats.json"), ids=lambda e: e["name"])
 def test_vmtests_pyoracle(entry):
     assert _value(entry) == int(entry["expected"], 16)
+
+
+def test_vmtests_cover_the_listed_kats():
+    """>= 400 of the 457 VMTests storage KATs of vmArithmeticTest / vmBitwiseLogicOperation are
+    pinned, the EXP programs (exp*.json, expPowerOf*) among them with their Power constraints."""
+    kats = load("vmtests_kats.json")
+    assert len(kats) >= 400
+    exp = [e for e in kats if "constraint" in e]
+    assert len(exp) >= 300 and all(e["power"] for e in exp)
+    assert any("expPowerOf256Of256" in e["name"] for e in exp)
+
+
+def test_exp_constraints_through_cref():
+    """The EXP programs' constraints c == Power(b, e) (the product's create_condition, lowered by
+    the product lowering): true under a model whose Power table holds the entries, and under the
+    empty table (z3 completion: Power = 0) exactly when every result is 0."""
+    kats = [e for e in load("vmtests_kats.json") if "constraint" in e]
+    tb = TapeBatch([constraint_tape(e) for e in kats])
+    mb = power_models(kats)
+    v = cref.verdicts(tb, mb)
+    assert v[:, 0].all()
+    want_empty = np.array([all(int(r, 16) == 0 for _, _, r in e["power"]) for e in kats])
+    assert (v[:, 1] == want_empty).all()
+    assert not want_empty.all()
+    # the Python restatement agrees on a sample
+    for i in range(0, len(kats), 37):
+        t = constraint_tape(kats[i])
+        arr, consts = t.packed()
+        assert pyoracle.eval_nodes(arr, np.asarray(consts, np.uint32), mb, 0)[-1] == 1
 
 
 def test_golden_through_cref():
