@@ -101,6 +101,9 @@ def parse():
     p.add_argument("--context", action="store_true",
                    help="drive the GPUs through one multi-device mq_ctx even at --gpus 1 (in-library RCCL with "
                         "one rank: a 1-GPU rehearsal of the one-process N-GPU path)")
+    p.add_argument("--engine", choices=["gpu", "oracle"], default="gpu",
+                   help="oracle: CPU rehearsal of the N-rank protocol (shards, MIN all-reduce over gloo, the line's "
+                        "keys) with oracle/cref.c in place of the GPU -- a test of bench.py itself, never a measurement")
     return p.parse_args()
 
 
@@ -318,14 +321,27 @@ def calls_avoided_leg(ev, n_forks: int = 256, n_models: int = 100, seed: int = 2
             for m in reversed(recs):
                 sp.model_cache.put(m, 1)
             cs = [sp.Constraints(st) for st in states]
+            eng = sp.model_cache.engine
+            e0, l0 = sum(eng.timing.values()), eng.launches
             t0 = time.perf_counter()
             alive = sp.is_possible_batch(cs)
             dt = time.perf_counter() - t0
             c = dict(sp.counters)
+            mc = sp.model_cache.stats
             avoided = c["get_model_calls"] - c["solver_calls"]
+            engine_s = sum(eng.timing.values()) - e0
+            pool_s = sp.timing["solver_pool"]
             out["candidates_on" if cand else "candidates_off"] = {
                 **c, "states_alive": int(sum(alive)), "solver_calls_avoided": avoided,
                 "fraction_avoided": avoided / max(c["get_model_calls"], 1), "ms_per_state": dt * 1e3 / len(cs),
+                # the per-state cost split: the verdict engine's host stages and launches
+                # (lower / serialize / upload / compile / evaluate), get_model's ThreadPool +
+                # solver stand-in, and the rest (the reference loop's Python: memo, LRU, answers)
+                "engine_ms_per_state": engine_s * 1e3 / len(cs),
+                "solver_pool_ms_per_state": pool_s * 1e3 / len(cs),
+                "other_ms_per_state": (dt - engine_s - pool_s) * 1e3 / len(cs),
+                "engine_launches": eng.launches - l0,
+                "late_fills": mc.get("late_fills", 0), "late_fill_exprs": mc.get("late_fill_exprs", 0),
                 "candidate_budget": budget if cand else 0, "solver_stand_in_calls": solver.calls,
                 "models_inserted_by_solver": solver.sat_calls}
     finally:
@@ -390,6 +406,65 @@ def pmc_traffic(workload_key: str):
     return None if e is None else {"bytes": e["fetch_bytes"] + e["write_bytes"], "source": e["source"]}
 
 
+class OracleRehearsal:
+    """``--engine oracle``: the evaluator calls bench.py's timed loop makes, answered by the oracle
+    (oracle/cref.c) on the host -- so a CPU test can run the N-rank protocol end to end (shards,
+    reduce encoding, gloo MIN all-reduce, per-rank timing keys).  Test infrastructure only: the
+    line it prints carries ``"engine": "oracle"`` and is not a measurement."""
+
+    rccl_active = False
+
+    def __init__(self):
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import cref  # oracle: rehearsal only
+        self.cref = cref
+        self.mb = None
+        self._counts = [0.0, 0.0, 0.0]
+        self._times = []
+
+    def upload_models(self, mb):
+        self.mb = mb
+
+    def compile(self, tb):
+        from mythril_amd.evaluator import tape_alg_ops
+        self.tb, self.alg = tb, np.array([tape_alg_ops(tb, t) for t in range(tb.n_tapes)])
+
+    def launch_first_hit(self, best):
+        t0 = time.perf_counter()
+        fh, pairs = self.cref.first_hit(self.tb, self.mb)
+        self._times.append((time.perf_counter() - t0) * 1e3)
+        best.copy_(torch_tensor(np.where(fh < 0, np.iinfo(np.int32).max, fh).astype(np.int32)))
+        sizes = self.tb.sizes()
+        evals = np.where(fh < 0, self.mb.n_models, fh - self.mb.index_base + 1).astype(np.float64)
+        self._counts[0] += float(evals.sum())
+        self._counts[1] += float((evals * sizes).sum())
+        self._counts[2] += float((evals * self.alg).sum())
+
+    @staticmethod
+    def finalize_first_hit(best):
+        best[best == np.iinfo(np.int32).max] = -1
+
+    def counters(self, reset=False):
+        c = tuple(self._counts)
+        if reset:
+            self._counts = [0.0, 0.0, 0.0]
+        return c
+
+    def kernel_times(self, reset=True):
+        t = list(self._times)
+        if reset:
+            self._times = []
+        return t
+
+    def time_kernels(self, on=True):
+        self._times = []
+
+
+def torch_tensor(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
 def launch_mode(args):
     """How the N GPUs of ``--gpus N`` are driven:
     * ``torchrun``: WORLD_SIZE > 1 in the environment (the driver's N > 1 launch): one process per
@@ -426,8 +501,12 @@ def main():
         local = args.device
     import torch
     import torch.distributed as dist
+    oracle = args.engine == "oracle"
+    if oracle:
+        args.dist_backend = "gloo"
     if world > 1:
-        torch.cuda.set_device(local)
+        if not oracle:
+            torch.cuda.set_device(local)
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -436,7 +515,7 @@ def main():
     def all_reduce(t, op):
         if world == 1:
             return
-        if args.dist_backend == "nccl":
+        if args.dist_backend == "nccl" or t.device.type == "cpu":
             dist.all_reduce(t, op=op)
         else:
             h = t.cpu()
@@ -458,27 +537,57 @@ def main():
         tb, mb, expected = build_workload(args.config, args.tapes, M, args.seed, rank, world, hoist=not args.no_hoist)
     t_gen = time.perf_counter() - t_gen
 
-    ev = Evaluator(devices=list(range(n_gpus)), use_rccl=True) if mode == "context" else Evaluator(local)
-    if args.no_early_exit:
-        ev.set_option(Evaluator.OPT_EARLY_EXIT, 0)
-    ev.upload_models(mb)
-    ct = ev.compile(tb)
-    if ct.n_unsupported:
-        raise SystemExit(f"{ct.n_unsupported} {args.config} tapes unsupported by the evaluator")
-    dev = torch.device("cuda", local)
-    best = torch.empty(tb.n_tapes, dtype=torch.int32, device=dev)
-    # a dedicated (non-null) stream: the kernels, the HIP events and RCCL all order on it
-    stream = torch.cuda.Stream(dev)
-    torch.cuda.set_stream(stream)
-    sptr = stream.cuda_stream
-    assert sptr != 0
+    if oracle:
+        ev = OracleRehearsal()
+        ev.upload_models(mb)
+        ev.compile(tb)
+        ct = None
+        dev = torch.device("cpu")
+        best = torch.empty(tb.n_tapes, dtype=torch.int32)
+        stream = None
+    else:
+        ev = Evaluator(devices=list(range(n_gpus)), use_rccl=True) if mode == "context" else Evaluator(local)
+        if args.no_early_exit:
+            ev.set_option(Evaluator.OPT_EARLY_EXIT, 0)
+        ev.upload_models(mb)
+        ct = ev.compile(tb)
+        if ct.n_unsupported:
+            raise SystemExit(f"{ct.n_unsupported} {args.config} tapes unsupported by the evaluator")
+        dev = torch.device("cuda", local)
+        best = torch.empty(tb.n_tapes, dtype=torch.int32, device=dev)
+        # a dedicated (non-null) stream: the kernels, the HIP events and RCCL all order on it
+        stream = torch.cuda.Stream(dev)
+        torch.cuda.set_stream(stream)
+        sptr = stream.cuda_stream
+        assert sptr != 0
+    # per timed step: the MIN all-reduce of the first hits, bracketed on the launch stream by
+    # events (RCCL) or host clocks (gloo / the oracle rehearsal), apart from the kernels
+    reduce_ms = []
+    red_ev = None
 
-    def step():
-        ev.launch_first_hit(ct, best.data_ptr(), sptr)
-        all_reduce(best, dist.ReduceOp.MIN)
-        ev.finalize_first_hit(ct, best.data_ptr(), sptr)
+    def step(i=None):
+        if oracle:
+            ev.launch_first_hit(best)
+        else:
+            ev.launch_first_hit(ct, best.data_ptr(), sptr)
+        if world > 1 and i is not None and red_ev is not None:
+            red_ev[i][0].record(stream)
+            all_reduce(best, dist.ReduceOp.MIN)
+            red_ev[i][1].record(stream)
+        elif world > 1 and i is not None:
+            t0 = time.perf_counter()
+            all_reduce(best, dist.ReduceOp.MIN)
+            reduce_ms.append((time.perf_counter() - t0) * 1e3)
+        else:
+            all_reduce(best, dist.ReduceOp.MIN)
+        if oracle:
+            ev.finalize_first_hit(best)
+        else:
+            ev.finalize_first_hit(ct, best.data_ptr(), sptr)
 
     def sync_all():
+        if oracle:
+            return
         for d in (range(n_gpus) if mode == "context" else [local]):
             torch.cuda.synchronize(d)
 
@@ -494,16 +603,21 @@ def main():
 
     # where the batch ran (after a launch): tapes on the P / G assembly interpreters vs the HIP C++
     # kernels, hoisted columns on G / the keccak column kernel / the C++ column kernel
-    n_p, n_g, asm_live = ct.asm_split()
-    n_cols = int(getattr(ct, "n_columns", 0))
-    cols_g, cols_live = ct.column_asm_split() if n_cols else (0, False)
-    kcols = int(ct.keccak_columns()) if n_cols else 0
-    kpreds = int(ct.keccak_predicate_columns()) if n_cols else 0
-    kernel_split = {"tapes": tb.n_tapes, "tapes_p": n_p, "tapes_g": n_g,
-                    "tapes_cpp": tb.n_tapes - ((n_p + n_g) if asm_live else 0),
-                    "columns": n_cols, "columns_g": cols_g if cols_live else 0, "columns_keccak": kcols,
-                    "columns_keccak_predicates": kpreds,
-                    "columns_cpp": n_cols - kcols - kpreds - (cols_g if cols_live else 0)}
+    if oracle:
+        kernel_split = {"tapes": tb.n_tapes, "engine": "oracle (CPU rehearsal)"}
+    else:
+        n_p, n_g, asm_live = ct.asm_split()
+        n_cols = int(getattr(ct, "n_columns", 0))
+        cols_g, cols_live = ct.column_asm_split() if n_cols else (0, False)
+        kcols = int(ct.keccak_columns()) if n_cols else 0
+        kpreds = int(ct.keccak_predicate_columns()) if n_cols else 0
+        kernel_split = {"tapes": tb.n_tapes, "tapes_p": n_p, "tapes_g": n_g,
+                        "tapes_cpp": tb.n_tapes - ((n_p + n_g) if asm_live else 0),
+                        "columns": n_cols, "columns_g": cols_g if cols_live else 0, "columns_keccak": kcols,
+                        "columns_keccak_predicates": kpreds,
+                        "columns_cpp": n_cols - kcols - kpreds - (cols_g if cols_live else 0)}
+    if world > 1 and not oracle and args.dist_backend == "nccl":
+        red_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
     ev.counters(reset=True)
     # HIP event pair recorded by libmq on `stream` around the evaluation kernel(s) of each launch
@@ -513,18 +627,27 @@ def main():
     sync_all()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step()
+        step(i)
     sync_all()
+    t_sync = time.perf_counter()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
+    t_end = time.perf_counter()
+    elapsed = t_end - t0
     pairs, node_evals, alg_ops = ev.counters(reset=True)
     ktimes = ev.kernel_times(reset=True)
     ev.time_kernels(False)
     assert len(ktimes) == args.steps, ktimes
     kern_ms = float(np.mean(ktimes))
+    if red_ev is not None:
+        reduce_ms = [a.elapsed_time(b) for a, b in red_ev]
+    red_ms = float(np.mean(reduce_ms)) if reduce_ms else 0.0
+    # this rank's wait in the closing barrier: how far it ran ahead of the slowest rank
+    barrier_ms = (t_end - t_sync) * 1e3
 
-    stats = torch.tensor([elapsed, node_evals, alg_ops, float(ok)], dtype=torch.float64, device=dev)
+    stats = torch.tensor([elapsed, node_evals, alg_ops, float(ok), kern_ms, red_ms, barrier_ms], dtype=torch.float64,
+                         device=dev)
+    per_rank = None
     if world > 1:
         mx = stats.clone()
         all_reduce(mx, dist.ReduceOp.MAX)
@@ -533,6 +656,10 @@ def main():
         mn = stats.clone()
         all_reduce(mn, dist.ReduceOp.MIN)
         elapsed, node_evals, alg_ops, ok = float(mx[0]), float(sm[1]), float(sm[2]), bool(mn[3] > 0)
+        per_rank = {k: {"min": float(mn[j]), "max": float(mx[j])}
+                    for j, k in ((4, "kernel_ms"), (5, "allreduce_ms"), (6, "barrier_wait_ms"))}
+        per_rank["allreduce_timer"] = "hip events on the launch stream (RCCL)" if red_ev is not None else \
+            "host clock around the gloo all_reduce"
     hits = int((got >= 0).sum())
 
     if rank == 0:
@@ -583,12 +710,17 @@ def main():
             },
             "planted_first_hits": {"hits": hits, "tapes": tb.n_tapes},
             "kernel_split": kernel_split,
+            # N > 1: per-rank kernel time (mean over steps), the MIN all-reduce of the first hits
+            # and each rank's wait in the closing barrier, as (min, max) over ranks
+            "per_rank": per_rank,
             "parity_ok": ok,
             "pairs_evaluated": pairs,
             "nominal_node_evals_per_step": float(tb.sizes().sum()) * M * n_gpus,
             "gen_seconds": t_gen,
         }
-        if n_gpus == 1 and not args.no_cpu_baseline:
+        if oracle:
+            out["engine"] = "oracle (CPU rehearsal of the protocol; not a measurement)"
+        if n_gpus == 1 and not args.no_cpu_baseline and not oracle:
             if getattr(tb, "columns", None) is not None:
                 # the reference evaluates every conjunction in full per model: time the oracle on
                 # the same conjunctions lowered without hoisting
@@ -598,7 +730,7 @@ def main():
                 cb = cpu_baseline(tb, mb, args.cpu_seconds)
             out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample", "single_core_value", "host")}
             out["gpu_over_cpu"] = out["value"] / cb["value"]
-        if n_gpus == 1 and not args.no_dropin:
+        if n_gpus == 1 and not args.no_dropin and not oracle:
             out["dropin"] = dropin_leg(ev)
             out["dropin_stream"] = dropin_stream_leg(ev)
             out["z3_calls_avoided"] = calls_avoided_leg(ev)

@@ -500,6 +500,7 @@ class ModelCache:
     """support_utils.py:56-70 with the GPU verdict engine behind ``check_quick_sat``."""
 
     MEMO_SIZE = 2 ** 10   # @lru_cache(maxsize=2**10) on check_quick_sat (support_utils.py:60)
+    LOOKAHEAD_MIN = 4     # pending conjunctions a late fill always carries besides its query
 
     def __init__(self, engine: Optional[VerdictEngine] = None):
         self.model_cache = LRUCache(size=100)
@@ -516,7 +517,16 @@ class ModelCache:
         # can tell which conjunctions will never reach the evaluator again
         self._memo: "OrderedDict[object, object]" = OrderedDict()
         self._cand: Dict[object, object] = {}   # prefetched generated-candidate answers
-        self.stats = {"queries": 0, "hits": 0, "unsupported": 0}
+        self.stats = {"queries": 0, "hits": 0, "unsupported": 0,
+                      # launches for models a query found unevaluated (a solver model inserted
+                      # since its prefetch), and the conjunctions they carried
+                      "late_fills": 0, "late_fill_exprs": 0}
+        # pending conjunctions that ride along when a query meets a model inserted after their
+        # prefetch: doubles while late fills keep serving later queries, reset when a query
+        # arrives after another insertion (on a fork stream nearly every miss inserts a model,
+        # and evaluating every pending conjunction per insertion was the per-state cost)
+        self._lookahead = 0
+        self._served_since_fill = 0
 
     def check_quick_sat(self, constraints):
         """support_utils.py:60-67, memoized per ``(self, constraints)`` like the reference's
@@ -686,12 +696,25 @@ class ModelCache:
         if d is not _UNSUPPORTED:
             got = d[slots] if slots.size and int(slots.max()) < len(d) else None
             if got is None or (got < 0).any():
-                # evaluate every still-pending conjunction against the new models in one launch
+                # the query, and the next few pending conjunctions, against the models it has not
+                # seen, in one launch; the window grows while such fills keep answering later
+                # queries and shrinks to the query alone when models keep arriving in between
                 known = np.zeros(len(slots), bool) if got is None else got >= 0
                 miss = np.flatnonzero(~known)
-                batch = [expr] + [e for e in self._pending if e is not expr and self._rows.get(e) is not _UNSUPPORTED]
+                self._lookahead = max(self.LOOKAHEAD_MIN, 2 * self._served_since_fill)
+                batch = [expr]
+                for e in self._pending:
+                    if len(batch) > self._lookahead:
+                        break
+                    if e is not expr and self._rows.get(e) is not _UNSUPPORTED:
+                        batch.append(e)
                 self._fill(batch, [order[i] for i in miss], slots[miss])
+                self.stats["late_fills"] += 1
+                self.stats["late_fill_exprs"] += len(batch)
+                self._served_since_fill = 0
                 d = self._rows[expr]
+            else:
+                self._served_since_fill += 1
         self._rows.pop(expr, None)
         self._pending.pop(expr, None)
         if d is _UNSUPPORTED:
@@ -758,6 +781,9 @@ def _default_backend() -> SolverBackend:
 model_cache = ModelCache()
 solver_backend: SolverBackend = None  # type: ignore[assignment]
 counters = {"get_model_calls": 0, "quick_sat_answers": 0, "candidate_answers": 0, "solver_calls": 0}
+# host seconds of get_model's solver path: ThreadPool(1) create + apply + terminate around the
+# solver (model.py:104-113, which the reference pays too) and the solver itself
+timing = {"solver_pool": 0.0}
 
 
 def set_solver_backend(backend: Optional[SolverBackend]) -> None:
@@ -817,6 +843,7 @@ def get_model(constraints, minimize=(), maximize=(), solver_timeout=None, verdic
             # (same call form as Constraints.get_model: lru_cache keys depend on it)
             return get_model(asked, solver_timeout=asked_timeout)
     counters["solver_calls"] += 1
+    t_pool = time.perf_counter()
     pool = ThreadPool(1)
     try:
         res = pool.apply_async(solver_worker, args=(constraints, minimize, maximize, solver_timeout))
@@ -831,6 +858,7 @@ def get_model(constraints, minimize=(), maximize=(), solver_timeout=None, verdic
             status, factory = "unknown", None
     finally:
         pool.terminate()
+        timing["solver_pool"] += time.perf_counter() - t_pool
 
     if status == "sat":
         model_cache.model_cache.put(factory(), 1)
@@ -945,3 +973,5 @@ def reset_caches() -> None:
     model_cache = ModelCache(engine)
     for k in counters:
         counters[k] = 0
+    for k in timing:
+        timing[k] = 0.0

@@ -58,3 +58,30 @@ def test_calls_avoided_leg_counts_at_get_model(monkeypatch):
         assert d["solver_calls_avoided"] == d["get_model_calls"] - d["solver_calls"]
     assert off["candidate_answers"] == 0 and off["quick_sat_answers"] == 12
     assert on["solver_calls_avoided"] >= off["solver_calls_avoided"]
+
+
+def test_two_rank_line_under_gloo_with_the_oracle_engine():
+    """bench.py's N > 1 protocol end to end on CPU: torchrun world 2, gloo, the oracle answering
+    for the GPU (--engine oracle).  The line keeps the driver's keys, the per-rank split of
+    kernel / all-reduce / barrier time, and the planted first hits of the global model order."""
+    import json
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--engine", "oracle", "--config", "c2", "--tapes", "50", "--models", "64",
+                        "--steps", "2", "--warmup", "1"], capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "per_rank", "parity_ok"):
+        assert k in line, k
+    assert line["n_gpus"] == 2 and line["steps"] == 2 and line["parity_ok"] is True
+    assert line["config"]["models_total"] == 128
+    pr = line["per_rank"]
+    for k in ("kernel_ms", "allreduce_ms", "barrier_wait_ms"):
+        assert 0 <= pr[k]["min"] <= pr[k]["max"], (k, pr[k])
+    assert line["engine"].startswith("oracle")
