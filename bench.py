@@ -323,6 +323,7 @@ def calls_avoided_leg(ev, n_forks: int = 256, n_models: int = 100, seed: int = 2
             cs = [sp.Constraints(st) for st in states]
             eng = sp.model_cache.engine
             e0, l0 = sum(eng.timing.values()), eng.launches
+            t_stage0 = dict(eng.timing)
             t0 = time.perf_counter()
             alive = sp.is_possible_batch(cs)
             dt = time.perf_counter() - t0
@@ -330,6 +331,7 @@ def calls_avoided_leg(ev, n_forks: int = 256, n_models: int = 100, seed: int = 2
             mc = sp.model_cache.stats
             avoided = c["get_model_calls"] - c["solver_calls"]
             engine_s = sum(eng.timing.values()) - e0
+            stage_ms = {k: (eng.timing[k] - t_stage0[k]) * 1e3 / len(cs) for k in eng.timing}
             pool_s = sp.timing["solver_pool"]
             out["candidates_on" if cand else "candidates_off"] = {
                 **c, "states_alive": int(sum(alive)), "solver_calls_avoided": avoided,
@@ -340,7 +342,8 @@ def calls_avoided_leg(ev, n_forks: int = 256, n_models: int = 100, seed: int = 2
                 "engine_ms_per_state": engine_s * 1e3 / len(cs),
                 "solver_pool_ms_per_state": pool_s * 1e3 / len(cs),
                 "other_ms_per_state": (dt - engine_s - pool_s) * 1e3 / len(cs),
-                "engine_launches": eng.launches - l0,
+                "engine_launches": eng.launches - l0, "engine_stage_ms_per_state": stage_ms,
+                "conjunct_batches_reused": eng.stats.get("conjunct_batches_reused", 0),
                 "late_fills": mc.get("late_fills", 0), "late_fill_exprs": mc.get("late_fill_exprs", 0),
                 "candidate_budget": budget if cand else 0, "solver_stand_in_calls": solver.calls,
                 "models_inserted_by_solver": solver.sat_calls}
@@ -611,11 +614,13 @@ def main():
         cols_g, cols_live = ct.column_asm_split() if n_cols else (0, False)
         kcols = int(ct.keccak_columns()) if n_cols else 0
         kpreds = int(ct.keccak_predicate_columns()) if n_cols else 0
-        kernel_split = {"tapes": tb.n_tapes, "tapes_p": n_p, "tapes_g": n_g,
-                        "tapes_cpp": tb.n_tapes - ((n_p + n_g) if asm_live else 0),
+        n_fc, cols_fc = ct.flat_split()
+        kernel_split = {"tapes": tb.n_tapes, "tapes_p": n_p, "tapes_g": n_g, "tapes_flat": n_fc,
+                        "tapes_cpp": tb.n_tapes - ((n_p + n_g + n_fc) if asm_live else 0),
+                        "columns_flat": cols_fc,
                         "columns": n_cols, "columns_g": cols_g if cols_live else 0, "columns_keccak": kcols,
                         "columns_keccak_predicates": kpreds,
-                        "columns_cpp": n_cols - kcols - kpreds - (cols_g if cols_live else 0)}
+                        "columns_cpp": n_cols - kcols - kpreds - cols_fc - (cols_g if cols_live else 0)}
     if world > 1 and not oracle and args.dist_backend == "nccl":
         red_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 

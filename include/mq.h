@@ -346,6 +346,9 @@ int mq_tapes_qsa_split(mq_tapes* tapes, int32_t* n_p, int32_t* n_g, int32_t* liv
    mode 3) for the current model batch, and whether that path ran (the others, and all of them
    when it did not, run on the HIP C++ column kernel).  Introspection for tests and the bench. */
 int mq_tapes_column_split(mq_tapes* tapes, int32_t* n_asm, int32_t* live);
+/* Tapes / hoisted Bool columns of the current translation that run on the flat-conjunction
+   kernel (an AND of Bool variables and variable-constant compares: no interpreter). */
+int mq_tapes_flat_split(mq_tapes* tapes, int32_t* n_flat_tapes, int32_t* n_flat_columns);
 
 /* Hoisted columns that are exactly keccak256(concat of model variables and constants) — the
    keccak applications of kfm.py:95-114 / instructions.py:1043-1052 over candidate models —

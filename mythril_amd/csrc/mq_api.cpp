@@ -405,6 +405,10 @@ struct mq_tapes {
   uint64_t kc_gen = ~0ull;                      // models_gen of the uploaded map
   DevBuf kc_cols_dev, kc_map_dev, kc_pred_dev;
   std::vector<char> col_direct_mask;            // per column: its lane masks are stored by its kernel
+  // flat conjunctions (fc.hip): QSA-eligible tapes that are an AND of Bool variables and
+  // variable-constant compares, run on fc_kernel instead of P / G (per model batch: qsa_prepare)
+  int fc_count = 0;
+  DevBuf fc_tapes_dev, fc_mask_dev, fc_cmp_dev;
   // multi-device context: the same batch compiled on each peer device (ctx->peers order)
   std::vector<mq_tapes*> peers;
   ~mq_tapes() {
@@ -2474,6 +2478,130 @@ static void plan_stage(const mq_ctx* c, const std::vector<int64_t>& pushes, cons
 // (Re)translate the QSA-eligible tapes for the current model batch (variable rows, function
 // table): the P kernel when every variable a tape reads is preloaded, the G kernel otherwise.
 // If one tape does not translate, the whole group runs on the HIP C++ kernel for this batch.
+// A flat conjunction (fc.hip): the stack program of x, run abstractly, leaves an AND of Bool
+// variables (negated or not) and compares of one model variable of at most 256 bits with a
+// constant; temps, arithmetic and anything else do not match.  Bool variables without a lane-mask
+// index are compared with their 0/1 row.  Appends the masks / compares to the lists.
+static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_t>& masks, std::vector<FcCmp>& cmps) {
+  struct Item {
+    int kind = 0;   // 0 model variable (BV), 1 constant, 2 conjunction
+    uint32_t v = 0;
+    std::vector<uint32_t> m;
+    std::vector<FcCmp> q;
+  };
+  std::vector<Item> st;
+  const auto& pr = x.prog;
+  auto bool_item = [&](uint32_t v, bool neg, Item& it) {
+    it.kind = 2;
+    if (v < c->bmask_of_var.size() && c->bmask_of_var[v] >= 0) {
+      it.m.push_back((uint32_t)c->bmask_of_var[v] | (neg ? 0x80000000u : 0u));
+    } else {
+      FcCmp q{};
+      q.row = c->var_off_h[v];
+      q.nl = 1;
+      q.op = neg ? FC_NE : FC_EQ;
+      q.c[0] = 1;
+      it.q.push_back(q);
+    }
+  };
+  for (size_t pc = 0; pc < pr.size(); pc++) {
+    const uint32_t w = pr[pc], op = w & 0xFFu, imm = w >> 12;
+    if (op == G_END) break;
+    if (has_imm2(op)) return false;
+    Item it;
+    switch (op) {
+      case G_PUSH_VAR:
+        if (imm >= c->var_nl_h.size() || c->var_width[imm] == 0 || c->var_nl_h[imm] > 8) return false;
+        it.kind = 0;
+        it.v = imm;
+        st.push_back(std::move(it));
+        break;
+      case G_PUSH_VAR_B:
+        if (imm >= c->var_nl_h.size() || c->var_width[imm] != 0) return false;
+        bool_item(imm, false, it);
+        st.push_back(std::move(it));
+        break;
+      case G_PUSH_CONST:
+        if ((size_t)imm + 8 > x.consts.size()) return false;
+        it.kind = 1;
+        it.v = imm;
+        st.push_back(std::move(it));
+        break;
+      case G_PUSH_BOOL:
+        if (imm != 1) return false;
+        it.kind = 2;   // TRUE: the empty conjunction
+        st.push_back(std::move(it));
+        break;
+      case G_NOT: {
+        if (st.empty() || st.back().kind != 2) return false;
+        Item& a = st.back();
+        if (a.m.size() + a.q.size() != 1) return false;
+        if (!a.m.empty()) {
+          a.m[0] ^= 0x80000000u;
+        } else {
+          static const uint32_t neg[6] = {FC_NE, FC_EQ, FC_GE, FC_GT, FC_LE, FC_LT};
+          a.q[0].op = neg[a.q[0].op];
+        }
+        break;
+      }
+      case G_AND: {
+        if (st.size() < 2 || st.back().kind != 2 || st[st.size() - 2].kind != 2) return false;
+        Item b = std::move(st.back());
+        st.pop_back();
+        Item& a = st.back();
+        a.m.insert(a.m.end(), b.m.begin(), b.m.end());
+        a.q.insert(a.q.end(), b.q.begin(), b.q.end());
+        break;
+      }
+      case G_EQ: case G_ULT: case G_ULE: case G_UGT: case G_UGE:
+      case G_SLT: case G_SLE: case G_SGT: case G_SGE: {
+        if (st.size() < 2) return false;
+        Item r = std::move(st.back());
+        st.pop_back();
+        Item l = std::move(st.back());
+        st.pop_back();
+        bool swap;
+        if (l.kind == 0 && r.kind == 1) swap = false;
+        else if (l.kind == 1 && r.kind == 0) swap = true;
+        else return false;
+        const Item& var = swap ? r : l;
+        const Item& cst = swap ? l : r;
+        const uint32_t wdt = imm;
+        if (wdt == 0 || c->var_width[var.v] != wdt) return false;
+        FcCmp q{};
+        q.row = c->var_off_h[var.v];
+        q.nl = c->var_nl_h[var.v];
+        for (uint32_t i = 0; i < q.nl; i++) q.c[i] = x.consts[cst.v + i];
+        const bool sgn = op >= G_SLT;
+        // x OP c with the variable on the left; a constant on the left mirrors the order
+        uint32_t o;
+        switch (op) {
+          case G_EQ: o = FC_EQ; break;
+          case G_ULT: case G_SLT: o = swap ? FC_GT : FC_LT; break;
+          case G_ULE: case G_SLE: o = swap ? FC_GE : FC_LE; break;
+          case G_UGT: case G_SGT: o = swap ? FC_LT : FC_GT; break;
+          default: o = swap ? FC_LE : FC_GE; break;
+        }
+        q.op = o;
+        if (sgn) {
+          q.flip = 1u << ((wdt - 1) % 32);
+          q.c[q.nl - 1] ^= q.flip;
+        }
+        it.kind = 2;
+        it.q.push_back(q);
+        st.push_back(std::move(it));
+        break;
+      }
+      default:
+        return false;
+    }
+  }
+  if (st.size() != 1 || st[0].kind != 2) return false;
+  masks.insert(masks.end(), st[0].m.begin(), st[0].m.end());
+  cmps.insert(cmps.end(), st[0].q.begin(), st[0].q.end());
+  return true;
+}
+
 static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
   if (T->qsa_gen == c->models_gen) return MQ_OK;
   T->qsa_gen = c->models_gen;
@@ -2486,6 +2614,15 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
   const int64_t nq = (int64_t)T->qct.size();
   std::vector<char> on_p(nq, 0);
   std::unique_ptr<PhaseTimer> pt(new PhaseTimer(&c->host_t[3]));
+  // flat conjunctions first: they run on fc_kernel (no interpreter); MQ_NO_FLAT=1 keeps them on P / G
+  const bool no_flat = std::getenv("MQ_NO_FLAT") != nullptr;
+  std::vector<char> on_fc(nq, 0);
+  std::vector<std::vector<uint32_t>> fc_m(nq);
+  std::vector<std::vector<FcCmp>> fc_q(nq);
+  if (!no_flat)
+    parallel_for(nq, 32, [&](int, int64_t b, int64_t e) {
+      for (int64_t i = b; i < e; i++) on_fc[i] = fc_match(c, T->qct[i], fc_m[i], fc_q[i]) ? 1 : 0;
+    });
   // (P preloads variables 0-7 only: a program pushing any other variable is not tried on P)
   auto p_candidate = [](const CompiledTape& x) {
     for (size_t pc = 0; pc < x.prog.size(); pc++) {
@@ -2501,11 +2638,11 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
   if (!latency)
     parallel_for(nq, 32, [&](int, int64_t b, int64_t e) {
       for (int64_t i = b; i < e; i++)
-        on_p[i] = p_candidate(T->qct[i]) && qsa_translate(c, 0, true, T->qct[i], nullptr, nullptr) ? 1 : 0;
+        on_p[i] = !on_fc[i] && p_candidate(T->qct[i]) && qsa_translate(c, 0, true, T->qct[i], nullptr, nullptr) ? 1 : 0;
     });
   std::vector<int64_t> pushes(c->var_nl_h.size(), 0);
   for (size_t i = 0; i < T->qct.size(); i++) {
-    if (on_p[i]) continue;
+    if (on_p[i] || on_fc[i]) continue;
     const auto& pr = T->qct[i].prog;
     for (size_t pc = 0; pc < pr.size(); pc++) {
       const uint32_t op = pr[pc] & 0xFFu, imm = pr[pc] >> 12;
@@ -2531,9 +2668,9 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
   }
   int g_temps = 0;
   for (size_t i = 0; i < T->qct.size(); i++)
-    if (!on_p[i]) g_temps = std::max(g_temps, qsa_temps(T->qct[i], 1));
+    if (!on_p[i] && !on_fc[i]) g_temps = std::max(g_temps, qsa_temps(T->qct[i], 1));
   int64_t n_g = 0;
-  for (size_t i = 0; i < T->qct.size(); i++) n_g += on_p[i] ? 0 : 1;
+  for (size_t i = 0; i < T->qct.size(); i++) n_g += (on_p[i] || on_fc[i]) ? 0 : 1;
   const double g_share = n_g ? std::min(1.0, 4.0 * (double)g_tapes_per_group(n_g, c->M) / (double)n_g) : 1.0;
   plan_stage(c, pushes, &T->gpre, g_temps, g_share, T->gstage, T->stage_rows);
   T->qhist[0].assign(QK_COUNT, 0);
@@ -2548,6 +2685,10 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
   parallel_for(nq, 32, [&](int, int64_t b, int64_t e) {
     std::vector<uint32_t> ex;
     for (int64_t i = b; i < e && !g_fail.load(std::memory_order_relaxed); i++) {
+      if (on_fc[i]) {
+        kind_of[i] = 2;
+        continue;
+      }
       if (on_p[i] && qsa_translate(c, 0, true, T->qct[i], &trs[i], &ex)) continue;
       kind_of[i] = 1;
       if (!qsa_translate(c, 1, true, T->qct[i], &trs[i], &ex, &T->gpre, &T->gstage)) {
@@ -2558,8 +2699,26 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
     }
   });
   if (g_fail) return MQ_OK;
+  std::vector<FcTape> fct;
+  std::vector<uint32_t> fcm;
+  std::vector<FcCmp> fcq;
   for (int64_t i = 0; i < nq; i++) {
     const int k = kind_of[i];
+    if (k == 2) {
+      FcTape f{};
+      f.out = T->qbase[i].tape;
+      f.mask_out = -1;
+      f.mask_off = (uint32_t)fcm.size();
+      f.n_mask = (uint32_t)fc_m[i].size();
+      f.cmp_off = (uint32_t)fcq.size();
+      f.n_cmp = (uint32_t)fc_q[i].size();
+      f.n_nodes = T->qbase[i].n_nodes;
+      f.alg_ops = T->qbase[i].alg_ops;
+      fcm.insert(fcm.end(), fc_m[i].begin(), fc_m[i].end());
+      fcq.insert(fcq.end(), fc_q[i].begin(), fc_q[i].end());
+      fct.push_back(f);
+      continue;
+    }
     const std::vector<uint32_t>& t = trs[i];
     qsa_count(c, k, t, T->qhist[k], k == 1 ? &T->qpairs : &T->qpairs_p);
     GDesc d = T->qbase[i];
@@ -2602,6 +2761,14 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
   if (descs.empty()) descs.push_back(GDesc{});
   HIPCHK(T->qdescs.upload(descs.data(), descs.size(), c->stream));
   HIPCHK(T->qprog.upload(prog.data(), prog.size(), c->stream));
+  T->fc_count = (int)fct.size();
+  if (!fct.empty()) {
+    HIPCHK(T->fc_tapes_dev.upload(fct.data(), fct.size(), c->stream));
+    if (fcm.empty()) fcm.push_back(0);
+    if (fcq.empty()) fcq.push_back(FcCmp{});
+    HIPCHK(T->fc_mask_dev.upload(fcm.data(), fcm.size(), c->stream));
+    HIPCHK(T->fc_cmp_dev.upload(fcq.data(), fcq.size(), c->stream));
+  }
   if (T->stage_rows.empty()) HIPCHK(T->stage_dev.ensure(sizeof(uint32_t)));
   else HIPCHK(T->stage_dev.upload(T->stage_rows.data(), T->stage_rows.size(), c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -3036,6 +3203,27 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     HIPCHK(start_timer());
     HIPCHK(launch_qsa(k, T->qargs[k].as<QArgs>(), gx, gy, lds, st));
   }
+  if (use_qsa && T->fc_count > 0) {
+    FcArgs f{};
+    f.tapes = T->fc_tapes_dev.as<FcTape>();
+    f.n = T->fc_count;
+    const int64_t tiles = (c->M + 63) / 64;
+    f.tpg = latency ? 1 : (int)std::max<int64_t>(1, std::min<int64_t>(f.n, (f.n * tiles + 65535) / 65536));
+    f.mask_idx = T->fc_mask_dev.as<uint32_t>();
+    f.cmps = T->fc_cmp_dev.as<FcCmp>();
+    f.vars = c->vars.as<uint32_t>();
+    f.bool_masks = c->bmasks.as<uint64_t>();
+    f.n_bool_masks = c->n_bmask;
+    f.mode = verdicts ? 1 : 0;
+    f.early_exit = verdicts ? 0 : c->early_exit;
+    f.M = c->M;
+    f.index_base = c->index_base;
+    f.best = best;
+    f.verdicts = verdicts;
+    f.counters = c->counters.as<unsigned long long>();
+    HIPCHK(start_timer());
+    HIPCHK(launch_fc(f, st));
+  }
   for (const auto& v : cpp) {
     if (v.count <= 0) continue;
     KArgs a = make_args(c, T, v);
@@ -3350,6 +3538,13 @@ int mq_qsa_profile(mq_ctx* c, int64_t* out, int32_t cap, int32_t* n_out, int res
     if (reset) HIPCHK(hipMemset(d->prof.p, 0, (size_t)kQsaProfBytes));
   }
   for (int i = 0; i < std::min(n, cap); i++) out[i] = sum[i];
+  return MQ_OK;
+}
+
+int mq_tapes_flat_split(mq_tapes* T, int32_t* n_flat_tapes, int32_t* n_flat_columns) {
+  if (!T) return MQ_ERR_ARG;
+  if (n_flat_tapes) *n_flat_tapes = T->qsa_live ? T->fc_count : 0;
+  if (n_flat_columns) *n_flat_columns = 0;
   return MQ_OK;
 }
 

@@ -157,5 +157,47 @@ hipError_t launch_keccak_columns(const KcCol* cols, int n_cols, const KcMapEntry
                                  uint32_t* vars, int64_t M, unsigned long long* counters, uint64_t* bool_masks,
                                  int n_bool_masks, int bool_rows, hipStream_t st);
 
+// Flat conjunctions (fc.hip, mq_api.cpp fc_match): a tape or Bool column that is an AND of Bool
+// model variables (negated or not) and comparisons of one variable with a constant.
+enum FcOp : uint32_t { FC_EQ = 0, FC_NE = 1, FC_LT = 2, FC_LE = 3, FC_GT = 4, FC_GE = 5 };
+struct FcCmp {
+  uint32_t row;     // first limb row of the variable
+  uint32_t nl;      // its limbs (1..8)
+  uint32_t op;      // FcOp, unsigned over the nl limbs
+  uint32_t flip;    // XOR-ed into the variable's top limb (a signed compare's sign bit; c pre-flipped)
+  uint32_t c[8];    // the constant, little-endian limbs
+};
+struct FcTape {
+  uint32_t out;       // modes 0/1: tape index; mode 3: the Bool column's variable row
+  int32_t mask_out;   // mode 3: its packed lane-mask index (-1: none, the 0/1 row is written)
+  uint32_t mask_off;  // its Bool variables: FcArgs.mask_idx[mask_off ..] = mask index | negated << 31
+  uint32_t n_mask;
+  uint32_t cmp_off;   // its compares: FcArgs.cmps[cmp_off ..]
+  uint32_t n_cmp;
+  uint32_t n_nodes;   // DAG nodes (metric)
+  uint32_t alg_ops;   // SURVEY §8(d) algorithmic ops per model (metric)
+};
+struct FcArgs {
+  const FcTape* tapes;
+  int n;                         // tapes / columns of the launch
+  int tpg;                       // per wave (grid.y = groups)
+  const uint32_t* mask_idx;
+  const FcCmp* cmps;
+  const uint32_t* vars;
+  const uint64_t* bool_masks;    // [tile][n_bool_masks] packed Bool rows (read)
+  uint64_t* bool_masks_out;      // mode 3: the same array, the level's columns written
+  uint32_t* vars_out;            // mode 3: 0/1 rows
+  int n_bool_masks;
+  int mode;                      // 0 first hit, 1 verdict bytes, 3 Bool columns
+  int early_exit;
+  int bool_rows;                 // mode 3: also write the 0/1 row of a column with a mask index
+  int64_t M;
+  int64_t index_base;
+  int32_t* best;
+  uint8_t* verdicts;             // mode 1: [tape][M] bytes
+  unsigned long long* counters;
+};
+hipError_t launch_fc(const FcArgs& a, hipStream_t st);
+
 }  // namespace mq
 #endif

@@ -63,6 +63,7 @@ def load_library(path: str = LIB_PATH):
         L.mq_tapes_info.argtypes = [P] + [C.POINTER(C.c_int32)] * 3
         L.mq_tapes_qsa_split.argtypes = [P] + [C.POINTER(C.c_int32)] * 3
         L.mq_tapes_column_split.argtypes = [P] + [C.POINTER(C.c_int32)] * 2
+        L.mq_tapes_flat_split.argtypes = [P] + [C.POINTER(C.c_int32)] * 2
         L.mq_tapes_column_keccak.argtypes = [P, C.POINTER(C.c_int32)]
         L.mq_tapes_qsa_histogram.argtypes = [P, C.c_int32, C.POINTER(C.c_int64), C.c_int32, C.POINTER(C.c_int64),
                                              C.POINTER(C.c_int32)]
@@ -246,6 +247,12 @@ class CompiledTapes:
         a, b, c = C.c_int32(), C.c_int32(), C.c_int32()
         _check(self.ev.lib.mq_tapes_qsa_split(self.handle, C.byref(a), C.byref(b), C.byref(c)), "mq_tapes_qsa_split")
         return a.value, b.value, bool(c.value)
+
+    def flat_split(self):
+        """After a launch: (tapes, hoisted Bool columns) on the flat-conjunction kernel (fc.hip)."""
+        a, b = C.c_int32(), C.c_int32()
+        _check(self.ev.lib.mq_tapes_flat_split(self.handle, C.byref(a), C.byref(b)), "mq_tapes_flat_split")
+        return a.value, b.value
 
     def column_asm_split(self):
         """After a launch: (hoisted columns on the general assembly kernel, whether that path ran)."""

@@ -227,6 +227,8 @@ class VerdictEngine:
     # launches of at most this many waves run the G kernel one tape per wave (MQ_OPT_LATENCY_WAVES)
     latency_waves = int(os.environ.get("MQ_LATENCY_WAVES", "4096"))
     STAGES = ("lower", "serialize", "upload", "compile", "evaluate")
+    # a compiled conjunct batch is launched again for a subset of its conjuncts up to this size
+    REUSE_MAX = 4096
 
     def __init__(self, evaluator=None):
         from .lower import IncrementalLowering
@@ -437,7 +439,9 @@ class VerdictEngine:
             prev = self._conj_ct
             # (the evaluator that compiled it is part of the key: a batch is bound to its context)
             gen = (inc.dag_gen, inc.slot_epoch, id(self._ev))
-            if prev is not None and prev[0] == gen and len(prev[1]) <= 4 * n_unk + 64 and \
+            # (a superset launch costs device microseconds per extra conjunct; compiling the subset
+            # costs ~1 ms: reuse while the superset is at most REUSE_MAX conjuncts)
+            if prev is not None and prev[0] == gen and len(prev[1]) <= max(4 * n_unk + 64, self.REUSE_MAX) and \
                     np.isin(todo, prev[1], assume_unique=True).all():
                 todo, ct = prev[1], prev[2]
                 self.stats["conjunct_batches_reused"] += 1

@@ -360,3 +360,64 @@ def const_op_workload(seed: int, n_tapes: int, n_models: int):
             root = t.or_(cmp(x, y), t.eq(x, t.const(interesting_value(rng, w), w)))
         tapes.append(t.finish(root))
     return TapeBatch(tapes), fuzz_models(rng, var_widths, n_models, funcs)
+
+
+# ---------------------------------------------------------------- flat conjunctions (fc.hip parity)
+FLAT_WIDTHS = (1, 8, 31, 32, 33, 64, 160, 255, 256)
+
+
+def flat_workload(seed: int, n_tapes: int, n_models: int, n_bool: int = 6, planted_frac: float = 0.5,
+                  max_items: int = 12):
+    """Tapes that are ANDs of Bool variables (negated or not) and comparisons of one variable with
+    a constant -- every predicate (EQ / distinct / unsigned and signed orders), the constant on
+    either side, NOT over a compare, widths that end inside a limb -- the shape the flat-
+    conjunction kernel (fc.hip) takes.  About ``planted_frac`` of the tapes are built to hold on a
+    random model (items chosen true there, constants at or next to its values).  Returns
+    (tapes, models)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    bv_widths = [int(w) for w in rng.choice(FLAT_WIDTHS, 10)] + [256, 8]
+    var_widths = [BOOL] * n_bool + bv_widths
+    mb = fuzz_models(rng, var_widths, n_models)
+    preds = ("eq", "distinct", "ult", "ule", "ugt", "uge", "slt", "sle", "sgt", "sge")
+
+    def holds(p, x, c, w):
+        sx = x - (1 << w) if x >> (w - 1) else x
+        sc = c - (1 << w) if c >> (w - 1) else c
+        return {"eq": x == c, "distinct": x != c, "ult": x < c, "ule": x <= c, "ugt": x > c, "uge": x >= c,
+                "slt": sx < sc, "sle": sx <= sc, "sgt": sx > sc, "sge": sx >= sc}[p]
+
+    tapes = []
+    for _ in range(n_tapes):
+        t = Tape()
+        target = int(rng.integers(n_models)) if rng.random() < planted_frac else None
+        items = []
+        for _ in range(int(rng.integers(1, max_items + 1))):
+            if rng.random() < 0.4:
+                v = int(rng.integers(n_bool))
+                b = t.var(v, BOOL)
+                val = mb.var_value(v, target) if target is not None else int(rng.integers(2))
+                items.append(b if val or target is None and rng.random() < 0.5 else t.not_(b))
+                continue
+            v = n_bool + int(rng.integers(len(bv_widths)))
+            w = var_widths[v]
+            m = (1 << w) - 1
+            if target is not None:
+                x = mb.var_value(v, target)
+                c = (x + int(rng.integers(-1, 2))) & m if rng.random() < 0.7 else interesting_value(rng, w)
+            else:
+                c = interesting_value(rng, w)
+            p = str(rng.choice(preds))
+            left = rng.random() < 0.3           # the constant on the left: c OP x
+            negate = rng.random() < 0.2
+            if target is not None:
+                xv = mb.var_value(v, target)
+                ok = holds(p, c, xv, w) if left else holds(p, xv, c, w)
+                if ok == negate:                 # make the item true on the target
+                    negate = not negate
+            a, b = (t.const(c, w), t.var(v, w)) if left else (t.var(v, w), t.const(c, w))
+            node = getattr(t, p)(a, b)
+            items.append(t.not_(node) if negate else node)
+        if rng.random() < 0.1:
+            items.append(t.true())
+        tapes.append(t.finish(t.and_(*items)))
+    return TapeBatch(tapes), mb

@@ -1171,3 +1171,68 @@ def test_g_kernel_calldata_words_and_signed_constant_compares(evaluator, monkeyp
     assert 0.02 < v.mean() < 0.98
     fh_ref, _ = cref.first_hit(tb, mb)
     assert (evaluator.first_hit(ct) == fh_ref).all()
+
+
+# ---------------------------------------------------------------- flat conjunctions (fc.hip)
+@pytest.mark.parametrize("bmask_cap", [None, "0", "3"])
+def test_flat_conjunctions_match_oracle(evaluator, monkeypatch, bmask_cap):
+    """ANDs of Bool variables and variable-constant compares (every predicate, constant on either
+    side, NOT, widths ending inside a limb) on the flat-conjunction kernel: first hits and the
+    verdict matrix against the oracle, and against the same batch on the interpreters
+    (MQ_NO_FLAT=1).  bmask_cap "0" / "3": none / some of the Bool variables have a packed lane
+    mask, the others are read from their 0/1 rows."""
+    from mythril_amd.synth import flat_workload
+    if bmask_cap is not None:
+        monkeypatch.setenv("MQ_BMASK_CAP", bmask_cap)
+    tb, mb = flat_workload(31, 300, 1000)
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    fh = evaluator.first_hit(ct)
+    n_flat, _ = ct.flat_split()
+    assert n_flat >= 0.9 * tb.n_tapes, n_flat
+    ref, _ = cref.first_hit(tb, mb)
+    assert (fh == ref).all(), np.flatnonzero(fh != ref)[:10]
+    assert (ref >= 0).mean() > 0.4
+    v, fh2 = evaluator.verdicts(ct)
+    vref = cref.verdicts(tb, mb)
+    assert (v == vref).all() and (fh2 == ref).all()
+    monkeypatch.setenv("MQ_NO_FLAT", "1")
+    ct2 = evaluator.compile(tb)
+    assert (evaluator.first_hit(ct2) == ref).all() and ct2.flat_split()[0] == 0
+    ct.free()
+    ct2.free()
+
+
+def test_flat_conjunctions_ragged_and_sharded(evaluator):
+    """Model counts that end inside a tile, and a shard with a nonzero index base."""
+    from mythril_amd.synth import flat_workload
+    for M in (1, 63, 65, 200):
+        tb, mb = flat_workload(32 + M, 80, M)
+        evaluator.upload_models(mb)
+        fh = evaluator.first_hit(tb)
+        assert (fh == cref.first_hit(tb, mb)[0]).all(), M
+    tb, mb = flat_workload(40, 120, 700)
+    sh = mb.shard(300, 700)
+    evaluator.upload_models(sh)
+    assert (evaluator.first_hit(tb) == cref.first_hit(tb, sh)[0]).all()
+
+
+def test_c4_tapes_on_the_flat_kernel(evaluator, monkeypatch):
+    """C4's hoisted tapes (ANDs of keccak-predicate / calldata Bool columns and word compares) run
+    on the flat-conjunction kernel; first hits and verdicts equal the unhoisted oracle's, with the
+    flat path on and off."""
+    from mythril_amd.synth_evm import c4_workload
+    plain = c4_workload(40, 1500, seed=24, planted_frac=0.4, hasher_many=evaluator.keccak256_array)
+    tb, mb, exp, _ = c4_workload(40, 1500, seed=24, planted_frac=0.4, hasher_many=evaluator.keccak256_array,
+                                 interpret_keccak=True, hoist=True)
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    fh = evaluator.first_hit(ct)
+    assert ct.flat_split()[0] >= 0.9 * tb.n_tapes, ct.flat_split()
+    ref, _ = cref.first_hit(plain[0], plain[1])
+    assert (ref == exp).all() and (fh == ref).all()
+    v, _ = evaluator.verdicts(ct)
+    assert (v == cref.verdicts(plain[0], plain[1])).all()
+    monkeypatch.setenv("MQ_NO_FLAT", "1")
+    ct2 = evaluator.compile(tb)
+    assert (evaluator.first_hit(ct2) == ref).all() and ct2.flat_split()[0] == 0
