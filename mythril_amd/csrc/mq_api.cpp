@@ -408,7 +408,8 @@ struct mq_tapes {
   // flat conjunctions (fc.hip): QSA-eligible tapes that are an AND of Bool variables and
   // variable-constant compares, run on fc_kernel instead of P / G (per model batch: qsa_prepare)
   int fc_count = 0;
-  DevBuf fc_tapes_dev, fc_mask_dev, fc_cmp_dev;
+  int fc_stage_n = 0;
+  DevBuf fc_tapes_dev, fc_mask_dev, fc_cmp_dev, fc_stage_dev;
   // multi-device context: the same batch compiled on each peer device (ctx->peers order)
   std::vector<mq_tapes*> peers;
   ~mq_tapes() {
@@ -2482,6 +2483,9 @@ static void plan_stage(const mq_ctx* c, const std::vector<int64_t>& pushes, cons
 // variables (negated or not) and compares of one model variable of at most 256 bits with a
 // constant; temps, arithmetic and anything else do not match.  Bool variables without a lane-mask
 // index are compared with their 0/1 row.  Appends the masks / compares to the lists.
+// LDS rows of the flat-conjunction kernel's staging (256 B each: 24 KB per workgroup)
+static constexpr int kFcStageRows = 96;
+
 static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_t>& masks, std::vector<FcCmp>& cmps) {
   struct Item {
     int kind = 0;   // 0 model variable (BV), 1 constant, 2 conjunction
@@ -2596,7 +2600,7 @@ static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_
         return false;
     }
   }
-  if (st.size() != 1 || st[0].kind != 2) return false;
+  if (st.size() != 1 || st[0].kind != 2 || st[0].m.size() > 30000) return false;
   masks.insert(masks.end(), st[0].m.begin(), st[0].m.end());
   cmps.insert(cmps.end(), st[0].q.begin(), st[0].q.end());
   return true;
@@ -2709,12 +2713,20 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
       f.out = T->qbase[i].tape;
       f.mask_out = -1;
       f.mask_off = (uint32_t)fcm.size();
-      f.n_mask = (uint32_t)fc_m[i].size();
+      // byte offsets of the plain masks, then of the negated ones, each group padded to 16
+      // entries (fc.hip reads a group sixteen at a time)
+      uint32_t n_pos = 0, n_neg = 0;
+      for (uint32_t e : fc_m[i])
+        if (!(e >> 31)) fcm.push_back(8u * e), n_pos++;
+      while (fcm.size() % 16) fcm.push_back(fcm.back());   // (a repeated mask: the same AND)
+      for (uint32_t e : fc_m[i])
+        if (e >> 31) fcm.push_back(8u * (e & 0x7FFFFFFFu)), n_neg++;
+      while (fcm.size() % 16) fcm.push_back(fcm.back());
+      f.n_mask = n_pos | (n_neg << 16);
       f.cmp_off = (uint32_t)fcq.size();
       f.n_cmp = (uint32_t)fc_q[i].size();
       f.n_nodes = T->qbase[i].n_nodes;
       f.alg_ops = T->qbase[i].alg_ops;
-      fcm.insert(fcm.end(), fc_m[i].begin(), fc_m[i].end());
       fcq.insert(fcq.end(), fc_q[i].begin(), fc_q[i].end());
       fct.push_back(f);
       continue;
@@ -2762,7 +2774,33 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
   HIPCHK(T->qdescs.upload(descs.data(), descs.size(), c->stream));
   HIPCHK(T->qprog.upload(prog.data(), prog.size(), c->stream));
   T->fc_count = (int)fct.size();
+  T->fc_stage_n = 0;
   if (!fct.empty()) {
+    // stage the compared variables read by the most compares in LDS (up to kFcStageRows rows)
+    std::map<uint32_t, std::pair<int64_t, uint32_t>> use;   // first row -> (compares, limbs)
+    for (const FcCmp& q : fcq) {
+      auto& u = use[q.row];
+      u.first++;
+      u.second = std::max(u.second, q.nl);
+    }
+    std::vector<std::pair<int64_t, uint32_t>> order;
+    for (const auto& kv : use) order.push_back({kv.second.first, kv.first});
+    std::stable_sort(order.begin(), order.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+    std::map<uint32_t, uint32_t> slot_of;
+    std::vector<uint32_t> srows;
+    for (const auto& o : order) {
+      const uint32_t nl = use[o.second].second;
+      if (o.first < 2 || srows.size() + nl > (size_t)kFcStageRows) continue;   // (a row read once gains nothing)
+      slot_of[o.second] = (uint32_t)srows.size();
+      for (uint32_t l = 0; l < nl; l++) srows.push_back(o.second + l);
+    }
+    for (FcCmp& q : fcq) {
+      auto it = slot_of.find(q.row);
+      if (it != slot_of.end()) q.row = 0x80000000u | it->second;
+    }
+    T->fc_stage_n = (int)srows.size();
+    if (srows.empty()) srows.push_back(0);
+    HIPCHK(T->fc_stage_dev.upload(srows.data(), srows.size(), c->stream));
     HIPCHK(T->fc_tapes_dev.upload(fct.data(), fct.size(), c->stream));
     if (fcm.empty()) fcm.push_back(0);
     if (fcq.empty()) fcq.push_back(FcCmp{});
@@ -3208,7 +3246,12 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     f.tapes = T->fc_tapes_dev.as<FcTape>();
     f.n = T->fc_count;
     const int64_t tiles = (c->M + 63) / 64;
-    f.tpg = latency ? 1 : (int)std::max<int64_t>(1, std::min<int64_t>(f.n, (f.n * tiles + 65535) / 65536));
+    // a workgroup's 4 waves split the launch's tapes on one tile (the staged rows serve all of
+    // them); more tapes than ~256 a tile, or a latency-bound launch, go to several workgroups
+    f.tpg = latency ? 1 : (int)std::max<int64_t>(1, std::min<int64_t>((f.n + 3) / 4, 64));
+    (void)tiles;
+    f.stage_rows = T->fc_stage_dev.as<uint32_t>();
+    f.n_stage = T->fc_stage_n;
     f.mask_idx = T->fc_mask_dev.as<uint32_t>();
     f.cmps = T->fc_cmp_dev.as<FcCmp>();
     f.vars = c->vars.as<uint32_t>();

@@ -161,7 +161,7 @@ hipError_t launch_keccak_columns(const KcCol* cols, int n_cols, const KcMapEntry
 // model variables (negated or not) and comparisons of one variable with a constant.
 enum FcOp : uint32_t { FC_EQ = 0, FC_NE = 1, FC_LT = 2, FC_LE = 3, FC_GT = 4, FC_GE = 5 };
 struct FcCmp {
-  uint32_t row;     // first limb row of the variable
+  uint32_t row;     // first limb row of the variable (bit 31: the first of its LDS-staged slots)
   uint32_t nl;      // its limbs (1..8)
   uint32_t op;      // FcOp, unsigned over the nl limbs
   uint32_t flip;    // XOR-ed into the variable's top limb (a signed compare's sign bit; c pre-flipped)
@@ -170,8 +170,8 @@ struct FcCmp {
 struct FcTape {
   uint32_t out;       // modes 0/1: tape index; mode 3: the Bool column's variable row
   int32_t mask_out;   // mode 3: its packed lane-mask index (-1: none, the 0/1 row is written)
-  uint32_t mask_off;  // its Bool variables: FcArgs.mask_idx[mask_off ..] = mask index | negated << 31
-  uint32_t n_mask;
+  uint32_t mask_off;  // its Bool variables: FcArgs.mask_idx[mask_off ..] = byte offset (8 x mask index)
+  uint32_t n_mask;    // plain | negated << 16 (the plain offsets first)
   uint32_t cmp_off;   // its compares: FcArgs.cmps[cmp_off ..]
   uint32_t n_cmp;
   uint32_t n_nodes;   // DAG nodes (metric)
@@ -196,6 +196,19 @@ struct FcArgs {
   int32_t* best;
   uint8_t* verdicts;             // mode 1: [tape][M] bytes
   unsigned long long* counters;
+  const uint32_t* stage_rows;    // rows staged in LDS per workgroup (FcCmp.row bit 31 = slot)
+  int n_stage;
+};
+// fc_kernel's by-value block (the read-only tables are separate __restrict__ arguments)
+struct FcRun {
+  int n, tpg, n_bool_masks, mode, early_exit, bool_rows;
+  int64_t M, index_base;
+  int32_t* best;
+  uint8_t* verdicts;
+  uint64_t* masks_out;
+  uint32_t* vars_out;
+  unsigned long long* counters;
+  int n_stage;
 };
 hipError_t launch_fc(const FcArgs& a, hipStream_t st);
 

@@ -622,8 +622,8 @@ double tape_alg_ops(const mq_tape_batch* batch, int32_t t) {
         ops += L;
         break;
       case MQ_OP_KECCAK:
-        // keccak-f[1600] permutations: one per started 136-byte block (padding included)
-        ops += kKeccakOpsPerBlock * std::floor((La * 4 + 1 + 135) / 136);
+        // keccak-f[1600] permutations: one per started 136-byte block (the pad byte included)
+        ops += kKeccakOpsPerBlock * std::floor(((n.a < (uint32_t)i ? nd[n.a].width / 8.0 : La * 4) + 1 + 135) / 136);
         break;
       default:
         return -1;

@@ -11,9 +11,19 @@ namespace mq {
 
 constexpr int kMaxWidth = 2048;   // widest value a tape may hold (64 limbs)
 
-// keccak-f[1600] cost per absorbed 136-byte block in 32-bit VALU ops; the
-// per-block instruction mix is counted in profiles/ 
-constexpr double kKeccakOpsPerBlock = 7974.0;  // counted: SQ_INSTS_VALU per lane, 2-block minus 1-block messages (profiles/r02tr/kec_{64,200}.json)
+// keccak-f[1600] cost per absorbed 136-byte block in 32-bit ops, counted from the
+// permutation's definition in two-input operations with the lane-complementing transform (the
+// Keccak team's implementation overview: one NOT per row of chi instead of five), every 64-bit
+// lane operation on two 32-bit halves (a 64-bit rotation is two funnel shifts):
+//   theta: 20 XOR (column parities) + 5 ROT + 5 XOR (D) + 25 XOR (apply) = 55
+//   rho: 24 ROT (lane 0 is not rotated); pi: a lane permutation, no op   = 24
+//   chi: 25 AND/OR + 25 XOR + 5 NOT                                      = 55
+//   iota: 1 XOR                                                          =  1
+// 135 lane ops = 270 32-bit ops per round; 24 rounds = 6 480, + 34 XOR absorbing the block's 17
+// lanes = 6 514.  (Round 4 froze the kernel's counted VALU instructions instead, 7 974 per block
+// before the v_bitop3 kernel: a count the three-input instructions then beat, 1.17 of the peak.)
+constexpr double kKeccakOpsPerBlock = 24.0 * 2.0 * (55 + 24 + 55 + 1) + 34.0;
+static_assert(kKeccakOpsPerBlock == 6514.0, "keccak-f[1600] op count");
 
 struct CompiledTape {
   bool supported = false;

@@ -163,3 +163,16 @@ def test_host_keccak_path_matches_the_kats_and_the_oracle():
     msgs = [bytes((i * 13 + n) & 0xFF for i in range(n)) for n in list(range(0, 300)) + [1000, 4096]]
     assert keccak256_host(msgs) == [keccak_ref.keccak256(m) for m in msgs]
     assert keccak256_host([]) == []
+
+
+def test_keccak_op_count_is_the_first_principles_count():
+    """keccak-f[1600] is charged 6 514 ops per 136-byte block (tape_compiler.h: 135 two-input
+    64-bit lane ops per round with lane complementing, on 32-bit halves, x 24 rounds + 34 absorb
+    XORs): a 64-byte key ++ slot message is one block, a 200-byte one two."""
+    for nbytes, blocks in ((64, 1), (135, 1), (136, 2), (200, 2)):
+        t = Tape()
+        x = t.var(0, 8 * nbytes)
+        root = t.eq(t.keccak(x), t.const(1, 256))
+        tb = TapeBatch([t.finish(root)])
+        assert evaluator.tape_alg_ops(tb, 0) == 6514 * blocks + 8, nbytes
+    assert 24 * 2 * (55 + 24 + 55 + 1) + 34 == 6514
