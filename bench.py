@@ -322,6 +322,8 @@ def calls_avoided_leg(ev, n_forks: int = 256, n_models: int = 100, seed: int = 2
                 sp.model_cache.put(m, 1)
             cs = [sp.Constraints(st) for st in states]
             eng = sp.model_cache.engine
+            lib_times = getattr(ev, "host_times", lambda reset=True: {})
+            lib_times(reset=True)
             e0, l0 = sum(eng.timing.values()), eng.launches
             t_stage0 = dict(eng.timing)
             t0 = time.perf_counter()
@@ -343,6 +345,7 @@ def calls_avoided_leg(ev, n_forks: int = 256, n_models: int = 100, seed: int = 2
                 "solver_pool_ms_per_state": pool_s * 1e3 / len(cs),
                 "other_ms_per_state": (dt - engine_s - pool_s) * 1e3 / len(cs),
                 "engine_launches": eng.launches - l0, "engine_stage_ms_per_state": stage_ms,
+                "library_phase_ms_per_state": {k: v * 1e3 / len(cs) for k, v in lib_times(reset=True).items()},
                 "conjunct_batches_reused": eng.stats.get("conjunct_batches_reused", 0),
                 "late_fills": mc.get("late_fills", 0), "late_fill_exprs": mc.get("late_fill_exprs", 0),
                 "candidate_budget": budget if cand else 0, "solver_stand_in_calls": solver.calls,

@@ -4,21 +4,27 @@
 // most of a path's conjunction: the shared sub-terms are columns and what is left per path is the
 // AND of their Bool columns plus a few word compares (C4's tapes: ~11 packed masks and 2-3
 // compares).  On the G interpreter each (tape, 64-model tile) paid the tape frame (descriptor,
-// early-exit test, program window) and ~6 threaded dispatches; here the masks are scalar loads
-// AND-ed on the scalar unit and a compare is its variable's limb rows (coalesced, all in flight
-// together) against constants held in SGPRs, one ballot each.
+// early-exit test, program window) and ~6 threaded dispatches.
 //
 // One workgroup = one 64-model tile; its 4 waves take one tape group (FcRun.tpg tapes) each:
-// grid.x = tiles, grid.y = quads of groups.  The variable rows the launch's compares read most are
-// staged in LDS once per workgroup (FcCmp.row bit 31: an LDS slot), as the G interpreter stages
-// them: every tape of the tile then reads them there instead of from L2 (C4: 200 tapes a tile).
+// grid.x = tiles, grid.y = quads of groups.  The prologue stages in LDS, once per workgroup, the
+// variable rows the launch's compares read (256 B a limb row) and the tile's packed lane masks of
+// the Bool variables the launch reads (8 B each).
+//
+// The scalar unit (one per CU, shared by its four SIMDs) bound the first versions of this
+// kernel at ~190 scalar instructions a tape; the work is therefore laid out for the vector unit:
+//  * Bool variables: lane k of a wave reads the k-th mask of the tape (k < 16; the host pads a
+//    tape's list to 16 with its last entry, and lanes 16-63 repeat lanes 0-15) from LDS, negated
+//    where the list says so (bit 0 of its LDS offset), and a four-step DPP AND across the row of
+//    16 lanes leaves the AND of all 16 in lane 15: one vector load, one LDS read, ~12 VALU;
+//  * a compare reads its variable's limbs from LDS as 64-bit pairs and compares them with the
+//    constant's (two VALU compares a pair: x < c and x == c lane masks); the predicate is three
+//    accept masks over (x < c, x == c, x > c) (host-encoded, signed compares with the sign bit
+//    pre-flipped), so no scalar branching on it.  Variables of one or two limbs (most hoisted
+//    words are narrow) take one pair, wider ones four.
 // Modes: 0 first hit (best[] atomicMin, early exit on best[]), 1 verdict bytes, 3 Bool columns
 // (packed lane mask stored, and the 0/1 row when a HIP C++ kernel reads rows or the column has no
 // mask index).
-//
-// The read-only tables are separate __restrict__ kernel arguments so that their uniform reads
-// are scalar loads (s_load) rather than vector loads and v_readfirstlane; within one launch no
-// output is read back (a column level never reads its own columns).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -28,70 +34,57 @@ namespace mq {
 
 __device__ __forceinline__ uint32_t uniform(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
-struct alignas(64) U16 {
-  uint32_t v[16];
-};
-
-// x OP c over the NL little-endian limbs of the compare's variable, in VALU: the borrow of x - c
-// (lt) and the OR of x ^ c (ne) per lane; the op turns the two lane masks into the compare's (on
-// the scalar unit).  Unsigned; a signed compare arrives with the sign bit of the top limb flipped
-// on both sides (flip is XOR-ed into the variable, the constant is pre-flipped).  A staged
-// variable's limbs are LDS reads at fixed offsets from its slot, all issued before the first use.
-template <int NL>
-__device__ __forceinline__ uint64_t fc_compare_nl(const FcCmp& q, const uint32_t* __restrict__ vars, int64_t M,
-                                                  int64_t m, const uint32_t* lds, int lane) {
-  const uint32_t row = q.row, flip = q.flip, op = q.op;
-  uint32_t x[NL];
-  if (row & 0x80000000u) {   // staged: slot (row & 0x7fffffff) + limb
-    const uint32_t* sl = lds + (row & 0x7FFFFFFFu) * 64u + lane;
-#pragma unroll
-    for (int l = 0; l < NL; l++) x[l] = sl[l * 64];
-  } else {
-    const uint32_t* g = vars + (int64_t)row * M + m;
-#pragma unroll
-    for (int l = 0; l < NL; l++) x[l] = __builtin_nontemporal_load(g + (int64_t)l * M);
-  }
-  x[NL - 1] ^= flip;
-  uint64_t borrow = 0;
-  uint32_t ne = 0;
-#pragma unroll
-  for (int l = 0; l < NL; l++) {
-    const uint32_t c = q.c[l];
-    borrow = ((uint64_t)x[l] - (uint64_t)c - borrow) >> 63;
-    ne |= x[l] ^ c;
-  }
-  const uint64_t lt = __ballot(borrow != 0), eq = __ballot(ne == 0);
-  switch (op) {
-    case FC_EQ: return eq;
-    case FC_NE: return ~eq;
-    case FC_LT: return lt;
-    case FC_LE: return lt | eq;
-    case FC_GT: return ~(lt | eq);
-    default: return ~lt;   // FC_GE
-  }
+// lane 15 of each row of 16 = the AND of the row's 16 values of lo and of hi: v_and_b32 with a DPP
+// row_shr source (1, 2, 4, 8), lanes whose source lies before the row are not written (they keep
+// their own value); one wait state pads each VALU write -> DPP read of the same register
+__device__ __forceinline__ void and_row16(uint32_t& lo, uint32_t& hi) {
+  asm volatile(
+      "s_nop 1\n"
+      "v_and_b32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n"
+      "v_and_b32_dpp %1, %1, %1 row_shr:1 row_mask:0xf bank_mask:0xf\n"
+      "s_nop 0\n"
+      "v_and_b32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n"
+      "v_and_b32_dpp %1, %1, %1 row_shr:2 row_mask:0xf bank_mask:0xf\n"
+      "s_nop 0\n"
+      "v_and_b32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n"
+      "v_and_b32_dpp %1, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xf\n"
+      "s_nop 0\n"
+      "v_and_b32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n"
+      "v_and_b32_dpp %1, %1, %1 row_shr:8 row_mask:0xf bank_mask:0xf\n"
+      "s_nop 1"
+      : "+v"(lo), "+v"(hi));
 }
 
-// (the whole 48-byte compare descriptor is loaded at once: one scalar round trip)
-__device__ __forceinline__ uint64_t fc_compare(const FcCmp* __restrict__ qp, const uint32_t* __restrict__ vars,
-                                               int64_t M, int64_t m, const uint32_t* lds, int lane) {
-  const FcCmp q = *qp;
-  switch (q.nl) {
-    case 1: return fc_compare_nl<1>(q, vars, M, m, lds, lane);
-    case 2: return fc_compare_nl<2>(q, vars, M, m, lds, lane);
-    case 3: return fc_compare_nl<3>(q, vars, M, m, lds, lane);
-    case 4: return fc_compare_nl<4>(q, vars, M, m, lds, lane);
-    case 5: return fc_compare_nl<5>(q, vars, M, m, lds, lane);
-    case 6: return fc_compare_nl<6>(q, vars, M, m, lds, lane);
-    case 7: return fc_compare_nl<7>(q, vars, M, m, lds, lane);
-    default: return fc_compare_nl<8>(q, vars, M, m, lds, lane);
+// the lane mask of (x ACCEPT c) over a staged variable (limb l at LDS slot q.slot + l, the sign
+// bit of a signed compare flipped by q.f, c pre-flipped): 64-bit compares of limb pairs, each
+// higher pair refining the (lt, eq) of the ones below; per lane, the accept bit of the case (x < c, x == c, x > c) it falls in, so the
+// predicate costs no scalar work
+__device__ __forceinline__ uint64_t fc_cmp(const uint32_t* lds_lane, const FcCmp* __restrict__ qp) {
+  const FcCmpHead h = qp->h;
+  const uint32_t* p = lds_lane + h.slot * 64u;
+  const uint64_t x0 = ((uint64_t)(p[64] ^ (uint32_t)(h.f01 >> 32)) << 32) | (p[0] ^ (uint32_t)h.f01);
+  bool lt = x0 < h.c01, eq = x0 == h.c01;
+  if (h.nl > 2) {   // (eight staged limbs: the other pairs from the top)
+    const FcCmpTail t = qp->t;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {   // limbs 2-3, 4-5, 6-7: each pair above the ones before
+      const uint64_t x = ((uint64_t)(p[(2 * k + 3) * 64] ^ t.f[2 * k + 1]) << 32) | (p[(2 * k + 2) * 64] ^ t.f[2 * k]);
+      const uint64_t c = ((uint64_t)t.c[2 * k + 1] << 32) | t.c[2 * k];
+      // (lt, eq) of the pairs below, refined by this higher pair
+      lt = x < c || (x == c && lt);
+      eq = x == c && eq;
+    }
   }
+  const uint32_t bit = lt ? 1u : (eq ? 2u : 4u);
+  return __ballot((h.accept & bit) != 0);
 }
 
-__global__ __launch_bounds__(256) void fc_kernel(const FcTape* __restrict__ tapes, const uint32_t* __restrict__ mask_idx,
+__global__ __launch_bounds__(256) void fc_kernel(const FcTape* __restrict__ tapes, const uint32_t* __restrict__ mask_lds,
                                                  const FcCmp* __restrict__ cmps, const uint32_t* __restrict__ vars,
                                                  const uint64_t* __restrict__ masks_in,
                                                  const int32_t* __restrict__ best_ro,
-                                                 const uint32_t* __restrict__ stage_rows, FcRun r) {
+                                                 const uint32_t* __restrict__ stage_rows,
+                                                 const uint32_t* __restrict__ stage_masks, FcRun r) {
   extern __shared__ uint32_t lds[];
   const uint32_t wave = uniform(threadIdx.x >> 6);
   const int64_t tile = blockIdx.x;
@@ -100,7 +93,7 @@ __global__ __launch_bounds__(256) void fc_kernel(const FcTape* __restrict__ tape
   const int64_t m_raw = m0 + lane;
   const bool valid = m_raw < r.M;
   const int64_t m = valid ? m_raw : r.M - 1;   // (invalid lanes read a valid row; their bits are dropped)
-  // stage the launch's most read rows: wave w loads rows w, w + 4, ..., eight loads in flight
+  // stage the compared rows (slot s at s * 256 B) and the tile's masks (after the rows, 8 B each)
   for (int s0 = (int)wave; s0 < r.n_stage; s0 += 32) {
     uint32_t v[8];
 #pragma unroll
@@ -112,49 +105,42 @@ __global__ __launch_bounds__(256) void fc_kernel(const FcTape* __restrict__ tape
     for (int k = 0; k < 8; k++)
       if (s0 + 4 * k < r.n_stage) lds[(s0 + 4 * k) * 64 + lane] = v[k];
   }
-  if (r.n_stage) __syncthreads();
+  uint64_t* lmask = reinterpret_cast<uint64_t*>(lds + r.n_stage * 64);
+  const uint64_t* tmask = masks_in + tile * (int64_t)r.n_bool_masks;
+  for (int j = (int)threadIdx.x; j < r.n_smask; j += 256) lmask[j] = tmask[stage_masks[j]];
+  __syncthreads();
   const uint64_t valid_mask = __ballot(valid);
   const int32_t first = (int32_t)(r.index_base + m0);
-  const uint64_t* __restrict__ tmask = masks_in + tile * (int64_t)r.n_bool_masks;
   const int t0 = ((int)blockIdx.y * 4 + (int)wave) * r.tpg;
   const int t1 = min(r.n, t0 + r.tpg);
-  unsigned long long runs = 0, nodes = 0, ops = 0;
   if (t0 >= t1) return;
+  const uint32_t* lds_lane = lds + lane;
+  const char* lmask_b = reinterpret_cast<const char*>(lmask);
+  unsigned long long skipped_nodes = 0, skipped_ops = 0;
+  int skipped = 0;
   FcTape d = tapes[t0];
   for (int t = t0; t < t1; t++) {
-    // the next tape's descriptor is requested with this one's first loads (one round trip less)
+    // the next tape's descriptor is requested with this one's first loads
     const FcTape dn = tapes[min(t + 1, t1 - 1)];
     // best[] only decreases within a launch: a stale (scalar-cache) value only skips less
     if (r.mode == 0 && r.early_exit && first >= best_ro[d.out]) {
+      skipped++;
+      skipped_nodes += d.n_nodes;
+      skipped_ops += d.alg_ops;
       d = dn;
       continue;
     }
     uint64_t acc = valid_mask;
-    // Bool variables: byte offsets into the tile's packed masks, the plain ones then the negated
-    // ones (FcTape.n_mask = plain | negated << 16), each group padded to a multiple of 16 with its
-    // last offset (AND-ing a mask twice changes nothing): sixteen offsets are one scalar load and
-    // sixteen mask loads are in flight together
-    const U16* mi = reinterpret_cast<const U16*>(mask_idx + d.mask_off);
-    const char* tm = reinterpret_cast<const char*>(tmask);
-    const uint32_t n_pos = ((d.n_mask & 0xFFFFu) + 15u) >> 4, n_neg = ((d.n_mask >> 16) + 15u) >> 4;
-    for (uint32_t j = 0; j < n_pos; j++) {
-      const U16 o = mi[j];
-      uint64_t w = ~0ull;
-#pragma unroll
-      for (int k = 0; k < 16; k++) w &= *reinterpret_cast<const uint64_t*>(tm + o.v[k]);
-      acc &= w;
+    // Bool variables, 16 at a time: lane k's LDS offset (bit 0: negated), lanes 16-63 repeating
+    for (uint32_t j = 0; j < d.n_mask; j += 16) {
+      const uint32_t e = mask_lds[d.mask_off + j + (lane & 15)];
+      uint64_t w = *reinterpret_cast<const uint64_t*>(lmask_b + (e & ~7u));
+      if (e & 1u) w = ~w;
+      uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
+      and_row16(lo, hi);
+      acc &= ((uint64_t)__builtin_amdgcn_readlane(hi, 15) << 32) | (uint32_t)__builtin_amdgcn_readlane(lo, 15);
     }
-    for (uint32_t j = 0; j < n_neg; j++) {
-      const U16 o = mi[n_pos + j];
-      uint64_t w = 0;
-#pragma unroll
-      for (int k = 0; k < 16; k++) w |= *reinterpret_cast<const uint64_t*>(tm + o.v[k]);
-      acc &= ~w;
-    }
-    for (uint32_t k = 0; k < d.n_cmp; k++) acc &= fc_compare(cmps + d.cmp_off + k, vars, r.M, m, lds, lane);
-    runs++;
-    nodes += d.n_nodes;
-    ops += d.alg_ops;
+    for (uint32_t k = 0; k < d.n_cmp; k++) acc &= fc_cmp(lds_lane, cmps + d.cmp_off + k);
     if (r.mode == 0) {
       if (acc && lane == 0) atomicMin(r.best + d.out, first + (int32_t)__builtin_ctzll(acc));
     } else if (r.mode == 1) {
@@ -165,8 +151,12 @@ __global__ __launch_bounds__(256) void fc_kernel(const FcTape* __restrict__ tape
     }
     d = dn;
   }
-  if (lane == 0 && r.counters && runs) {
+  // counters: the group's totals (FcRun prefix sums over the tapes) less the skipped tapes'
+  if (lane == 0 && r.counters) {
     const unsigned long long nv = (unsigned long long)__popcll(valid_mask);
+    const unsigned long long runs = (unsigned long long)(t1 - t0 - skipped);
+    const unsigned long long nodes = r.prefix[2 * t1] - r.prefix[2 * t0] - skipped_nodes;
+    const unsigned long long ops = r.prefix[2 * t1 + 1] - r.prefix[2 * t0 + 1] - skipped_ops;
     unsigned long long* cnt = r.counters + ((blockIdx.x * 4 + wave + blockIdx.y) % kCounterSlots) * kCounterStride;
     atomicAdd(&cnt[0], runs * nv);
     atomicAdd(&cnt[1], nodes * nv);
@@ -194,9 +184,11 @@ hipError_t launch_fc(const FcArgs& a, hipStream_t st) {
   r.vars_out = a.vars_out;
   r.counters = a.counters;
   r.n_stage = a.n_stage;
-  hipLaunchKernelGGL(fc_kernel, dim3((unsigned)tiles, (unsigned)quads), dim3(256), (size_t)a.n_stage * 256u, st,
-                     a.tapes, a.mask_idx, a.cmps, a.vars, a.bool_masks, (const int32_t*)a.best,
-                     a.stage_rows, r);
+  r.n_smask = a.n_smask;
+  r.prefix = a.prefix;
+  const size_t lds = (size_t)a.n_stage * 256u + (size_t)a.n_smask * 8u;
+  hipLaunchKernelGGL(fc_kernel, dim3((unsigned)tiles, (unsigned)quads), dim3(256), lds, st, a.tapes, a.mask_lds, a.cmps,
+                     a.vars, a.bool_masks, (const int32_t*)a.best, a.stage_rows, a.stage_masks, r);
   return hipGetLastError();
 }
 

@@ -280,6 +280,12 @@ struct mq_ctx {
   std::vector<uint32_t> var_off_h, var_nl_h;
   std::vector<mq_func_desc> funcs_h;
   uint64_t models_gen = 0;      // bumped by every mq_models_upload
+  // bumped by an upload whose layout differs from the previous batch's (variables and their
+  // widths, Bool lane-mask indices, function signatures): the tape translations, column plans and
+  // keccak maps depend on the layout only, so a drop-in batch that differs in its models (a solver
+  // model inserted, another LRU subset) keeps them
+  uint64_t layout_gen = 0;
+  std::vector<uint8_t> layout_sig;
   int use_asm = 1;      // MQ_OPT_USE_ASM
   int early_exit = 1;   // MQ_OPT_EARLY_EXIT
   int64_t latency_waves = 0;   // MQ_OPT_LATENCY_WAVES
@@ -330,7 +336,7 @@ struct mq_tapes {
   Variant gen[kGen];                         // HIP C++ interpreter kinds (kGenL / kGenK)
   std::vector<CompiledTape> qct;             // compiled programs of the QSA-eligible tapes
   std::vector<GDesc> qbase;                  // their descriptors (const_base into consts)
-  uint64_t qsa_gen = ~0ull;                  // models_gen of the current translation
+  uint64_t qsa_gen = ~0ull;                  // layout_gen of the current translation
   bool qsa_live = false;                     // the translation succeeded for every tape
   int q_count[2] = {0, 0}, q_temps[2] = {0, 0};
   // G kernel preload for the current translation: gpre[var] = VGPR slot (or -1) of the (at
@@ -402,14 +408,14 @@ struct mq_tapes {
   std::vector<KcHost> kc;
   std::vector<uint32_t> kc_consts;
   std::vector<std::pair<int, int>> kc_level;   // (first, count) in kc, per column level
-  uint64_t kc_gen = ~0ull;                      // models_gen of the uploaded map
+  uint64_t kc_gen = ~0ull;                      // layout_gen of the uploaded map
   DevBuf kc_cols_dev, kc_map_dev, kc_pred_dev;
   std::vector<char> col_direct_mask;            // per column: its lane masks are stored by its kernel
   // flat conjunctions (fc.hip): QSA-eligible tapes that are an AND of Bool variables and
   // variable-constant compares, run on fc_kernel instead of P / G (per model batch: qsa_prepare)
   int fc_count = 0;
-  int fc_stage_n = 0;
-  DevBuf fc_tapes_dev, fc_mask_dev, fc_cmp_dev, fc_stage_dev;
+  int fc_stage_n = 0, fc_smask_n = 0;
+  DevBuf fc_tapes_dev, fc_mask_dev, fc_cmp_dev, fc_stage_dev, fc_smask_dev, fc_prefix_dev;
   // multi-device context: the same batch compiled on each peer device (ctx->peers order)
   std::vector<mq_tapes*> peers;
   ~mq_tapes() {
@@ -909,6 +915,25 @@ static int upload_one(mq_ctx* c, const mq_model_batch* mb) {
   c->funcs_h.assign(mb->funcs, mb->funcs + F);
   c->entry_words_n = F > 0 ? ew_total : 0;
   c->models_gen++;
+  {
+    std::vector<uint8_t> sig;
+    auto put = [&](const void* p, size_t n) {
+      const uint8_t* b = (const uint8_t*)p;
+      sig.insert(sig.end(), b, b + n);
+    };
+    const int32_t nv = mb->n_vars;
+    put(&nv, sizeof nv);
+    put(mb->var_width, sizeof(uint16_t) * (size_t)nv);
+    put(c->bmask_of_var.data(), sizeof(int32_t) * c->bmask_of_var.size());
+    put(&F, sizeof F);
+    put(c->funcs_h.data(), sizeof(mq_func_desc) * c->funcs_h.size());
+    const uint8_t fits = (uint64_t)(c->entry_words_n + (int64_t)kEntryPadWords) * 4 < (1ull << 32) ? 1 : 0;
+    put(&fits, 1);
+    if (sig != c->layout_sig) {
+      c->layout_sig.swap(sig);
+      c->layout_gen++;
+    }
+  }
   HIPCHK(c->var_off.upload(voff.data(), voff.size(), c->stream));
   HIPCHK(c->var_nl.upload(vnl.data(), vnl.size(), c->stream));
   HIPCHK(c->funcs.upload(fd.data(), fd.size(), c->stream));
@@ -2481,29 +2506,38 @@ static void plan_stage(const mq_ctx* c, const std::vector<int64_t>& pushes, cons
 // If one tape does not translate, the whole group runs on the HIP C++ kernel for this batch.
 // A flat conjunction (fc.hip): the stack program of x, run abstractly, leaves an AND of Bool
 // variables (negated or not) and compares of one model variable of at most 256 bits with a
-// constant; temps, arithmetic and anything else do not match.  Bool variables without a lane-mask
-// index are compared with their 0/1 row.  Appends the masks / compares to the lists.
-// LDS rows of the flat-conjunction kernel's staging (256 B each: 24 KB per workgroup)
+// constant; temps, arithmetic and anything else do not match.  A Bool variable without a lane-mask
+// index is a compare of its 0/1 row with 1.  Appends its masks (index | negated << 31) and
+// compares (FcCmpH: the variable's first row and limbs, the predicate as an accept mask over
+// (x < c, x == c, x > c), the constant; signed compares have the sign bit flipped) to the lists.
+struct FcCmpH {
+  uint32_t row, nl, accept;
+  uint32_t c[8], f[8];
+};
+// accept masks: bit 0 x < c, bit 1 x == c, bit 2 x > c
+static constexpr uint32_t kAccEq = 2, kAccNe = 5, kAccLt = 1, kAccLe = 3, kAccGt = 4, kAccGe = 6;
+// LDS budget of the flat-conjunction kernel's staging: rows of 256 B (24 KB) and masks of 8 B (16 KB)
 static constexpr int kFcStageRows = 96;
+static constexpr int kFcStageMasks = 2048;
 
-static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_t>& masks, std::vector<FcCmp>& cmps) {
+static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_t>& masks, std::vector<FcCmpH>& cmps) {
   struct Item {
     int kind = 0;   // 0 model variable (BV), 1 constant, 2 conjunction
     uint32_t v = 0;
     std::vector<uint32_t> m;
-    std::vector<FcCmp> q;
+    std::vector<FcCmpH> q;
   };
   std::vector<Item> st;
   const auto& pr = x.prog;
-  auto bool_item = [&](uint32_t v, bool neg, Item& it) {
+  auto bool_item = [&](uint32_t v, Item& it) {
     it.kind = 2;
     if (v < c->bmask_of_var.size() && c->bmask_of_var[v] >= 0) {
-      it.m.push_back((uint32_t)c->bmask_of_var[v] | (neg ? 0x80000000u : 0u));
+      it.m.push_back((uint32_t)c->bmask_of_var[v]);
     } else {
-      FcCmp q{};
+      FcCmpH q{};
       q.row = c->var_off_h[v];
       q.nl = 1;
-      q.op = neg ? FC_NE : FC_EQ;
+      q.accept = kAccEq;
       q.c[0] = 1;
       it.q.push_back(q);
     }
@@ -2522,7 +2556,7 @@ static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_
         break;
       case G_PUSH_VAR_B:
         if (imm >= c->var_nl_h.size() || c->var_width[imm] != 0) return false;
-        bool_item(imm, false, it);
+        bool_item(imm, it);
         st.push_back(std::move(it));
         break;
       case G_PUSH_CONST:
@@ -2540,12 +2574,8 @@ static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_
         if (st.empty() || st.back().kind != 2) return false;
         Item& a = st.back();
         if (a.m.size() + a.q.size() != 1) return false;
-        if (!a.m.empty()) {
-          a.m[0] ^= 0x80000000u;
-        } else {
-          static const uint32_t neg[6] = {FC_NE, FC_EQ, FC_GE, FC_GT, FC_LE, FC_LT};
-          a.q[0].op = neg[a.q[0].op];
-        }
+        if (!a.m.empty()) a.m[0] ^= 0x80000000u;
+        else a.q[0].accept ^= 7u;
         break;
       }
       case G_AND: {
@@ -2572,24 +2602,21 @@ static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_
         const Item& cst = swap ? l : r;
         const uint32_t wdt = imm;
         if (wdt == 0 || c->var_width[var.v] != wdt) return false;
-        FcCmp q{};
+        FcCmpH q{};
         q.row = c->var_off_h[var.v];
         q.nl = c->var_nl_h[var.v];
         for (uint32_t i = 0; i < q.nl; i++) q.c[i] = x.consts[cst.v + i];
-        const bool sgn = op >= G_SLT;
         // x OP c with the variable on the left; a constant on the left mirrors the order
-        uint32_t o;
         switch (op) {
-          case G_EQ: o = FC_EQ; break;
-          case G_ULT: case G_SLT: o = swap ? FC_GT : FC_LT; break;
-          case G_ULE: case G_SLE: o = swap ? FC_GE : FC_LE; break;
-          case G_UGT: case G_SGT: o = swap ? FC_LT : FC_GT; break;
-          default: o = swap ? FC_LE : FC_GE; break;
+          case G_EQ: q.accept = kAccEq; break;
+          case G_ULT: case G_SLT: q.accept = swap ? kAccGt : kAccLt; break;
+          case G_ULE: case G_SLE: q.accept = swap ? kAccGe : kAccLe; break;
+          case G_UGT: case G_SGT: q.accept = swap ? kAccLt : kAccGt; break;
+          default: q.accept = swap ? kAccLe : kAccGe; break;
         }
-        q.op = o;
-        if (sgn) {
-          q.flip = 1u << ((wdt - 1) % 32);
-          q.c[q.nl - 1] ^= q.flip;
+        if (op >= G_SLT) {   // signed: flip the sign bit of both sides, then compare unsigned
+          q.f[q.nl - 1] = 1u << ((wdt - 1) % 32);
+          q.c[q.nl - 1] ^= q.f[q.nl - 1];
         }
         it.kind = 2;
         it.q.push_back(q);
@@ -2600,15 +2627,102 @@ static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_
         return false;
     }
   }
-  if (st.size() != 1 || st[0].kind != 2 || st[0].m.size() > 30000) return false;
+  if (st.size() != 1 || st[0].kind != 2) return false;
   masks.insert(masks.end(), st[0].m.begin(), st[0].m.end());
   cmps.insert(cmps.end(), st[0].q.begin(), st[0].q.end());
   return true;
 }
 
+// The flat-conjunction kernel's tables for the tapes (or columns) `cand` of the lists `fm` / `fq`
+// (fc_match): the compared variables and the masks the most compares / tapes read are staged in
+// LDS within the budgets; a candidate reading one that is not staged is dropped from `cand`'s
+// kernel (keep[i] = 0: it stays on the interpreter).  out_of(i) and mask_out(i) give FcTape.out /
+// .mask_out, nodes_ops(i) its metric words.
+struct FcPlan {
+  std::vector<FcTape> tapes;
+  std::vector<uint32_t> mask_lds;
+  std::vector<FcCmp> cmps;
+  std::vector<uint32_t> stage_rows, stage_masks;
+  std::vector<unsigned long long> prefix;
+};
+static void fc_plan(const mq_ctx* c, const std::vector<std::vector<uint32_t>>& fm, const std::vector<std::vector<FcCmpH>>& fq,
+                    std::vector<char>& keep, const std::function<uint32_t(size_t)>& out_of,
+                    const std::function<int32_t(size_t)>& mask_out,
+                    const std::function<std::pair<uint32_t, uint32_t>(size_t)>& nodes_ops, FcPlan& P) {
+  const uint32_t zero_row = (uint32_t)(c->var_off_h.empty() ? 0 : c->var_off_h.back() + c->var_nl_h.back());
+  std::map<uint32_t, int64_t> row_use, mask_use;
+  std::map<uint32_t, uint32_t> row_nl;
+  for (size_t i = 0; i < keep.size(); i++) {
+    if (!keep[i]) continue;
+    for (const auto& q : fq[i]) {
+      row_use[q.row]++;
+      row_nl[q.row] = q.nl;
+    }
+    for (uint32_t e : fm[i]) mask_use[e & 0x7FFFFFFFu]++;
+  }
+  auto by_use = [](const std::map<uint32_t, int64_t>& u) {
+    std::vector<std::pair<int64_t, uint32_t>> o;
+    for (const auto& kv : u) o.push_back({kv.second, kv.first});
+    std::stable_sort(o.begin(), o.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+    return o;
+  };
+  std::map<uint32_t, uint32_t> slot_of, mslot_of;
+  for (const auto& o : by_use(row_use)) {
+    const uint32_t nl = row_nl[o.second], width = nl <= 2 ? 2 : 8;   // (padded with the zero row)
+    if (P.stage_rows.size() + width > (size_t)kFcStageRows) continue;
+    slot_of[o.second] = (uint32_t)P.stage_rows.size();
+    for (uint32_t l = 0; l < width; l++) P.stage_rows.push_back(l < nl ? o.second + l : zero_row);
+  }
+  for (const auto& o : by_use(mask_use)) {
+    if (P.stage_masks.size() >= (size_t)kFcStageMasks) break;
+    mslot_of[o.second] = (uint32_t)P.stage_masks.size();
+    P.stage_masks.push_back(o.second);
+  }
+  P.prefix.assign(2, 0);
+  for (size_t i = 0; i < keep.size(); i++) {
+    if (!keep[i]) continue;
+    bool ok = true;
+    for (const auto& q : fq[i]) ok = ok && slot_of.count(q.row);
+    for (uint32_t e : fm[i]) ok = ok && mslot_of.count(e & 0x7FFFFFFFu);
+    if (!ok) {
+      keep[i] = 0;
+      continue;
+    }
+    FcTape f{};
+    f.out = out_of(i);
+    f.mask_out = mask_out(i);
+    f.mask_off = (uint32_t)P.mask_lds.size();
+    f.n_mask = (uint32_t)fm[i].size();
+    for (uint32_t e : fm[i]) P.mask_lds.push_back(8u * mslot_of[e & 0x7FFFFFFFu] | (e >> 31));
+    if (!fm[i].empty())
+      while (P.mask_lds.size() % 16) P.mask_lds.push_back(P.mask_lds.back());   // (the same AND again)
+    f.cmp_off = (uint32_t)P.cmps.size();
+    f.n_cmp = (uint32_t)fq[i].size();
+    for (const auto& h : fq[i]) {
+      FcCmp q{};
+      q.h.slot = slot_of[h.row];
+      q.h.nl = h.nl;
+      q.h.accept = h.accept;
+      q.h.c01 = (uint64_t)h.c[0] | ((uint64_t)h.c[1] << 32);
+      q.h.f01 = (uint64_t)h.f[0] | ((uint64_t)h.f[1] << 32);
+      for (int l = 0; l < 6; l++) {
+        q.t.c[l] = h.c[2 + l];
+        q.t.f[l] = h.f[2 + l];
+      }
+      P.cmps.push_back(q);
+    }
+    const auto no = nodes_ops(i);
+    f.n_nodes = no.first;
+    f.alg_ops = no.second;
+    P.tapes.push_back(f);
+    P.prefix.push_back(P.prefix[P.prefix.size() - 2] + f.n_nodes);
+    P.prefix.push_back(P.prefix[P.prefix.size() - 2] + f.alg_ops);
+  }
+}
+
 static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
-  if (T->qsa_gen == c->models_gen) return MQ_OK;
-  T->qsa_gen = c->models_gen;
+  if (T->qsa_gen == c->layout_gen) return MQ_OK;
+  T->qsa_gen = c->layout_gen;
   T->qsa_live = false;
   std::vector<uint32_t> words[2], tr, extra;
   std::vector<GDesc> ds[2];
@@ -2622,11 +2736,14 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
   const bool no_flat = std::getenv("MQ_NO_FLAT") != nullptr;
   std::vector<char> on_fc(nq, 0);
   std::vector<std::vector<uint32_t>> fc_m(nq);
-  std::vector<std::vector<FcCmp>> fc_q(nq);
+  std::vector<std::vector<FcCmpH>> fc_q(nq);
   if (!no_flat)
     parallel_for(nq, 32, [&](int, int64_t b, int64_t e) {
       for (int64_t i = b; i < e; i++) on_fc[i] = fc_match(c, T->qct[i], fc_m[i], fc_q[i]) ? 1 : 0;
     });
+  FcPlan fcp;
+  fc_plan(c, fc_m, fc_q, on_fc, [&](size_t i) { return T->qbase[i].tape; }, [](size_t) { return (int32_t)-1; },
+          [&](size_t i) { return std::make_pair(T->qbase[i].n_nodes, T->qbase[i].alg_ops); }, fcp);
   // (P preloads variables 0-7 only: a program pushing any other variable is not tried on P)
   auto p_candidate = [](const CompiledTape& x) {
     for (size_t pc = 0; pc < x.prog.size(); pc++) {
@@ -2703,34 +2820,9 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
     }
   });
   if (g_fail) return MQ_OK;
-  std::vector<FcTape> fct;
-  std::vector<uint32_t> fcm;
-  std::vector<FcCmp> fcq;
   for (int64_t i = 0; i < nq; i++) {
     const int k = kind_of[i];
-    if (k == 2) {
-      FcTape f{};
-      f.out = T->qbase[i].tape;
-      f.mask_out = -1;
-      f.mask_off = (uint32_t)fcm.size();
-      // byte offsets of the plain masks, then of the negated ones, each group padded to 16
-      // entries (fc.hip reads a group sixteen at a time)
-      uint32_t n_pos = 0, n_neg = 0;
-      for (uint32_t e : fc_m[i])
-        if (!(e >> 31)) fcm.push_back(8u * e), n_pos++;
-      while (fcm.size() % 16) fcm.push_back(fcm.back());   // (a repeated mask: the same AND)
-      for (uint32_t e : fc_m[i])
-        if (e >> 31) fcm.push_back(8u * (e & 0x7FFFFFFFu)), n_neg++;
-      while (fcm.size() % 16) fcm.push_back(fcm.back());
-      f.n_mask = n_pos | (n_neg << 16);
-      f.cmp_off = (uint32_t)fcq.size();
-      f.n_cmp = (uint32_t)fc_q[i].size();
-      f.n_nodes = T->qbase[i].n_nodes;
-      f.alg_ops = T->qbase[i].alg_ops;
-      fcq.insert(fcq.end(), fc_q[i].begin(), fc_q[i].end());
-      fct.push_back(f);
-      continue;
-    }
+    if (k == 2) continue;
     const std::vector<uint32_t>& t = trs[i];
     qsa_count(c, k, t, T->qhist[k], k == 1 ? &T->qpairs : &T->qpairs_p);
     GDesc d = T->qbase[i];
@@ -2773,39 +2865,20 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
   if (descs.empty()) descs.push_back(GDesc{});
   HIPCHK(T->qdescs.upload(descs.data(), descs.size(), c->stream));
   HIPCHK(T->qprog.upload(prog.data(), prog.size(), c->stream));
-  T->fc_count = (int)fct.size();
-  T->fc_stage_n = 0;
-  if (!fct.empty()) {
-    // stage the compared variables read by the most compares in LDS (up to kFcStageRows rows)
-    std::map<uint32_t, std::pair<int64_t, uint32_t>> use;   // first row -> (compares, limbs)
-    for (const FcCmp& q : fcq) {
-      auto& u = use[q.row];
-      u.first++;
-      u.second = std::max(u.second, q.nl);
-    }
-    std::vector<std::pair<int64_t, uint32_t>> order;
-    for (const auto& kv : use) order.push_back({kv.second.first, kv.first});
-    std::stable_sort(order.begin(), order.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
-    std::map<uint32_t, uint32_t> slot_of;
-    std::vector<uint32_t> srows;
-    for (const auto& o : order) {
-      const uint32_t nl = use[o.second].second;
-      if (o.first < 2 || srows.size() + nl > (size_t)kFcStageRows) continue;   // (a row read once gains nothing)
-      slot_of[o.second] = (uint32_t)srows.size();
-      for (uint32_t l = 0; l < nl; l++) srows.push_back(o.second + l);
-    }
-    for (FcCmp& q : fcq) {
-      auto it = slot_of.find(q.row);
-      if (it != slot_of.end()) q.row = 0x80000000u | it->second;
-    }
-    T->fc_stage_n = (int)srows.size();
-    if (srows.empty()) srows.push_back(0);
-    HIPCHK(T->fc_stage_dev.upload(srows.data(), srows.size(), c->stream));
-    HIPCHK(T->fc_tapes_dev.upload(fct.data(), fct.size(), c->stream));
-    if (fcm.empty()) fcm.push_back(0);
-    if (fcq.empty()) fcq.push_back(FcCmp{});
-    HIPCHK(T->fc_mask_dev.upload(fcm.data(), fcm.size(), c->stream));
-    HIPCHK(T->fc_cmp_dev.upload(fcq.data(), fcq.size(), c->stream));
+  T->fc_count = (int)fcp.tapes.size();
+  T->fc_stage_n = (int)fcp.stage_rows.size();
+  T->fc_smask_n = (int)fcp.stage_masks.size();
+  if (!fcp.tapes.empty()) {
+    if (fcp.stage_rows.empty()) fcp.stage_rows.push_back(0);
+    if (fcp.stage_masks.empty()) fcp.stage_masks.push_back(0);
+    if (fcp.mask_lds.empty()) fcp.mask_lds.push_back(0);
+    if (fcp.cmps.empty()) fcp.cmps.push_back(FcCmp{});
+    HIPCHK(T->fc_tapes_dev.upload(fcp.tapes.data(), fcp.tapes.size(), c->stream));
+    HIPCHK(T->fc_mask_dev.upload(fcp.mask_lds.data(), fcp.mask_lds.size(), c->stream));
+    HIPCHK(T->fc_cmp_dev.upload(fcp.cmps.data(), fcp.cmps.size(), c->stream));
+    HIPCHK(T->fc_stage_dev.upload(fcp.stage_rows.data(), fcp.stage_rows.size(), c->stream));
+    HIPCHK(T->fc_smask_dev.upload(fcp.stage_masks.data(), fcp.stage_masks.size(), c->stream));
+    HIPCHK(T->fc_prefix_dev.upload(fcp.prefix.data(), fcp.prefix.size(), c->stream));
   }
   if (T->stage_rows.empty()) HIPCHK(T->stage_dev.ensure(sizeof(uint32_t)));
   else HIPCHK(T->stage_dev.upload(T->stage_rows.data(), T->stage_rows.size(), c->stream));
@@ -2820,8 +2893,8 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
 // of the target variable, n_temps = its limbs, depth = Bool root (gen_qsa.py store_column).
 // If one column does not translate, all columns run on the HIP C++ column kernel.
 static int cq_prepare(mq_ctx* c, mq_tapes* T) {
-  if (T->cq_gen == c->models_gen) return MQ_OK;
-  T->cq_gen = c->models_gen;
+  if (T->cq_gen == c->layout_gen) return MQ_OK;
+  T->cq_gen = c->layout_gen;
   T->cq_live = false;
   if (T->cq_ct.empty()) return MQ_OK;
   std::vector<uint32_t> prog, consts, tr, extra;
@@ -3007,7 +3080,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     T->cq_gen = ~0ull;
   }
   const uint32_t zero_row = (uint32_t)(c->var_off_h.empty() ? 0 : c->var_off_h.back() + c->var_nl_h.back());
-  if (T->bmask_gen != c->models_gen) {
+  if (T->bmask_gen != c->layout_gen) {
     // the mask indices of each level's Bool columns under this model batch
     T->lvl_bmask_h.assign(T->clevels.size(), {});
     T->lvl_bmask_cpp_h.assign(T->clevels.size(), {});
@@ -3032,9 +3105,9 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
         HIPCHK(T->lvl_bmask_cpp[li].upload(T->lvl_bmask_cpp_h[li].data(), T->lvl_bmask_cpp_h[li].size(), st));
     }
     HIPCHK(hipStreamSynchronize(st));
-    T->bmask_gen = c->models_gen;
+    T->bmask_gen = c->layout_gen;
   }
-  if (!T->kc.empty() && T->kc_gen != c->models_gen) {
+  if (!T->kc.empty() && T->kc_gen != c->layout_gen) {
     // the keccak columns' message maps under this model batch's variable rows
     std::vector<KcCol> cols;
     std::vector<KcMapEntry> map;
@@ -3081,7 +3154,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     if (preds.empty()) HIPCHK(T->kc_pred_dev.ensure(sizeof(KcPred)));
     else HIPCHK(T->kc_pred_dev.upload(preds.data(), preds.size(), st));
     HIPCHK(hipStreamSynchronize(st));
-    T->kc_gen = c->models_gen;
+    T->kc_gen = c->layout_gen;
   }
   // Bool columns' 0/1 rows are read only by the HIP C++ kernels (the assembly interpreters read
   // the packed lane masks, which G's column store writes itself): G writes the rows only when a
@@ -3252,7 +3325,10 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     (void)tiles;
     f.stage_rows = T->fc_stage_dev.as<uint32_t>();
     f.n_stage = T->fc_stage_n;
-    f.mask_idx = T->fc_mask_dev.as<uint32_t>();
+    f.stage_masks = T->fc_smask_dev.as<uint32_t>();
+    f.n_smask = T->fc_smask_n;
+    f.prefix = T->fc_prefix_dev.as<unsigned long long>();
+    f.mask_lds = T->fc_mask_dev.as<uint32_t>();
     f.cmps = T->fc_cmp_dev.as<FcCmp>();
     f.vars = c->vars.as<uint32_t>();
     f.bool_masks = c->bmasks.as<uint64_t>();

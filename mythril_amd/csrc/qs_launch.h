@@ -159,19 +159,27 @@ hipError_t launch_keccak_columns(const KcCol* cols, int n_cols, const KcMapEntry
 
 // Flat conjunctions (fc.hip, mq_api.cpp fc_match): a tape or Bool column that is an AND of Bool
 // model variables (negated or not) and comparisons of one variable with a constant.
-enum FcOp : uint32_t { FC_EQ = 0, FC_NE = 1, FC_LT = 2, FC_LE = 3, FC_GT = 4, FC_GE = 5 };
-struct FcCmp {
-  uint32_t row;     // first limb row of the variable (bit 31: the first of its LDS-staged slots)
-  uint32_t nl;      // its limbs (1..8)
-  uint32_t op;      // FcOp, unsigned over the nl limbs
-  uint32_t flip;    // XOR-ed into the variable's top limb (a signed compare's sign bit; c pre-flipped)
-  uint32_t c[8];    // the constant, little-endian limbs
+struct FcCmpHead {    // (one 32-byte scalar load: all a variable of one or two limbs needs)
+  uint32_t slot;      // LDS slot of the variable's limb 0 (limb l at slot + l; padded with zero rows)
+  uint32_t nl;        // its limbs (1..8): <= 2 reads two slots, else eight
+  uint32_t accept;    // bit 0: x < c, bit 1: x == c, bit 2: x > c (unsigned over the limbs)
+  uint32_t pad;
+  uint64_t c01;       // the constant's limbs 0-1 (sign bit flipped for a signed compare)
+  uint64_t f01;       // XOR-ed into the variable's limbs 0-1: the sign bit of a signed compare
+};
+struct FcCmpTail {    // limbs 2-7 of a wider variable
+  uint32_t c[6];
+  uint32_t f[6];
+};
+struct alignas(16) FcCmp {
+  FcCmpHead h;
+  FcCmpTail t;
 };
 struct FcTape {
   uint32_t out;       // modes 0/1: tape index; mode 3: the Bool column's variable row
   int32_t mask_out;   // mode 3: its packed lane-mask index (-1: none, the 0/1 row is written)
-  uint32_t mask_off;  // its Bool variables: FcArgs.mask_idx[mask_off ..] = byte offset (8 x mask index)
-  uint32_t n_mask;    // plain | negated << 16 (the plain offsets first)
+  uint32_t mask_off;  // its Bool variables: FcArgs.mask_lds[mask_off ..] = 8 x LDS mask slot | negated,
+  uint32_t n_mask;    //   n_mask of them, padded to a multiple of 16 with the last
   uint32_t cmp_off;   // its compares: FcArgs.cmps[cmp_off ..]
   uint32_t n_cmp;
   uint32_t n_nodes;   // DAG nodes (metric)
@@ -180,8 +188,8 @@ struct FcTape {
 struct FcArgs {
   const FcTape* tapes;
   int n;                         // tapes / columns of the launch
-  int tpg;                       // per wave (grid.y = groups)
-  const uint32_t* mask_idx;
+  int tpg;                       // per wave (a workgroup's 4 waves take 4 groups of one tile)
+  const uint32_t* mask_lds;
   const FcCmp* cmps;
   const uint32_t* vars;
   const uint64_t* bool_masks;    // [tile][n_bool_masks] packed Bool rows (read)
@@ -196,8 +204,11 @@ struct FcArgs {
   int32_t* best;
   uint8_t* verdicts;             // mode 1: [tape][M] bytes
   unsigned long long* counters;
-  const uint32_t* stage_rows;    // rows staged in LDS per workgroup (FcCmp.row bit 31 = slot)
+  const uint32_t* stage_rows;    // variable rows staged in LDS per workgroup, slot order
   int n_stage;
+  const uint32_t* stage_masks;   // mask indices staged in LDS per workgroup (after the rows)
+  int n_smask;
+  const unsigned long long* prefix;   // [2 (n + 1)]: running sums of n_nodes, alg_ops
 };
 // fc_kernel's by-value block (the read-only tables are separate __restrict__ arguments)
 struct FcRun {
@@ -208,7 +219,8 @@ struct FcRun {
   uint64_t* masks_out;
   uint32_t* vars_out;
   unsigned long long* counters;
-  int n_stage;
+  int n_stage, n_smask;
+  const unsigned long long* prefix;
 };
 hipError_t launch_fc(const FcArgs& a, hipStream_t st);
 
