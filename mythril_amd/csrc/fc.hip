@@ -34,6 +34,9 @@ namespace mq {
 
 __device__ __forceinline__ uint32_t uniform(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
+// 64-model tiles per workgroup (each wave runs its tape group over all of them)
+constexpr int FC_TILES = 4;
+
 // lane 15 of each row of 16 = the AND of the row's 16 values of lo and of hi: v_and_b32 with a DPP
 // row_shr source (1, 2, 4, 8), lanes whose source lies before the row are not written (they keep
 // their own value); one wait state pads each VALU write -> DPP read of the same register
@@ -55,22 +58,23 @@ __device__ __forceinline__ void and_row16(uint32_t& lo, uint32_t& hi) {
       : "+v"(lo), "+v"(hi));
 }
 
-// the lane mask of (x ACCEPT c) over a staged variable (limb l at LDS slot q.slot + l, the sign
-// bit of a signed compare flipped by q.f, c pre-flipped): 64-bit compares of limb pairs, each
-// higher pair refining the (lt, eq) of the ones below; per lane, the accept bit of the case (x < c, x == c, x > c) it falls in, so the
+// The lane mask of (x ACCEPT c) over a staged variable for tile j of the workgroup (limb l of
+// tile j at LDS row (q.slot + l) * FC_TILES + j, the sign bit of a signed compare flipped by q.f,
+// c pre-flipped): 64-bit compares of limb pairs, each higher pair refining the (lt, eq) of the
+// ones below; per lane, the accept bit of the case (x < c, x == c, x > c) it falls in, so the
 // predicate costs no scalar work
-__device__ __forceinline__ uint64_t fc_cmp(const uint32_t* lds_lane, const FcCmp* __restrict__ qp) {
-  const FcCmpHead h = qp->h;
-  const uint32_t* p = lds_lane + h.slot * 64u;
-  const uint64_t x0 = ((uint64_t)(p[64] ^ (uint32_t)(h.f01 >> 32)) << 32) | (p[0] ^ (uint32_t)h.f01);
+__device__ __forceinline__ uint64_t fc_cmp(const uint32_t* lds_lane, const FcCmpHead& h, const FcCmp* __restrict__ qp,
+                                           int j) {
+  const uint32_t* p = lds_lane + (h.slot * FC_TILES + (uint32_t)j) * 64u;
+  constexpr int R = FC_TILES * 64;   // one limb further
+  const uint64_t x0 = ((uint64_t)(p[R] ^ (uint32_t)(h.f01 >> 32)) << 32) | (p[0] ^ (uint32_t)h.f01);
   bool lt = x0 < h.c01, eq = x0 == h.c01;
-  if (h.nl > 2) {   // (eight staged limbs: the other pairs from the top)
+  if (h.nl > 2) {   // (eight staged limbs: the other pairs)
     const FcCmpTail t = qp->t;
 #pragma unroll
     for (int k = 0; k < 3; k++) {   // limbs 2-3, 4-5, 6-7: each pair above the ones before
-      const uint64_t x = ((uint64_t)(p[(2 * k + 3) * 64] ^ t.f[2 * k + 1]) << 32) | (p[(2 * k + 2) * 64] ^ t.f[2 * k]);
+      const uint64_t x = ((uint64_t)(p[(2 * k + 3) * R] ^ t.f[2 * k + 1]) << 32) | (p[(2 * k + 2) * R] ^ t.f[2 * k]);
       const uint64_t c = ((uint64_t)t.c[2 * k + 1] << 32) | t.c[2 * k];
-      // (lt, eq) of the pairs below, refined by this higher pair
       lt = x < c || (x == c && lt);
       eq = x == c && eq;
     }
@@ -79,6 +83,10 @@ __device__ __forceinline__ uint64_t fc_cmp(const uint32_t* lds_lane, const FcCmp
   return __ballot((h.accept & bit) != 0);
 }
 
+// One workgroup = FC_TILES consecutive 64-model tiles; each of its 4 waves runs one tape group
+// over all of them (lane l holds model l of every tile): a tape's descriptor, early-exit test,
+// mask list and compare constants are scalar work paid once for FC_TILES tiles, and the mask AND
+// of all FC_TILES tiles is one DPP reduction (lanes 16 j .. 16 j + 15 reduce tile j's masks).
 __global__ __launch_bounds__(256) void fc_kernel(const FcTape* __restrict__ tapes, const uint32_t* __restrict__ mask_lds,
                                                  const FcCmp* __restrict__ cmps, const uint32_t* __restrict__ vars,
                                                  const uint64_t* __restrict__ masks_in,
@@ -87,35 +95,44 @@ __global__ __launch_bounds__(256) void fc_kernel(const FcTape* __restrict__ tape
                                                  const uint32_t* __restrict__ stage_masks, FcRun r) {
   extern __shared__ uint32_t lds[];
   const uint32_t wave = uniform(threadIdx.x >> 6);
-  const int64_t tile = blockIdx.x;
-  const int64_t m0 = tile * 64;
+  const int64_t tile0 = (int64_t)blockIdx.x * FC_TILES;
+  const int64_t m0 = tile0 * 64;
   const int lane = threadIdx.x & 63;
-  const int64_t m_raw = m0 + lane;
-  const bool valid = m_raw < r.M;
-  const int64_t m = valid ? m_raw : r.M - 1;   // (invalid lanes read a valid row; their bits are dropped)
-  // stage the compared rows (slot s at s * 256 B) and the tile's masks (after the rows, 8 B each)
-  for (int s0 = (int)wave; s0 < r.n_stage; s0 += 32) {
-    uint32_t v[8];
+  // stage the compared rows (LDS row s * FC_TILES + j = slot s of tile j, 256 B) and the tiles'
+  // masks (after the rows: tile j's mask k at 8 (j * n_smask + k)); wave w stages tile w's rows
+  {
+    const int j = (int)wave;
+    const int64_t mj = min(m0 + 64 * j + lane, r.M - 1);
+    for (int s0 = 0; s0 < r.n_stage; s0 += 8) {
+      uint32_t v[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const int s = min(s0 + 4 * k, r.n_stage - 1);
-      v[k] = __builtin_nontemporal_load(vars + (int64_t)stage_rows[s] * r.M + m);
+      for (int k = 0; k < 8; k++) v[k] = __builtin_nontemporal_load(vars + (int64_t)stage_rows[min(s0 + k, r.n_stage - 1)] * r.M + mj);
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        if (s0 + k < r.n_stage) lds[((s0 + k) * FC_TILES + j) * 64 + lane] = v[k];
     }
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      if (s0 + 4 * k < r.n_stage) lds[(s0 + 4 * k) * 64 + lane] = v[k];
   }
-  uint64_t* lmask = reinterpret_cast<uint64_t*>(lds + r.n_stage * 64);
-  const uint64_t* tmask = masks_in + tile * (int64_t)r.n_bool_masks;
-  for (int j = (int)threadIdx.x; j < r.n_smask; j += 256) lmask[j] = tmask[stage_masks[j]];
+  uint64_t* lmask = reinterpret_cast<uint64_t*>(lds + r.n_stage * FC_TILES * 64);
+  const int64_t tiles = (r.M + 63) / 64;
+  for (int i = (int)threadIdx.x; i < FC_TILES * r.n_smask; i += 256) {
+    const int j = i / r.n_smask, k = i - j * r.n_smask;
+    const int64_t tj = min(tile0 + j, tiles - 1);
+    lmask[i] = masks_in[tj * (int64_t)r.n_bool_masks + stage_masks[k]];
+  }
   __syncthreads();
-  const uint64_t valid_mask = __ballot(valid);
-  const int32_t first = (int32_t)(r.index_base + m0);
+  uint64_t valid[FC_TILES];
+  int32_t first[FC_TILES];
+#pragma unroll
+  for (int j = 0; j < FC_TILES; j++) {
+    valid[j] = __ballot(m0 + 64 * j + lane < r.M);
+    first[j] = (int32_t)(r.index_base + m0 + 64 * j);
+  }
   const int t0 = ((int)blockIdx.y * 4 + (int)wave) * r.tpg;
   const int t1 = min(r.n, t0 + r.tpg);
   if (t0 >= t1) return;
   const uint32_t* lds_lane = lds + lane;
-  const char* lmask_b = reinterpret_cast<const char*>(lmask);
+  // lane l reads tile (l / 16)'s copy of the masks
+  const char* lmask_b = reinterpret_cast<const char*>(lmask + (lane >> 4) * r.n_smask);
   unsigned long long skipped_nodes = 0, skipped_ops = 0;
   int skipped = 0;
   FcTape d = tapes[t0];
@@ -123,37 +140,58 @@ __global__ __launch_bounds__(256) void fc_kernel(const FcTape* __restrict__ tape
     // the next tape's descriptor is requested with this one's first loads
     const FcTape dn = tapes[min(t + 1, t1 - 1)];
     // best[] only decreases within a launch: a stale (scalar-cache) value only skips less
-    if (r.mode == 0 && r.early_exit && first >= best_ro[d.out]) {
+    if (r.mode == 0 && r.early_exit && first[0] >= best_ro[d.out]) {
       skipped++;
       skipped_nodes += d.n_nodes;
       skipped_ops += d.alg_ops;
       d = dn;
       continue;
     }
-    uint64_t acc = valid_mask;
-    // Bool variables, 16 at a time: lane k's LDS offset (bit 0: negated), lanes 16-63 repeating
-    for (uint32_t j = 0; j < d.n_mask; j += 16) {
-      const uint32_t e = mask_lds[d.mask_off + j + (lane & 15)];
+    uint64_t acc[FC_TILES];
+#pragma unroll
+    for (int j = 0; j < FC_TILES; j++) acc[j] = valid[j];
+    // Bool variables, 16 at a time: lane l takes entry l % 16 of the list (LDS offset, bit 0:
+    // negated) for tile l / 16
+    for (uint32_t e0 = 0; e0 < d.n_mask; e0 += 16) {
+      const uint32_t e = mask_lds[d.mask_off + e0 + (lane & 15)];
       uint64_t w = *reinterpret_cast<const uint64_t*>(lmask_b + (e & ~7u));
       if (e & 1u) w = ~w;
       uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
       and_row16(lo, hi);
-      acc &= ((uint64_t)__builtin_amdgcn_readlane(hi, 15) << 32) | (uint32_t)__builtin_amdgcn_readlane(lo, 15);
+#pragma unroll
+      for (int j = 0; j < FC_TILES; j++)
+        acc[j] &= ((uint64_t)__builtin_amdgcn_readlane(hi, 16 * j + 15) << 32) |
+                  (uint32_t)__builtin_amdgcn_readlane(lo, 16 * j + 15);
     }
-    for (uint32_t k = 0; k < d.n_cmp; k++) acc &= fc_cmp(lds_lane, cmps + d.cmp_off + k);
-    if (r.mode == 0) {
-      if (acc && lane == 0) atomicMin(r.best + d.out, first + (int32_t)__builtin_ctzll(acc));
-    } else if (r.mode == 1) {
-      if (valid) r.verdicts[(int64_t)d.out * r.M + m_raw] = (uint8_t)((acc >> lane) & 1u);
-    } else {
-      if (d.mask_out >= 0 && lane == 0) r.masks_out[tile * (int64_t)r.n_bool_masks + d.mask_out] = acc;
-      if ((r.bool_rows || d.mask_out < 0) && valid) r.vars_out[(int64_t)d.out * r.M + m_raw] = (uint32_t)((acc >> lane) & 1u);
+    for (uint32_t k = 0; k < d.n_cmp; k++) {
+      const FcCmp* qp = cmps + d.cmp_off + k;
+      const FcCmpHead h = qp->h;
+#pragma unroll
+      for (int j = 0; j < FC_TILES; j++) acc[j] &= fc_cmp(lds_lane, h, qp, j);
+    }
+#pragma unroll
+    for (int j = 0; j < FC_TILES; j++) {
+      const int64_t mj = m0 + 64 * j + lane;
+      if (r.mode == 0) {
+        if (acc[j]) {   // the lowest tile with a hit has the lowest model
+          if (lane == 0) atomicMin(r.best + d.out, first[j] + (int32_t)__builtin_ctzll(acc[j]));
+          break;
+        }
+      } else if (r.mode == 1) {
+        if (mj < r.M) r.verdicts[(int64_t)d.out * r.M + mj] = (uint8_t)((acc[j] >> lane) & 1u);
+      } else if (mj - lane < r.M) {
+        if (d.mask_out >= 0 && lane == 0) r.masks_out[(tile0 + j) * (int64_t)r.n_bool_masks + d.mask_out] = acc[j];
+        if ((r.bool_rows || d.mask_out < 0) && mj < r.M) r.vars_out[(int64_t)d.out * r.M + mj] = (uint32_t)((acc[j] >> lane) & 1u);
+      }
     }
     d = dn;
   }
-  // counters: the group's totals (FcRun prefix sums over the tapes) less the skipped tapes'
+  // counters: the group's totals (FcRun prefix sums over the tapes) less the skipped tapes', times
+  // the workgroup's valid models
   if (lane == 0 && r.counters) {
-    const unsigned long long nv = (unsigned long long)__popcll(valid_mask);
+    unsigned long long nv = 0;
+#pragma unroll
+    for (int j = 0; j < FC_TILES; j++) nv += (unsigned long long)__popcll(valid[j]);
     const unsigned long long runs = (unsigned long long)(t1 - t0 - skipped);
     const unsigned long long nodes = r.prefix[2 * t1] - r.prefix[2 * t0] - skipped_nodes;
     const unsigned long long ops = r.prefix[2 * t1 + 1] - r.prefix[2 * t0 + 1] - skipped_ops;
@@ -166,9 +204,9 @@ __global__ __launch_bounds__(256) void fc_kernel(const FcTape* __restrict__ tape
 
 hipError_t launch_fc(const FcArgs& a, hipStream_t st) {
   if (a.n <= 0 || a.M <= 0) return hipSuccess;
-  const int64_t tiles = (a.M + 63) / 64;
+  const int64_t groups = (a.M + 64 * FC_TILES - 1) / (64 * FC_TILES);
   const int64_t quads = ((a.n + a.tpg - 1) / a.tpg + 3) / 4;
-  if (quads > 65535 || tiles > 0x7FFFFFFF) return hipErrorInvalidValue;
+  if (quads > 65535 || groups > 0x7FFFFFFF) return hipErrorInvalidValue;
   FcRun r{};
   r.n = a.n;
   r.tpg = a.tpg;
@@ -186,8 +224,8 @@ hipError_t launch_fc(const FcArgs& a, hipStream_t st) {
   r.n_stage = a.n_stage;
   r.n_smask = a.n_smask;
   r.prefix = a.prefix;
-  const size_t lds = (size_t)a.n_stage * 256u + (size_t)a.n_smask * 8u;
-  hipLaunchKernelGGL(fc_kernel, dim3((unsigned)tiles, (unsigned)quads), dim3(256), lds, st, a.tapes, a.mask_lds, a.cmps,
+  const size_t lds = ((size_t)a.n_stage * 256u + (size_t)a.n_smask * 8u) * FC_TILES;
+  hipLaunchKernelGGL(fc_kernel, dim3((unsigned)groups, (unsigned)quads), dim3(256), lds, st, a.tapes, a.mask_lds, a.cmps,
                      a.vars, a.bool_masks, (const int32_t*)a.best, a.stage_rows, a.stage_masks, r);
   return hipGetLastError();
 }

@@ -2516,9 +2516,11 @@ struct FcCmpH {
 };
 // accept masks: bit 0 x < c, bit 1 x == c, bit 2 x > c
 static constexpr uint32_t kAccEq = 2, kAccNe = 5, kAccLt = 1, kAccLe = 3, kAccGt = 4, kAccGe = 6;
-// LDS budget of the flat-conjunction kernel's staging: rows of 256 B (24 KB) and masks of 8 B (16 KB)
-static constexpr int kFcStageRows = 96;
-static constexpr int kFcStageMasks = 2048;
+// LDS budget of the flat-conjunction kernel's staging, per tile (fc.hip stages FC_TILES = 4
+// tiles a workgroup): rows of 256 B (40 KB for 4 tiles) and masks of 8 B (8 KB for 4 tiles);
+// only what a launch uses is allocated (C4's tapes: ~5 KB)
+static constexpr int kFcStageRows = 40;
+static constexpr int kFcStageMasks = 256;
 
 static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_t>& masks, std::vector<FcCmpH>& cmps) {
   struct Item {

@@ -785,9 +785,30 @@ def _default_backend() -> SolverBackend:
 model_cache = ModelCache()
 solver_backend: SolverBackend = None  # type: ignore[assignment]
 counters = {"get_model_calls": 0, "quick_sat_answers": 0, "candidate_answers": 0, "solver_calls": 0}
-# host seconds of get_model's solver path: ThreadPool(1) create + apply + terminate around the
-# solver (model.py:104-113, which the reference pays too) and the solver itself
+# host seconds of get_model's solver path: the worker-thread hand-off around the solver
+# (model.py:104-113) and the solver itself
 timing = {"solver_pool": 0.0}
+
+# model.py:104-113 creates a ThreadPool(1) per solver call and terminates it afterwards (~0.7 ms of
+# thread start-up per call).  The solver runs on one persistent worker instead; a call that times
+# out or raises discards that worker (as terminate() does), so a hung solver never blocks the next
+# call.  Answers, exceptions and timeouts are the reference's.
+_solver_pool: Optional[ThreadPool] = None
+_solver_pool_pid = None
+
+
+def _pool() -> ThreadPool:
+    global _solver_pool, _solver_pool_pid
+    if _solver_pool is None or _solver_pool_pid != os.getpid():   # (a forked child starts its own)
+        _solver_pool, _solver_pool_pid = ThreadPool(1), os.getpid()
+    return _solver_pool
+
+
+def _discard_pool() -> None:
+    global _solver_pool
+    if _solver_pool is not None:
+        _solver_pool.terminate()
+    _solver_pool = None
 
 
 def set_solver_backend(backend: Optional[SolverBackend]) -> None:
@@ -848,20 +869,22 @@ def get_model(constraints, minimize=(), maximize=(), solver_timeout=None, verdic
             return get_model(asked, solver_timeout=asked_timeout)
     counters["solver_calls"] += 1
     t_pool = time.perf_counter()
-    pool = ThreadPool(1)
+    ok = False
     try:
-        res = pool.apply_async(solver_worker, args=(constraints, minimize, maximize, solver_timeout))
+        res = _pool().apply_async(solver_worker, args=(constraints, minimize, maximize, solver_timeout))
         try:
             # model.py:110 hands the millisecond timeout to AsyncResult.get(), which reads it as
             # seconds: the pool wait never pre-empts the solver's own timeout.  Kept as is.
             status, factory = res.get(None if math.isinf(solver_timeout) else solver_timeout)
+            ok = True
         except _PoolTimeout:
             status, factory = "unknown", None
         except Exception:
             log.warning("Encountered an exception while solving expression")
             status, factory = "unknown", None
     finally:
-        pool.terminate()
+        if not ok:
+            _discard_pool()
         timing["solver_pool"] += time.perf_counter() - t_pool
 
     if status == "sat":

@@ -375,7 +375,7 @@ def flat_workload(seed: int, n_tapes: int, n_models: int, n_bool: int = 6, plant
     random model (items chosen true there, constants at or next to its values).  Returns
     (tapes, models)."""
     rng = np.random.Generator(np.random.PCG64(seed))
-    bv_widths = [int(w) for w in rng.choice(FLAT_WIDTHS, 10)] + [256, 8]
+    bv_widths = [int(w) for w in rng.choice(FLAT_WIDTHS, 6)] + [256, 8]
     var_widths = [BOOL] * n_bool + bv_widths
     mb = fuzz_models(rng, var_widths, n_models)
     preds = ("eq", "distinct", "ult", "ule", "ugt", "uge", "slt", "sle", "sgt", "sge")

@@ -1189,7 +1189,9 @@ def test_flat_conjunctions_match_oracle(evaluator, monkeypatch, bmask_cap):
     ct = evaluator.compile(tb)
     fh = evaluator.first_hit(ct)
     n_flat, _ = ct.flat_split()
-    assert n_flat >= 0.9 * tb.n_tapes, n_flat
+    # (Bool variables read from rows take LDS staging slots: past the kernel's budget the tapes
+    # reading them stay on the interpreter -- parity either way)
+    assert n_flat >= (0.9 if bmask_cap is None else 0.3) * tb.n_tapes, n_flat
     ref, _ = cref.first_hit(tb, mb)
     assert (fh == ref).all(), np.flatnonzero(fh != ref)[:10]
     assert (ref >= 0).mean() > 0.4

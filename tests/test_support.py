@@ -523,3 +523,34 @@ def test_model_slots_survive_solver_model_churn():
             n += 1
             assert cache.check_quick_sat(e) is False
     assert n == 400 and eng.incremental.slot_epoch == epoch
+
+
+def test_solver_worker_is_reused_and_replaced_after_a_failure(fresh):
+    """The solver runs on one persistent worker thread (model.py:104-113 starts a ThreadPool(1)
+    per call); a call that raises discards it, and the next call gets a new one -- answers and
+    exceptions as the reference's."""
+    import threading
+    seen = []
+
+    class Recording(sp.SolverBackend):
+        def __init__(self, fail=False):
+            self.fail = fail
+
+        def solve(self, constraints, minimize, maximize, timeout_ms):
+            seen.append(threading.get_ident())
+            if self.fail:
+                raise RuntimeError("solver crashed")
+            return "unsat", None
+
+    sp.set_solver_backend(Recording())
+    for v in (90, 91, 92):
+        with pytest.raises(UnsatError):
+            sp.get_model(sp.Constraints([x == v]))
+    assert len(set(seen)) == 1 and seen[0] != threading.get_ident()
+    sp.set_solver_backend(Recording(fail=True))
+    with pytest.raises(SolverTimeOutException):       # an exception is "unknown" (model.py:111-113)
+        sp.get_model(sp.Constraints([x == 93]))
+    sp.set_solver_backend(Recording())
+    with pytest.raises(UnsatError):
+        sp.get_model(sp.Constraints([x == 94]))
+    assert seen[-1] != seen[0]                         # a new worker after the failure
