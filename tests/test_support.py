@@ -547,10 +547,12 @@ def test_solver_worker_is_reused_and_replaced_after_a_failure(fresh):
         with pytest.raises(UnsatError):
             sp.get_model(sp.Constraints([x == v]))
     assert len(set(seen)) == 1 and seen[0] != threading.get_ident()
+    pool = sp._solver_pool
     sp.set_solver_backend(Recording(fail=True))
     with pytest.raises(SolverTimeOutException):       # an exception is "unknown" (model.py:111-113)
         sp.get_model(sp.Constraints([x == 93]))
+    assert sp._solver_pool is None                     # discarded, as terminate() does
     sp.set_solver_backend(Recording())
     with pytest.raises(UnsatError):
         sp.get_model(sp.Constraints([x == 94]))
-    assert seen[-1] != seen[0]                         # a new worker after the failure
+    assert sp._solver_pool is not None and sp._solver_pool is not pool   # a new worker
