@@ -608,7 +608,7 @@ def main():
         print(f"[rank {rank}] first-hit mismatch on {len(bad)} tapes, e.g. {bad[:5]}", file=sys.stderr)
 
     # where the batch ran (after a launch): tapes on the P / G assembly interpreters vs the HIP C++
-    # kernels, hoisted columns on G / the keccak column kernel / the C++ column kernel
+    # kernels, hoisted columns on G / the keccak and bit-gather column kernels / the C++ column kernel
     if oracle:
         kernel_split = {"tapes": tb.n_tapes, "engine": "oracle (CPU rehearsal)"}
     else:
@@ -617,13 +617,14 @@ def main():
         cols_g, cols_live = ct.column_asm_split() if n_cols else (0, False)
         kcols = int(ct.keccak_columns()) if n_cols else 0
         kpreds = int(ct.keccak_predicate_columns()) if n_cols else 0
+        gcols = int(ct.gather_columns()) if n_cols else 0
         n_fc, cols_fc = ct.flat_split()
         kernel_split = {"tapes": tb.n_tapes, "tapes_p": n_p, "tapes_g": n_g, "tapes_flat": n_fc,
                         "tapes_cpp": tb.n_tapes - ((n_p + n_g + n_fc) if asm_live else 0),
                         "columns_flat": cols_fc,
                         "columns": n_cols, "columns_g": cols_g if cols_live else 0, "columns_keccak": kcols,
-                        "columns_keccak_predicates": kpreds,
-                        "columns_cpp": n_cols - kcols - kpreds - cols_fc - (cols_g if cols_live else 0)}
+                        "columns_keccak_predicates": kpreds, "columns_gather": gcols,
+                        "columns_cpp": n_cols - kcols - kpreds - gcols - cols_fc - (cols_g if cols_live else 0)}
     if world > 1 and not oracle and args.dist_backend == "nccl":
         red_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 

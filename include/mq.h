@@ -350,6 +350,13 @@ int mq_tapes_column_split(mq_tapes* tapes, int32_t* n_asm, int32_t* live);
    kernel (an AND of Bool variables and variable-constant compares: no interpreter). */
 int mq_tapes_flat_split(mq_tapes* tapes, int32_t* n_flat_tapes, int32_t* n_flat_columns);
 
+/* Hoisted columns that only arrange model-variable bits and constants, runs of bits gated by
+   `i <s size` — the calldata words of calldata.py:48-55 (Concat of calldata.py:234-247 bytes
+   If(i < calldatasize, calldata[i], 0)), their extracts and constant masks — evaluated by the
+   bit-gather column kernel (cw.hip) instead of an interpreter.  Introspection for tests and the
+   bench (MQ_NO_GATHER_COLUMNS=1 disables the path). */
+int mq_tapes_column_gather(mq_tapes* tapes, int32_t* n_gather_columns);
+
 /* Hoisted columns that are exactly keccak256(concat of model variables and constants) — the
    keccak applications of kfm.py:95-114 / instructions.py:1043-1052 over candidate models —
    evaluated by the dedicated keccak-f[1600] column kernel instead of an interpreter.

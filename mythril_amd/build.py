@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libmq.so")
 OBJDIR = os.path.join(HERE, "csrc", "_obj")
-SOURCES = ["mq_api.cpp", "host_keccak.cpp", "tape_compiler.cpp", "qs_kernels.hip", "keccak.hip", "qsa.hip", "fc.hip"]
+SOURCES = ["mq_api.cpp", "host_keccak.cpp", "tape_compiler.cpp", "qs_kernels.hip", "keccak.hip", "qsa.hip", "fc.hip", "cw.hip"]
 HEADERS = ["host_keccak.h", "gprog.h", "bvops.h", "qs_launch.h", "tape_compiler.h", "qsa_table.h", "qsa_gen.inc"]
 ARCH = os.environ.get("MQ_OFFLOAD_ARCH", "gfx950")
 

@@ -22,6 +22,7 @@
 //    accept masks over (x < c, x == c, x > c) (host-encoded, signed compares with the sign bit
 //    pre-flipped), so no scalar branching on it.  Variables of one or two limbs (most hoisted
 //    words are narrow) take one pair, wider ones four.
+// A descriptor with bit 31 of n_mask set is the negation of its conjunction: an OR of atoms.
 // Modes: 0 first hit (best[] atomicMin, early exit on best[]), 1 verdict bytes, 3 Bool columns
 // (packed lane mask stored, and the 0/1 row when a HIP C++ kernel reads rows or the column has no
 // mask index).
@@ -152,7 +153,8 @@ __global__ __launch_bounds__(256) void fc_kernel(const FcTape* __restrict__ tape
     for (int j = 0; j < FC_TILES; j++) acc[j] = valid[j];
     // Bool variables, 16 at a time: lane l takes entry l % 16 of the list (LDS offset, bit 0:
     // negated) for tile l / 16
-    for (uint32_t e0 = 0; e0 < d.n_mask; e0 += 16) {
+    const uint32_t n_mask = d.n_mask & 0x7FFFFFFFu;
+    for (uint32_t e0 = 0; e0 < n_mask; e0 += 16) {
       const uint32_t e = mask_lds[d.mask_off + e0 + (lane & 15)];
       uint64_t w = *reinterpret_cast<const uint64_t*>(lmask_b + (e & ~7u));
       if (e & 1u) w = ~w;
@@ -168,6 +170,10 @@ __global__ __launch_bounds__(256) void fc_kernel(const FcTape* __restrict__ tape
       const FcCmpHead h = qp->h;
 #pragma unroll
       for (int j = 0; j < FC_TILES; j++) acc[j] &= fc_cmp(lds_lane, h, qp, j);
+    }
+    if (d.n_mask >> 31) {   // a negated conjunction (an OR of atoms, De Morgan)
+#pragma unroll
+      for (int j = 0; j < FC_TILES; j++) acc[j] = ~acc[j] & valid[j];
     }
 #pragma unroll
     for (int j = 0; j < FC_TILES; j++) {
@@ -196,7 +202,7 @@ __global__ __launch_bounds__(256) void fc_kernel(const FcTape* __restrict__ tape
     const unsigned long long nodes = r.prefix[2 * t1] - r.prefix[2 * t0] - skipped_nodes;
     const unsigned long long ops = r.prefix[2 * t1 + 1] - r.prefix[2 * t0 + 1] - skipped_ops;
     unsigned long long* cnt = r.counters + ((blockIdx.x * 4 + wave + blockIdx.y) % kCounterSlots) * kCounterStride;
-    atomicAdd(&cnt[0], runs * nv);
+    if (r.mode != 3) atomicAdd(&cnt[0], runs * nv);   // (tape evaluations; a column is not one)
     atomicAdd(&cnt[1], nodes * nv);
     atomicAdd(&cnt[2], ops * nv);
   }

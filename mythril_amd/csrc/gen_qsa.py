@@ -1752,6 +1752,17 @@ def frame(variant, pfx, handlers, subs):
         "s_add_u32 s25, s24, s83",
         "s_min_u32 s25, s25, s82",
     ] + ([
+        # G mode 3: a column level's groups are uneven (balanced by cost, mq_api.cpp
+        # balance_groups): group g spans descriptors [t[g], t[g+1]) of the u32 table t at
+        # args+0x38 (table_out, which only mode 2 writes)
+        "s_cmp_eq_u32 s31, 3",
+        f"s_cbranch_scc0 {pfx}_groups_done",
+        "s_lshl_b32 s68, s97, 2",
+        "s_load_dwordx2 s[24:25], s[78:79], s68",
+        "s_waitcnt lgkmcnt(0)",
+        "s_min_u32 s25, s25, s82",
+        f"{pfx}_groups_done:",
+    ] if G else []) + ([
         # G: s[96:97] = this tile's packed Bool masks, bool_masks + 8 * tile * n_bool_masks
         "s_load_dwordx2 s[64:65], s[10:11], 0x198",
         "s_load_dword s66, s[10:11], 0x1a0",

@@ -410,12 +410,39 @@ struct mq_tapes {
   std::vector<std::pair<int, int>> kc_level;   // (first, count) in kc, per column level
   uint64_t kc_gen = ~0ull;                      // layout_gen of the uploaded map
   DevBuf kc_cols_dev, kc_map_dev, kc_pred_dev;
+  // bit-gather columns (cw.hip, cw_compile): columns that are an arrangement of variable bits and
+  // constants, runs gated by `i <s size` (calldata words); per output limb its slots
+  struct CwSlotHost {
+    int32_t var;
+    uint32_t vlimb, mask, shifts, gate;
+  };
+  struct CwHost {
+    int32_t target = -1, size_var = -1;   // size_var -1: no gated slot
+    uint32_t n_nodes = 0, alg_ops = 0;
+    std::vector<std::vector<CwSlotHost>> limb_slots;
+    std::vector<uint32_t> const_or;
+  };
+  std::vector<CwHost> cw;
+  std::vector<std::pair<int, int>> cw_level;   // (first, count) in cw, per column level
+  uint64_t cw_gen = ~0ull;
+  DevBuf cw_cols_dev, cw_chunks_dev;
   std::vector<char> col_direct_mask;            // per column: its lane masks are stored by its kernel
   // flat conjunctions (fc.hip): QSA-eligible tapes that are an AND of Bool variables and
   // variable-constant compares, run on fc_kernel instead of P / G (per model batch: qsa_prepare)
   int fc_count = 0;
   int fc_stage_n = 0, fc_smask_n = 0;
   DevBuf fc_tapes_dev, fc_mask_dev, fc_cmp_dev, fc_stage_dev, fc_smask_dev, fc_prefix_dev;
+  // the G-eligible Bool columns of a level that are flat (fc_match) run on fc_kernel, mode 3,
+  // before the level's G launch (cq_prepare); the level's G descriptors are the others
+  struct FcLevel {
+    int count = 0, stage_n = 0, smask_n = 0;
+    DevBuf tapes, mask, cmp, stage, smask, prefix;
+  };
+  std::vector<std::unique_ptr<FcLevel>> fc_lvl;
+  std::vector<int> cq_lvl_desc_off, cq_lvl_desc_n;
+  std::vector<uint32_t> cq_group_tab, cq_lvl_tab_off;   // per level: its G groups' descriptor bounds
+  std::vector<int> cq_lvl_groups;
+  DevBuf cq_group_dev;
   // multi-device context: the same batch compiled on each peer device (ctx->peers order)
   std::vector<mq_tapes*> peers;
   ~mq_tapes() {
@@ -2163,6 +2190,145 @@ static bool kp_match(const mq_tape_batch* progs, int32_t k, int32_t* var, uint32
   return true;
 }
 
+// A column program that only arranges bits (cw.hip): VAR, CONST, CONCAT, EXTRACT, ZEXT, BAND
+// with a constant operand, and ITE(SLT(CONST i, VAR size), x, 0) with 0 <= i < 2^31 and one
+// 256-bit size variable per column (lower.py's calldata bytes, calldata.py:234-247), over a
+// bit-vector root of at most 256 bits.  Each node's value is evaluated symbolically bit by bit
+// (a source variable bit or a constant, and the gate); the root's bits are then grouped into
+// runs of consecutive bits of one variable limb under one gate: the slots of its output limbs.
+static bool cw_compile(const mq_tape_batch* progs, int32_t k, mq_tapes::CwHost& h) {
+  const int64_t base = progs->tape_offsets[k];
+  const int64_t nn = progs->tape_offsets[k + 1] - base;
+  if (nn < 2 || nn > 4096) return false;
+  const mq_node* nd = progs->nodes + base;
+  const mq_node& root = nd[nn - 1];
+  if (root.width == 0 || root.width > 256) return false;
+  struct Bit {
+    int32_t var;    // >= 0: a variable; -1: constant 0; -2: constant 1
+    uint32_t bit;   // the variable's bit
+    uint32_t gate;  // ~0u: ungated; else i of `i <s size`
+  };
+  std::vector<std::vector<Bit>> val(nn);
+  std::vector<char> need(nn, 0);
+  need[nn - 1] = 1;
+  // which nodes the root reaches (a dead node of any op does not block the match)
+  for (int64_t i = nn - 1; i >= 0; i--) {
+    if (!need[i]) continue;
+    const mq_node& n = nd[i];
+    auto mark = [&](uint32_t j) -> bool {
+      if (j >= (uint32_t)i) return false;
+      need[j] = 1;
+      return true;
+    };
+    switch (n.op) {
+      case MQ_OP_VAR: case MQ_OP_CONST: break;
+      case MQ_OP_EXTRACT: case MQ_OP_ZEXT: if (!mark(n.a)) return false; break;
+      case MQ_OP_CONCAT: case MQ_OP_BAND: case MQ_OP_SLT: if (!mark(n.a) || !mark(n.b)) return false; break;
+      case MQ_OP_ITE: if (!mark(n.a) || !mark(n.b) || !mark(n.c)) return false; break;
+      default: return false;
+    }
+  }
+  int32_t size_var = -1;
+  const Bit zero{-1, 0, ~0u};
+  auto is_const = [&](const std::vector<Bit>& v) {
+    for (const Bit& b : v)
+      if (b.var >= 0) return false;
+    return true;
+  };
+  for (int64_t i = 0; i < nn; i++) {
+    if (!need[i]) continue;
+    const mq_node& n = nd[i];
+    std::vector<Bit>& r = val[i];
+    switch (n.op) {
+      case MQ_OP_VAR:
+        if (n.width == 0 || n.width > 256) return false;
+        for (uint32_t b = 0; b < n.width; b++) r.push_back(Bit{(int32_t)n.a, b, ~0u});
+        break;
+      case MQ_OP_CONST: {
+        if (n.width == 0 || n.width > 256 || (int64_t)n.a + (n.width + 31) / 32 > progs->n_const_words) return false;
+        for (uint32_t b = 0; b < n.width; b++)
+          r.push_back((progs->const_words[n.a + b / 32] >> (b % 32)) & 1u ? Bit{-2, 0, ~0u} : zero);
+        break;
+      }
+      case MQ_OP_CONCAT:
+        r = val[n.b];
+        r.insert(r.end(), val[n.a].begin(), val[n.a].end());
+        break;
+      case MQ_OP_EXTRACT:
+        if (n.c > n.b || n.b >= val[n.a].size()) return false;
+        r.assign(val[n.a].begin() + n.c, val[n.a].begin() + n.b + 1);
+        break;
+      case MQ_OP_ZEXT:
+        r = val[n.a];
+        r.resize(n.width, zero);
+        break;
+      case MQ_OP_BAND: {
+        const std::vector<Bit>&x = val[n.a], &y = val[n.b];
+        if (x.size() != y.size()) return false;
+        const bool cy = is_const(y), cx = is_const(x);
+        if (!cx && !cy) return false;
+        const std::vector<Bit>&v = cy ? x : y, &c = cy ? y : x;
+        for (size_t b = 0; b < v.size(); b++) r.push_back(c[b].var == -2 ? v[b] : zero);
+        break;
+      }
+      case MQ_OP_SLT: {   // only as an ITE condition: checked there
+        const mq_node &a = nd[n.a], &s = nd[n.b];
+        if (a.op != MQ_OP_CONST || a.width != 256 || s.op != MQ_OP_VAR || s.width != 256) return false;
+        if ((int64_t)a.a + 8 > progs->n_const_words) return false;
+        for (int l = 1; l < 8; l++)
+          if (progs->const_words[a.a + l]) return false;
+        if (progs->const_words[a.a] >= 0x80000000u) return false;
+        if (size_var >= 0 && size_var != (int32_t)s.a) return false;
+        size_var = (int32_t)s.a;
+        break;
+      }
+      case MQ_OP_ITE: {
+        const mq_node& cnd = nd[n.a];
+        if (cnd.op != MQ_OP_SLT) return false;
+        const uint32_t gate = progs->const_words[nd[cnd.a].a];
+        const std::vector<Bit>&t = val[n.b], &e = val[n.c];
+        if (t.size() != e.size()) return false;
+        for (const Bit& b : e)
+          if (b.var != -1) return false;   // else branch: 0
+        for (const Bit& b : t) {
+          if (b.gate != ~0u) return false;   // nested gates
+          r.push_back(b.var == -1 ? zero : Bit{b.var, b.bit, gate});   // (a constant 1 bit would need a gated const)
+          if (b.var == -2) return false;
+        }
+        break;
+      }
+      default: return false;
+    }
+    if (n.op != MQ_OP_SLT && r.size() != n.width) return false;
+  }
+  const std::vector<Bit>& out = val[nn - 1];
+  const uint32_t W = root.width, nl = (W + 31) / 32;
+  h.size_var = size_var;
+  h.limb_slots.assign(nl, {});
+  h.const_or.assign(nl, 0);
+  for (uint32_t l = 0; l < nl; l++) {
+    for (uint32_t b = 32 * l; b < std::min(W, 32 * l + 32);) {
+      const Bit& s = out[b];
+      if (s.var < 0) {
+        if (s.var == -2) h.const_or[l] |= 1u << (b - 32 * l);
+        b++;
+        continue;
+      }
+      uint32_t len = 1;
+      while (b + len < std::min(W, 32 * l + 32)) {
+        const Bit& t = out[b + len];
+        if (t.var != s.var || t.gate != s.gate || t.bit != s.bit + len || t.bit / 32 != s.bit / 32) break;
+        len++;
+      }
+      const uint32_t mask = len == 32 ? ~0u : (1u << len) - 1u;
+      h.limb_slots[l].push_back(
+          mq_tapes::CwSlotHost{s.var, s.bit / 32, mask, (s.bit % 32) | ((b - 32 * l) << 8), s.gate});
+      b += len;
+    }
+  }
+  return true;
+}
+
 static int set_columns_one(mq_tapes* T, const mq_tape_batch* progs, const int32_t* var_index, const int32_t* level_in,
                            int32_t n_columns) {
   mq_ctx* c = T->ctx;
@@ -2176,6 +2342,8 @@ static int set_columns_one(mq_tapes* T, const mq_tape_batch* progs, const int32_
   T->col_width.assign(n_columns, 0);
   T->kc.clear();
   T->kc_level.clear();
+  T->cw.clear();
+  T->cw_level.clear();
   if (n_columns == 0) return MQ_OK;
   CompileLimits lim;
   lim.g_depth = kQsaStackG;
@@ -2207,6 +2375,15 @@ static int set_columns_one(mq_tapes* T, const mq_tape_batch* progs, const int32_
         kcm[k] = 1;
         kcol_of_var[var_index[k]] = k;
       }
+  }
+  // bit-gather columns (calldata words; MQ_NO_GATHER_COLUMNS=1: leave them to the interpreters)
+  std::vector<char> cwm(n_columns, 0);
+  std::vector<mq_tapes::CwHost> cwh(n_columns);
+  if (!std::getenv("MQ_NO_GATHER_COLUMNS")) {
+    parallel_for(n_columns, 16, [&](int, int64_t b, int64_t e) {
+      for (int64_t k = b; k < e; k++)
+        if (!kcm[k] && T->col_width[k] != 0 && cw_compile(progs, (int32_t)k, cwh[k])) cwm[k] = 1;
+    });
   }
   std::vector<int> kp_of(n_columns, -1);   // predicate column -> its keccak column
   std::vector<mq_tapes::KcPredHost> kp_host(n_columns);
@@ -2298,6 +2475,23 @@ static int set_columns_one(mq_tapes* T, const mq_tape_batch* progs, const int32_
     }
     T->kc_level[lv].second = (int)T->kc.size() - T->kc_level[lv].first;
   }
+  T->cw.clear();
+  T->cw_gen = ~0ull;
+  T->cw_level.assign((size_t)max_level + 1, {0, 0});
+  for (int lv = 0; lv <= max_level; lv++) {
+    T->cw_level[lv].first = (int)T->cw.size();
+    for (int k = 0; k < n_columns; k++) {
+      if (level[k] != lv || !cwm[k]) continue;
+      mq_tapes::CwHost& h = cwh[k];
+      h.target = var_index[k];
+      h.n_nodes = ct[k].n_nodes;
+      h.alg_ops = (uint32_t)std::min(ct[k].alg_ops, 4.0e9);
+      T->cw.push_back(std::move(h));
+    }
+    T->cw_level[lv].second = (int)T->cw.size() - T->cw_level[lv].first;
+  }
+  for (int k = 0; k < n_columns; k++)
+    if (cwm[k]) kcm[k] = 2;   // (off the interpreters below, as keccak columns)
   std::vector<char> gq(n_columns, 0);
   if (c->qsa_ready)
     for (int k = 0; k < n_columns; k++)
@@ -2522,12 +2716,28 @@ static constexpr uint32_t kAccEq = 2, kAccNe = 5, kAccLt = 1, kAccLe = 3, kAccGt
 static constexpr int kFcStageRows = 40;
 static constexpr int kFcStageMasks = 256;
 
-static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_t>& masks, std::vector<FcCmpH>& cmps) {
+// A program that is a flat conjunction of atoms (Bool variables, variable-constant compares),
+// or the negation of one: ORs of atoms and of negated conjunctions are taken by De Morgan
+// (OR(a, b) = NOT(AND(NOT a, NOT b))), the result negation returned in *neg.
+static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_t>& masks, std::vector<FcCmpH>& cmps,
+                     bool* neg = nullptr) {
   struct Item {
-    int kind = 0;   // 0 model variable (BV), 1 constant, 2 conjunction
+    int kind = 0;   // 0 model variable (BV), 1 constant, 2 conjunction (negated when neg)
     uint32_t v = 0;
+    bool neg = false;
     std::vector<uint32_t> m;
     std::vector<FcCmpH> q;
+  };
+  // NOT of an item as a plain conjunction: a single atom negated, or a negated conjunction's body
+  auto negate_to_conj = [](Item& a) -> bool {
+    if (a.neg) {
+      a.neg = false;
+      return true;
+    }
+    if (a.m.size() + a.q.size() != 1) return false;
+    if (!a.m.empty()) a.m[0] ^= 0x80000000u;
+    else a.q[0].accept ^= 7u;
+    return true;
   };
   std::vector<Item> st;
   const auto& pr = x.prog;
@@ -2575,16 +2785,20 @@ static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_
       case G_NOT: {
         if (st.empty() || st.back().kind != 2) return false;
         Item& a = st.back();
-        if (a.m.size() + a.q.size() != 1) return false;
-        if (!a.m.empty()) a.m[0] ^= 0x80000000u;
-        else a.q[0].accept ^= 7u;
+        if (!negate_to_conj(a)) a.neg = true;   // NOT of a conjunction of several atoms
         break;
       }
-      case G_AND: {
+      case G_AND: case G_OR: {
         if (st.size() < 2 || st.back().kind != 2 || st[st.size() - 2].kind != 2) return false;
         Item b = std::move(st.back());
         st.pop_back();
         Item& a = st.back();
+        if (op == G_OR) {   // NOT(AND(NOT a, NOT b))
+          if (!negate_to_conj(a) || !negate_to_conj(b)) return false;
+          a.neg = true;
+        } else if (a.neg || b.neg) {
+          return false;
+        }
         a.m.insert(a.m.end(), b.m.begin(), b.m.end());
         a.q.insert(a.q.end(), b.q.begin(), b.q.end());
         break;
@@ -2630,6 +2844,8 @@ static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_
     }
   }
   if (st.size() != 1 || st[0].kind != 2) return false;
+  if (st[0].neg && !neg) return false;
+  if (neg) *neg = st[0].neg;
   masks.insert(masks.end(), st[0].m.begin(), st[0].m.end());
   cmps.insert(cmps.end(), st[0].q.begin(), st[0].q.end());
   return true;
@@ -2648,7 +2864,7 @@ struct FcPlan {
   std::vector<unsigned long long> prefix;
 };
 static void fc_plan(const mq_ctx* c, const std::vector<std::vector<uint32_t>>& fm, const std::vector<std::vector<FcCmpH>>& fq,
-                    std::vector<char>& keep, const std::function<uint32_t(size_t)>& out_of,
+                    const std::vector<char>& negated, std::vector<char>& keep, const std::function<uint32_t(size_t)>& out_of,
                     const std::function<int32_t(size_t)>& mask_out,
                     const std::function<std::pair<uint32_t, uint32_t>(size_t)>& nodes_ops, FcPlan& P) {
   const uint32_t zero_row = (uint32_t)(c->var_off_h.empty() ? 0 : c->var_off_h.back() + c->var_nl_h.back());
@@ -2694,7 +2910,7 @@ static void fc_plan(const mq_ctx* c, const std::vector<std::vector<uint32_t>>& f
     f.out = out_of(i);
     f.mask_out = mask_out(i);
     f.mask_off = (uint32_t)P.mask_lds.size();
-    f.n_mask = (uint32_t)fm[i].size();
+    f.n_mask = (uint32_t)fm[i].size() | (negated[i] ? 0x80000000u : 0u);
     for (uint32_t e : fm[i]) P.mask_lds.push_back(8u * mslot_of[e & 0x7FFFFFFFu] | (e >> 31));
     if (!fm[i].empty())
       while (P.mask_lds.size() % 16) P.mask_lds.push_back(P.mask_lds.back());   // (the same AND again)
@@ -2739,12 +2955,17 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
   std::vector<char> on_fc(nq, 0);
   std::vector<std::vector<uint32_t>> fc_m(nq);
   std::vector<std::vector<FcCmpH>> fc_q(nq);
+  std::vector<char> fc_neg(nq, 0);
   if (!no_flat)
     parallel_for(nq, 32, [&](int, int64_t b, int64_t e) {
-      for (int64_t i = b; i < e; i++) on_fc[i] = fc_match(c, T->qct[i], fc_m[i], fc_q[i]) ? 1 : 0;
+      for (int64_t i = b; i < e; i++) {
+        bool ng = false;
+        on_fc[i] = fc_match(c, T->qct[i], fc_m[i], fc_q[i], &ng) ? 1 : 0;
+        fc_neg[i] = ng ? 1 : 0;
+      }
     });
   FcPlan fcp;
-  fc_plan(c, fc_m, fc_q, on_fc, [&](size_t i) { return T->qbase[i].tape; }, [](size_t) { return (int32_t)-1; },
+  fc_plan(c, fc_m, fc_q, fc_neg, on_fc, [&](size_t i) { return T->qbase[i].tape; }, [](size_t) { return (int32_t)-1; },
           [&](size_t i) { return std::make_pair(T->qbase[i].n_nodes, T->qbase[i].alg_ops); }, fcp);
   // (P preloads variables 0-7 only: a program pushing any other variable is not tried on P)
   auto p_candidate = [](const CompiledTape& x) {
@@ -2890,6 +3111,52 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
   return MQ_OK;
 }
 
+// Latency weight of a G program on one tile: its ops, plus the round trips of its variable
+// pushes and table lookups (a store chain's select ends in a lookup; these dominate a column level)
+static double g_cost(const CompiledTape& x) {
+  double w = 0;
+  for (size_t pc = 0; pc < x.prog.size(); pc++) {
+    const uint32_t op = x.prog[pc] & 0xFFu;
+    w += 1;
+    if (op == G_PUSH_VAR || op == G_PUSH_VAR_B) w += 4;
+    if (op == G_UF1 || op == G_UF2 || op == G_UFK0 || op == G_UFK || op == G_UFKV) w += 24;
+    if (has_imm2(op)) pc++;
+  }
+  return w;
+}
+
+// Split a column level's G programs into groups (a group = one wave of G on one tile; group g
+// = descriptors [tab[g], tab[g+1]), the table gen_qsa.py's mode-3 prologue reads) so the
+// heaviest group is as light as it can be: longest processing time first over
+// min(n, ceil(n / tpg) rounded up to the workgroup's 4 waves) groups, of any sizes.  A workgroup
+// holds its LDS until its slowest wave ends, so a level's time follows its heaviest group (C4
+// level 2, five store chains: three in one wave of three 0.69 ms; 2-2-1 0.50 ms).  Reorders idx
+// group by group; tab gets groups rounded up to 4, + 1 entries (empty groups past the last).
+static void balance_groups(const std::vector<CompiledTape>& ct, std::vector<int>& idx, int tpg,
+                           std::vector<uint32_t>& tab) {
+  const int n = (int)idx.size();
+  const int groups = std::max(1, std::min(n, ((n + tpg - 1) / tpg + 3) / 4 * 4));
+  std::vector<std::pair<double, int>> w;
+  for (int i : idx) w.push_back({g_cost(ct[i]), i});
+  std::stable_sort(w.begin(), w.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+  std::vector<double> load(groups, 0);
+  std::vector<std::vector<int>> members(groups);
+  for (const auto& x : w) {
+    int best = 0;
+    for (int g = 1; g < groups; g++)
+      if (load[g] < load[best]) best = g;
+    members[best].push_back(x.second);
+    load[best] += x.first;
+  }
+  idx.clear();
+  tab.assign(1, 0);
+  for (const auto& m : members) {
+    idx.insert(idx.end(), m.begin(), m.end());
+    tab.push_back((uint32_t)idx.size());
+  }
+  while ((tab.size() - 1) % 4) tab.push_back((uint32_t)n);
+}
+
 // Translate the G-eligible column programs for the current model batch (variable rows): one
 // program segment and descriptor list, levels contiguous.  GDesc for mode 3: tape = first row
 // of the target variable, n_temps = its limbs, depth = Bool root (gen_qsa.py store_column).
@@ -2907,10 +3174,71 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
   T->cq_lvl_stage_off.assign(T->clevels.size(), 0);
   T->cq_lvl_stage_n.assign(T->clevels.size(), 0);
   T->cq_lvl_temps.assign(T->clevels.size(), 0);
+  T->cq_lvl_desc_off.assign(T->clevels.size(), 0);
+  T->cq_lvl_desc_n.assign(T->clevels.size(), 0);
+  T->cq_lvl_tab_off.assign(T->clevels.size(), 0);
+  T->cq_lvl_groups.assign(T->clevels.size(), 0);
+  T->cq_group_tab.clear();
+  T->fc_lvl.clear();
+  T->fc_lvl.resize(T->clevels.size());
+  const bool no_flat = std::getenv("MQ_NO_FLAT") != nullptr;
   for (size_t li = 0; li < T->clevels.size(); li++) {
-    const int b = T->clevels[li].cq_begin, n = T->clevels[li].v8q;
+    T->fc_lvl[li].reset(new mq_tapes::FcLevel());
+    T->cq_lvl_desc_off[li] = (int)descs.size();
+    const int b = T->clevels[li].cq_begin, n0 = T->clevels[li].v8q;
+    if (n0 <= 0) continue;
+    // the level's flat Bool columns (fc_kernel, mode 3)
+    std::vector<char> on_fc(n0, 0), fneg(n0, 0);
+    std::vector<std::vector<uint32_t>> fm(n0);
+    std::vector<std::vector<FcCmpH>> fq(n0);
+    if (!no_flat)
+      for (int i = 0; i < n0; i++) {
+        bool ng = false;
+        on_fc[i] = T->cq_bool[b + i] && fc_match(c, T->cq_ct[b + i], fm[i], fq[i], &ng) ? 1 : 0;
+        fneg[i] = ng ? 1 : 0;
+      }
+    FcPlan fcp;
+    fc_plan(c, fm, fq, fneg, on_fc, [&](size_t i) { return c->var_off_h[T->cq_var[b + i]]; },
+            [&](size_t i) {
+              const int v = T->cq_var[b + i];
+              return (int32_t)(v < (int)c->bmask_of_var.size() ? c->bmask_of_var[v] : -1);
+            },
+            [&](size_t i) {
+              const CompiledTape& x = T->cq_ct[b + i];
+              return std::make_pair(x.n_nodes, (uint32_t)std::min(x.alg_ops, 4.0e9));
+            },
+            fcp);
+    mq_tapes::FcLevel& fl = *T->fc_lvl[li];
+    fl.count = (int)fcp.tapes.size();
+    if (fl.count > 0) {
+      fl.stage_n = (int)fcp.stage_rows.size();
+      fl.smask_n = (int)fcp.stage_masks.size();
+      if (fcp.mask_lds.empty()) fcp.mask_lds.push_back(0);
+      if (fcp.cmps.empty()) fcp.cmps.push_back(FcCmp{});
+      if (fcp.stage_rows.empty()) fcp.stage_rows.push_back(0);
+      if (fcp.stage_masks.empty()) fcp.stage_masks.push_back(0);
+      HIPCHK(fl.tapes.upload(fcp.tapes.data(), fcp.tapes.size(), c->stream));
+      HIPCHK(fl.mask.upload(fcp.mask_lds.data(), fcp.mask_lds.size(), c->stream));
+      HIPCHK(fl.cmp.upload(fcp.cmps.data(), fcp.cmps.size(), c->stream));
+      HIPCHK(fl.stage.upload(fcp.stage_rows.data(), fcp.stage_rows.size(), c->stream));
+      HIPCHK(fl.smask.upload(fcp.stage_masks.data(), fcp.stage_masks.size(), c->stream));
+      HIPCHK(fl.prefix.upload(fcp.prefix.data(), fcp.prefix.size(), c->stream));
+    }
+    std::vector<int> rest;   // the level's columns left to G
+    for (int i = 0; i < n0; i++)
+      if (!on_fc[i]) rest.push_back(b + i);
+    const int n = (int)rest.size();
+    T->cq_lvl_desc_n[li] = n;
     if (n <= 0) continue;
-    const std::vector<CompiledTape> lvl(T->cq_ct.begin() + b, T->cq_ct.begin() + b + n);
+    {
+      std::vector<uint32_t> tab;
+      balance_groups(T->cq_ct, rest, (int)std::max<int64_t>(1, std::min<int64_t>(cq_tapes_per_group(n, c->M), n)), tab);
+      T->cq_lvl_tab_off[li] = (uint32_t)T->cq_group_tab.size();
+      T->cq_lvl_groups[li] = (int)tab.size() - 1;
+      T->cq_group_tab.insert(T->cq_group_tab.end(), tab.begin(), tab.end());
+    }
+    std::vector<CompiledTape> lvl;
+    for (int i : rest) lvl.push_back(T->cq_ct[i]);
     int temps = 0;
     for (const CompiledTape& x : lvl) temps = std::max(temps, qsa_temps(x, 1));
     const double share = std::min(1.0, 4.0 * (double)cq_tapes_per_group(n, c->M) / (double)n);
@@ -2921,7 +3249,7 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
     T->cq_lvl_stage_n[li] = (uint32_t)rows.size();
     T->cq_lvl_temps[li] = temps;
     T->cq_stage_rows.insert(T->cq_stage_rows.end(), rows.begin(), rows.end());
-    for (int i = b; i < b + n; i++) {
+    for (int i : rest) {
       const CompiledTape& x = T->cq_ct[i];
       if (!qsa_translate(c, 1, true, x, &tr, &extra, nullptr, &gstage)) return MQ_OK;
       qsa_window_layout(c, tr);
@@ -2952,6 +3280,8 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
   HIPCHK(T->cqargs.ensure(sizeof(QArgs) * T->clevels.size()));
   if (T->cq_stage_rows.empty()) HIPCHK(T->cq_stage_dev.ensure(sizeof(uint32_t)));
   else HIPCHK(T->cq_stage_dev.upload(T->cq_stage_rows.data(), T->cq_stage_rows.size(), c->stream));
+  if (T->cq_group_tab.empty()) T->cq_group_tab.assign(5, 0);
+  HIPCHK(T->cq_group_dev.upload(T->cq_group_tab.data(), T->cq_group_tab.size(), c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   T->cqargs_host.assign(T->clevels.size(), QArgs{});
   T->cq_live = true;
@@ -3158,6 +3488,54 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     HIPCHK(hipStreamSynchronize(st));
     T->kc_gen = c->layout_gen;
   }
+  if (!T->cw.empty() && T->cw_gen != c->layout_gen) {
+    // the bit-gather columns' slots under this model batch's variable rows (a variable the batch
+    // lacks, or a limb past its width, reads the zero row: VAR of an absent variable is 0)
+    std::vector<CwCol> cols;
+    std::vector<CwChunk> chunks;
+    auto row_of = [&](int32_t v, uint32_t l) -> uint32_t {
+      return (v >= 0 && v < c->n_vars && l < c->var_nl_h[v]) ? c->var_off_h[v] + l : zero_row;
+    };
+    for (const auto& h : T->cw) {
+      const uint32_t nl = (uint32_t)h.limb_slots.size();
+      if (h.target < 0 || h.target >= c->n_vars || c->var_nl_h[h.target] != nl) {
+        g_last_error = "bit-gather column target does not match the uploaded model batch";
+        return MQ_ERR_ARG;
+      }
+      if (h.size_var >= 0 && (h.size_var >= c->n_vars || c->var_nl_h[h.size_var] != 8)) {
+        g_last_error = "bit-gather column size variable is not a 256-bit variable of the uploaded model batch";
+        return MQ_ERR_ARG;
+      }
+      CwCol col{};
+      col.chunk_off = (uint32_t)chunks.size();
+      col.target_row = c->var_off_h[h.target];
+      col.size_row = h.size_var >= 0 ? c->var_off_h[h.size_var] : ~0u;
+      col.n_nodes = h.n_nodes;
+      col.alg_ops = h.alg_ops;
+      for (uint32_t l = 0; l < nl; l++) {
+        const auto& sl = h.limb_slots[l];
+        const size_t nch = std::max<size_t>(1, (sl.size() + 3) / 4);
+        for (size_t q = 0; q < nch; q++) {
+          CwChunk ch{};
+          for (int j = 0; j < 4; j++) {
+            const size_t i = 4 * q + j;
+            ch.s[j] = i < sl.size() ? CwSlot{row_of(sl[i].var, sl[i].vlimb), sl[i].mask, sl[i].shifts, sl[i].gate}
+                                    : CwSlot{zero_row, 0u, 0u, ~0u};
+          }
+          ch.limb = l;
+          ch.store = q + 1 == nch ? 1u : 0u;
+          ch.const_or = q == 0 ? h.const_or[l] : 0u;
+          chunks.push_back(ch);
+        }
+      }
+      col.n_chunks = (uint32_t)chunks.size() - col.chunk_off;
+      cols.push_back(col);
+    }
+    HIPCHK(T->cw_cols_dev.upload(cols.data(), cols.size(), st));
+    HIPCHK(T->cw_chunks_dev.upload(chunks.data(), chunks.size(), st));
+    HIPCHK(hipStreamSynchronize(st));
+    T->cw_gen = c->layout_gen;
+  }
   // Bool columns' 0/1 rows are read only by the HIP C++ kernels (the assembly interpreters read
   // the packed lane masks, which G's column store writes itself): G writes the rows only when a
   // C++ tape or column kernel, or P (rows of preloaded variables), runs in this launch
@@ -3178,13 +3556,47 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
                                    c->counters.as<unsigned long long>(), c->bmasks.as<uint64_t>(), c->n_bmask,
                                    bool_rows ? 1 : 0, st));
     }
+    if (li < T->cw_level.size() && T->cw_level[li].second > 0) {
+      HIPCHK(start_timer());
+      HIPCHK(launch_cw_columns(T->cw_cols_dev.as<CwCol>() + T->cw_level[li].first, T->cw_level[li].second,
+                               T->cw_chunks_dev.as<CwChunk>(), const_cast<uint32_t*>(c->vars.as<uint32_t>()), c->M,
+                               c->counters.as<unsigned long long>(), st));
+    }
     const mq_tapes::Variant v8 = use_cq ? cut_front(lv.v[0], lv.v8q) : lv.v[0];
-    if (use_cq && lv.v8q > 0) {
+    if (use_cq && li < T->fc_lvl.size() && T->fc_lvl[li] && T->fc_lvl[li]->count > 0) {
+      // the level's flat Bool columns on fc_kernel, mode 3
+      const mq_tapes::FcLevel& fl = *T->fc_lvl[li];
+      FcArgs f{};
+      f.tapes = fl.tapes.as<FcTape>();
+      f.n = fl.count;
+      f.tpg = (int)std::max<int64_t>(1, std::min<int64_t>((f.n + 3) / 4, 64));
+      f.stage_rows = fl.stage.as<uint32_t>();
+      f.n_stage = fl.stage_n;
+      f.stage_masks = fl.smask.as<uint32_t>();
+      f.n_smask = fl.smask_n;
+      f.prefix = fl.prefix.as<unsigned long long>();
+      f.mask_lds = fl.mask.as<uint32_t>();
+      f.cmps = fl.cmp.as<FcCmp>();
+      f.vars = c->vars.as<uint32_t>();
+      f.bool_masks = c->bmasks.as<uint64_t>();
+      f.bool_masks_out = c->bmasks.as<uint64_t>();
+      f.vars_out = const_cast<uint32_t*>(c->vars.as<uint32_t>());
+      f.n_bool_masks = c->n_bmask;
+      f.mode = 3;
+      f.bool_rows = bool_rows ? 1 : 0;
+      f.M = c->M;
+      f.index_base = c->index_base;
+      f.counters = c->counters.as<unsigned long long>();
+      HIPCHK(start_timer());
+      HIPCHK(launch_fc(f, st));
+    }
+    const int n_gcol = use_cq && li < T->cq_lvl_desc_n.size() ? T->cq_lvl_desc_n[li] : 0;
+    if (n_gcol > 0) {
       // the level's G columns on qsg_kernel, mode 3 (no preloaded variables)
-      const int n = lv.v8q;
+      const int n = n_gcol;
       const int64_t tpg = std::max<int64_t>(1, std::min<int64_t>(cq_tapes_per_group(n, c->M), n));
       QArgs q{};
-      q.descs = T->cqdescs.as<GDesc>() + lv.cq_begin;
+      q.descs = T->cqdescs.as<GDesc>() + T->cq_lvl_desc_off[li];
       q.prog = T->cqprog.p;
       q.consts = T->cqconsts.p;
       q.vars = c->vars.p;
@@ -3197,6 +3609,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       q.tapes_per_group = (uint32_t)tpg;
       q.early_exit = 0;
       q.mode = 3;
+      q.table_out = T->cq_group_dev.as<uint32_t>() + T->cq_lvl_tab_off[li];   // the level's group bounds
       q.bool_rows = bool_rows ? 1u : 0u;
       q.lds_wave_bytes = (uint32_t)T->cq_lvl_temps[li] * 2048u;
       q.n_stage = T->cq_lvl_stage_n[li];
@@ -3221,7 +3634,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
         HIPCHK(hipStreamSynchronize(st));  // q is host memory
         T->cqargs_host[li] = q;
       }
-      const int64_t groups = (n + tpg - 1) / tpg;
+      const int64_t groups = T->cq_lvl_groups[li];
       const int64_t rows = ((c->M + 63) / 64 + 7) / 8;
       if (rows > 65535) {
         g_last_error = "G kernel: more than 33.5M models in one launch (grid.y limit); shard the model axis";
@@ -3665,14 +4078,30 @@ int mq_qsa_profile(mq_ctx* c, int64_t* out, int32_t cap, int32_t* n_out, int res
 int mq_tapes_flat_split(mq_tapes* T, int32_t* n_flat_tapes, int32_t* n_flat_columns) {
   if (!T) return MQ_ERR_ARG;
   if (n_flat_tapes) *n_flat_tapes = T->qsa_live ? T->fc_count : 0;
-  if (n_flat_columns) *n_flat_columns = 0;
+  if (n_flat_columns) {
+    int32_t n = 0;
+    if (T->cq_live)
+      for (const auto& fl : T->fc_lvl) n += fl ? fl->count : 0;
+    *n_flat_columns = n;
+  }
   return MQ_OK;
 }
 
 int mq_tapes_column_split(mq_tapes* T, int32_t* n_asm, int32_t* live) {
   if (!T) return MQ_ERR_ARG;
-  if (n_asm) *n_asm = T->cq_live ? (int32_t)T->cq_ct.size() : 0;
+  if (n_asm) {   // (on qsg_kernel: the G-eligible columns less the flat ones fc_kernel runs)
+    int32_t n = 0;
+    if (T->cq_live)
+      for (int x : T->cq_lvl_desc_n) n += x;
+    *n_asm = n;
+  }
   if (live) *live = T->cq_live ? 1 : 0;
+  return MQ_OK;
+}
+
+int mq_tapes_column_gather(mq_tapes* T, int32_t* n_gather_columns) {
+  if (!T || !n_gather_columns) return MQ_ERR_ARG;
+  *n_gather_columns = (int32_t)T->cw.size();
   return MQ_OK;
 }
 

@@ -157,6 +157,31 @@ hipError_t launch_keccak_columns(const KcCol* cols, int n_cols, const KcMapEntry
                                  uint32_t* vars, int64_t M, unsigned long long* counters, uint64_t* bool_masks,
                                  int n_bool_masks, int bool_rows, hipStream_t st);
 
+// Bit-gather columns (cw.hip, mq_api.cpp cw_compile): a hoisted column whose value is model
+// variable bits and constants, runs of bits optionally gated by `i <s size` (one 256-bit size
+// variable per column).  Output limb `limb` = const_or | OR over its slots of
+// (((vars[row] >> sb) & mask) << db), a slot whose gate fails giving 0; chunks of one limb are
+// consecutive, the last one with store = 1.
+struct CwSlot {
+  uint32_t row;     // the variable row (a zero row, mask 0: an empty slot)
+  uint32_t mask;
+  uint32_t shifts;  // sb | db << 8
+  uint32_t gate;    // i (< 2^31): the slot counts when i <s size; ~0u: ungated
+};
+struct CwChunk {
+  CwSlot s[4];
+  uint32_t limb, store, const_or, pad;
+};
+struct CwCol {
+  uint32_t chunk_off, n_chunks;
+  uint32_t target_row;  // limb 0 row of the column's variable
+  uint32_t size_row;    // limb 0 row of the size variable (~0u: no gated slots)
+  uint32_t n_nodes, alg_ops;   // of the column program (metric)
+  uint32_t pad[2];
+};
+hipError_t launch_cw_columns(const CwCol* cols, int n_cols, const CwChunk* chunks, uint32_t* vars, int64_t M,
+                             unsigned long long* counters, hipStream_t st);
+
 // Flat conjunctions (fc.hip, mq_api.cpp fc_match): a tape or Bool column that is an AND of Bool
 // model variables (negated or not) and comparisons of one variable with a constant.
 struct FcCmpHead {    // (one 32-byte scalar load: all a variable of one or two limbs needs)
@@ -179,7 +204,8 @@ struct FcTape {
   uint32_t out;       // modes 0/1: tape index; mode 3: the Bool column's variable row
   int32_t mask_out;   // mode 3: its packed lane-mask index (-1: none, the 0/1 row is written)
   uint32_t mask_off;  // its Bool variables: FcArgs.mask_lds[mask_off ..] = 8 x LDS mask slot | negated,
-  uint32_t n_mask;    //   n_mask of them, padded to a multiple of 16 with the last
+  uint32_t n_mask;    //   n_mask of them, padded to a multiple of 16 with the last (bit 31: the
+                      //   result is negated, an OR of atoms)
   uint32_t cmp_off;   // its compares: FcArgs.cmps[cmp_off ..]
   uint32_t n_cmp;
   uint32_t n_nodes;   // DAG nodes (metric)

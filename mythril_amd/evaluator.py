@@ -65,6 +65,7 @@ def load_library(path: str = LIB_PATH):
         L.mq_tapes_column_split.argtypes = [P] + [C.POINTER(C.c_int32)] * 2
         L.mq_tapes_flat_split.argtypes = [P] + [C.POINTER(C.c_int32)] * 2
         L.mq_tapes_column_keccak.argtypes = [P, C.POINTER(C.c_int32)]
+        L.mq_tapes_column_gather.argtypes = [P, C.POINTER(C.c_int32)]
         L.mq_tapes_qsa_histogram.argtypes = [P, C.c_int32, C.POINTER(C.c_int64), C.c_int32, C.POINTER(C.c_int64),
                                              C.POINTER(C.c_int32)]
         L.mq_qsa_kind_name.argtypes = [C.c_int32]
@@ -265,6 +266,13 @@ class CompiledTapes:
         (mq_tapes_column_keccak_predicates)."""
         n = C.c_int32()
         _check(self.ev.lib.mq_tapes_column_keccak_predicates(self.handle, C.byref(n)), "mq_tapes_column_keccak_predicates")
+        return n.value
+
+    def gather_columns(self) -> int:
+        """Hoisted columns computed by the bit-gather column kernel (cw.hip: calldata words,
+        their extracts and masks; mq_tapes_column_gather)."""
+        n = C.c_int32()
+        _check(self.ev.lib.mq_tapes_column_gather(self.handle, C.byref(n)), "mq_tapes_column_gather")
         return n.value
 
     def keccak_columns(self) -> int:

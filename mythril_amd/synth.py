@@ -367,12 +367,14 @@ FLAT_WIDTHS = (1, 8, 31, 32, 33, 64, 160, 255, 256)
 
 
 def flat_workload(seed: int, n_tapes: int, n_models: int, n_bool: int = 6, planted_frac: float = 0.5,
-                  max_items: int = 12):
+                  max_items: int = 12, or_frac: float = 0.0):
     """Tapes that are ANDs of Bool variables (negated or not) and comparisons of one variable with
     a constant -- every predicate (EQ / distinct / unsigned and signed orders), the constant on
     either side, NOT over a compare, widths that end inside a limb -- the shape the flat-
     conjunction kernel (fc.hip) takes.  About ``planted_frac`` of the tapes are built to hold on a
-    random model (items chosen true there, constants at or next to its values).  Returns
+    random model (items chosen true there, constants at or next to its values).  With
+    ``or_frac``, that share of the tapes are instead an OR of the items, NOT of their AND, or an
+    OR of a NOT(AND) with the rest (the kernel's negated conjunctions, by De Morgan).  Returns
     (tapes, models)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     bv_widths = [int(w) for w in rng.choice(FLAT_WIDTHS, 6)] + [256, 8]
@@ -419,5 +421,15 @@ def flat_workload(seed: int, n_tapes: int, n_models: int, n_bool: int = 6, plant
             items.append(t.not_(node) if negate else node)
         if rng.random() < 0.1:
             items.append(t.true())
+        if len(items) >= 2 and rng.random() < or_frac:
+            k, half = int(rng.integers(3)), len(items) // 2
+            if k == 0:
+                root = t.or_(*items)
+            elif k == 1:
+                root = t.not_(t.and_(*items))
+            else:
+                root = t.or_(t.not_(t.and_(*items[:half])), *items[half:])
+            tapes.append(t.finish(root))
+            continue
         tapes.append(t.finish(t.and_(*items)))
     return TapeBatch(tapes), mb

@@ -492,11 +492,13 @@ def test_c5_deep_tapes_match_oracle(evaluator, hoist):
 
 
 # ---------------------------------------------------------------- batch-level hoisting (column programs)
-@pytest.mark.parametrize("col_min_nodes", ["0", None, "40"])
+@pytest.mark.parametrize("col_min_nodes", ["0", None, "8"])
 def test_c3_hoisted_columns_match_unhoisted_oracle(evaluator, monkeypatch, col_min_nodes):
-    """col_min_nodes "0": every column on the G assembly kernel (mode 3); None: the default split;
-    "40": columns under 40 nodes on the HIP C++ column kernel, the rest on G, in one launch (G
-    then writes its Bool columns' 0/1 rows too, and only the C++ columns' masks are packed)."""
+    """col_min_nodes "0": every column on the G assembly kernel (mode 3) or the kernels that take
+    their shapes (flat Bool columns: fc_kernel; calldata words: the bit-gather kernel); None: the
+    default split; "8": columns under 8 nodes on the HIP C++ column kernel, the rest on G, in one
+    launch (G then writes its Bool columns' 0/1 rows too, and only the C++ columns' masks are
+    packed)."""
     from mythril_amd.synth_evm import c3_workload
     if col_min_nodes is not None:
         monkeypatch.setenv("MQ_G_COL_MIN_NODES", col_min_nodes)
@@ -510,9 +512,11 @@ def test_c3_hoisted_columns_match_unhoisted_oracle(evaluator, monkeypatch, col_m
     ref, _ = cref.first_hit(plain[0], plain[1])
     assert (ref == exp).all() and (fh == ref).all(), np.flatnonzero(fh != ref)[:10]
     n_cols_asm, cols_live = ct.column_asm_split()
+    n_flat_cols = ct.flat_split()[1]
     if col_min_nodes == "0":
-        assert cols_live and n_cols_asm >= 0.5 * tb.columns.n, (n_cols_asm, tb.columns.n)
-    if col_min_nodes == "40":
+        assert cols_live and n_cols_asm + n_flat_cols >= 0.5 * tb.columns.n, (n_cols_asm, n_flat_cols, tb.columns.n)
+        assert ct.gather_columns() > 0
+    if col_min_nodes == "8":
         assert cols_live and 0 < n_cols_asm < tb.columns.n, (n_cols_asm, tb.columns.n)
     vref = cref.verdicts(plain[0], plain[1])
     v, _ = evaluator.verdicts(ct)
@@ -604,6 +608,95 @@ def test_c4_keccak_predicates_in_the_keccak_column_kernel(evaluator, monkeypatch
     ref, _ = cref.first_hit(plain[0], plain[1])
     assert (ref == exp).all() and (fh == ref).all(), np.flatnonzero(fh != ref)[:10]
     assert (v == cref.verdicts(plain[0], plain[1])).all()
+
+
+def _calldata_roots(n_roots: int, seed: int):
+    """Conjunctions over one tx's calldata words (calldata.py:48-55 / 234-247 as lower.py sees
+    them): the selector (Extract(255, 224) of word 0), an address word masked to 160 bits, full
+    words, a 31-byte tail, and a word whose top is another column (a 248-bit prefix)."""
+    from mythril_amd import smt as S
+    rng = np.random.default_rng(seed)
+    cds = S.BitVecSym("1_calldatasize", 256)
+    cd = S.Array("1_calldata", 256, 8)
+
+    def byte(i):
+        return S.If(S.BitVecVal(i, 256) < cds, cd[S.BitVecVal(i, 256)], S.BitVecVal(0, 8))
+
+    def word(off, n=32):
+        return S.Concat(*[byte(off + j) for j in range(n)])
+
+    sel = S.Extract(255, 224, word(0))
+    addr = word(4) & S.BitVecVal((1 << 160) - 1, 256)
+    w36, tail = word(36), word(68, 31)
+    glued = S.Concat(tail, byte(99))
+    roots = []
+    for j in range(n_roots):
+        c = [int(x) for x in rng.integers(0, 1 << 62, 4)]
+        roots.append(S.And(sel == S.BitVecVal(0xA9059CBB if j % 3 else 0x23B872DD, 32),
+                           S.ULT(addr, S.BitVecVal(c[0] << 100 | c[1], 256)),
+                           S.ULT(w36, S.BitVecVal(c[2] << 190, 256)),
+                           S.Not(glued == S.BitVecVal(c[3], 256)),
+                           S.ULT(S.BitVecVal(j, 248), tail)))
+    return roots
+
+
+def _calldata_models(n: int, seed: int):
+    """Models whose calldatasize crosses every gate: around the word offsets, 2^31 +- 1, >= 2^32,
+    negative (signed `<`: every byte reads 0), and bytes only partly present."""
+    from mythril_amd.smt_model import Model
+    rng = np.random.default_rng(seed)
+    sizes = [0, 3, 4, 5, 35, 36, 37, 67, 68, 69, 98, 99, 100, 1000, (1 << 31) - 1, 1 << 31, (1 << 32) + 5,
+             1 << 200, 1 << 255, (1 << 256) - 1, (1 << 255) + 77]
+    out = []
+    for i in range(n):
+        cds = sizes[i % len(sizes)] if i % 2 else int(rng.integers(0, 110))
+        present = 100 if i % 5 else int(rng.integers(0, 100))
+        entries = {k: int(rng.integers(0, 256)) for k in range(present)}
+        if i % 3 == 0:
+            entries.update({0: 0xA9, 1: 0x05, 2: 0x9C, 3: 0xBB})
+        for k in range(4, 16):
+            if i % 4 == 0 and k in entries:
+                entries[k] = 0   # address words with clean top bytes
+        out.append(Model({"1_calldatasize": cds}, {"1_calldata": (entries, 0)}))
+    return out
+
+
+@pytest.mark.parametrize("variant", ["gather", "no_gather"])
+def test_calldata_word_columns_on_the_gather_kernel(evaluator, monkeypatch, variant):
+    """Hoisted calldata words (selector extract, masked address, full words, a 31-byte tail and
+    a word with a column prefix) on the bit-gather column kernel (cw.hip) vs the oracle on the
+    UNhoisted lowering: full verdict matrix and first hits, calldatasize across every gate
+    (signed compare: a negative size reads no byte).  no_gather: the same columns on the
+    interpreters (MQ_NO_GATHER_COLUMNS=1)."""
+    from mythril_amd.lower import lower_batch, serialize_models
+    if variant == "no_gather":
+        monkeypatch.setenv("MQ_NO_GATHER_COLUMNS", "1")
+    roots = _calldata_roots(24, 7)
+    models = _calldata_models(3000, 8)
+    tb, syms, _ = lower_batch(roots, hoist=True, hoist_min_nodes=3)
+    tb2, syms2, _ = lower_batch(roots)
+    assert tb.columns.n >= 5
+    evaluator.upload_models(serialize_models(models, syms))
+    ct = evaluator.compile(tb)
+    assert ct.n_unsupported == 0
+    v, fh = evaluator.verdicts(ct)
+    mb2 = serialize_models(models, syms2)
+    vref = cref.verdicts(tb2, mb2)
+    assert (v == vref).all(), np.argwhere(v != vref)[:10]
+    ref, _ = cref.first_hit(tb2, mb2)
+    assert (evaluator.first_hit(ct) == ref).all()
+    assert vref.any() and not vref.all()
+    if variant == "gather":
+        assert ct.gather_columns() >= 5, ct.gather_columns()
+    else:
+        assert ct.gather_columns() == 0
+    # the HIP C++ kernels read the gather columns' rows too
+    evaluator.use_asm(False)
+    try:
+        v3, _ = evaluator.verdicts(ct)
+    finally:
+        evaluator.use_asm(True)
+    assert (v3 == vref).all()
 
 
 # ---------------------------------------------------------------- assembly interpreters: P and G kernels
@@ -1205,6 +1298,26 @@ def test_flat_conjunctions_match_oracle(evaluator, monkeypatch, bmask_cap):
     ct2.free()
 
 
+def test_flat_disjunctions_match_oracle(evaluator, monkeypatch):
+    """ORs of atoms, NOT of an AND, and OR(NOT(AND), atoms...) run on the flat kernel as negated
+    conjunctions (De Morgan); an OR over a multi-atom AND is not flat and stays on the
+    interpreters.  First hits and verdicts against the oracle and against MQ_NO_FLAT=1."""
+    from mythril_amd.synth import flat_workload
+    tb, mb = flat_workload(31, 300, 1000, or_frac=0.6)
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    fh = evaluator.first_hit(ct)
+    assert ct.flat_split()[0] >= 0.9 * tb.n_tapes, ct.flat_split()
+    ref, _ = cref.first_hit(tb, mb)
+    assert (fh == ref).all(), np.flatnonzero(fh != ref)[:10]
+    v, _ = evaluator.verdicts(ct)
+    vref = cref.verdicts(tb, mb)
+    assert (v == vref).all() and 0.05 < vref.mean() < 0.95
+    monkeypatch.setenv("MQ_NO_FLAT", "1")
+    ct2 = evaluator.compile(tb)
+    assert (evaluator.first_hit(ct2) == ref).all() and ct2.flat_split()[0] == 0
+
+
 def test_flat_conjunctions_ragged_and_sharded(evaluator):
     """Model counts that end inside a tile, and a shard with a nonzero index base."""
     from mythril_amd.synth import flat_workload
@@ -1230,11 +1343,13 @@ def test_c4_tapes_on_the_flat_kernel(evaluator, monkeypatch):
     evaluator.upload_models(mb)
     ct = evaluator.compile(tb)
     fh = evaluator.first_hit(ct)
+    # tapes, and the flat Bool columns of every level (ORs of compares among them)
     assert ct.flat_split()[0] >= 0.9 * tb.n_tapes, ct.flat_split()
+    assert ct.flat_split()[1] >= 6, ct.flat_split()
     ref, _ = cref.first_hit(plain[0], plain[1])
     assert (ref == exp).all() and (fh == ref).all()
     v, _ = evaluator.verdicts(ct)
     assert (v == cref.verdicts(plain[0], plain[1])).all()
     monkeypatch.setenv("MQ_NO_FLAT", "1")
     ct2 = evaluator.compile(tb)
-    assert (evaluator.first_hit(ct2) == ref).all() and ct2.flat_split()[0] == 0
+    assert (evaluator.first_hit(ct2) == ref).all() and ct2.flat_split() == (0, 0)
