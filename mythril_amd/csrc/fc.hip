@@ -208,6 +208,151 @@ __global__ __launch_bounds__(256) void fc_kernel(const FcTape* __restrict__ tape
   }
 }
 
+// Two-phase form for tapes (FcaArgs).  fc_kernel pays a tape's scalar frame, mask reduction and
+// compares once per (tape, tile): ~110 instructions.  Here a workgroup of FC_TILES tiles first
+// evaluates the launch's DISTINCT compares (C4: 647 compares in 200 tapes, 390 distinct) into LDS
+// lane masks, waves taking every fourth atom; then each wave takes chunks of 64 tapes, one tape
+// per lane, and ANDs the tape's list of LDS masks (entries k-major per chunk: one coalesced load
+// per entry) for the FC_TILES tiles: ~6 instructions per entry and tile, for 64 tapes at once.
+__global__ __launch_bounds__(256) void fca_kernel(const FcCmp* __restrict__ atoms, const uint32_t* __restrict__ lists,
+                                                  const uint32_t* __restrict__ chunk_off,
+                                                  const uint32_t* __restrict__ tape_out,
+                                                  const uint32_t* __restrict__ tape_metric,
+                                                  const uint32_t* __restrict__ vars,
+                                                  const uint64_t* __restrict__ masks_in,
+                                                  const uint32_t* __restrict__ stage_rows,
+                                                  const uint32_t* __restrict__ stage_masks, FcaArgs r) {
+  extern __shared__ uint32_t lds[];
+  const uint32_t wave = uniform(threadIdx.x >> 6);
+  const int64_t tile0 = (int64_t)blockIdx.x * FC_TILES;
+  const int64_t m0 = tile0 * 64;
+  const int lane = threadIdx.x & 63;
+  {   // the compared rows, as fc_kernel: wave w stages tile w's
+    const int j = (int)wave;
+    const int64_t mj = min(m0 + 64 * j + lane, r.M - 1);
+    for (int s0 = 0; s0 < r.n_stage; s0 += 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) v[k] = __builtin_nontemporal_load(vars + (int64_t)stage_rows[min(s0 + k, r.n_stage - 1)] * r.M + mj);
+#pragma unroll
+      for (int k = 0; k < 8; k++)
+        if (s0 + k < r.n_stage) lds[((s0 + k) * FC_TILES + j) * 64 + lane] = v[k];
+    }
+  }
+  // the mask tables, tile j's at tab + j * T: all ones, the staged Bool masks, the atoms
+  const int T = 1 + r.n_smask + r.n_atoms;
+  uint64_t* tab = reinterpret_cast<uint64_t*>(lds + r.n_stage * FC_TILES * 64);
+  const int64_t tiles = (r.M + 63) / 64;
+  for (int i = (int)threadIdx.x; i < FC_TILES * (1 + r.n_smask); i += 256) {
+    const int j = i / (1 + r.n_smask), k = i - j * (1 + r.n_smask);
+    const int64_t tj = min(tile0 + j, tiles - 1);
+    tab[j * T + k] = k == 0 ? ~0ull : masks_in[tj * (int64_t)r.n_bool_masks + stage_masks[k - 1]];
+  }
+  __syncthreads();   // (the staged rows)
+  const uint32_t* lds_lane = lds + lane;
+  for (int a = (int)wave; a < r.n_atoms; a += 4) {
+    const FcCmp* qp = atoms + a;
+    const FcCmpHead h = qp->h;
+#pragma unroll
+    for (int j = 0; j < FC_TILES; j++) {
+      const uint64_t m = fc_cmp(lds_lane, h, qp, j);
+      if (lane == 0) tab[j * T + 1 + r.n_smask + a] = m;
+    }
+  }
+  __syncthreads();
+  uint64_t valid[FC_TILES];
+#pragma unroll
+  for (int j = 0; j < FC_TILES; j++) {
+    const int64_t mj = m0 + 64 * j;
+    valid[j] = mj >= r.M ? 0ull : (r.M - mj >= 64 ? ~0ull : ((1ull << (r.M - mj)) - 1ull));
+  }
+  const int32_t first0 = (int32_t)(r.index_base + m0);
+  const int n_chunks = (r.n + 63) / 64;
+  unsigned long long run_nodes = 0, run_ops = 0, runs = 0;
+  for (int c = (int)wave; c < n_chunks; c += 4) {
+    const int t = c * 64 + lane;
+    const bool live = t < r.n;
+    const uint32_t out = live ? tape_out[t] : 0u;
+    const uint32_t row = out & 0x7FFFFFFFu;
+    bool run = live;
+    if (run && r.mode == 0 && r.early_exit) run = first0 < r.best[row];   // (best[] only decreases)
+    const uint32_t o0 = chunk_off[c], kmax = (chunk_off[c + 1] - o0) / 64u;
+    uint64_t acc[FC_TILES];
+#pragma unroll
+    for (int j = 0; j < FC_TILES; j++) acc[j] = valid[j];
+    const uint32_t* lp = lists + o0 + lane;
+    for (uint32_t k = 0; k < kmax; k++) {
+      const uint32_t e = lp[64u * k];
+      const uint32_t idx = e & 0x7FFFFFFFu;
+      const uint64_t neg = (e >> 31) ? ~0ull : 0ull;
+#pragma unroll
+      for (int j = 0; j < FC_TILES; j++) acc[j] &= tab[j * T + idx] ^ neg;
+    }
+    if (out >> 31) {
+#pragma unroll
+      for (int j = 0; j < FC_TILES; j++) acc[j] = ~acc[j] & valid[j];
+    }
+    if (run) {
+      runs++;
+      run_nodes += tape_metric[2 * t];
+      run_ops += tape_metric[2 * t + 1];
+      if (r.mode == 0) {
+#pragma unroll
+        for (int j = 0; j < FC_TILES; j++)
+          if (acc[j]) {   // the lowest tile with a hit has the lowest model
+            atomicMin(r.best + row, first0 + 64 * j + (int32_t)__builtin_ctzll(acc[j]));
+            break;
+          }
+      } else {
+        // verdict bytes: four models a dword where the row's whole tile lies below M, else bytes
+#pragma unroll
+        for (int j = 0; j < FC_TILES; j++) {
+          const int64_t mj = m0 + 64 * j;
+          if (mj >= r.M) break;
+          uint8_t* vrow = r.verdicts + (int64_t)row * r.M + mj;
+          if (r.M - mj >= 64 && ((((uintptr_t)vrow) & 3u) == 0)) {
+            for (int q = 0; q < 16; q++) {
+              const uint32_t b = (uint32_t)(acc[j] >> (4 * q)) & 0xFu;
+              reinterpret_cast<uint32_t*>(vrow)[q] = (b & 1u) | ((b & 2u) << 7) | ((b & 4u) << 14) | ((b & 8u) << 21);
+            }
+          } else {
+            const int lim = (int)min<int64_t>(64, r.M - mj);
+            for (int q = 0; q < lim; q++) vrow[q] = (uint8_t)((acc[j] >> q) & 1u);
+          }
+        }
+      }
+    }
+  }
+  // counters: this wave's evaluated tapes x the workgroup's valid models (lane sums, then lane 0)
+  if (r.counters) {
+    unsigned long long nv = 0;
+#pragma unroll
+    for (int j = 0; j < FC_TILES; j++) nv += (unsigned long long)__popcll(valid[j]);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      runs += __shfl_xor(runs, d);
+      run_nodes += __shfl_xor(run_nodes, d);
+      run_ops += __shfl_xor(run_ops, d);
+    }
+    if (lane == 0 && runs) {
+      unsigned long long* cnt = r.counters + ((blockIdx.x * 4 + wave) % kCounterSlots) * kCounterStride;
+      atomicAdd(&cnt[0], runs * nv);
+      atomicAdd(&cnt[1], run_nodes * nv);
+      atomicAdd(&cnt[2], run_ops * nv);
+    }
+  }
+}
+
+hipError_t launch_fca(const FcaArgs& a, hipStream_t st) {
+  if (a.n <= 0 || a.M <= 0) return hipSuccess;
+  const int64_t groups = (a.M + 64 * FC_TILES - 1) / (64 * FC_TILES);
+  if (groups > 0x7FFFFFFF) return hipErrorInvalidValue;
+  const size_t lds = (size_t)a.n_stage * 256u * FC_TILES + (size_t)(1 + a.n_smask + a.n_atoms) * 8u * FC_TILES;
+  hipLaunchKernelGGL(fca_kernel, dim3((unsigned)groups), dim3(256), lds, st, a.atoms, a.lists, a.chunk_off, a.tape_out,
+                     a.tape_metric, a.vars, a.bool_masks, a.stage_rows, a.stage_masks, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_fc(const FcArgs& a, hipStream_t st) {
   if (a.n <= 0 || a.M <= 0) return hipSuccess;
   const int64_t groups = (a.M + 64 * FC_TILES - 1) / (64 * FC_TILES);

@@ -305,6 +305,10 @@ struct mq_ctx {
   int64_t M_total = 0;
 };
 
+struct FcaPlanSeg {   // one fca_kernel launch (FcaPlan::Seg)
+  int atom_off, n_atoms, tape_first, n_tapes, chunk_first;
+};
+
 struct mq_tapes {
   mq_ctx* ctx = nullptr;
   int32_t n_tapes = 0;
@@ -432,6 +436,12 @@ struct mq_tapes {
   int fc_count = 0;
   int fc_stage_n = 0, fc_smask_n = 0;
   DevBuf fc_tapes_dev, fc_mask_dev, fc_cmp_dev, fc_stage_dev, fc_smask_dev, fc_prefix_dev;
+  // the two-phase form (fca_kernel; MQ_FC_ONEPHASE=1: fc_kernel): atoms in fc_cmp_dev, lists in
+  // fc_mask_dev
+  bool fca = false;
+  int fca_atoms = 0;
+  std::vector<FcaPlanSeg> fca_segs;
+  DevBuf fca_chunk_dev, fca_out_dev, fca_metric_dev;
   // the G-eligible Bool columns of a level that are flat (fc_match) run on fc_kernel, mode 3,
   // before the level's G launch (cq_prepare); the level's G descriptors are the others
   struct FcLevel {
@@ -2938,6 +2948,154 @@ static void fc_plan(const mq_ctx* c, const std::vector<std::vector<uint32_t>>& f
   }
 }
 
+// The two-phase kernel's tables for the tapes `keep` of fm / fq (fca_kernel): rows and masks
+// staged as fc_plan does, the compares deduplicated into atoms (a compare and its negation are
+// one atom: accept canonicalised to {1, 2, 3}, the negation moved into the list entry); a tape
+// reading an unstaged row or mask, or past the atom budget, is dropped (keep[i] = 0).
+struct FcaPlan {
+  std::vector<FcCmp> atoms;
+  std::vector<uint32_t> lists, chunk_off, tape_out, metric, stage_rows, stage_masks;
+  // launches: at most kFcaMaxAtoms atoms each (atom_off / n_atoms into atoms, their tapes from
+  // tape_first, their chunks from chunk_first; lists index atoms relative to the segment)
+  struct Seg {
+    int atom_off, n_atoms, tape_first, n_tapes, chunk_first;
+  };
+  std::vector<Seg> segs;
+};
+static constexpr int kFcaMaxAtoms = 1024;   // 32 KB of LDS masks for the 4 tiles of a workgroup
+static void fca_plan(const mq_ctx* c, const std::vector<std::vector<uint32_t>>& fm, const std::vector<std::vector<FcCmpH>>& fq,
+                     const std::vector<char>& negated, std::vector<char>& keep, const std::function<uint32_t(size_t)>& out_of,
+                     const std::function<std::pair<uint32_t, uint32_t>(size_t)>& nodes_ops, FcaPlan& P) {
+  const uint32_t zero_row = (uint32_t)(c->var_off_h.empty() ? 0 : c->var_off_h.back() + c->var_nl_h.back());
+  std::map<uint32_t, int64_t> row_use, mask_use;
+  std::map<uint32_t, uint32_t> row_nl;
+  for (size_t i = 0; i < keep.size(); i++) {
+    if (!keep[i]) continue;
+    for (const auto& q : fq[i]) {
+      row_use[q.row]++;
+      row_nl[q.row] = q.nl;
+    }
+    for (uint32_t e : fm[i]) mask_use[e & 0x7FFFFFFFu]++;
+  }
+  auto by_use = [](const std::map<uint32_t, int64_t>& u) {
+    std::vector<std::pair<int64_t, uint32_t>> o;
+    for (const auto& kv : u) o.push_back({kv.second, kv.first});
+    std::stable_sort(o.begin(), o.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+    return o;
+  };
+  std::map<uint32_t, uint32_t> slot_of, mslot_of;
+  for (const auto& o : by_use(row_use)) {
+    const uint32_t nl = row_nl[o.second], width = nl <= 2 ? 2 : 8;
+    if (P.stage_rows.size() + width > (size_t)kFcStageRows) continue;
+    slot_of[o.second] = (uint32_t)P.stage_rows.size();
+    for (uint32_t l = 0; l < width; l++) P.stage_rows.push_back(l < nl ? o.second + l : zero_row);
+  }
+  for (const auto& o : by_use(mask_use)) {
+    if (P.stage_masks.size() >= (size_t)kFcStageMasks) break;
+    mslot_of[o.second] = (uint32_t)P.stage_masks.size();
+    P.stage_masks.push_back(o.second);
+  }
+  const uint32_t abase = 1u + (uint32_t)P.stage_masks.size();
+  std::map<std::vector<uint32_t>, uint32_t> atom_of;   // (this segment's atoms)
+  std::vector<std::vector<uint32_t>> tl;   // kept tapes' entries
+  std::vector<size_t> seg_start{0};        // segment boundaries in tl
+  for (size_t i = 0; i < keep.size(); i++) {
+    if (!keep[i]) continue;
+    if (!atom_of.empty() && atom_of.size() + fq[i].size() > (size_t)kFcaMaxAtoms) {
+      atom_of.clear();   // a new launch with its own atom table
+      seg_start.push_back(tl.size());
+    }
+    bool ok = true;
+    for (const auto& q : fq[i]) ok = ok && slot_of.count(q.row);
+    for (uint32_t e : fm[i]) ok = ok && mslot_of.count(e & 0x7FFFFFFFu);
+    std::vector<uint32_t> ent;
+    for (uint32_t e : fm[i]) ent.push_back(ok ? (1u + mslot_of[e & 0x7FFFFFFFu]) | (e & 0x80000000u) : 0u);
+    std::vector<std::vector<uint32_t>> fresh;
+    for (const auto& h : fq[i]) {
+      if (!ok) break;
+      const bool ng = h.accept >= 4;
+      std::vector<uint32_t> key{h.row, h.nl, ng ? (h.accept ^ 7u) : h.accept};
+      for (uint32_t l = 0; l < h.nl; l++) {
+        key.push_back(h.c[l]);
+        key.push_back(h.f[l]);
+      }
+      auto it = atom_of.find(key);
+      uint32_t a;
+      if (it != atom_of.end()) {
+        a = it->second;
+      } else {
+        a = (uint32_t)(atom_of.size() + fresh.size());
+        bool dup = false;
+        for (size_t f = 0; f < fresh.size(); f++)
+          if (fresh[f] == key) {
+            a = (uint32_t)(atom_of.size() + f);
+            dup = true;
+          }
+        if (!dup) fresh.push_back(key);
+      }
+      ent.push_back((abase + a) | (ng ? 0x80000000u : 0u));
+    }
+    if (!ok || fresh.size() > (size_t)kFcaMaxAtoms) {
+      keep[i] = 0;
+      continue;
+    }
+    for (const auto& key : fresh) {
+      FcCmp q{};
+      q.h.slot = slot_of[key[0]];
+      q.h.nl = key[1];
+      q.h.accept = key[2];
+      uint32_t cc[8] = {0}, ff[8] = {0};
+      for (uint32_t l = 0; l < key[1]; l++) {
+        cc[l] = key[3 + 2 * l];
+        ff[l] = key[4 + 2 * l];
+      }
+      q.h.c01 = (uint64_t)cc[0] | ((uint64_t)cc[1] << 32);
+      q.h.f01 = (uint64_t)ff[0] | ((uint64_t)ff[1] << 32);
+      for (int l = 0; l < 6; l++) {
+        q.t.c[l] = cc[2 + l];
+        q.t.f[l] = ff[2 + l];
+      }
+      atom_of[key] = (uint32_t)atom_of.size();
+      P.atoms.push_back(q);
+    }
+    tl.push_back(std::move(ent));
+    P.tape_out.push_back(out_of(i) | (negated[i] ? 0x80000000u : 0u));
+    const auto no = nodes_ops(i);
+    P.metric.push_back(no.first);
+    P.metric.push_back(no.second);
+  }
+  // per segment: chunks of 64 tapes, entries k-major; short lists padded with entry 0 (all ones)
+  seg_start.push_back(tl.size());
+  P.chunk_off.assign(1, 0);
+  int atom_off = 0;
+  for (size_t s = 0; s + 1 < seg_start.size(); s++) {
+    const size_t b = seg_start[s], e = seg_start[s + 1];
+    if (b == e) continue;
+    FcaPlan::Seg sg{};
+    sg.tape_first = (int)b;
+    sg.n_tapes = (int)(e - b);
+    sg.chunk_first = (int)P.chunk_off.size() - 1;
+    int na = 0;
+    for (size_t t = b; t < e; t++)
+      for (uint32_t x : tl[t])
+        if ((x & 0x7FFFFFFFu) >= abase) na = std::max(na, (int)((x & 0x7FFFFFFFu) - abase) + 1);
+    sg.atom_off = atom_off;
+    sg.n_atoms = na;
+    atom_off += na;
+    for (size_t c0 = b; c0 < e; c0 += 64) {
+      size_t kmax = 0;
+      for (size_t t = c0; t < std::min(e, c0 + 64); t++) kmax = std::max(kmax, tl[t].size());
+      for (size_t k = 0; k < kmax; k++)
+        for (size_t l = 0; l < 64; l++) {
+          const size_t t = c0 + l;
+          P.lists.push_back(t < e && k < tl[t].size() ? tl[t][k] : 0u);
+        }
+      P.chunk_off.push_back((uint32_t)P.lists.size());
+    }
+    P.segs.push_back(sg);
+  }
+}
+
 static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
   if (T->qsa_gen == c->layout_gen) return MQ_OK;
   T->qsa_gen = c->layout_gen;
@@ -2965,8 +3123,14 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
       }
     });
   FcPlan fcp;
-  fc_plan(c, fc_m, fc_q, fc_neg, on_fc, [&](size_t i) { return T->qbase[i].tape; }, [](size_t) { return (int32_t)-1; },
-          [&](size_t i) { return std::make_pair(T->qbase[i].n_nodes, T->qbase[i].alg_ops); }, fcp);
+  FcaPlan fap;
+  T->fca = std::getenv("MQ_FC_ONEPHASE") == nullptr;
+  if (T->fca)
+    fca_plan(c, fc_m, fc_q, fc_neg, on_fc, [&](size_t i) { return T->qbase[i].tape; },
+             [&](size_t i) { return std::make_pair(T->qbase[i].n_nodes, T->qbase[i].alg_ops); }, fap);
+  else
+    fc_plan(c, fc_m, fc_q, fc_neg, on_fc, [&](size_t i) { return T->qbase[i].tape; }, [](size_t) { return (int32_t)-1; },
+            [&](size_t i) { return std::make_pair(T->qbase[i].n_nodes, T->qbase[i].alg_ops); }, fcp);
   // (P preloads variables 0-7 only: a program pushing any other variable is not tried on P)
   auto p_candidate = [](const CompiledTape& x) {
     for (size_t pc = 0; pc < x.prog.size(); pc++) {
@@ -3088,10 +3252,32 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
   if (descs.empty()) descs.push_back(GDesc{});
   HIPCHK(T->qdescs.upload(descs.data(), descs.size(), c->stream));
   HIPCHK(T->qprog.upload(prog.data(), prog.size(), c->stream));
-  T->fc_count = (int)fcp.tapes.size();
-  T->fc_stage_n = (int)fcp.stage_rows.size();
-  T->fc_smask_n = (int)fcp.stage_masks.size();
-  if (!fcp.tapes.empty()) {
+  if (T->fca) {
+    T->fc_count = (int)fap.tape_out.size();
+    T->fc_stage_n = (int)fap.stage_rows.size();
+    T->fc_smask_n = (int)fap.stage_masks.size();
+    T->fca_atoms = (int)fap.atoms.size();
+    T->fca_segs.clear();
+    for (const auto& sg : fap.segs) T->fca_segs.push_back({sg.atom_off, sg.n_atoms, sg.tape_first, sg.n_tapes, sg.chunk_first});
+    if (T->fc_count > 0) {
+      if (fap.stage_rows.empty()) fap.stage_rows.push_back(0);
+      if (fap.stage_masks.empty()) fap.stage_masks.push_back(0);
+      if (fap.atoms.empty()) fap.atoms.push_back(FcCmp{});
+      if (fap.lists.empty()) fap.lists.push_back(0);
+      HIPCHK(T->fc_cmp_dev.upload(fap.atoms.data(), fap.atoms.size(), c->stream));
+      HIPCHK(T->fc_mask_dev.upload(fap.lists.data(), fap.lists.size(), c->stream));
+      HIPCHK(T->fca_chunk_dev.upload(fap.chunk_off.data(), fap.chunk_off.size(), c->stream));
+      HIPCHK(T->fca_out_dev.upload(fap.tape_out.data(), fap.tape_out.size(), c->stream));
+      HIPCHK(T->fca_metric_dev.upload(fap.metric.data(), fap.metric.size(), c->stream));
+      HIPCHK(T->fc_stage_dev.upload(fap.stage_rows.data(), fap.stage_rows.size(), c->stream));
+      HIPCHK(T->fc_smask_dev.upload(fap.stage_masks.data(), fap.stage_masks.size(), c->stream));
+    }
+  } else {
+    T->fc_count = (int)fcp.tapes.size();
+    T->fc_stage_n = (int)fcp.stage_rows.size();
+    T->fc_smask_n = (int)fcp.stage_masks.size();
+  }
+  if (!T->fca && !fcp.tapes.empty()) {
     if (fcp.stage_rows.empty()) fcp.stage_rows.push_back(0);
     if (fcp.stage_masks.empty()) fcp.stage_masks.push_back(0);
     if (fcp.mask_lds.empty()) fcp.mask_lds.push_back(0);
@@ -3729,7 +3915,34 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     HIPCHK(start_timer());
     HIPCHK(launch_qsa(k, T->qargs[k].as<QArgs>(), gx, gy, lds, st));
   }
-  if (use_qsa && T->fc_count > 0) {
+  for (size_t sgi = 0; use_qsa && T->fc_count > 0 && T->fca && sgi < T->fca_segs.size(); sgi++) {
+    const FcaPlanSeg& sg = T->fca_segs[sgi];
+    FcaArgs f{};
+    f.n = sg.n_tapes;
+    f.n_atoms = sg.n_atoms;
+    f.atoms = T->fc_cmp_dev.as<FcCmp>() + sg.atom_off;
+    f.lists = T->fc_mask_dev.as<uint32_t>();
+    f.chunk_off = T->fca_chunk_dev.as<uint32_t>() + sg.chunk_first;
+    f.tape_out = T->fca_out_dev.as<uint32_t>() + sg.tape_first;
+    f.tape_metric = T->fca_metric_dev.as<uint32_t>() + 2 * (size_t)sg.tape_first;
+    f.vars = c->vars.as<uint32_t>();
+    f.bool_masks = c->bmasks.as<uint64_t>();
+    f.n_bool_masks = c->n_bmask;
+    f.mode = verdicts ? 1 : 0;
+    f.early_exit = verdicts ? 0 : c->early_exit;
+    f.M = c->M;
+    f.index_base = c->index_base;
+    f.best = best;
+    f.verdicts = verdicts;
+    f.counters = c->counters.as<unsigned long long>();
+    f.stage_rows = T->fc_stage_dev.as<uint32_t>();
+    f.n_stage = T->fc_stage_n;
+    f.stage_masks = T->fc_smask_dev.as<uint32_t>();
+    f.n_smask = T->fc_smask_n;
+    HIPCHK(start_timer());
+    HIPCHK(launch_fca(f, st));
+  }
+  if (use_qsa && T->fc_count > 0 && !T->fca) {
     FcArgs f{};
     f.tapes = T->fc_tapes_dev.as<FcTape>();
     f.n = T->fc_count;

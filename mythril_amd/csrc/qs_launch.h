@@ -250,5 +250,35 @@ struct FcRun {
 };
 hipError_t launch_fc(const FcArgs& a, hipStream_t st);
 
+// Two-phase flat conjunctions (fc.hip fca_kernel, mq_api.cpp fca_plan), for tapes: the launch's
+// distinct compares ("atoms") are evaluated once per 64-model tile into lane masks in LDS (model
+// lanes), then every tape ANDs its atoms' and Bool variables' masks with one lane per tape.  A
+// workgroup's LDS table per tile: entry 0 all ones, 1 .. n_smask the staged Bool masks, then the
+// atoms; a list entry is a table index | negated << 31.
+struct FcaArgs {
+  int n;                          // tapes
+  int n_atoms;
+  const FcCmp* atoms;             // accept in {1, 2, 3} (x < c, x == c, x <= c); negations in the lists
+  const uint32_t* lists;          // chunk c of 64 tapes: kmax(c) entries x 64 lanes, k-major, from chunk_off[c]
+  const uint32_t* chunk_off;      // [n_chunks + 1]: kmax(c) = (chunk_off[c + 1] - chunk_off[c]) / 64
+  const uint32_t* tape_out;       // per tape: its best / verdict row | negated result << 31
+  const uint32_t* tape_metric;    // per tape: n_nodes, alg_ops
+  const uint32_t* vars;
+  const uint64_t* bool_masks;
+  int n_bool_masks;
+  int mode;                       // 0 first hit, 1 verdict bytes
+  int early_exit;
+  int64_t M;
+  int64_t index_base;
+  int32_t* best;
+  uint8_t* verdicts;
+  unsigned long long* counters;
+  const uint32_t* stage_rows;
+  int n_stage;
+  const uint32_t* stage_masks;
+  int n_smask;
+};
+hipError_t launch_fca(const FcaArgs& a, hipStream_t st);
+
 }  // namespace mq
 #endif

@@ -1298,6 +1298,25 @@ def test_flat_conjunctions_match_oracle(evaluator, monkeypatch, bmask_cap):
     ct2.free()
 
 
+@pytest.mark.parametrize("variant", ["two_phase_segments", "one_phase"])
+def test_flat_kernel_forms_match_oracle(evaluator, monkeypatch, variant):
+    """The two-phase flat kernel (fca_kernel: distinct compares into LDS masks, then one lane per
+    tape) over more distinct compares than one launch's atom budget (several launches), and the
+    one-phase fc_kernel (MQ_FC_ONEPHASE=1): first hits and verdicts against the oracle."""
+    from mythril_amd.synth import flat_workload
+    if variant == "one_phase":
+        monkeypatch.setenv("MQ_FC_ONEPHASE", "1")
+    tb, mb = flat_workload(31, 900, 700, max_items=14, or_frac=0.3)
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    fh = evaluator.first_hit(ct)
+    assert ct.flat_split()[0] >= 0.9 * tb.n_tapes, ct.flat_split()
+    ref, _ = cref.first_hit(tb, mb)
+    assert (fh == ref).all(), np.flatnonzero(fh != ref)[:10]
+    v, _ = evaluator.verdicts(ct)
+    assert (v == cref.verdicts(tb, mb)).all()
+
+
 def test_flat_disjunctions_match_oracle(evaluator, monkeypatch):
     """ORs of atoms, NOT of an AND, and OR(NOT(AND), atoms...) run on the flat kernel as negated
     conjunctions (De Morgan); an OR over a multi-atom AND is not flat and stays on the
