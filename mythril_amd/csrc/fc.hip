@@ -209,25 +209,48 @@ __global__ __launch_bounds__(256) void fc_kernel(const FcTape* __restrict__ tape
 }
 
 // Two-phase form for tapes (FcaArgs).  fc_kernel pays a tape's scalar frame, mask reduction and
-// compares once per (tape, tile): ~110 instructions.  Here a workgroup of FC_TILES tiles first
-// evaluates the launch's DISTINCT compares (C4: 647 compares in 200 tapes, 390 distinct) into LDS
-// lane masks, waves taking every fourth atom; then each wave takes chunks of 64 tapes, one tape
-// per lane, and ANDs the tape's list of LDS masks (entries k-major per chunk: one coalesced load
-// per entry) for the FC_TILES tiles: ~6 instructions per entry and tile, for 64 tapes at once.
-__global__ __launch_bounds__(256) void fca_kernel(const FcCmp* __restrict__ atoms, const uint32_t* __restrict__ lists,
+// compares once per (tape, tile): ~110 instructions, and it can only compare variables staged in
+// LDS.  Here a workgroup of FC_TILES tiles first evaluates the launch's DISTINCT compares (C4: 647
+// compares in 200 tapes, 390 distinct; C3: 8 835 in 1 000, 6 626) into LDS lane masks: the atoms
+// are grouped by variable, a wave loads a group's variable limbs for its FC_TILES tiles into
+// registers once (any variable: nothing is staged) and compares them with each atom's constant.
+// Then each wave takes chunks of 64 tapes, one tape per lane, and ANDs the tape's list of LDS masks
+// (entries k-major per chunk: one coalesced load per entry) for the FC_TILES tiles.
+
+// x OP c over limbs in registers (x: the variable's limbs; q.f flips the sign bit of a signed
+// compare, c is pre-flipped): lane mask of (accept & (x < c ? 1 : x == c ? 2 : 4))
+__device__ __forceinline__ uint64_t fca_cmp(const uint32_t* x, const FcCmpHead& h, const FcCmp* __restrict__ qp) {
+  const uint64_t x0 = ((uint64_t)(x[1] ^ (uint32_t)(h.f01 >> 32)) << 32) | (x[0] ^ (uint32_t)h.f01);
+  bool lt = x0 < h.c01, eq = x0 == h.c01;
+  if (h.nl > 2) {
+    const FcCmpTail t = qp->t;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const uint64_t xv = ((uint64_t)(x[2 * k + 3] ^ t.f[2 * k + 1]) << 32) | (x[2 * k + 2] ^ t.f[2 * k]);
+      const uint64_t c = ((uint64_t)t.c[2 * k + 1] << 32) | t.c[2 * k];
+      lt = xv < c || (xv == c && lt);
+      eq = xv == c && eq;
+    }
+  }
+  const uint32_t bit = lt ? 1u : (eq ? 2u : 4u);
+  return __ballot((h.accept & bit) != 0);
+}
+
+__global__ __launch_bounds__(256) void fca_kernel(const FcaGroup* __restrict__ groups, const FcCmp* __restrict__ atoms,
+                                                  const uint32_t* __restrict__ lists,
                                                   const uint32_t* __restrict__ chunk_off,
                                                   const uint32_t* __restrict__ tape_out,
                                                   const uint32_t* __restrict__ tape_metric,
                                                   const uint32_t* __restrict__ vars,
                                                   const uint64_t* __restrict__ masks_in,
-                                                  const uint32_t* __restrict__ stage_rows,
-                                                  const uint32_t* __restrict__ stage_masks, FcaArgs r) {
+                                                  const uint32_t* __restrict__ stage_masks,
+                                                  const uint32_t* __restrict__ stage_rows, FcaArgs r) {
   extern __shared__ uint32_t lds[];
   const uint32_t wave = uniform(threadIdx.x >> 6);
   const int64_t tile0 = (int64_t)blockIdx.x * FC_TILES;
   const int64_t m0 = tile0 * 64;
   const int lane = threadIdx.x & 63;
-  {   // the compared rows, as fc_kernel: wave w stages tile w's
+  {   // the staged rows (LDS row s * FC_TILES + j = slot s of tile j), as fc_kernel: wave w stages tile w's
     const int j = (int)wave;
     const int64_t mj = min(m0 + 64 * j + lane, r.M - 1);
     for (int s0 = 0; s0 < r.n_stage; s0 += 8) {
@@ -239,32 +262,64 @@ __global__ __launch_bounds__(256) void fca_kernel(const FcCmp* __restrict__ atom
         if (s0 + k < r.n_stage) lds[((s0 + k) * FC_TILES + j) * 64 + lane] = v[k];
     }
   }
-  // the mask tables, tile j's at tab + j * T: all ones, the staged Bool masks, the atoms
-  const int T = 1 + r.n_smask + r.n_atoms;
+  // the mask tables, tile j's at tab + j * T: all ones, the Bool masks, the atoms
   uint64_t* tab = reinterpret_cast<uint64_t*>(lds + r.n_stage * FC_TILES * 64);
+  const int T = 1 + r.n_smask + r.n_atoms;
   const int64_t tiles = (r.M + 63) / 64;
   for (int i = (int)threadIdx.x; i < FC_TILES * (1 + r.n_smask); i += 256) {
     const int j = i / (1 + r.n_smask), k = i - j * (1 + r.n_smask);
     const int64_t tj = min(tile0 + j, tiles - 1);
     tab[j * T + k] = k == 0 ? ~0ull : masks_in[tj * (int64_t)r.n_bool_masks + stage_masks[k - 1]];
   }
-  __syncthreads();   // (the staged rows)
-  const uint32_t* lds_lane = lds + lane;
-  for (int a = (int)wave; a < r.n_atoms; a += 4) {
-    const FcCmp* qp = atoms + a;
-    const FcCmpHead h = qp->h;
+  // phase 1: the atoms, a variable group at a time (wave w: groups w, w + 4, ...)
+  int64_t mj[FC_TILES];
 #pragma unroll
-    for (int j = 0; j < FC_TILES; j++) {
-      const uint64_t m = fc_cmp(lds_lane, h, qp, j);
-      if (lane == 0) tab[j * T + 1 + r.n_smask + a] = m;
+  for (int j = 0; j < FC_TILES; j++) mj[j] = min(m0 + 64 * j + lane, r.M - 1);
+  __syncthreads();   // (the staged rows)
+  for (int g = (int)wave; g < r.n_groups; g += 4) {
+    const FcaGroup G = groups[g];
+    uint32_t x[FC_TILES][8];
+    if (G.slot != ~0u) {   // staged: limb l of tile j at LDS row (slot + l) * FC_TILES + j
+      const int nread = G.nl <= 2 ? 2 : 8;
+#pragma unroll
+      for (int j = 0; j < FC_TILES; j++)
+#pragma unroll
+        for (int l = 0; l < 8; l++) x[j][l] = l < nread ? lds[((G.slot + l) * FC_TILES + j) * 64 + lane] : 0u;
+    } else if (G.nl <= 2) {
+#pragma unroll
+      for (int j = 0; j < FC_TILES; j++) {
+        x[j][0] = vars[(int64_t)G.rows[0] * r.M + mj[j]];
+        x[j][1] = vars[(int64_t)G.rows[1] * r.M + mj[j]];
+#pragma unroll
+        for (int l = 2; l < 8; l++) x[j][l] = 0;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < FC_TILES; j++)
+#pragma unroll
+        for (int l = 0; l < 8; l++) x[j][l] = vars[(int64_t)G.rows[l] * r.M + mj[j]];
+    }
+    // (the next atom's head is requested before this one is compared: one scalar round trip
+    // per group, not per atom)
+    FcCmpHead h = atoms[G.first].h;
+    for (uint32_t a = G.first; a < G.first + G.count; a++) {
+      const FcCmp* qp = atoms + a;
+      const FcCmpHead hn = atoms[min(a + 1, G.first + G.count - 1)].h;
+#pragma unroll
+      for (int j = 0; j < FC_TILES; j++) {
+        const uint64_t m = fca_cmp(x[j], h, qp);
+        if (lane == 0) tab[j * T + 1 + r.n_smask + a] = m;
+      }
+      h = hn;
     }
   }
   __syncthreads();
+  // phase 2: the tapes, one per lane
   uint64_t valid[FC_TILES];
 #pragma unroll
   for (int j = 0; j < FC_TILES; j++) {
-    const int64_t mj = m0 + 64 * j;
-    valid[j] = mj >= r.M ? 0ull : (r.M - mj >= 64 ? ~0ull : ((1ull << (r.M - mj)) - 1ull));
+    const int64_t mt = m0 + 64 * j;
+    valid[j] = mt >= r.M ? 0ull : (r.M - mt >= 64 ? ~0ull : ((1ull << (r.M - mt)) - 1ull));
   }
   const int32_t first0 = (int32_t)(r.index_base + m0);
   const int n_chunks = (r.n + 63) / 64;
@@ -288,7 +343,7 @@ __global__ __launch_bounds__(256) void fca_kernel(const FcCmp* __restrict__ atom
 #pragma unroll
       for (int j = 0; j < FC_TILES; j++) acc[j] &= tab[j * T + idx] ^ neg;
     }
-    if (out >> 31) {
+    if (out >> 31) {   // a negated conjunction (an OR of atoms)
 #pragma unroll
       for (int j = 0; j < FC_TILES; j++) acc[j] = ~acc[j] & valid[j];
     }
@@ -307,16 +362,16 @@ __global__ __launch_bounds__(256) void fca_kernel(const FcCmp* __restrict__ atom
         // verdict bytes: four models a dword where the row's whole tile lies below M, else bytes
 #pragma unroll
         for (int j = 0; j < FC_TILES; j++) {
-          const int64_t mj = m0 + 64 * j;
-          if (mj >= r.M) break;
-          uint8_t* vrow = r.verdicts + (int64_t)row * r.M + mj;
-          if (r.M - mj >= 64 && ((((uintptr_t)vrow) & 3u) == 0)) {
+          const int64_t mt = m0 + 64 * j;
+          if (mt >= r.M) break;
+          uint8_t* vrow = r.verdicts + (int64_t)row * r.M + mt;
+          if (r.M - mt >= 64 && ((((uintptr_t)vrow) & 3u) == 0)) {
             for (int q = 0; q < 16; q++) {
               const uint32_t b = (uint32_t)(acc[j] >> (4 * q)) & 0xFu;
               reinterpret_cast<uint32_t*>(vrow)[q] = (b & 1u) | ((b & 2u) << 7) | ((b & 4u) << 14) | ((b & 8u) << 21);
             }
           } else {
-            const int lim = (int)min<int64_t>(64, r.M - mj);
+            const int lim = (int)min<int64_t>(64, r.M - mt);
             for (int q = 0; q < lim; q++) vrow[q] = (uint8_t)((acc[j] >> q) & 1u);
           }
         }
@@ -348,8 +403,8 @@ hipError_t launch_fca(const FcaArgs& a, hipStream_t st) {
   const int64_t groups = (a.M + 64 * FC_TILES - 1) / (64 * FC_TILES);
   if (groups > 0x7FFFFFFF) return hipErrorInvalidValue;
   const size_t lds = (size_t)a.n_stage * 256u * FC_TILES + (size_t)(1 + a.n_smask + a.n_atoms) * 8u * FC_TILES;
-  hipLaunchKernelGGL(fca_kernel, dim3((unsigned)groups), dim3(256), lds, st, a.atoms, a.lists, a.chunk_off, a.tape_out,
-                     a.tape_metric, a.vars, a.bool_masks, a.stage_rows, a.stage_masks, a);
+  hipLaunchKernelGGL(fca_kernel, dim3((unsigned)groups), dim3(256), lds, st, a.groups, a.atoms, a.lists, a.chunk_off,
+                     a.tape_out, a.tape_metric, a.vars, a.bool_masks, a.stage_masks, a.stage_rows, a);
   return hipGetLastError();
 }
 

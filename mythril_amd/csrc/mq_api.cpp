@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <set>
 #include <unordered_set>
 #include <memory>
 #include <string>
@@ -305,8 +306,8 @@ struct mq_ctx {
   int64_t M_total = 0;
 };
 
-struct FcaPlanSeg {   // one fca_kernel launch (FcaPlan::Seg)
-  int atom_off, n_atoms, tape_first, n_tapes, chunk_first;
+struct FcaPlanSeg {   // one fca_kernel launch (fca_plan)
+  int atom_off, n_atoms, group_off, n_groups, tape_first, n_tapes, chunk_first, smask_off, n_smask, stage_off, n_stage;
 };
 
 struct mq_tapes {
@@ -441,7 +442,7 @@ struct mq_tapes {
   bool fca = false;
   int fca_atoms = 0;
   std::vector<FcaPlanSeg> fca_segs;
-  DevBuf fca_chunk_dev, fca_out_dev, fca_metric_dev;
+  DevBuf fca_chunk_dev, fca_out_dev, fca_metric_dev, fca_group_dev;
   // the G-eligible Bool columns of a level that are flat (fc_match) run on fc_kernel, mode 3,
   // before the level's G launch (cq_prepare); the level's G descriptors are the others
   struct FcLevel {
@@ -2948,100 +2949,107 @@ static void fc_plan(const mq_ctx* c, const std::vector<std::vector<uint32_t>>& f
   }
 }
 
-// The two-phase kernel's tables for the tapes `keep` of fm / fq (fca_kernel): rows and masks
-// staged as fc_plan does, the compares deduplicated into atoms (a compare and its negation are
-// one atom: accept canonicalised to {1, 2, 3}, the negation moved into the list entry); a tape
-// reading an unstaged row or mask, or past the atom budget, is dropped (keep[i] = 0).
+// The two-phase kernel's tables for the tapes `keep` of fm / fq (fca_kernel).  Tapes are taken
+// in order into launches ("segments") of at most kFcaMaxAtoms distinct compares ("atoms": a
+// compare and its negation are one atom, accept canonicalised to {1, 2, 3} and the negation moved
+// into the list entry) and kFcStageMasks distinct Bool masks; a segment's atoms are ordered by
+// the variable they read (one group per variable: its limbs are loaded once per tile).
 struct FcaPlan {
   std::vector<FcCmp> atoms;
-  std::vector<uint32_t> lists, chunk_off, tape_out, metric, stage_rows, stage_masks;
-  // launches: at most kFcaMaxAtoms atoms each (atom_off / n_atoms into atoms, their tapes from
-  // tape_first, their chunks from chunk_first; lists index atoms relative to the segment)
-  struct Seg {
-    int atom_off, n_atoms, tape_first, n_tapes, chunk_first;
-  };
-  std::vector<Seg> segs;
+  std::vector<FcaGroup> groups;
+  std::vector<uint32_t> lists, chunk_off, tape_out, metric, stage_masks, stage_rows;
+  std::vector<FcaPlanSeg> segs;
 };
 static constexpr int kFcaMaxAtoms = 1024;   // 32 KB of LDS masks for the 4 tiles of a workgroup
+static constexpr int kFcaGroupAtoms = 16;   // (C4 fca: 4 -> 213 us, 8 -> 196, 16 -> 186, 32 -> 199)
 static void fca_plan(const mq_ctx* c, const std::vector<std::vector<uint32_t>>& fm, const std::vector<std::vector<FcCmpH>>& fq,
                      const std::vector<char>& negated, std::vector<char>& keep, const std::function<uint32_t(size_t)>& out_of,
                      const std::function<std::pair<uint32_t, uint32_t>(size_t)>& nodes_ops, FcaPlan& P) {
   const uint32_t zero_row = (uint32_t)(c->var_off_h.empty() ? 0 : c->var_off_h.back() + c->var_nl_h.back());
-  std::map<uint32_t, int64_t> row_use, mask_use;
-  std::map<uint32_t, uint32_t> row_nl;
-  for (size_t i = 0; i < keep.size(); i++) {
-    if (!keep[i]) continue;
-    for (const auto& q : fq[i]) {
-      row_use[q.row]++;
-      row_nl[q.row] = q.nl;
+  auto atom_key = [](const FcCmpH& h, bool* ng) {
+    *ng = h.accept >= 4;
+    std::vector<uint32_t> key{h.row, h.nl, *ng ? (h.accept ^ 7u) : h.accept};
+    for (uint32_t l = 0; l < h.nl; l++) {
+      key.push_back(h.c[l]);
+      key.push_back(h.f[l]);
     }
-    for (uint32_t e : fm[i]) mask_use[e & 0x7FFFFFFFu]++;
-  }
-  auto by_use = [](const std::map<uint32_t, int64_t>& u) {
-    std::vector<std::pair<int64_t, uint32_t>> o;
-    for (const auto& kv : u) o.push_back({kv.second, kv.first});
-    std::stable_sort(o.begin(), o.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
-    return o;
+    return key;
   };
-  std::map<uint32_t, uint32_t> slot_of, mslot_of;
-  for (const auto& o : by_use(row_use)) {
-    const uint32_t nl = row_nl[o.second], width = nl <= 2 ? 2 : 8;
-    if (P.stage_rows.size() + width > (size_t)kFcStageRows) continue;
-    slot_of[o.second] = (uint32_t)P.stage_rows.size();
-    for (uint32_t l = 0; l < width; l++) P.stage_rows.push_back(l < nl ? o.second + l : zero_row);
-  }
-  for (const auto& o : by_use(mask_use)) {
-    if (P.stage_masks.size() >= (size_t)kFcStageMasks) break;
-    mslot_of[o.second] = (uint32_t)P.stage_masks.size();
-    P.stage_masks.push_back(o.second);
-  }
-  const uint32_t abase = 1u + (uint32_t)P.stage_masks.size();
-  std::map<std::vector<uint32_t>, uint32_t> atom_of;   // (this segment's atoms)
-  std::vector<std::vector<uint32_t>> tl;   // kept tapes' entries
-  std::vector<size_t> seg_start{0};        // segment boundaries in tl
-  for (size_t i = 0; i < keep.size(); i++) {
-    if (!keep[i]) continue;
-    if (!atom_of.empty() && atom_of.size() + fq[i].size() > (size_t)kFcaMaxAtoms) {
-      atom_of.clear();   // a new launch with its own atom table
-      seg_start.push_back(tl.size());
+  // the segment being built: its atoms / masks in arrival order, and its tapes' symbolic entries
+  // (kind 0 mask slot, 1 atom; local id; negated)
+  struct Ent {
+    uint32_t kind, id, neg;
+  };
+  std::map<std::vector<uint32_t>, uint32_t> atom_of;
+  std::vector<std::vector<uint32_t>> akeys;
+  std::map<uint32_t, uint32_t> mask_of;
+  std::vector<uint32_t> masks;
+  std::vector<std::vector<Ent>> tl;
+  std::vector<size_t> tsrc;
+  P.chunk_off.assign(1, 0);
+  auto close = [&]() {
+    if (tl.empty()) return;
+    FcaPlanSeg sg{};
+    sg.atom_off = (int)P.atoms.size();
+    sg.n_atoms = (int)akeys.size();
+    sg.group_off = (int)P.groups.size();
+    sg.tape_first = (int)P.tape_out.size();
+    sg.n_tapes = (int)tl.size();
+    sg.chunk_first = (int)P.chunk_off.size() - 1;
+    sg.smask_off = (int)P.stage_masks.size();
+    sg.n_smask = (int)masks.size();
+    // the variables the most atoms read are staged in LDS (kFcStageRows rows: 2 for a variable
+    // of <= 2 limbs, else 8; the zero row past its limbs); the others are read from the rows
+    std::map<std::pair<uint32_t, uint32_t>, int64_t> use;
+    for (const auto& key : akeys) use[{key[0], key[1]}]++;
+    std::vector<std::pair<int64_t, std::pair<uint32_t, uint32_t>>> byu;
+    for (const auto& kv : use) byu.push_back({kv.second, kv.first});
+    std::stable_sort(byu.begin(), byu.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
+    std::map<std::pair<uint32_t, uint32_t>, uint32_t> slot_of;
+    sg.stage_off = (int)P.stage_rows.size();
+    uint32_t nst = 0;
+    static const uint32_t stage_budget = [] {
+      const char* e = std::getenv("MQ_FCA_STAGE_ROWS");
+      return e ? (uint32_t)std::atoi(e) : 0u;   // (none: C4 fca 252 us with 40 rows, 196 without -- occupancy)
+    }();
+    for (const auto& u : byu) {
+      const uint32_t nl = u.second.second, width = nl <= 2 ? 2 : 8;
+      if (nst + width > stage_budget) continue;
+      slot_of[u.second] = nst;
+      for (uint32_t l = 0; l < width; l++) P.stage_rows.push_back(l < nl ? u.second.first + l : zero_row);
+      nst += width;
     }
-    bool ok = true;
-    for (const auto& q : fq[i]) ok = ok && slot_of.count(q.row);
-    for (uint32_t e : fm[i]) ok = ok && mslot_of.count(e & 0x7FFFFFFFu);
-    std::vector<uint32_t> ent;
-    for (uint32_t e : fm[i]) ent.push_back(ok ? (1u + mslot_of[e & 0x7FFFFFFFu]) | (e & 0x80000000u) : 0u);
-    std::vector<std::vector<uint32_t>> fresh;
-    for (const auto& h : fq[i]) {
-      if (!ok) break;
-      const bool ng = h.accept >= 4;
-      std::vector<uint32_t> key{h.row, h.nl, ng ? (h.accept ^ 7u) : h.accept};
-      for (uint32_t l = 0; l < h.nl; l++) {
-        key.push_back(h.c[l]);
-        key.push_back(h.f[l]);
+    sg.n_stage = (int)nst;
+    // atoms ordered by (variable row, limbs): groups
+    std::vector<uint32_t> ord(akeys.size());
+    for (size_t i = 0; i < ord.size(); i++) ord[i] = (uint32_t)i;
+    std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
+      return akeys[x][0] != akeys[y][0] ? akeys[x][0] < akeys[y][0] : akeys[x][1] < akeys[y][1];
+    });
+    static const uint32_t group_atoms = [] {
+      const char* e = std::getenv("MQ_FCA_GROUP_ATOMS");
+      return e ? (uint32_t)std::max(1, std::atoi(e)) : (uint32_t)kFcaGroupAtoms;
+    }();
+    std::vector<uint32_t> pos(akeys.size());
+    for (size_t r = 0; r < ord.size(); r++) {
+      const std::vector<uint32_t>& key = akeys[ord[r]];
+      pos[ord[r]] = (uint32_t)r;
+      // (a group holds at most kFcaGroupAtoms atoms: the 4 waves take every fourth group, so one
+      // variable's many compares must not land on one wave)
+      if (r == 0 || akeys[ord[r - 1]][0] != key[0] || akeys[ord[r - 1]][1] != key[1] ||
+          P.groups.back().count >= group_atoms) {
+        FcaGroup g{};
+        const uint32_t nl = key[1];
+        for (uint32_t l = 0; l < 8; l++) g.rows[l] = l < nl ? key[0] + l : zero_row;
+        g.first = (uint32_t)r;
+        g.nl = nl;
+        auto sl = slot_of.find({key[0], nl});
+        g.slot = sl == slot_of.end() ? ~0u : sl->second;
+        P.groups.push_back(g);
       }
-      auto it = atom_of.find(key);
-      uint32_t a;
-      if (it != atom_of.end()) {
-        a = it->second;
-      } else {
-        a = (uint32_t)(atom_of.size() + fresh.size());
-        bool dup = false;
-        for (size_t f = 0; f < fresh.size(); f++)
-          if (fresh[f] == key) {
-            a = (uint32_t)(atom_of.size() + f);
-            dup = true;
-          }
-        if (!dup) fresh.push_back(key);
-      }
-      ent.push_back((abase + a) | (ng ? 0x80000000u : 0u));
-    }
-    if (!ok || fresh.size() > (size_t)kFcaMaxAtoms) {
-      keep[i] = 0;
-      continue;
-    }
-    for (const auto& key : fresh) {
+      P.groups.back().count++;
       FcCmp q{};
-      q.h.slot = slot_of[key[0]];
+      q.h.slot = 0;
       q.h.nl = key[1];
       q.h.accept = key[2];
       uint32_t cc[8] = {0}, ff[8] = {0};
@@ -3055,45 +3063,95 @@ static void fca_plan(const mq_ctx* c, const std::vector<std::vector<uint32_t>>& 
         q.t.c[l] = cc[2 + l];
         q.t.f[l] = ff[2 + l];
       }
-      atom_of[key] = (uint32_t)atom_of.size();
       P.atoms.push_back(q);
     }
-    tl.push_back(std::move(ent));
-    P.tape_out.push_back(out_of(i) | (negated[i] ? 0x80000000u : 0u));
-    const auto no = nodes_ops(i);
-    P.metric.push_back(no.first);
-    P.metric.push_back(no.second);
-  }
-  // per segment: chunks of 64 tapes, entries k-major; short lists padded with entry 0 (all ones)
-  seg_start.push_back(tl.size());
-  P.chunk_off.assign(1, 0);
-  int atom_off = 0;
-  for (size_t s = 0; s + 1 < seg_start.size(); s++) {
-    const size_t b = seg_start[s], e = seg_start[s + 1];
-    if (b == e) continue;
-    FcaPlan::Seg sg{};
-    sg.tape_first = (int)b;
-    sg.n_tapes = (int)(e - b);
-    sg.chunk_first = (int)P.chunk_off.size() - 1;
-    int na = 0;
-    for (size_t t = b; t < e; t++)
-      for (uint32_t x : tl[t])
-        if ((x & 0x7FFFFFFFu) >= abase) na = std::max(na, (int)((x & 0x7FFFFFFFu) - abase) + 1);
-    sg.atom_off = atom_off;
-    sg.n_atoms = na;
-    atom_off += na;
-    for (size_t c0 = b; c0 < e; c0 += 64) {
+    sg.n_groups = (int)P.groups.size() - sg.group_off;
+    P.stage_masks.insert(P.stage_masks.end(), masks.begin(), masks.end());
+    const uint32_t abase = 1u + (uint32_t)masks.size();
+    // chunks of 64 tapes, entries k-major; short lists padded with entry 0 (all ones)
+    for (size_t c0 = 0; c0 < tl.size(); c0 += 64) {
       size_t kmax = 0;
-      for (size_t t = c0; t < std::min(e, c0 + 64); t++) kmax = std::max(kmax, tl[t].size());
+      for (size_t t = c0; t < std::min(tl.size(), c0 + 64); t++) kmax = std::max(kmax, tl[t].size());
       for (size_t k = 0; k < kmax; k++)
         for (size_t l = 0; l < 64; l++) {
           const size_t t = c0 + l;
-          P.lists.push_back(t < e && k < tl[t].size() ? tl[t][k] : 0u);
+          uint32_t e = 0;
+          if (t < tl.size() && k < tl[t].size()) {
+            const Ent& x = tl[t][k];
+            e = (x.kind == 0 ? 1u + x.id : abase + pos[x.id]) | (x.neg ? 0x80000000u : 0u);
+          }
+          P.lists.push_back(e);
         }
       P.chunk_off.push_back((uint32_t)P.lists.size());
     }
+    for (size_t t = 0; t < tl.size(); t++) {
+      P.tape_out.push_back(out_of(tsrc[t]) | (negated[tsrc[t]] ? 0x80000000u : 0u));
+      const auto no = nodes_ops(tsrc[t]);
+      P.metric.push_back(no.first);
+      P.metric.push_back(no.second);
+    }
     P.segs.push_back(sg);
+    atom_of.clear();
+    akeys.clear();
+    mask_of.clear();
+    masks.clear();
+    tl.clear();
+    tsrc.clear();
+  };
+  for (size_t i = 0; i < keep.size(); i++) {
+    if (!keep[i]) continue;
+    if (fq[i].size() > (size_t)kFcaMaxAtoms || fm[i].size() > (size_t)kFcStageMasks) {
+      keep[i] = 0;
+      continue;
+    }
+    // this tape's new atoms / masks; a new segment when they do not fit
+    size_t new_a = 0, new_m = 0;
+    {
+      std::set<std::vector<uint32_t>> fa;
+      std::set<uint32_t> fmk;
+      for (const auto& h : fq[i]) {
+        bool ng;
+        auto key = atom_key(h, &ng);
+        if (!atom_of.count(key)) fa.insert(key);
+      }
+      for (uint32_t e : fm[i])
+        if (!mask_of.count(e & 0x7FFFFFFFu)) fmk.insert(e & 0x7FFFFFFFu);
+      new_a = fa.size();
+      new_m = fmk.size();
+    }
+    if (akeys.size() + new_a > (size_t)kFcaMaxAtoms || masks.size() + new_m > (size_t)kFcStageMasks) close();
+    std::vector<Ent> ent;
+    for (uint32_t e : fm[i]) {
+      const uint32_t v = e & 0x7FFFFFFFu;
+      auto it = mask_of.find(v);
+      uint32_t id;
+      if (it == mask_of.end()) {
+        id = (uint32_t)masks.size();
+        mask_of[v] = id;
+        masks.push_back(v);
+      } else {
+        id = it->second;
+      }
+      ent.push_back(Ent{0, id, e >> 31});
+    }
+    for (const auto& h : fq[i]) {
+      bool ng;
+      auto key = atom_key(h, &ng);
+      auto it = atom_of.find(key);
+      uint32_t id;
+      if (it == atom_of.end()) {
+        id = (uint32_t)akeys.size();
+        atom_of[key] = id;
+        akeys.push_back(key);
+      } else {
+        id = it->second;
+      }
+      ent.push_back(Ent{1, id, ng ? 1u : 0u});
+    }
+    tl.push_back(std::move(ent));
+    tsrc.push_back(i);
   }
+  close();
 }
 
 static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
@@ -3254,23 +3312,22 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
   HIPCHK(T->qprog.upload(prog.data(), prog.size(), c->stream));
   if (T->fca) {
     T->fc_count = (int)fap.tape_out.size();
-    T->fc_stage_n = (int)fap.stage_rows.size();
-    T->fc_smask_n = (int)fap.stage_masks.size();
     T->fca_atoms = (int)fap.atoms.size();
-    T->fca_segs.clear();
-    for (const auto& sg : fap.segs) T->fca_segs.push_back({sg.atom_off, sg.n_atoms, sg.tape_first, sg.n_tapes, sg.chunk_first});
+    T->fca_segs = fap.segs;
     if (T->fc_count > 0) {
-      if (fap.stage_rows.empty()) fap.stage_rows.push_back(0);
       if (fap.stage_masks.empty()) fap.stage_masks.push_back(0);
       if (fap.atoms.empty()) fap.atoms.push_back(FcCmp{});
+      if (fap.groups.empty()) fap.groups.push_back(FcaGroup{});
       if (fap.lists.empty()) fap.lists.push_back(0);
       HIPCHK(T->fc_cmp_dev.upload(fap.atoms.data(), fap.atoms.size(), c->stream));
+      HIPCHK(T->fca_group_dev.upload(fap.groups.data(), fap.groups.size(), c->stream));
       HIPCHK(T->fc_mask_dev.upload(fap.lists.data(), fap.lists.size(), c->stream));
       HIPCHK(T->fca_chunk_dev.upload(fap.chunk_off.data(), fap.chunk_off.size(), c->stream));
       HIPCHK(T->fca_out_dev.upload(fap.tape_out.data(), fap.tape_out.size(), c->stream));
       HIPCHK(T->fca_metric_dev.upload(fap.metric.data(), fap.metric.size(), c->stream));
-      HIPCHK(T->fc_stage_dev.upload(fap.stage_rows.data(), fap.stage_rows.size(), c->stream));
       HIPCHK(T->fc_smask_dev.upload(fap.stage_masks.data(), fap.stage_masks.size(), c->stream));
+      if (fap.stage_rows.empty()) fap.stage_rows.push_back(0);
+      HIPCHK(T->fc_stage_dev.upload(fap.stage_rows.data(), fap.stage_rows.size(), c->stream));
     }
   } else {
     T->fc_count = (int)fcp.tapes.size();
@@ -3920,6 +3977,8 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     FcaArgs f{};
     f.n = sg.n_tapes;
     f.n_atoms = sg.n_atoms;
+    f.n_groups = sg.n_groups;
+    f.groups = T->fca_group_dev.as<FcaGroup>() + sg.group_off;
     f.atoms = T->fc_cmp_dev.as<FcCmp>() + sg.atom_off;
     f.lists = T->fc_mask_dev.as<uint32_t>();
     f.chunk_off = T->fca_chunk_dev.as<uint32_t>() + sg.chunk_first;
@@ -3935,10 +3994,10 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     f.best = best;
     f.verdicts = verdicts;
     f.counters = c->counters.as<unsigned long long>();
-    f.stage_rows = T->fc_stage_dev.as<uint32_t>();
-    f.n_stage = T->fc_stage_n;
-    f.stage_masks = T->fc_smask_dev.as<uint32_t>();
-    f.n_smask = T->fc_smask_n;
+    f.stage_masks = T->fc_smask_dev.as<uint32_t>() + sg.smask_off;
+    f.n_smask = sg.n_smask;
+    f.stage_rows = T->fc_stage_dev.as<uint32_t>() + sg.stage_off;
+    f.n_stage = sg.n_stage;
     HIPCHK(start_timer());
     HIPCHK(launch_fca(f, st));
   }

@@ -252,12 +252,22 @@ hipError_t launch_fc(const FcArgs& a, hipStream_t st);
 
 // Two-phase flat conjunctions (fc.hip fca_kernel, mq_api.cpp fca_plan), for tapes: the launch's
 // distinct compares ("atoms") are evaluated once per 64-model tile into lane masks in LDS (model
-// lanes), then every tape ANDs its atoms' and Bool variables' masks with one lane per tape.  A
-// workgroup's LDS table per tile: entry 0 all ones, 1 .. n_smask the staged Bool masks, then the
-// atoms; a list entry is a table index | negated << 31.
+// lanes), grouped by the variable they read (one read of its limbs per group), then every tape
+// ANDs its atoms' and Bool variables' masks with one lane per tape.  A workgroup's LDS table per
+// tile: entry 0 all ones, 1 .. n_smask the Bool masks, then the atoms; a list entry is a table
+// index | negated << 31.
+struct FcaGroup {
+  uint32_t rows[8];   // the variable's limb rows (nl <= 2: rows[0..1]; else 8, the zero row past nl)
+  uint32_t first;     // its atoms: atoms[first .. first + count)
+  uint32_t count;
+  uint32_t nl;
+  uint32_t slot;      // its limbs' LDS slot (staged rows, as fc_kernel's), or ~0u: read from vars
+};
 struct FcaArgs {
   int n;                          // tapes
   int n_atoms;
+  int n_groups;
+  const FcaGroup* groups;
   const FcCmp* atoms;             // accept in {1, 2, 3} (x < c, x == c, x <= c); negations in the lists
   const uint32_t* lists;          // chunk c of 64 tapes: kmax(c) entries x 64 lanes, k-major, from chunk_off[c]
   const uint32_t* chunk_off;      // [n_chunks + 1]: kmax(c) = (chunk_off[c + 1] - chunk_off[c]) / 64
@@ -273,10 +283,10 @@ struct FcaArgs {
   int32_t* best;
   uint8_t* verdicts;
   unsigned long long* counters;
-  const uint32_t* stage_rows;
-  int n_stage;
-  const uint32_t* stage_masks;
+  const uint32_t* stage_masks;    // the Bool mask indices of table entries 1 .. n_smask
   int n_smask;
+  const uint32_t* stage_rows;     // variable rows staged in LDS per workgroup (FcaGroup.slot)
+  int n_stage;
 };
 hipError_t launch_fca(const FcaArgs& a, hipStream_t st);
 
