@@ -351,7 +351,22 @@ __global__ __launch_bounds__(256) void fca_kernel(const FcaGroup* __restrict__ g
       runs++;
       run_nodes += tape_metric[2 * t];
       run_ops += tape_metric[2 * t + 1];
-      if (r.mode == 0) {
+      if (r.mode == 3) {
+        // a Bool column: its tiles' lane masks, and its 0/1 row where a HIP C++ kernel reads rows
+        // or it has no mask index (one lane per column: these row stores do not coalesce; the
+        // assembly-only launches C4 / C3 / C5 make need none)
+        const int32_t mo = r.col_mask[t];
+#pragma unroll
+        for (int j = 0; j < FC_TILES; j++) {
+          const int64_t mt = m0 + 64 * j;
+          if (mt >= r.M) break;
+          if (mo >= 0) r.bool_masks_out[(tile0 + j) * (int64_t)r.n_bool_masks + mo] = acc[j];
+          if (r.bool_rows || mo < 0) {
+            const int lim = (int)min<int64_t>(64, r.M - mt);
+            for (int q = 0; q < lim; q++) r.vars_out[(int64_t)row * r.M + mt + q] = (uint32_t)((acc[j] >> q) & 1u);
+          }
+        }
+      } else if (r.mode == 0) {
 #pragma unroll
         for (int j = 0; j < FC_TILES; j++)
           if (acc[j]) {   // the lowest tile with a hit has the lowest model
@@ -391,7 +406,7 @@ __global__ __launch_bounds__(256) void fca_kernel(const FcaGroup* __restrict__ g
     }
     if (lane == 0 && runs) {
       unsigned long long* cnt = r.counters + ((blockIdx.x * 4 + wave) % kCounterSlots) * kCounterStride;
-      atomicAdd(&cnt[0], runs * nv);
+      if (r.mode != 3) atomicAdd(&cnt[0], runs * nv);   // (tape evaluations; a column is not one)
       atomicAdd(&cnt[1], run_nodes * nv);
       atomicAdd(&cnt[2], run_ops * nv);
     }

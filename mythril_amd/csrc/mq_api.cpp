@@ -445,9 +445,10 @@ struct mq_tapes {
   DevBuf fca_chunk_dev, fca_out_dev, fca_metric_dev, fca_group_dev;
   // the G-eligible Bool columns of a level that are flat (fc_match) run on fc_kernel, mode 3,
   // before the level's G launch (cq_prepare); the level's G descriptors are the others
-  struct FcLevel {
-    int count = 0, stage_n = 0, smask_n = 0;
-    DevBuf tapes, mask, cmp, stage, smask, prefix;
+  struct FcLevel {   // fca_kernel mode 3 (fca_plan per level)
+    int count = 0;
+    std::vector<FcaPlanSeg> segs;
+    DevBuf atoms, groups, lists, chunk, out, metric, smask, stage, colmask;
   };
   std::vector<std::unique_ptr<FcLevel>> fc_lvl;
   std::vector<int> cq_lvl_desc_off, cq_lvl_desc_n;
@@ -2958,13 +2959,15 @@ struct FcaPlan {
   std::vector<FcCmp> atoms;
   std::vector<FcaGroup> groups;
   std::vector<uint32_t> lists, chunk_off, tape_out, metric, stage_masks, stage_rows;
+  std::vector<int32_t> col_mask;   // (columns: per kept column its lane-mask index)
   std::vector<FcaPlanSeg> segs;
 };
 static constexpr int kFcaMaxAtoms = 1024;   // 32 KB of LDS masks for the 4 tiles of a workgroup
 static constexpr int kFcaGroupAtoms = 16;   // (C4 fca: 4 -> 213 us, 8 -> 196, 16 -> 186, 32 -> 199)
 static void fca_plan(const mq_ctx* c, const std::vector<std::vector<uint32_t>>& fm, const std::vector<std::vector<FcCmpH>>& fq,
                      const std::vector<char>& negated, std::vector<char>& keep, const std::function<uint32_t(size_t)>& out_of,
-                     const std::function<std::pair<uint32_t, uint32_t>(size_t)>& nodes_ops, FcaPlan& P) {
+                     const std::function<std::pair<uint32_t, uint32_t>(size_t)>& nodes_ops, FcaPlan& P,
+                     const std::function<int32_t(size_t)>& mask_out = nullptr) {
   const uint32_t zero_row = (uint32_t)(c->var_off_h.empty() ? 0 : c->var_off_h.back() + c->var_nl_h.back());
   auto atom_key = [](const FcCmpH& h, bool* ng) {
     *ng = h.accept >= 4;
@@ -3089,6 +3092,7 @@ static void fca_plan(const mq_ctx* c, const std::vector<std::vector<uint32_t>>& 
       const auto no = nodes_ops(tsrc[t]);
       P.metric.push_back(no.first);
       P.metric.push_back(no.second);
+      if (mask_out) P.col_mask.push_back(mask_out(tsrc[t]));
     }
     P.segs.push_back(sg);
     atom_of.clear();
@@ -3440,32 +3444,35 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
         on_fc[i] = T->cq_bool[b + i] && fc_match(c, T->cq_ct[b + i], fm[i], fq[i], &ng) ? 1 : 0;
         fneg[i] = ng ? 1 : 0;
       }
-    FcPlan fcp;
-    fc_plan(c, fm, fq, fneg, on_fc, [&](size_t i) { return c->var_off_h[T->cq_var[b + i]]; },
-            [&](size_t i) {
-              const int v = T->cq_var[b + i];
-              return (int32_t)(v < (int)c->bmask_of_var.size() ? c->bmask_of_var[v] : -1);
-            },
-            [&](size_t i) {
-              const CompiledTape& x = T->cq_ct[b + i];
-              return std::make_pair(x.n_nodes, (uint32_t)std::min(x.alg_ops, 4.0e9));
-            },
-            fcp);
+    FcaPlan fap;
+    fca_plan(c, fm, fq, fneg, on_fc, [&](size_t i) { return c->var_off_h[T->cq_var[b + i]]; },
+             [&](size_t i) {
+               const CompiledTape& x = T->cq_ct[b + i];
+               return std::make_pair(x.n_nodes, (uint32_t)std::min(x.alg_ops, 4.0e9));
+             },
+             fap,
+             [&](size_t i) {
+               const int v = T->cq_var[b + i];
+               return (int32_t)(v < (int)c->bmask_of_var.size() ? c->bmask_of_var[v] : -1);
+             });
     mq_tapes::FcLevel& fl = *T->fc_lvl[li];
-    fl.count = (int)fcp.tapes.size();
+    fl.count = (int)fap.tape_out.size();
+    fl.segs = fap.segs;
     if (fl.count > 0) {
-      fl.stage_n = (int)fcp.stage_rows.size();
-      fl.smask_n = (int)fcp.stage_masks.size();
-      if (fcp.mask_lds.empty()) fcp.mask_lds.push_back(0);
-      if (fcp.cmps.empty()) fcp.cmps.push_back(FcCmp{});
-      if (fcp.stage_rows.empty()) fcp.stage_rows.push_back(0);
-      if (fcp.stage_masks.empty()) fcp.stage_masks.push_back(0);
-      HIPCHK(fl.tapes.upload(fcp.tapes.data(), fcp.tapes.size(), c->stream));
-      HIPCHK(fl.mask.upload(fcp.mask_lds.data(), fcp.mask_lds.size(), c->stream));
-      HIPCHK(fl.cmp.upload(fcp.cmps.data(), fcp.cmps.size(), c->stream));
-      HIPCHK(fl.stage.upload(fcp.stage_rows.data(), fcp.stage_rows.size(), c->stream));
-      HIPCHK(fl.smask.upload(fcp.stage_masks.data(), fcp.stage_masks.size(), c->stream));
-      HIPCHK(fl.prefix.upload(fcp.prefix.data(), fcp.prefix.size(), c->stream));
+      if (fap.stage_masks.empty()) fap.stage_masks.push_back(0);
+      if (fap.stage_rows.empty()) fap.stage_rows.push_back(0);
+      if (fap.atoms.empty()) fap.atoms.push_back(FcCmp{});
+      if (fap.groups.empty()) fap.groups.push_back(FcaGroup{});
+      if (fap.lists.empty()) fap.lists.push_back(0);
+      HIPCHK(fl.atoms.upload(fap.atoms.data(), fap.atoms.size(), c->stream));
+      HIPCHK(fl.groups.upload(fap.groups.data(), fap.groups.size(), c->stream));
+      HIPCHK(fl.lists.upload(fap.lists.data(), fap.lists.size(), c->stream));
+      HIPCHK(fl.chunk.upload(fap.chunk_off.data(), fap.chunk_off.size(), c->stream));
+      HIPCHK(fl.out.upload(fap.tape_out.data(), fap.tape_out.size(), c->stream));
+      HIPCHK(fl.metric.upload(fap.metric.data(), fap.metric.size(), c->stream));
+      HIPCHK(fl.smask.upload(fap.stage_masks.data(), fap.stage_masks.size(), c->stream));
+      HIPCHK(fl.stage.upload(fap.stage_rows.data(), fap.stage_rows.size(), c->stream));
+      HIPCHK(fl.colmask.upload(fap.col_mask.data(), fap.col_mask.size(), c->stream));
     }
     std::vector<int> rest;   // the level's columns left to G
     for (int i = 0; i < n0; i++)
@@ -3807,31 +3814,37 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     }
     const mq_tapes::Variant v8 = use_cq ? cut_front(lv.v[0], lv.v8q) : lv.v[0];
     if (use_cq && li < T->fc_lvl.size() && T->fc_lvl[li] && T->fc_lvl[li]->count > 0) {
-      // the level's flat Bool columns on fc_kernel, mode 3
+      // the level's flat Bool columns on fca_kernel, mode 3
       const mq_tapes::FcLevel& fl = *T->fc_lvl[li];
-      FcArgs f{};
-      f.tapes = fl.tapes.as<FcTape>();
-      f.n = fl.count;
-      f.tpg = (int)std::max<int64_t>(1, std::min<int64_t>((f.n + 3) / 4, 64));
-      f.stage_rows = fl.stage.as<uint32_t>();
-      f.n_stage = fl.stage_n;
-      f.stage_masks = fl.smask.as<uint32_t>();
-      f.n_smask = fl.smask_n;
-      f.prefix = fl.prefix.as<unsigned long long>();
-      f.mask_lds = fl.mask.as<uint32_t>();
-      f.cmps = fl.cmp.as<FcCmp>();
-      f.vars = c->vars.as<uint32_t>();
-      f.bool_masks = c->bmasks.as<uint64_t>();
-      f.bool_masks_out = c->bmasks.as<uint64_t>();
-      f.vars_out = const_cast<uint32_t*>(c->vars.as<uint32_t>());
-      f.n_bool_masks = c->n_bmask;
-      f.mode = 3;
-      f.bool_rows = bool_rows ? 1 : 0;
-      f.M = c->M;
-      f.index_base = c->index_base;
-      f.counters = c->counters.as<unsigned long long>();
-      HIPCHK(start_timer());
-      HIPCHK(launch_fc(f, st));
+      for (const FcaPlanSeg& sg : fl.segs) {
+        FcaArgs f{};
+        f.n = sg.n_tapes;
+        f.n_atoms = sg.n_atoms;
+        f.n_groups = sg.n_groups;
+        f.groups = fl.groups.as<FcaGroup>() + sg.group_off;
+        f.atoms = fl.atoms.as<FcCmp>() + sg.atom_off;
+        f.lists = fl.lists.as<uint32_t>();
+        f.chunk_off = fl.chunk.as<uint32_t>() + sg.chunk_first;
+        f.tape_out = fl.out.as<uint32_t>() + sg.tape_first;
+        f.tape_metric = fl.metric.as<uint32_t>() + 2 * (size_t)sg.tape_first;
+        f.col_mask = fl.colmask.as<int32_t>() + sg.tape_first;
+        f.vars = c->vars.as<uint32_t>();
+        f.bool_masks = c->bmasks.as<uint64_t>();
+        f.bool_masks_out = c->bmasks.as<uint64_t>();
+        f.vars_out = const_cast<uint32_t*>(c->vars.as<uint32_t>());
+        f.n_bool_masks = c->n_bmask;
+        f.bool_rows = bool_rows ? 1 : 0;
+        f.mode = 3;
+        f.M = c->M;
+        f.index_base = c->index_base;
+        f.counters = c->counters.as<unsigned long long>();
+        f.stage_masks = fl.smask.as<uint32_t>() + sg.smask_off;
+        f.n_smask = sg.n_smask;
+        f.stage_rows = fl.stage.as<uint32_t>() + sg.stage_off;
+        f.n_stage = sg.n_stage;
+        HIPCHK(start_timer());
+        HIPCHK(launch_fca(f, st));
+      }
     }
     const int n_gcol = use_cq && li < T->cq_lvl_desc_n.size() ? T->cq_lvl_desc_n[li] : 0;
     if (n_gcol > 0) {

@@ -276,13 +276,17 @@ struct FcaArgs {
   const uint32_t* vars;
   const uint64_t* bool_masks;
   int n_bool_masks;
-  int mode;                       // 0 first hit, 1 verdict bytes
+  int mode;                       // 0 first hit, 1 verdict bytes, 3 Bool columns (tape_out = the column's row)
   int early_exit;
   int64_t M;
   int64_t index_base;
   int32_t* best;
   uint8_t* verdicts;
   unsigned long long* counters;
+  const int32_t* col_mask;        // mode 3: per column its packed lane-mask index (-1: none, the 0/1 row is written)
+  uint64_t* bool_masks_out;       // mode 3: the same array as bool_masks, the level's columns written
+  uint32_t* vars_out;             // mode 3: 0/1 rows
+  int bool_rows;                  // mode 3: also write the 0/1 row of a column with a mask index
   const uint32_t* stage_masks;    // the Bool mask indices of table entries 1 .. n_smask
   int n_smask;
   const uint32_t* stage_rows;     // variable rows staged in LDS per workgroup (FcaGroup.slot)
