@@ -998,11 +998,25 @@ def sub_uf1(pfx):
             "v_lshlrev_b32 v4, 1, v2",
             "global_load_dword v5, v4, s[66:67]",
             "global_load_dword v6, v4, s[66:67] offset:8",
-            "s_waitcnt vmcnt(0)",
-            "v_sub_u32 v6, v6, v5",                          # this model's entries
             "s_mov_b64 s[60:61], exec",
             "s_mov_b64 s[64:65], 0",
-            "s_mov_b32 s98, 0",
+            "s_mov_b32 s98, 0"]
+    # round 0's key limbs are requested together with the entry counts (one round trip less;
+    # a slot past a model's count is read but never matched)
+    for j in range(8):
+        out += [f"s_add_u32 s39, s98, {j}", "s_cmp_ge_u32 s39, s38", f"s_cbranch_scc1 {P}_ufd_ld0",
+                "s_mul_i32 s39, s39, s36",
+                "s_mul_i32 s78, s39, s74", "s_mul_hi_u32 s79, s39, s74",
+                "s_add_u32 s78, s78, s68", "s_addc_u32 s79, s79, s69",
+                f"global_load_dword v{UBASE + j}, v2, s[78:79]"]
+    out += [f"{P}_ufd_ld0:",
+            "s_waitcnt vmcnt(0)",
+            "v_sub_u32 v6, v6, v5",                          # this model's entries
+            "v_cmp_lt_u32_e64 s[66:67], s98, v6",
+            "s_nop 3",
+            "s_and_b64 exec, exec, s[66:67]",
+            f"s_cbranch_execz {P}_ufd_done",
+            f"s_branch {P}_ufd_ld",
             f"{P}_ufd_loop:",
             "v_cmp_lt_u32_e64 s[66:67], s98, v6",
             "s_nop 3",
@@ -1015,6 +1029,56 @@ def sub_uf1(pfx):
                 "s_add_u32 s78, s78, s68", "s_addc_u32 s79, s79, s69",
                 f"global_load_dword v{UBASE + j}, v2, s[78:79]"]
     out += [f"{P}_ufd_ld:", "s_mov_b64 s[66:67], exec", "s_waitcnt vmcnt(0)"]
+    # Fast path: each lane's candidate = its lowest slot of the round whose key limb 0 matches
+    # (v137, -1: none), then ONE round trip for the candidates' other key limbs (a per-lane
+    # gather) and the full compare.  The per-slot path below took one round trip per slot that
+    # any lane matched -- up to 8 a round, since 64 lanes are 64 models with their own tables.
+    # Lanes whose limb 0 matched but whose key did not (a false candidate: another slot of the
+    # round may still match) send the round to the per-slot path.
+    out += ["v_mov_b32 v137, -1"]
+    for j in reversed(range(8)):
+        out += [f"s_add_u32 s39, s98, {j}", "s_cmp_ge_u32 s39, s38", f"s_cbranch_scc1 {P}_ufc_s{j}",
+                f"v_cmp_eq_u32_e64 s[34:35], v{UBASE + j}, {W(0)}",
+                "v_cmp_lt_u32_e64 s[78:79], s39, v6",
+                "s_nop 3",
+                "s_and_b64 s[34:35], s[34:35], s[78:79]",
+                "v_mov_b32 v139, s39",
+                "v_cndmask_b32 v137, v137, v139, s[34:35]",
+                f"{P}_ufc_s{j}:"]
+    out += ["v_cmp_ne_u32_e64 s[34:35], -1, v137",
+            "s_nop 3",
+            "s_and_b64 exec, s[34:35], s[66:67]",
+            f"s_cbranch_execz {P}_ufc_none",
+            "s_mul_i32 s39, s36, s74",                        # nl_a0 * M * 4: one slot's key rows
+            "v_mov_b32 v149, s39",
+            "v_mad_u64_u32 v[150:151], s[34:35], v137, v149, s[68:69]",
+            "v_add_co_u32 v150, vcc, v150, v2",
+            "v_addc_co_u32 v151, vcc, 0, v151, vcc"]
+    for l in range(1, L):
+        out += [f"s_cmp_le_u32 s36, {l}", f"s_cbranch_scc1 {P}_ufc_kl",
+                "v_add_co_u32 v150, vcc, s74, v150", "v_addc_co_u32 v151, vcc, 0, v151, vcc",
+                f"global_load_dword v{UBASE + 12 + l}, v[150:151], off"]
+    out += [f"{P}_ufc_kl:", "s_waitcnt vmcnt(0)", "v_mov_b32 v148, 0"]
+    for l in range(1, L):
+        out += [f"s_cmp_le_u32 s36, {l}", f"s_cbranch_scc1 {P}_ufc_kc",
+                f"v_xor_b32 v149, v{UBASE + 12 + l}, {W(l)}", "v_or_b32 v148, v148, v149"]
+    out += [f"{P}_ufc_kc:",
+            "v_cmp_eq_u32_e64 s[34:35], 0, v148",
+            "s_nop 3",
+            "s_and_b64 s[34:35], s[34:35], exec",
+            "s_andn2_b64 s[78:79], exec, s[34:35]",           # false candidates
+            "s_or_b64 s[64:65], s[64:65], s[34:35]",
+            "s_mov_b64 exec, s[34:35]",
+            "v_mov_b32 v138, v137",                           # matched slot
+            "s_andn2_b64 s[66:67], s[66:67], s[34:35]",
+            "s_mov_b64 exec, s[66:67]",
+            "s_cmp_lg_u64 s[78:79], 0",
+            f"s_cbranch_scc1 {P}_ufd_slow",
+            f"s_branch {P}_ufd_next",
+            f"{P}_ufc_none:",
+            "s_mov_b64 exec, s[66:67]",
+            f"s_branch {P}_ufd_next",
+            f"{P}_ufd_slow:"]
     for j in range(8):
         nj = f"{P}_ufd_nj{j}"
         out += [f"s_add_u32 s39, s98, {j}", "s_cmp_ge_u32 s39, s38", f"s_cbranch_scc1 {P}_ufd_next",
