@@ -3,9 +3,11 @@
 
 Inputs: the C4 bench line (bench.py --config c4: alg ops per launch, kernel_ms over the whole step,
 keccak_columns, models) and the rocprofv3 kernel trace of the same workload (tools/rocpd_summary.py
-JSON; evaluation kernels only, per launch of the traced run = warmup + steps).  The keccak-f[1600] column kernel's algorithmic work is keccak_columns x M x 7 974 VALU ops
-(one 136-byte block per 64-byte key ++ slot message; tape_compiler.h kKeccakOpsPerBlock); the
-interpreters (G tapes, G columns, HIP C++ columns, Bool-mask packing) share the rest; each
+JSON; evaluation kernels only, per launch of the traced run = warmup + steps).  The keccak-f[1600] column kernel's algorithmic work is keccak_columns x M x 6 514 ops
+(one 136-byte block per 64-byte key ++ slot message; tape_compiler.h kKeccakOpsPerBlock, counted from
+the permutation's definition); the
+other kernels ("interpreters": G column levels, the flat-conjunction kernel on tapes and Bool
+columns, the bit-gather columns, Bool-mask packing) share the rest; each
 class's time per step is its traced total / launches.  Peaks: 39.3 T
 lane-ops/s (SIMD-16 issue of the carry / compare / multiply classes) for the
 interpreters; for keccak-f, whose instructions are mostly two-operand VGPR bitwise ops, also the
@@ -30,8 +32,9 @@ def main():
     # evaluation kernels only (the trace also holds the workload generation: model keccaks,
     # copies, row masking at upload); launches = warmup + steps of the traced bench run
     launches = int(sys.argv[4]) if len(sys.argv) > 4 else 4
-    groups = {"keccak_column_kernel": 0.0, "qsg_kernel": 0.0, "qs_column_kernel": 0.0,
-              "qs_pack_bool": 0.0, "qs_init_best": 0.0, "qs_finalize_best": 0.0}
+    groups = {"keccak_column_kernel": 0.0, "qsg_kernel": 0.0, "qs_column_kernel": 0.0, "fca_kernel": 0.0,
+              "fc_kernel": 0.0, "cw_column_kernel": 0.0, "qs_pack_bool": 0.0, "qs_init_best": 0.0,
+              "qs_finalize_best": 0.0}
     for k in kt:
         g = next((x for x in groups if "mq::" + x in k["kernel"]), None)
         if g is not None:
