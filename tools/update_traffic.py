@@ -15,6 +15,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EVAL = ("mq::qsa_kernel", "mq::qsg_kernel", "mq::qs_first_hit_kernel", "mq::qs_column_kernel", "mq::keccak_column_kernel",
+        "mq::fca_kernel", "mq::fc_kernel", "mq::cw_column_kernel",
         "mq::qs_pack_bool", "mq::qs_init_best", "mq::qs_finalize_best")
 SHAPES = {"c2": (10000, 100000, 2), "c3": (1000, 1000000, 3), "c4": (200, 1000000, 4), "c5": (256, 1250000, 5)}
 LAUNCHES = 2
