@@ -1029,6 +1029,24 @@ def sub_uf1(pfx):
                 "s_add_u32 s78, s78, s68", "s_addc_u32 s79, s79, s69",
                 f"global_load_dword v{UBASE + j}, v2, s[78:79]"]
     out += [f"{P}_ufd_ld:", "s_mov_b64 s[66:67], exec", "s_waitcnt vmcnt(0)"]
+    def dense_values(lbl):
+        # the value limbs of the matched lanes' slots (v138) into U[0 .. nl_res): value limb l of
+        # slot e at keys + (dense_e * nl_a0 + e * nl_res + l) * M * 4 (exec = the lanes to load)
+        o = ["s_mul_i32 s99, s38, s36",                      # dense_e * nl_a0
+             "s_mul_i32 s78, s99, s74", "s_mul_hi_u32 s79, s99, s74",
+             "s_add_u32 s78, s78, s68", "s_addc_u32 s79, s79, s69",
+             "s_mul_i32 s39, s37, s74",                      # nl_res * M * 4
+             "v_mov_b32 v149, s39",                          # (one SGPR operand per VALU)
+             "v_mad_u64_u32 v[150:151], s[34:35], v138, v149, s[78:79]",
+             "v_add_co_u32 v150, vcc, v150, v2",
+             "v_addc_co_u32 v151, vcc, 0, v151, vcc"]
+        for l in range(L):
+            o += [f"s_cmp_le_u32 s37, {l}", f"s_cbranch_scc1 {lbl}",
+                  f"global_load_dword v{UBASE + l}, v[150:151], off"]
+            if l < L - 1:
+                o += ["v_add_co_u32 v150, vcc, s74, v150", "v_addc_co_u32 v151, vcc, 0, v151, vcc"]
+        return o + [f"{lbl}:"]
+
     # Fast path: each lane's candidate = its lowest slot of the round whose key limb 0 matches
     # (v137, -1: none), then ONE round trip for the candidates' other key limbs (a per-lane
     # gather) and the full compare.  The per-slot path below took one round trip per slot that
@@ -1058,7 +1076,10 @@ def sub_uf1(pfx):
         out += [f"s_cmp_le_u32 s36, {l}", f"s_cbranch_scc1 {P}_ufc_kl",
                 "v_add_co_u32 v150, vcc, s74, v150", "v_addc_co_u32 v151, vcc, 0, v151, vcc",
                 f"global_load_dword v{UBASE + 12 + l}, v[150:151], off"]
-    out += [f"{P}_ufc_kl:", "s_waitcnt vmcnt(0)", "v_mov_b32 v148, 0"]
+    # ... and the candidate slot's value limbs in the same round trip (into U, whose limb-0 words
+    # the candidate choice has consumed; a false candidate reloads them on the per-slot path)
+    out += [f"{P}_ufc_kl:", "v_mov_b32 v138, v137"] + dense_values(f"{P}_ufc_vl")
+    out += ["s_waitcnt vmcnt(0)", "v_mov_b32 v148, 0"]
     for l in range(1, L):
         out += [f"s_cmp_le_u32 s36, {l}", f"s_cbranch_scc1 {P}_ufc_kc",
                 f"v_xor_b32 v149, v{UBASE + 12 + l}, {W(l)}", "v_or_b32 v148, v148, v149"]
@@ -1080,8 +1101,15 @@ def sub_uf1(pfx):
             f"s_branch {P}_ufd_next",
             f"{P}_ufd_slow:"]
     for j in range(8):
+        out += [f"s_add_u32 s39, s98, {j}", "s_cmp_ge_u32 s39, s38", f"s_cbranch_scc1 {P}_ufs_ld",
+                "s_mul_i32 s39, s39, s36",
+                "s_mul_i32 s78, s39, s74", "s_mul_hi_u32 s79, s39, s74",
+                "s_add_u32 s78, s78, s68", "s_addc_u32 s79, s79, s69",
+                f"global_load_dword v{UBASE + j}, v2, s[78:79]"]
+    out += [f"{P}_ufs_ld:", "s_waitcnt vmcnt(0)"]
+    for j in range(8):
         nj = f"{P}_ufd_nj{j}"
-        out += [f"s_add_u32 s39, s98, {j}", "s_cmp_ge_u32 s39, s38", f"s_cbranch_scc1 {P}_ufd_next",
+        out += [f"s_add_u32 s39, s98, {j}", "s_cmp_ge_u32 s39, s38", f"s_cbranch_scc1 {P}_ufs_end",
                 f"v_cmp_eq_u32_e64 s[34:35], v{UBASE + j}, {W(0)}",
                 "v_cmp_lt_u32_e64 s[78:79], s39, v6",
                 "s_nop 3",
@@ -1110,29 +1138,21 @@ def sub_uf1(pfx):
                 "s_andn2_b64 s[66:67], s[66:67], s[34:35]",
                 "s_mov_b64 exec, s[66:67]",
                 f"{nj}:"]
+    # (per-slot path only) the values of every lane matched so far, then scan on
+    out += [f"{P}_ufs_end:",
+            "s_and_b64 exec, s[60:61], s[64:65]",
+            f"s_cbranch_execz {P}_ufs_vd"] + dense_values(f"{P}_ufs_vl") + [
+            "s_waitcnt vmcnt(0)",
+            f"{P}_ufs_vd:"]
     out += [f"{P}_ufd_next:",
             "s_mov_b64 exec, s[66:67]",
             "s_add_u32 s98, s98, 8",
             f"s_branch {P}_ufd_loop",
             f"{P}_ufd_done:",
             "s_mov_b64 exec, s[60:61]"]
-    out += [f"v_mov_b64 v[{UBASE + l}:{UBASE + 1 + l}], 0" for l in range(0, 8, 2)]
-    # matched lanes: value limb l of slot e at keys + (dense_e * nl_a0 + e * nl_res + l) * M * 4
-    out += ["s_and_b64 exec, s[60:61], s[64:65]",
-            f"s_cbranch_execz {P}_uf_vl_issued",
-            "s_mul_i32 s99, s38, s36",                      # dense_e * nl_a0
-            "s_mul_i32 s78, s99, s74", "s_mul_hi_u32 s79, s99, s74",
-            "s_add_u32 s78, s78, s68", "s_addc_u32 s79, s79, s69",
-            "s_mul_i32 s39, s37, s74",                      # nl_res * M * 4
-            "v_mov_b32 v149, s39",                          # (one SGPR operand per VALU)
-            "v_mad_u64_u32 v[150:151], s[34:35], v138, v149, s[78:79]",
-            "v_add_co_u32 v150, vcc, v150, v2",
-            "v_addc_co_u32 v151, vcc, 0, v151, vcc"]
+    # matched lanes hold their values in U[0 .. nl_res); limbs past nl_res are zero for every lane
     for l in range(L):
-        out += [f"s_cmp_le_u32 s37, {l}", f"s_cbranch_scc1 {P}_uf_vl_issued",
-                f"global_load_dword v{UBASE + l}, v[150:151], off"]
-        if l < L - 1:
-            out += ["v_add_co_u32 v150, vcc, s74, v150", "v_addc_co_u32 v151, vcc, 0, v151, vcc"]
+        out += [f"s_cmp_le_u32 s37, {l}", f"s_cbranch_scc0 {P}_ufz{l}", f"v_mov_b32 v{UBASE + l}, 0", f"{P}_ufz{l}:"]
     out += [f"s_branch {P}_uf_vl_issued"]
     # the lookup's pointer / match registers were written as v128..v151: move them to UBASE + k
     def remap(line):

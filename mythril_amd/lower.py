@@ -27,7 +27,7 @@ from .exceptions import LoweringError, note_fail_closed
 from .models import FuncSpec, ModelBatch
 from .smt_model import Model
 from .smt_model import as_record
-from .tape import BOOL, NODE_DTYPE, NONE, ColumnSet, Op, Tape, TapeBatch, limbs, to_words
+from .tape import BOOL, NODE_DTYPE, NONE, ColumnSet, Op, SortError, Tape, TapeBatch, limbs, to_words
 
 MAX_WIDTH = 0xFFFF
 # keys wider than this are looked up chunk by chunk (the evaluator holds values of <= 2048 bits)
@@ -686,6 +686,11 @@ def _is_keccak_uf(name: str) -> bool:
 _BIN = {S.ADD: "add", S.SUB: "sub", S.MUL: "mul", S.UDIV: "udiv", S.UREM: "urem", S.SDIV: "sdiv",
         S.SREM: "srem", S.SMOD: "smod", S.BAND: "band", S.BOR: "bor", S.BXOR: "bxor",
         S.SHL: "shl", S.LSHR: "lshr", S.ASHR: "ashr"}
+# IncrementalLowering._lower's inline kinds: binary BV ops and BV predicates (tape opcodes)
+_FAST_BIN = {k: int(getattr(Op, name.upper())) for k, name in _BIN.items()}
+_FAST_PRED = {S.EQ: int(Op.EQ), S.BVULT: int(Op.ULT), S.BVULE: int(Op.ULE), S.BVSLT: int(Op.SLT),
+              S.BVSLE: int(Op.SLE)}
+_OP_CONST, _OP_NOT = int(Op.CONST), int(Op.NOT)
 
 
 def lower_batch(roots: Sequence[S.Term], syms: Optional[SymbolTable] = None, hoist: bool = False,
@@ -904,29 +909,73 @@ class IncrementalLowering:
         if id(root) in self._bad:
             raise LoweringError(self._bad[id(root)][1])
         node, tp, syms = self._node, self.tape, self.syms
-        order: List[S.Term] = []
-        seen = set()
-        stack = [(root, False)]
-        pop, push, add = stack.pop, stack.append, seen.add
-        while stack:
-            t, done = pop()
-            if done:
-                order.append(t)
-                continue
-            i = id(t)
-            if i in seen or i in node:
-                continue
-            add(i)
-            push((t, True))
-            for a in reversed(t.args):
-                j = id(a)
-                if j not in seen and j not in node:
-                    push((a, False))
         keep = self._keep
         get = node.get
+        # the kinds a fresh path's new terms are made of (constants, equalities, orders, binary
+        # arithmetic, NOT: 99 % of the drop-in workload's new nodes) are added to the tape inline,
+        # with the same sort checks and hash-consing as Tape's methods; the rest go through
+        # _lower_one.  One pass over the new terms: a term is lowered when it is on top of the
+        # stack with every argument lowered, else its unlowered arguments go on top (first
+        # argument first: the same postorder, so the same node numbering, as a separate walk).
+        nodes, kinds, memo, cmemo, consts = tp.nodes, tp.kind, tp._memo, tp._const_memo, tp.consts
+        fast_bin, fast_pred = _FAST_BIN, _FAST_PRED
+        stack = [root]
+        push, pop = stack.append, stack.pop
         try:
-            for t in order:
-                node[id(t)] = _lower_one(t, [get(id(x), -1) for x in t.args], tp, syms, node)
+            while stack:
+                t = stack[-1]
+                if id(t) in node:
+                    pop()
+                    continue
+                args = t.args
+                pending = False
+                for x in reversed(args):
+                    if id(x) not in node:
+                        push(x)
+                        pending = True
+                if pending:
+                    continue
+                pop()
+                k = t.kind
+                r = None
+                key = None
+                if k == S.VAL:
+                    w = t.width
+                    if 0 < w <= MAX_WIDTH:
+                        v = t.params[0] & ((1 << w) - 1)
+                        off = cmemo.get((v, w))
+                        if off is None:
+                            off = len(consts)
+                            consts.extend(to_words(v, w))
+                            cmemo[(v, w)] = off
+                        key, kind = (_OP_CONST, w, off, 0, 0), "bv"
+                        r = memo.get(key)
+                elif k in fast_bin or k in fast_pred:
+                    a, b = node[id(args[0])], node[id(args[1])]
+                    if a >= 0 and b >= 0 and kinds[a] == "bv" and kinds[b] == "bv":
+                        w = nodes[a][1]
+                        if nodes[b][1] != w:
+                            raise SortError(f"width mismatch {w} vs {nodes[b][1]}")
+                        if k in fast_bin:
+                            key, kind = (fast_bin[k], w, a, b, 0), "bv"
+                        elif k != S.EQ or w <= 256:   # (wider equalities: _wide_eq)
+                            key, kind = (fast_pred[k], BOOL, a, b, 0), "bool"
+                        if key is not None:
+                            r = memo.get(key)
+                elif k == S.NOT:
+                    a = node[id(args[0])]
+                    if a >= 0 and kinds[a] == "bool":
+                        key, kind = (_OP_NOT, BOOL, a, 0, 0), "bool"
+                        r = memo.get(key)
+                if r is None:
+                    if key is None:
+                        r = _lower_one(t, [get(id(x), -1) for x in args], tp, syms, node)
+                    else:
+                        r = len(nodes)
+                        nodes.append(key)
+                        kinds.append(kind)
+                        memo[key] = r
+                node[id(t)] = r
                 keep[id(t)] = t
         except (LoweringError, TypeError) as e:
             self._bad[id(root)] = (root, str(e) or "conjunct not in the tape vocabulary")

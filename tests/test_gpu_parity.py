@@ -1162,6 +1162,48 @@ def test_table_lookups_dense_and_csr_match_oracle(evaluator, monkeypatch, dense,
     assert 0 < v.mean() < 1
 
 
+@pytest.mark.parametrize("dense", [True, False])
+def test_table_lookups_with_shared_first_key_limb(evaluator, monkeypatch, dense):
+    """Table keys that agree in their first 32-bit limb and differ above it (small integers
+    and their 2^32 offsets): the dense scan's candidate (lowest slot whose limb 0 matches) is then
+    often the wrong entry, so the lookup must fall back to its per-slot pass — keys at every slot,
+    absent keys, more than 8 slots (two scan rounds), values of 1, 2 and 8 limbs."""
+    import random
+    from mythril_amd import smt as S
+    from mythril_amd.lower import lower_batch, serialize_models
+    from mythril_amd.smt_model import Model
+    if not dense:
+        monkeypatch.setenv("MQ_NO_DENSE_TABLES", "1")
+    rng = random.Random(11)
+    f = S.Function("inv", [256], 256)
+    g = S.Function("narrow", [256], 32)
+    h = S.Function("mid", [256], 64)
+    x = S.BitVecSym("x", 256)
+    exprs = [f(x) == S.BitVecVal(7, 256), S.ULT(f(x), S.BitVecVal(1 << 200, 256)), g(x) == S.BitVecVal(5, 32),
+             S.ULT(h(x), S.BitVecVal(1 << 40, 64)), S.And(g(x) == S.BitVecVal(9, 32), S.ULT(f(x), S.BitVecVal(100, 256)))]
+    models = []
+    for m in range(400):
+        n = rng.randrange(1, 15)
+        low = rng.choice([3, 0xFFFFFFFF, rng.getrandbits(32)])
+        keys = list({low | (rng.getrandbits(224) << 32 if rng.random() < 0.8 else rng.randrange(4) << 32) for _ in range(n)})
+        rng.shuffle(keys)
+        r = rng.random()
+        xv = keys[-1] if r < 0.5 else (rng.choice(keys) if r < 0.8 else low | (rng.getrandbits(224) << 32))
+        ft = {(k,): rng.choice([7, rng.getrandbits(256), rng.randrange(100)]) for k in keys}
+        gt = {(k,): rng.choice([5, 9, rng.getrandbits(32)]) for k in keys}
+        ht = {(k,): rng.getrandbits(rng.choice([20, 64])) for k in keys}
+        models.append(Model({"x": xv}, {"inv": (ft, rng.choice([0, 7])), "narrow": (gt, rng.choice([0, 5])),
+                                        "mid": (ht, rng.getrandbits(64))}))
+    tb, syms, ok = lower_batch(exprs)
+    assert ok.all()
+    mb = serialize_models(models, syms)
+    evaluator.upload_models(mb)
+    v, fh = evaluator.verdicts(tb)
+    assert (v == cref.verdicts(tb, mb)).all()
+    assert (fh == cref.first_hit(tb, mb)[0]).all()
+    assert 0 < v.mean() < 1
+
+
 # ---------------------------------------------------------------- G kernel: calldata words, signed compares with constants
 def _calldata_word_workload(n_tapes, M, seed):
     """Mythril's symbolic calldata words (laser/ethereum/state/calldata.py: a word is the Concat
