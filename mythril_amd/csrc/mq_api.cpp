@@ -245,6 +245,11 @@ struct mq_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // a column level's kernels are independent of each other (a column reads only lower levels):
+  // the keccak columns run on aux[0], the bit-gather and flat columns on aux[1], next to the
+  // interpreters on the launch stream, forked and joined per level with these events
+  hipStream_t aux[2] = {nullptr, nullptr};
+  hipEvent_t fork_ev = nullptr, join_ev[2] = {nullptr, nullptr};
   bool have_models = false;
   // models
   int64_t M = 0, index_base = 0;
@@ -730,11 +735,18 @@ static int create_one(int dev, mq_ctx** out) {
   auto* c = new mq_ctx();
   c->device = dev;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->aux[0], hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->aux[1], hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->join_ev[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->join_ev[1], hipEventDisableTiming) != hipSuccess) {
     mq_ctx_destroy(c);
     return MQ_ERR_HIP;
   }
   DevPool::get().register_stream(dev, c->stream);
+  DevPool::get().register_stream(dev, c->aux[0]);
+  DevPool::get().register_stream(dev, c->aux[1]);
   if (c->counters.ensure(kCounterBytes) != hipSuccess) {
     mq_ctx_destroy(c);
     return MQ_ERR_NOMEM;
@@ -809,6 +821,15 @@ void mq_ctx_destroy(mq_ctx* c) {
   c->peers.clear();
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (hipStream_t a : c->aux)
+    if (a) {
+      (void)hipStreamSynchronize(a);
+      (void)hipStreamDestroy(a);
+      DevPool::get().unregister_stream(c->device, a);
+    }
+  if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+  for (hipEvent_t e : c->join_ev)
+    if (e) (void)hipEventDestroy(e);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   for (auto& e : c->kev) {
@@ -3796,24 +3817,46 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     for (int g = 0; g < kGen && !bool_rows; g++)
       bool_rows = (g == 0 ? (use_cq ? lv.v[0].count - lv.v8q : lv.v[0].count) : lv.v[g].count) > 0;
   }
+  // MQ_NO_LEVEL_STREAMS=1: every kernel of a level on the launch stream, one after another
+  static const bool level_streams = std::getenv("MQ_NO_LEVEL_STREAMS") == nullptr;
   for (size_t li = 0; li < T->clevels.size(); li++) {
     const auto& lv = T->clevels[li];
-    if (li < T->kc_level.size() && T->kc_level[li].second > 0) {
+    // the level's kernels that run beside the interpreters: keccak columns on aux[0], bit-gather
+    // and flat columns on aux[1], each stream waiting for the level's start on the launch stream
+    // and the launch stream for them before the next level
+    const bool has_kc = li < T->kc_level.size() && T->kc_level[li].second > 0;
+    const bool has_cw = li < T->cw_level.size() && T->cw_level[li].second > 0;
+    const bool has_fc = use_cq && li < T->fc_lvl.size() && T->fc_lvl[li] && T->fc_lvl[li]->count > 0;
+    const bool fork = level_streams && (has_kc || has_cw || has_fc);
+    hipStream_t s_kc = st, s_cf = st;
+    if (fork) {
+      HIPCHK(start_timer());
+      HIPCHK(hipEventRecord(c->fork_ev, st));
+      if (has_kc) {
+        s_kc = c->aux[0];
+        HIPCHK(hipStreamWaitEvent(s_kc, c->fork_ev, 0));
+      }
+      if (has_cw || has_fc) {
+        s_cf = c->aux[1];
+        HIPCHK(hipStreamWaitEvent(s_cf, c->fork_ev, 0));
+      }
+    }
+    if (has_kc) {
       HIPCHK(start_timer());
       HIPCHK(launch_keccak_columns(T->kc_cols_dev.as<KcCol>() + T->kc_level[li].first, T->kc_level[li].second,
                                    T->kc_map_dev.as<KcMapEntry>(), T->kc_pred_dev.as<KcPred>(),
                                    const_cast<uint32_t*>(c->vars.as<uint32_t>()), c->M,
                                    c->counters.as<unsigned long long>(), c->bmasks.as<uint64_t>(), c->n_bmask,
-                                   bool_rows ? 1 : 0, st));
+                                   bool_rows ? 1 : 0, s_kc));
     }
-    if (li < T->cw_level.size() && T->cw_level[li].second > 0) {
+    if (has_cw) {
       HIPCHK(start_timer());
       HIPCHK(launch_cw_columns(T->cw_cols_dev.as<CwCol>() + T->cw_level[li].first, T->cw_level[li].second,
                                T->cw_chunks_dev.as<CwChunk>(), const_cast<uint32_t*>(c->vars.as<uint32_t>()), c->M,
-                               c->counters.as<unsigned long long>(), st));
+                               c->counters.as<unsigned long long>(), s_cf));
     }
     const mq_tapes::Variant v8 = use_cq ? cut_front(lv.v[0], lv.v8q) : lv.v[0];
-    if (use_cq && li < T->fc_lvl.size() && T->fc_lvl[li] && T->fc_lvl[li]->count > 0) {
+    if (has_fc) {
       // the level's flat Bool columns on fca_kernel, mode 3
       const mq_tapes::FcLevel& fl = *T->fc_lvl[li];
       for (const FcaPlanSeg& sg : fl.segs) {
@@ -3843,7 +3886,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
         f.stage_rows = fl.stage.as<uint32_t>() + sg.stage_off;
         f.n_stage = sg.n_stage;
         HIPCHK(start_timer());
-        HIPCHK(launch_fca(f, st));
+        HIPCHK(launch_fca(f, s_cf));
       }
     }
     const int n_gcol = use_cq && li < T->cq_lvl_desc_n.size() ? T->cq_lvl_desc_n[li] : 0;
@@ -3919,6 +3962,16 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       HIPCHK(launch_pack_bool(c->vars.as<uint32_t>(), c->bmasks.as<uint64_t>(), c->bmask_rows.as<uint32_t>(),
                               (use_cq ? T->lvl_bmask_cpp[li] : T->lvl_bmask[li]).as<int32_t>(), (int)pk_h.size(),
                               c->n_bmask, c->M, st));
+    }
+    if (fork) {   // join: the next level (or the tapes) reads this level's columns
+      if (s_kc != st) {
+        HIPCHK(hipEventRecord(c->join_ev[0], s_kc));
+        HIPCHK(hipStreamWaitEvent(st, c->join_ev[0], 0));
+      }
+      if (s_cf != st) {
+        HIPCHK(hipEventRecord(c->join_ev[1], s_cf));
+        HIPCHK(hipStreamWaitEvent(st, c->join_ev[1], 0));
+      }
     }
   }
   for (int k = 0; use_qsa && k < 2; k++) {
