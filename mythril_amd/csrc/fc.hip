@@ -217,25 +217,9 @@ __global__ __launch_bounds__(256) void fc_kernel(const FcTape* __restrict__ tape
 // Then each wave takes chunks of 64 tapes, one tape per lane, and ANDs the tape's list of LDS masks
 // (entries k-major per chunk: one coalesced load per entry) for the FC_TILES tiles.
 
-// x OP c over limbs in registers (x: the variable's limbs; q.f flips the sign bit of a signed
-// compare, c is pre-flipped): lane mask of (accept & (x < c ? 1 : x == c ? 2 : 4))
-__device__ __forceinline__ uint64_t fca_cmp(const uint32_t* x, const FcCmpHead& h, const FcCmp* __restrict__ qp) {
-  const uint64_t x0 = ((uint64_t)(x[1] ^ (uint32_t)(h.f01 >> 32)) << 32) | (x[0] ^ (uint32_t)h.f01);
-  bool lt = x0 < h.c01, eq = x0 == h.c01;
-  if (h.nl > 2) {
-    const FcCmpTail t = qp->t;
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      const uint64_t xv = ((uint64_t)(x[2 * k + 3] ^ t.f[2 * k + 1]) << 32) | (x[2 * k + 2] ^ t.f[2 * k]);
-      const uint64_t c = ((uint64_t)t.c[2 * k + 1] << 32) | t.c[2 * k];
-      lt = xv < c || (xv == c && lt);
-      eq = xv == c && eq;
-    }
-  }
-  const uint32_t bit = lt ? 1u : (eq ? 2u : 4u);
-  return __ballot((h.accept & bit) != 0);
-}
-
+// (MODE: the launch's r.mode as a template parameter, so the first-hit kernel carries none of the
+// verdict / column store code and its loop-invariant addresses)
+template <int MODE>
 __global__ __launch_bounds__(256) void fca_kernel(const FcaGroup* __restrict__ groups, const FcCmp* __restrict__ atoms,
                                                   const uint32_t* __restrict__ lists,
                                                   const uint32_t* __restrict__ chunk_off,
@@ -243,74 +227,81 @@ __global__ __launch_bounds__(256) void fca_kernel(const FcaGroup* __restrict__ g
                                                   const uint32_t* __restrict__ tape_metric,
                                                   const uint32_t* __restrict__ vars,
                                                   const uint64_t* __restrict__ masks_in,
-                                                  const uint32_t* __restrict__ stage_masks,
-                                                  const uint32_t* __restrict__ stage_rows, FcaArgs r) {
-  extern __shared__ uint32_t lds[];
+                                                  const uint32_t* __restrict__ stage_masks, FcaArgs r) {
+  static_assert(FC_TILES == 4, "the table entries are read and written as two 16-byte pairs");
+  // the mask table: entry e of tile j at tab[e * FC_TILES + j] (an entry's four tiles in 32
+  // bytes); entries: 0 all ones, 1 .. n_smask the Bool masks, then the atoms
+  extern __shared__ __align__(16) uint64_t tab[];
   const uint32_t wave = uniform(threadIdx.x >> 6);
   const int64_t tile0 = (int64_t)blockIdx.x * FC_TILES;
   const int64_t m0 = tile0 * 64;
   const int lane = threadIdx.x & 63;
-  {   // the staged rows (LDS row s * FC_TILES + j = slot s of tile j), as fc_kernel: wave w stages tile w's
-    const int j = (int)wave;
-    const int64_t mj = min(m0 + 64 * j + lane, r.M - 1);
-    for (int s0 = 0; s0 < r.n_stage; s0 += 8) {
-      uint32_t v[8];
-#pragma unroll
-      for (int k = 0; k < 8; k++) v[k] = __builtin_nontemporal_load(vars + (int64_t)stage_rows[min(s0 + k, r.n_stage - 1)] * r.M + mj);
-#pragma unroll
-      for (int k = 0; k < 8; k++)
-        if (s0 + k < r.n_stage) lds[((s0 + k) * FC_TILES + j) * 64 + lane] = v[k];
-    }
-  }
-  // the mask tables, tile j's at tab + j * T: all ones, the Bool masks, the atoms
-  uint64_t* tab = reinterpret_cast<uint64_t*>(lds + r.n_stage * FC_TILES * 64);
-  const int T = 1 + r.n_smask + r.n_atoms;
   const int64_t tiles = (r.M + 63) / 64;
   for (int i = (int)threadIdx.x; i < FC_TILES * (1 + r.n_smask); i += 256) {
-    const int j = i / (1 + r.n_smask), k = i - j * (1 + r.n_smask);
+    const int k = i / FC_TILES, j = i - k * FC_TILES;
     const int64_t tj = min(tile0 + j, tiles - 1);
-    tab[j * T + k] = k == 0 ? ~0ull : masks_in[tj * (int64_t)r.n_bool_masks + stage_masks[k - 1]];
+    tab[i] = k == 0 ? ~0ull : masks_in[tj * (int64_t)r.n_bool_masks + stage_masks[k - 1]];
   }
-  // phase 1: the atoms, a variable group at a time (wave w: groups w, w + 4, ...)
+  // phase 1: the atoms, a variable group at a time (wave w: groups w, w + 4, ...).  A compare's
+  // lane masks are two VALU compares of 64-bit limb pairs into SGPR masks a tile; the accept
+  // (canonical: 1 x < c, 2 x == c, 3 x <= c) selects them on the scalar unit; lane 0 stores the
+  // atom's four tiles as two 16-byte LDS writes
   int64_t mj[FC_TILES];
 #pragma unroll
   for (int j = 0; j < FC_TILES; j++) mj[j] = min(m0 + 64 * j + lane, r.M - 1);
-  __syncthreads();   // (the staged rows)
+  const int abase = 1 + r.n_smask;
   for (int g = (int)wave; g < r.n_groups; g += 4) {
     const FcaGroup G = groups[g];
-    uint32_t x[FC_TILES][8];
-    if (G.slot != ~0u) {   // staged: limb l of tile j at LDS row (slot + l) * FC_TILES + j
-      const int nread = G.nl <= 2 ? 2 : 8;
+    if (G.nl <= 2) {
+      uint64_t x[FC_TILES];
 #pragma unroll
       for (int j = 0; j < FC_TILES; j++)
+        x[j] = ((uint64_t)vars[(int64_t)G.rows[1] * r.M + mj[j]] << 32) | vars[(int64_t)G.rows[0] * r.M + mj[j]];
+      for (uint32_t a = G.first; a < G.first + G.count; a++) {
+        const FcCmpHead h = atoms[a].h;
+        uint64_t m[FC_TILES];
 #pragma unroll
-        for (int l = 0; l < 8; l++) x[j][l] = l < nread ? lds[((G.slot + l) * FC_TILES + j) * 64 + lane] : 0u;
-    } else if (G.nl <= 2) {
-#pragma unroll
-      for (int j = 0; j < FC_TILES; j++) {
-        x[j][0] = vars[(int64_t)G.rows[0] * r.M + mj[j]];
-        x[j][1] = vars[(int64_t)G.rows[1] * r.M + mj[j]];
-#pragma unroll
-        for (int l = 2; l < 8; l++) x[j][l] = 0;
+        for (int j = 0; j < FC_TILES; j++) {
+          const uint64_t xv = x[j] ^ h.f01;
+          const uint64_t lt = __ballot(xv < h.c01), eq = __ballot(xv == h.c01);
+          m[j] = ((h.accept & 1u) ? lt : 0ull) | ((h.accept & 2u) ? eq : 0ull);
+        }
+        if (lane == 0) {
+          ulonglong2* p = reinterpret_cast<ulonglong2*>(tab + (abase + (int)a) * FC_TILES);
+          p[0] = make_ulonglong2(m[0], m[1]);
+          p[1] = make_ulonglong2(m[2], m[3]);
+        }
       }
     } else {
+      uint32_t x[FC_TILES][8];
 #pragma unroll
       for (int j = 0; j < FC_TILES; j++)
 #pragma unroll
         for (int l = 0; l < 8; l++) x[j][l] = vars[(int64_t)G.rows[l] * r.M + mj[j]];
-    }
-    // (the next atom's head is requested before this one is compared: one scalar round trip
-    // per group, not per atom)
-    FcCmpHead h = atoms[G.first].h;
-    for (uint32_t a = G.first; a < G.first + G.count; a++) {
-      const FcCmp* qp = atoms + a;
-      const FcCmpHead hn = atoms[min(a + 1, G.first + G.count - 1)].h;
+      for (uint32_t a = G.first; a < G.first + G.count; a++) {
+        const FcCmpHead h = atoms[a].h;
+        const FcCmpTail t = atoms[a].t;
+        uint64_t m[FC_TILES];
 #pragma unroll
-      for (int j = 0; j < FC_TILES; j++) {
-        const uint64_t m = fca_cmp(x[j], h, qp);
-        if (lane == 0) tab[j * T + 1 + r.n_smask + a] = m;
+        for (int j = 0; j < FC_TILES; j++) {
+          const uint64_t x0 = (((uint64_t)x[j][1] << 32) | x[j][0]) ^ h.f01;
+          bool lt = x0 < h.c01, eq = x0 == h.c01;
+#pragma unroll
+          for (int k = 0; k < 3; k++) {   // limbs 2-3, 4-5, 6-7: each pair above the ones before
+            const uint64_t xv = ((uint64_t)(x[j][2 * k + 3] ^ t.f[2 * k + 1]) << 32) | (x[j][2 * k + 2] ^ t.f[2 * k]);
+            const uint64_t c = ((uint64_t)t.c[2 * k + 1] << 32) | t.c[2 * k];
+            lt = xv < c || (xv == c && lt);
+            eq = xv == c && eq;
+          }
+          const uint64_t lm = __ballot(lt), em = __ballot(eq);
+          m[j] = ((h.accept & 1u) ? lm : 0ull) | ((h.accept & 2u) ? em : 0ull);
+        }
+        if (lane == 0) {
+          ulonglong2* p = reinterpret_cast<ulonglong2*>(tab + (abase + (int)a) * FC_TILES);
+          p[0] = make_ulonglong2(m[0], m[1]);
+          p[1] = make_ulonglong2(m[2], m[3]);
+        }
       }
-      h = hn;
     }
   }
   __syncthreads();
@@ -330,7 +321,7 @@ __global__ __launch_bounds__(256) void fca_kernel(const FcaGroup* __restrict__ g
     const uint32_t out = live ? tape_out[t] : 0u;
     const uint32_t row = out & 0x7FFFFFFFu;
     bool run = live;
-    if (run && r.mode == 0 && r.early_exit) run = first0 < r.best[row];   // (best[] only decreases)
+    if (run && MODE == 0 && r.early_exit) run = first0 < r.best[row];   // (best[] only decreases)
     const uint32_t o0 = chunk_off[c], kmax = (chunk_off[c + 1] - o0) / 64u;
     uint64_t acc[FC_TILES];
 #pragma unroll
@@ -340,8 +331,12 @@ __global__ __launch_bounds__(256) void fca_kernel(const FcaGroup* __restrict__ g
       const uint32_t e = lp[64u * k];
       const uint32_t idx = e & 0x7FFFFFFFu;
       const uint64_t neg = (e >> 31) ? ~0ull : 0ull;
-#pragma unroll
-      for (int j = 0; j < FC_TILES; j++) acc[j] &= tab[j * T + idx] ^ neg;
+      const ulonglong2* p = reinterpret_cast<const ulonglong2*>(tab + idx * FC_TILES);
+      const ulonglong2 q0 = p[0], q1 = p[1];
+      acc[0] &= q0.x ^ neg;
+      acc[1] &= q0.y ^ neg;
+      acc[2] &= q1.x ^ neg;
+      acc[3] &= q1.y ^ neg;
     }
     if (out >> 31) {   // a negated conjunction (an OR of atoms)
 #pragma unroll
@@ -351,7 +346,7 @@ __global__ __launch_bounds__(256) void fca_kernel(const FcaGroup* __restrict__ g
       runs++;
       run_nodes += tape_metric[2 * t];
       run_ops += tape_metric[2 * t + 1];
-      if (r.mode == 3) {
+      if (MODE == 3) {
         // a Bool column: its tiles' lane masks, and its 0/1 row where a HIP C++ kernel reads rows
         // or it has no mask index (one lane per column: these row stores do not coalesce; the
         // assembly-only launches C4 / C3 / C5 make need none)
@@ -366,7 +361,7 @@ __global__ __launch_bounds__(256) void fca_kernel(const FcaGroup* __restrict__ g
             for (int q = 0; q < lim; q++) r.vars_out[(int64_t)row * r.M + mt + q] = (uint32_t)((acc[j] >> q) & 1u);
           }
         }
-      } else if (r.mode == 0) {
+      } else if (MODE == 0) {
 #pragma unroll
         for (int j = 0; j < FC_TILES; j++)
           if (acc[j]) {   // the lowest tile with a hit has the lowest model
@@ -406,7 +401,7 @@ __global__ __launch_bounds__(256) void fca_kernel(const FcaGroup* __restrict__ g
     }
     if (lane == 0 && runs) {
       unsigned long long* cnt = r.counters + ((blockIdx.x * 4 + wave) % kCounterSlots) * kCounterStride;
-      if (r.mode != 3) atomicAdd(&cnt[0], runs * nv);   // (tape evaluations; a column is not one)
+      if (MODE != 3) atomicAdd(&cnt[0], runs * nv);   // (tape evaluations; a column is not one)
       atomicAdd(&cnt[1], run_nodes * nv);
       atomicAdd(&cnt[2], run_ops * nv);
     }
@@ -417,9 +412,18 @@ hipError_t launch_fca(const FcaArgs& a, hipStream_t st) {
   if (a.n <= 0 || a.M <= 0) return hipSuccess;
   const int64_t groups = (a.M + 64 * FC_TILES - 1) / (64 * FC_TILES);
   if (groups > 0x7FFFFFFF) return hipErrorInvalidValue;
-  const size_t lds = (size_t)a.n_stage * 256u * FC_TILES + (size_t)(1 + a.n_smask + a.n_atoms) * 8u * FC_TILES;
-  hipLaunchKernelGGL(fca_kernel, dim3((unsigned)groups), dim3(256), lds, st, a.groups, a.atoms, a.lists, a.chunk_off,
-                     a.tape_out, a.tape_metric, a.vars, a.bool_masks, a.stage_masks, a.stage_rows, a);
+  const size_t lds = (size_t)(1 + a.n_smask + a.n_atoms) * 8u * FC_TILES;
+  if (a.mode == 0)
+    hipLaunchKernelGGL(fca_kernel<0>, dim3((unsigned)groups), dim3(256), lds, st, a.groups, a.atoms, a.lists,
+                       a.chunk_off, a.tape_out, a.tape_metric, a.vars, a.bool_masks, a.stage_masks, a);
+  else if (a.mode == 1)
+    hipLaunchKernelGGL(fca_kernel<1>, dim3((unsigned)groups), dim3(256), lds, st, a.groups, a.atoms, a.lists,
+                       a.chunk_off, a.tape_out, a.tape_metric, a.vars, a.bool_masks, a.stage_masks, a);
+  else if (a.mode == 3)
+    hipLaunchKernelGGL(fca_kernel<3>, dim3((unsigned)groups), dim3(256), lds, st, a.groups, a.atoms, a.lists,
+                       a.chunk_off, a.tape_out, a.tape_metric, a.vars, a.bool_masks, a.stage_masks, a);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

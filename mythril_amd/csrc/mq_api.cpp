@@ -312,7 +312,7 @@ struct mq_ctx {
 };
 
 struct FcaPlanSeg {   // one fca_kernel launch (fca_plan)
-  int atom_off, n_atoms, group_off, n_groups, tape_first, n_tapes, chunk_first, smask_off, n_smask, stage_off, n_stage;
+  int atom_off, n_atoms, group_off, n_groups, tape_first, n_tapes, chunk_first, smask_off, n_smask;
 };
 
 struct mq_tapes {
@@ -453,7 +453,7 @@ struct mq_tapes {
   struct FcLevel {   // fca_kernel mode 3 (fca_plan per level)
     int count = 0;
     std::vector<FcaPlanSeg> segs;
-    DevBuf atoms, groups, lists, chunk, out, metric, smask, stage, colmask;
+    DevBuf atoms, groups, lists, chunk, out, metric, smask, colmask;
   };
   std::vector<std::unique_ptr<FcLevel>> fc_lvl;
   std::vector<int> cq_lvl_desc_off, cq_lvl_desc_n;
@@ -2979,7 +2979,7 @@ static void fc_plan(const mq_ctx* c, const std::vector<std::vector<uint32_t>>& f
 struct FcaPlan {
   std::vector<FcCmp> atoms;
   std::vector<FcaGroup> groups;
-  std::vector<uint32_t> lists, chunk_off, tape_out, metric, stage_masks, stage_rows;
+  std::vector<uint32_t> lists, chunk_off, tape_out, metric, stage_masks;
   std::vector<int32_t> col_mask;   // (columns: per kept column its lane-mask index)
   std::vector<FcaPlanSeg> segs;
 };
@@ -3022,28 +3022,7 @@ static void fca_plan(const mq_ctx* c, const std::vector<std::vector<uint32_t>>& 
     sg.chunk_first = (int)P.chunk_off.size() - 1;
     sg.smask_off = (int)P.stage_masks.size();
     sg.n_smask = (int)masks.size();
-    // the variables the most atoms read are staged in LDS (kFcStageRows rows: 2 for a variable
-    // of <= 2 limbs, else 8; the zero row past its limbs); the others are read from the rows
-    std::map<std::pair<uint32_t, uint32_t>, int64_t> use;
-    for (const auto& key : akeys) use[{key[0], key[1]}]++;
-    std::vector<std::pair<int64_t, std::pair<uint32_t, uint32_t>>> byu;
-    for (const auto& kv : use) byu.push_back({kv.second, kv.first});
-    std::stable_sort(byu.begin(), byu.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
-    std::map<std::pair<uint32_t, uint32_t>, uint32_t> slot_of;
-    sg.stage_off = (int)P.stage_rows.size();
-    uint32_t nst = 0;
-    static const uint32_t stage_budget = [] {
-      const char* e = std::getenv("MQ_FCA_STAGE_ROWS");
-      return e ? (uint32_t)std::atoi(e) : 0u;   // (none: C4 fca 252 us with 40 rows, 196 without -- occupancy)
-    }();
-    for (const auto& u : byu) {
-      const uint32_t nl = u.second.second, width = nl <= 2 ? 2 : 8;
-      if (nst + width > stage_budget) continue;
-      slot_of[u.second] = nst;
-      for (uint32_t l = 0; l < width; l++) P.stage_rows.push_back(l < nl ? u.second.first + l : zero_row);
-      nst += width;
-    }
-    sg.n_stage = (int)nst;
+
     // atoms ordered by (variable row, limbs): groups
     std::vector<uint32_t> ord(akeys.size());
     for (size_t i = 0; i < ord.size(); i++) ord[i] = (uint32_t)i;
@@ -3067,8 +3046,6 @@ static void fca_plan(const mq_ctx* c, const std::vector<std::vector<uint32_t>>& 
         for (uint32_t l = 0; l < 8; l++) g.rows[l] = l < nl ? key[0] + l : zero_row;
         g.first = (uint32_t)r;
         g.nl = nl;
-        auto sl = slot_of.find({key[0], nl});
-        g.slot = sl == slot_of.end() ? ~0u : sl->second;
         P.groups.push_back(g);
       }
       P.groups.back().count++;
@@ -3351,8 +3328,6 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
       HIPCHK(T->fca_out_dev.upload(fap.tape_out.data(), fap.tape_out.size(), c->stream));
       HIPCHK(T->fca_metric_dev.upload(fap.metric.data(), fap.metric.size(), c->stream));
       HIPCHK(T->fc_smask_dev.upload(fap.stage_masks.data(), fap.stage_masks.size(), c->stream));
-      if (fap.stage_rows.empty()) fap.stage_rows.push_back(0);
-      HIPCHK(T->fc_stage_dev.upload(fap.stage_rows.data(), fap.stage_rows.size(), c->stream));
     }
   } else {
     T->fc_count = (int)fcp.tapes.size();
@@ -3481,7 +3456,6 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
     fl.segs = fap.segs;
     if (fl.count > 0) {
       if (fap.stage_masks.empty()) fap.stage_masks.push_back(0);
-      if (fap.stage_rows.empty()) fap.stage_rows.push_back(0);
       if (fap.atoms.empty()) fap.atoms.push_back(FcCmp{});
       if (fap.groups.empty()) fap.groups.push_back(FcaGroup{});
       if (fap.lists.empty()) fap.lists.push_back(0);
@@ -3492,7 +3466,6 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
       HIPCHK(fl.out.upload(fap.tape_out.data(), fap.tape_out.size(), c->stream));
       HIPCHK(fl.metric.upload(fap.metric.data(), fap.metric.size(), c->stream));
       HIPCHK(fl.smask.upload(fap.stage_masks.data(), fap.stage_masks.size(), c->stream));
-      HIPCHK(fl.stage.upload(fap.stage_rows.data(), fap.stage_rows.size(), c->stream));
       HIPCHK(fl.colmask.upload(fap.col_mask.data(), fap.col_mask.size(), c->stream));
     }
     std::vector<int> rest;   // the level's columns left to G
@@ -3883,8 +3856,6 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
         f.counters = c->counters.as<unsigned long long>();
         f.stage_masks = fl.smask.as<uint32_t>() + sg.smask_off;
         f.n_smask = sg.n_smask;
-        f.stage_rows = fl.stage.as<uint32_t>() + sg.stage_off;
-        f.n_stage = sg.n_stage;
         HIPCHK(start_timer());
         HIPCHK(launch_fca(f, s_cf));
       }
@@ -4062,8 +4033,6 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     f.counters = c->counters.as<unsigned long long>();
     f.stage_masks = T->fc_smask_dev.as<uint32_t>() + sg.smask_off;
     f.n_smask = sg.n_smask;
-    f.stage_rows = T->fc_stage_dev.as<uint32_t>() + sg.stage_off;
-    f.n_stage = sg.n_stage;
     HIPCHK(start_timer());
     HIPCHK(launch_fca(f, st));
   }

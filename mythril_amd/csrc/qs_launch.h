@@ -261,7 +261,7 @@ struct FcaGroup {
   uint32_t first;     // its atoms: atoms[first .. first + count)
   uint32_t count;
   uint32_t nl;
-  uint32_t slot;      // its limbs' LDS slot (staged rows, as fc_kernel's), or ~0u: read from vars
+  uint32_t pad;
 };
 struct FcaArgs {
   int n;                          // tapes
@@ -289,8 +289,6 @@ struct FcaArgs {
   int bool_rows;                  // mode 3: also write the 0/1 row of a column with a mask index
   const uint32_t* stage_masks;    // the Bool mask indices of table entries 1 .. n_smask
   int n_smask;
-  const uint32_t* stage_rows;     // variable rows staged in LDS per workgroup (FcaGroup.slot)
-  int n_stage;
 };
 hipError_t launch_fca(const FcaArgs& a, hipStream_t st);
 

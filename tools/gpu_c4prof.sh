@@ -18,7 +18,7 @@ import json, sys
 d = json.load(open(sys.argv[1]))
 ld = d["last_dispatches"]
 i = max(k for k, x in enumerate(ld) if x["kernel"] == "mq::qs_init_best")
-print(" ".join(f"{x['kernel'].split('::')[-1][:14]}:{x['ns']/1e3:.0f}" for x in ld[i:] if x["kernel"].startswith("mq::")))
+print(" ".join(f"{x['kernel'].split('mq::')[-1][:14]}:{x['ns']/1e3:.0f}" for x in ld[i:] if "mq::" in x["kernel"]))
 PY
 timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_LDS SQ_BUSY_CYCLES SQ_WAVES -d /tmp/sq -o run -- python3 "$R/bench.py" --config $CFG --steps 1 --warmup 1 --no-cpu-baseline --no-dropin > "$OUT/sq.log" 2>&1 || exit 6
 db=$(find /tmp/sq -name '*.db' | head -1); python3 "$R/tools/rocpd_summary.py" "$OUT/sq_$CFG.json" "pmc=$db" > /dev/null; rm -rf /tmp/sq

@@ -19,7 +19,7 @@ b = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
 ld = d["last_dispatches"]
 i = max(k for k, x in enumerate(ld) if x["kernel"] == "mq::qs_init_best")
 print(sys.argv[3], round(b["ms_per_step"], 3), b.get("parity_ok"),
-      " ".join(f"{x['kernel'].split('::')[-1][:6]}:{x['ns']/1e3:.0f}" for x in ld[i:] if x["kernel"].startswith("mq::")))
+      " ".join(f"{x['kernel'].split('mq::')[-1][:6]}:{x['ns']/1e3:.0f}" for x in ld[i:] if "mq::" in x["kernel"]))
 PY
 done
 rm -rf /tmp/kt
