@@ -204,6 +204,14 @@ def load_window(first, pfx=None):
     lane4 = LANE4 or "v5"
     out = [] if LANE4 else ["v_mbcnt_lo_u32_b32 v5, -1, 0", "v_mbcnt_hi_u32_b32 v5, -1, v5", "v_lshlrev_b32 v5, 2, v5"]
     if first:
+        # A program may start inside a block (column programs are packed back to back,
+        # mq_api.cpp qsa_pack_program): s16 = its word offset, s[36:37] = the block.  A program
+        # starting in the current window needs no load: the window is decoded already.
+        out += ["s_and_b32 s16, s36, 0xff",
+                "s_lshr_b32 s16, s16, 2",
+                "s_andn2_b32 s36, s36, 0xff",
+                "s_cmp_eq_u64 s[36:37], s[14:15]"] + (["s_cselect_b32 s39, 1, 0"] if PROF else []) + [
+                f"s_cbranch_scc1 {pfx}_wsame{k}"]
         # the prefetched window was issued before the previous tape's stores (s59 of them, column
         # rows / a verdict byte / a hit's atomic): wait for it, not for them (vector memory
         # operations complete in order)
@@ -228,12 +236,16 @@ def load_window(first, pfx=None):
     else:
         out += ["s_add_u32 s14, s14, 256", "s_addc_u32 s15, s15, 0", "s_waitcnt vmcnt(0)"]
     out += [f"v_mov_b32 {WIN}, {NWIN}",
-            f"global_load_dword {NWIN}, {lane4}, s[14:15] offset:256",
-            "s_mov_b32 s16, 0",
-            f"v_and_b32 v5, 0xffff, {WIN}",
+            f"global_load_dword {NWIN}, {lane4}, s[14:15] offset:256"]
+    out += [] if first else ["s_mov_b32 s16, 0"]
+    out += [f"v_and_b32 v5, 0xffff, {WIN}",
             f"v_lshl_add_u32 {WINA}, v5, {3 if PROF else 2}, s12",
             f"v_lshrrev_b32 {WINI}, 16, {WIN}",
             "s_nop 1"]                      # VALU VGPR write -> v_readlane of it
+    if first:
+        # (the same-window path wrote s16 a few SALU instructions ago: an SGPR a SALU wrote is
+        # read as v_readlane's lane select only after 4 wait states)
+        out += [f"s_branch {pfx}_wdone{k}", f"{pfx}_wsame{k}:", "s_nop 3", f"{pfx}_wdone{k}:"]
     return out
 
 

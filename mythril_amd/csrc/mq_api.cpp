@@ -2672,6 +2672,37 @@ static void qsa_window_layout(const mq_ctx* c, std::vector<uint32_t>& prog) {
   prog.swap(out);
 }
 
+// Column programs are short (C3: ~6 nodes): padding each to whole 64-word blocks made every column
+// start with a window load, a memory round trip per column program (the G profile charged it to
+// FRAME3: ~20 % of C3's cycles).  They are packed back to back instead: a program starts at the
+// next word (or, when its first handler group would not fit the block, at the next block), the
+// REFILL rule of qsa_window_layout applies inside it, and the kernel starts a program that lies in
+// its current window without a load (gen_qsa.py load_window).  Returns the program's word offset;
+// pos = the next word's position in its block.
+static uint32_t qsa_pack_program(const mq_ctx* c, std::vector<uint32_t>& out, size_t& pos,
+                                 const std::vector<uint32_t>& prog) {
+  const std::vector<uint8_t>& data_words = c->qsa_data_words;
+  const uint32_t refill = hword(1, c->qsa_off[1][c->qsa_index[1][QK_REFILL][0][0]]);
+  const uint32_t endw = hword(1, c->qsa_off[1][c->qsa_index[1][QK_END][0][0]]);
+  if (!prog.empty() && pos + 1 + (size_t)data_words[prog[0] & 0xFFFFu] > 63) {
+    out.insert(out.end(), 64 - pos, endw);
+    pos = 0;
+  }
+  const uint32_t start = (uint32_t)out.size();
+  for (size_t i = 0; i < prog.size();) {
+    const size_t g = 1 + (size_t)data_words[prog[i] & 0xFFFFu];
+    if (pos + g > 63) {
+      out.push_back(refill);
+      out.insert(out.end(), 63 - pos, endw);
+      pos = 0;
+    }
+    for (size_t j = 0; j < g && i + j < prog.size(); j++) out.push_back(prog[i + j]);
+    pos += g;
+    i += g;
+  }
+  return start;
+}
+
 // Push counts of the variables (<= 256 bits) a set of compiled programs reads.
 static std::vector<int64_t> count_pushes(const mq_ctx* c, const std::vector<CompiledTape>& cts,
                                          const std::vector<char>* skip = nullptr) {
@@ -3285,6 +3316,9 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
   std::vector<uint32_t> prog;
   std::vector<GDesc> descs;
   for (int k = 0; k < 2; k++) {
+    // G's program windows are the buffer's aligned 64-word blocks (gen_qsa.py load_window rounds
+    // a program's address down to its block): G's programs start at a block boundary
+    if (k == 1) prog.resize((prog.size() + 63) / 64 * 64, 0);
     const uint32_t base = (uint32_t)prog.size();
     for (GDesc d : ds[k]) {
       d.prog_off += base;
@@ -3411,6 +3445,10 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
   if (T->cq_ct.empty()) return MQ_OK;
   std::vector<uint32_t> prog, consts, tr, extra;
   std::vector<GDesc> descs;
+  // column programs packed back to back (qsa_pack_program; MQ_G_COL_BLOCKS=1: each padded to
+  // whole blocks, as tape programs are)
+  const bool pack_block = std::getenv("MQ_G_COL_BLOCKS") != nullptr;
+  size_t pack_pos = 0;
   // one LDS staging plan per column level: a level's launch stages only the rows its own
   // programs push (one plan for all levels made every level stage every level's rows)
   T->cq_stage_rows.clear();
@@ -3496,12 +3534,11 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
     for (int i : rest) {
       const CompiledTape& x = T->cq_ct[i];
       if (!qsa_translate(c, 1, true, x, &tr, &extra, nullptr, &gstage)) return MQ_OK;
-      qsa_window_layout(c, tr);
       qsa_count(c, 1, tr, T->qhist[2], nullptr);
       const int v = T->cq_var[i];
       GDesc d{};
-      d.prog_off = (uint32_t)prog.size();
       d.prog_len = (uint32_t)tr.size();
+      d.prog_off = pack_block ? (qsa_window_layout(c, tr), (uint32_t)prog.size()) : qsa_pack_program(c, prog, pack_pos, tr);
       d.tape = c->var_off_h[v];
       d.const_base = (uint32_t)consts.size();
       d.n_nodes = x.n_nodes;
@@ -3509,13 +3546,14 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
       // Bool root: bit 0, and the packed lane-mask index + 1 above it (store_column)
       d.depth = T->cq_bool[i] ? 1u | ((uint32_t)(v < (int)c->bmask_of_var.size() ? c->bmask_of_var[v] + 1 : 0) << 1) : 0u;
       d.alg_ops = (uint32_t)std::min(x.alg_ops, 4.0e9);
-      prog.insert(prog.end(), tr.begin(), tr.end());
+      if (pack_block) prog.insert(prog.end(), tr.begin(), tr.end());
       consts.insert(consts.end(), x.consts.begin(), x.consts.end());
       consts.insert(consts.end(), extra.begin(), extra.end());
       descs.push_back(d);
     }
   }
   const uint32_t endw = hword(1, c->qsa_off[1][c->qsa_index[1][QK_END][0][0]]);
+  if (pack_pos) prog.insert(prog.end(), 64 - pack_pos, endw);   // (whole blocks)
   prog.insert(prog.end(), 130, endw);   // the window + next-window prefetch read up to 127 words past the last END
   consts.resize(consts.size() + 16, 0);
   HIPCHK(T->cqdescs.upload(descs.data(), descs.size(), c->stream));
