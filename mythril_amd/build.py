@@ -65,6 +65,22 @@ def _generated_current() -> bool:
     return True
 
 
+def build_lowerwalk(force: bool = False) -> str:
+    """The drop-in lowering's term walk (csrc/lowerwalk.cpp), a CPython extension built with the
+    host compiler next to this file (lower.py imports it)."""
+    import sysconfig
+    src = os.path.join(CSRC, "lowerwalk.cpp")
+    out = os.path.join(HERE, "_lowerwalk" + sysconfig.get_config_var("EXT_SUFFIX"))
+    if force or not os.path.exists(out) or os.path.getmtime(out) < os.path.getmtime(src):
+        cmd = [os.environ.get("CXX", "g++"), "-O2", "-shared", "-fPIC", "-std=c++17", "-Wall",
+               f"-I{sysconfig.get_paths()['include']}", src, "-o", out]
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode:
+            sys.stderr.write(res.stderr)
+            raise RuntimeError("lowerwalk build failed")
+    return out
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     hipcc = _hipcc()
     if force or not _generated_current():
@@ -92,6 +108,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if res.returncode:
             sys.stderr.write(res.stderr)
             raise RuntimeError("link failed")
+    build_lowerwalk(force)
     tool = os.path.join(HERE, "valu_peak")
     tsrc = os.path.join(CSRC, "valu_peak.hip")
     if force or not os.path.exists(tool) or os.path.getmtime(tool) < os.path.getmtime(tsrc):

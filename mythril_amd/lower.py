@@ -691,6 +691,26 @@ _FAST_BIN = {k: int(getattr(Op, name.upper())) for k, name in _BIN.items()}
 _FAST_PRED = {S.EQ: int(Op.EQ), S.BVULT: int(Op.ULT), S.BVULE: int(Op.ULE), S.BVSLT: int(Op.SLT),
               S.BVSLE: int(Op.SLE)}
 _OP_CONST, _OP_NOT = int(Op.CONST), int(Op.NOT)
+# the same kinds for csrc/lowerwalk.cpp: 1 VAL, 2 NOT, 3 binary BV op, 4 BV predicate
+_KIND_CODE = {S.VAL: 1, S.NOT: 2, **{k: 3 for k in _FAST_BIN}, **{k: 4 for k in _FAST_PRED}}
+_WALKER = []
+
+
+def _walker():
+    """The C++ term walk (csrc/lowerwalk.cpp, built by build.py next to this file).  Required:
+    MQ_PY_LOWER=1 selects the Python loop of IncrementalLowering._lower instead (the tests
+    compare the two)."""
+    if os.environ.get("MQ_PY_LOWER") == "1":
+        return None
+    if not _WALKER:
+        try:
+            from . import _lowerwalk
+        except ImportError as e:
+            raise ImportError("mythril_amd._lowerwalk is not built (python -m mythril_amd.build); "
+                              "MQ_PY_LOWER=1 runs the Python lowering walk instead") from e
+        _lowerwalk.bind(S.Term)
+        _WALKER.append(_lowerwalk)
+    return _WALKER[0]
 
 
 def lower_batch(roots: Sequence[S.Term], syms: Optional[SymbolTable] = None, hoist: bool = False,
@@ -990,10 +1010,14 @@ class IncrementalLowering:
             grow[:self._np_n] = self._np_nodes[:self._np_n]
             self._np_nodes = grow
         if n > self._np_n:
-            tail = np.array(self.tape.nodes[self._np_n:n], dtype=np.uint64).reshape(-1, 5)
-            blk = self._np_nodes[self._np_n:n]
-            for j, fld in enumerate(("op", "width", "a", "b", "c")):
-                blk[fld] = tail[:, j]
+            walker = _walker()
+            if walker is not None:
+                walker.pack_nodes(self.tape.nodes, self._np_n, n, self._np_nodes[self._np_n:n])
+            else:
+                tail = np.array(self.tape.nodes[self._np_n:n], dtype=np.uint64).reshape(-1, 5)
+                blk = self._np_nodes[self._np_n:n]
+                for j, fld in enumerate(("op", "width", "a", "b", "c")):
+                    blk[fld] = tail[:, j]
             self._np_n = n
         if nc > self._np_consts.size:
             grow = np.zeros(max(nc, 2 * self._np_consts.size), np.uint32)
@@ -1012,6 +1036,23 @@ class IncrementalLowering:
         offs, flat = [0], []
         ok = np.ones(len(roots), bool)
         false_node = None
+        walker = _walker()
+        if walker is not None:
+            # csrc/lowerwalk.cpp: the same walk (same nodes, numbering, memo and bad-root records)
+            tp = self.tape
+            state = (self._node, self._keep, self._bad, tp.nodes, tp.kind, tp._memo, tp._const_memo, tp.consts,
+                     _KIND_CODE, _FAST_BIN, _FAST_PRED, _lower_one, to_words, tp, self.syms, LoweringError,
+                     SortError, S.AND, S.EQ, "bv", "bool", _OP_CONST, _OP_NOT, MAX_WIDTH, tp.false)
+            for i, ids in enumerate(walker.lower_roots(roots, state)):
+                if isinstance(ids, BaseException):
+                    note_fail_closed(ids)
+                    ok[i] = False
+                    if false_node is None:
+                        false_node = self.tape.false()
+                    ids = [false_node]
+                flat.extend(ids)
+                offs.append(len(flat))
+            roots = ()
         for i, r in enumerate(roots):
             if r.sort != "bool":
                 raise LoweringError("quick-sat root must be Bool")

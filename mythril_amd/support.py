@@ -560,6 +560,12 @@ class ModelCache:
 
     def _slots_of(self, models) -> np.ndarray:
         slot, keep = self._slot, self._slot_model
+        try:
+            # every model seen before (the LRU reordered after a hit): keep holds each model with
+            # a slot alive, so no other object can carry its id
+            return np.fromiter(map(slot.__getitem__, map(id, models)), np.int64, len(models))
+        except KeyError:
+            pass
         out = np.empty(len(models), np.int64)
         for i, m in enumerate(models):
             s = slot.get(id(m))

@@ -187,6 +187,46 @@ def test_incremental_lowering_shares_the_dag_across_queries():
     assert len(db2.nodes) == n                # nothing new to lower
 
 
+def test_native_lowering_walk_matches_the_python_walk(monkeypatch):
+    """csrc/lowerwalk.cpp (the product's term walk) builds the same DAG as the Python loop of
+    IncrementalLowering (MQ_PY_LOWER=1): node table, numbering, constant pool, roots, the
+    supported mask and the fail-closed reasons — over fresh and repeated EVM-shaped batches,
+    queries with conjuncts outside the vocabulary (also met again), width mismatches, negated
+    compares, wide equalities and deep chains."""
+    from mythril_amd import exceptions
+    from mythril_amd.lower import IncrementalLowering
+    from mythril_amd.synth_evm import dropin_workload
+    g = S.Function("g", [8, 8, 8], 8)
+    v, x, y = S.BitVecSym("v", 8), S.BitVecSym("x", 256), S.BitVecSym("y", 512)
+    deep = x
+    for i in range(3000):
+        deep = deep + (i & 7)
+    odd = [S.And(v == 3, g(v, v, v) == 0), S.And(S.Not(S.ULT(x, S.BitVecVal(5, 256))), x == 7), S.And(y == 9, S.UGT(y, S.BitVecVal(1, 512))),
+           deep == 17, S.And(v == 3, g(v, v, v) == 0, S.BitVecVal(3, 8) == v), S.And(S.Not(S.Not(x == 1)))]
+    batches = [dropin_workload(48, 20, seed=5)[0], odd, dropin_workload(48, 20, seed=5, query_seed=1)[0],
+               dropin_workload(48, 20, seed=5)[0][:7] + odd[::-1]]
+    # a width mismatch raised by the sort check of a fast kind: (bypasses the smt constructors)
+    bad = S.Term(S.EQ, "bool", 0, (S.BitVecSym("p", 8), S.BitVecSym("q", 16)))
+    batches.append([bad, x == 2])
+    runs = []
+    for py in ("1", "0"):
+        monkeypatch.setenv("MQ_PY_LOWER", py)
+        exceptions.fail_closed.clear()
+        inc = IncrementalLowering()
+        out = []
+        for b in batches:
+            db, ok = inc.lower(b)
+            out.append((db.nodes.copy(), db.consts.copy(), db.roots.copy(), db.root_offsets.copy(), ok.copy()))
+        runs.append((out, sorted((str(r), m) for r, m in inc._bad.values()), dict(exceptions.fail_closed)))
+    (a, bad_a, fc_a), (b, bad_b, fc_b) = runs
+    for x1, x2 in zip(a, b):
+        for f1, f2 in zip(x1, x2):
+            assert np.array_equal(f1, f2)
+    assert bad_a == bad_b and len(bad_a) >= 2
+    assert fc_a == fc_b
+    assert not a[1][4].all() and not a[4][4][0] and a[4][4][1]
+
+
 def test_incremental_serialization_matches_whole_batch_serialization():
     """IncrementalLowering.serialize (rows and function tables cached per model slot, built as
     byte strings) == serialize_models (the whole-batch form), also after the symbol table grows
