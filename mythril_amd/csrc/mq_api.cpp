@@ -1809,8 +1809,10 @@ static bool qsa_translate(const mq_ctx* c, int k, bool models, const CompiledTap
   return x.consts.size() + extra.size() <= 0x10000u;
 }
 
-// Upload a compiled batch to ONE device.
-static int tapes_upload_one(mq_ctx* c, int32_t n_tapes, const std::vector<CompiledTape>& ct, mq_tapes** out) {
+// Upload a compiled batch to ONE device.  may_move: the batch's last device takes the QSA-eligible
+// tapes' programs out of ct instead of copying them (~3 000 tapes of a fresh drop-in batch).
+static int tapes_upload_one(mq_ctx* c, int32_t n_tapes, std::vector<CompiledTape>& ct, mq_tapes** out,
+                            bool may_move) {
   *out = nullptr;
   HIPCHK(hipSetDevice(c->device));
   auto T = std::make_unique<mq_tapes>();
@@ -1853,6 +1855,26 @@ static int tapes_upload_one(mq_ctx* c, int32_t n_tapes, const std::vector<Compil
           qsa_ok[t] = qsa_translate(c, 1, false, ct[t], nullptr, &qextra[t]) ? 1 : 0;
     });
   pt.reset(new PhaseTimer(&c->host_t[2]));
+  // (before the descriptor passes: with may_move they empty the eligible tapes' vectors)
+  T->wide_funcs.assign(n_tapes, {});
+  for (int t = 0; t < n_tapes; t++) {
+    T->wide_funcs[t] = ct[t].wide_funcs;
+    T->wide_any = T->wide_any || !ct[t].wide_funcs.empty();
+  }
+  for (int t = 0; t < n_tapes; t++) {
+    T->unsupported[t] = ct[t].supported ? 0 : 1;
+    T->n_unsupported += ct[t].supported ? 0 : 1;
+    T->n_nodes[t] = ct[t].n_nodes;
+    T->alg_ops[t] = ct[t].alg_ops;
+  }
+  size_t prog_words = 1, const_words = 24;
+  for (int t = 0; t < n_tapes; t++) {
+    prog_words += ct[t].prog.size();
+    const_words += ct[t].consts.size() + qextra[t].size();
+  }
+  prog.reserve(prog_words);
+  consts.reserve(const_words);
+  descs.reserve((size_t)n_tapes + 1);
   for (int pass = -1; pass < kGen; pass++) {
     mq_tapes::Variant& v = pass < 0 ? T->qsa : T->gen[pass];
     v.L = pass < 0 ? 8 : kGenL[pass];
@@ -1866,7 +1888,10 @@ static int tapes_upload_one(mq_ctx* c, int32_t n_tapes, const std::vector<Compil
       if (pass < 0) {
         consts.insert(consts.end(), qextra[t].begin(), qextra[t].end());
         T->qbase.push_back(d);
-        T->qct.push_back(x);
+        if (may_move)
+          T->qct.push_back(std::move(ct[t]));
+        else
+          T->qct.push_back(x);
       }
       v.max_temps = std::max(v.max_temps, x.n_temps);
       v.max_depth = std::max(v.max_depth, x.depth);
@@ -1880,17 +1905,6 @@ static int tapes_upload_one(mq_ctx* c, int32_t n_tapes, const std::vector<Compil
   T->l8_all.max_depth = std::max(T->qsa.max_depth, T->gen[0].max_depth);
   consts.resize(consts.size() + 16, 0);
   prog.push_back(gword(G_END, 0, 0));
-  T->wide_funcs.assign(n_tapes, {});
-  for (int t = 0; t < n_tapes; t++) {
-    T->wide_funcs[t] = ct[t].wide_funcs;
-    T->wide_any = T->wide_any || !ct[t].wide_funcs.empty();
-  }
-  for (int t = 0; t < n_tapes; t++) {
-    T->unsupported[t] = ct[t].supported ? 0 : 1;
-    T->n_unsupported += ct[t].supported ? 0 : 1;
-    T->n_nodes[t] = ct[t].n_nodes;
-    T->alg_ops[t] = ct[t].alg_ops;
-  }
   if (descs.empty()) descs.push_back(GDesc{});
   HIPCHK(T->descs.upload(descs.data(), descs.size(), c->stream));
   HIPCHK(T->qargs[0].ensure(sizeof(QArgs)));
@@ -1907,18 +1921,27 @@ static int tapes_upload_one(mq_ctx* c, int32_t n_tapes, const std::vector<Compil
 }
 
 // Upload compiled tapes to every device of the context (lead + peers).
-static int tapes_upload_all(mq_ctx* c, int32_t n_tapes, const std::vector<CompiledTape>& ct, mq_tapes** out,
+static int tapes_upload_all(mq_ctx* c, int32_t n_tapes, std::vector<CompiledTape>& ct, mq_tapes** out,
                             int32_t* n_unsup_out) {
-  mq_tapes* T = nullptr;
-  int rc = tapes_upload_one(c, n_tapes, ct, &T);
-  if (rc) return rc;
-  std::unique_ptr<mq_tapes> guard(T);
+  // the peers copy the compiled programs, the lead (uploaded last) takes them
+  std::vector<mq_tapes*> peers;
   for (mq_ctx* p : c->peers) {
     mq_tapes* pt = nullptr;
-    rc = tapes_upload_one(p, n_tapes, ct, &pt);
-    if (rc) return rc;
-    T->peers.push_back(pt);
+    const int rc = tapes_upload_one(p, n_tapes, ct, &pt, false);
+    if (rc) {
+      for (mq_tapes* q : peers) mq_tapes_free(q);
+      return rc;
+    }
+    peers.push_back(pt);
   }
+  mq_tapes* T = nullptr;
+  int rc = tapes_upload_one(c, n_tapes, ct, &T, true);
+  if (rc) {
+    for (mq_tapes* q : peers) mq_tapes_free(q);
+    return rc;
+  }
+  std::unique_ptr<mq_tapes> guard(T);
+  T->peers = peers;
   if (n_unsup_out) *n_unsup_out = T->n_unsupported;
   *out = guard.release();
   return MQ_OK;

@@ -165,25 +165,33 @@ class ConjunctRows:
 
     def reset(self, key) -> None:
         self.key = key
-        self.row: Dict[int, int] = {}
+        self.n_rows = 0
+        self.row_of = np.full(1024, -1, np.int64)   # DAG node -> row (-1: none yet)
         self.R = np.full((256, 128), -1, np.int8)
         self.bad: set = set()   # conjunct nodes whose tape the evaluator does not support
 
     def sync(self, key) -> None:
-        if key != self.key or len(self.row) > self.MAX_ROWS:
+        if key != self.key or self.n_rows > self.MAX_ROWS:
             self.reset(key)
 
     def rows_for(self, nodes: np.ndarray, n_slots: int) -> np.ndarray:
-        row = self.row
-        out = np.empty(len(nodes), np.int64)
-        for i, x in enumerate(nodes.tolist()):
-            r = row.get(x)
-            if r is None:
-                r = row[x] = len(row)
-            out[i] = r
+        """Rows of the conjunct nodes (new rows numbered in order of first appearance)."""
+        nodes = np.asarray(nodes, np.int64)
+        if len(nodes) and int(nodes.max()) >= len(self.row_of):
+            grow = np.full(max(2 * len(self.row_of), int(nodes.max()) + 1), -1, np.int64)
+            grow[:len(self.row_of)] = self.row_of
+            self.row_of = grow
+        out = self.row_of[nodes]
+        new = out < 0
+        if new.any():
+            u, first = np.unique(nodes[new], return_index=True)
+            u = u[np.argsort(first)]   # first-appearance order
+            self.row_of[u] = self.n_rows + np.arange(len(u))
+            self.n_rows += len(u)
+            out = self.row_of[nodes]
         nr, ns = self.R.shape
-        if len(row) > nr or n_slots > ns:
-            grow = np.full((max(nr, 2 * len(row)) if len(row) > nr else nr,
+        if self.n_rows > nr or n_slots > ns:
+            grow = np.full((max(nr, 2 * self.n_rows) if self.n_rows > nr else nr,
                             max(ns, 2 * n_slots) if n_slots > ns else ns), -1, np.int8)
             grow[:nr, :ns] = self.R
             self.R = grow
@@ -428,7 +436,7 @@ class VerdictEngine:
         cache.sync((inc.dag_gen, inc.slot_epoch))
         uroots, inv = np.unique(db.roots, return_inverse=True)
         urows = cache.rows_for(uroots, int(slots.max()) + 1)
-        unk = (cache.R[np.ix_(urows, slots)] < 0).any(axis=1)
+        unk = (cache.R.take(urows, 0).take(slots, 1) < 0).any(axis=1)   # (take: 3x np.ix_)
         n_unk = int(unk.sum())
         self.stats["conjuncts_cached"] += int(len(uroots) - n_unk)
         if n_unk > self.conj_tapes:
@@ -463,19 +471,22 @@ class VerdictEngine:
             self.launches += 1
             self.pairs += len(todo) * len(dev_slots)
         # each query: the AND of its conjuncts' rows, in the caller's model order
-        occ = cache.R[np.ix_(urows[inv], slots)] > 0
+        occ = (cache.R.take(urows, 0).take(slots, 1) > 0)[inv]
         offs = db.root_offsets
         lens = np.diff(offs)
-        out: List[Optional[np.ndarray]] = []
+        rows = np.ones((len(exprs), len(slots)), bool)   # And() of nothing: true
+        full = lens > 0
+        if full.any():
+            # (the segments of the non-empty queries, back to back: empty ones add no conjuncts)
+            rows[full] = np.logical_and.reduceat(occ, offs[:-1][full], axis=0)
         bad = cache.bad
-        for q in range(len(exprs)):
-            a, b = int(offs[q]), int(offs[q + 1])
-            if not ok[q] or (bad and any(int(x) in bad for x in db.roots[a:b])):
-                out.append(None)
-            elif lens[q] == 0:
-                out.append(np.ones(len(slots), bool))
-            else:
-                out.append(occ[a:b].all(axis=0))
+        out: List[Optional[np.ndarray]] = list(rows)
+        for q in np.flatnonzero(~np.asarray(ok, bool)).tolist():
+            out[q] = None
+        if bad:
+            for q in range(len(exprs)):
+                if out[q] is not None and any(int(x) in bad for x in db.roots[offs[q]:offs[q + 1]]):
+                    out[q] = None
         return out
 
     def _rows_whole(self, db, ok, slots, dev_slots, n_exprs) -> List[Optional[np.ndarray]]:
