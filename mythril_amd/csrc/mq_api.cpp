@@ -135,6 +135,29 @@ class DevPool {
   std::vector<hipStream_t> streams_[16];
 };
 
+// page-locked host staging (readbacks of small batches skip the runtime's pageable bounce)
+struct PinnedBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  PinnedBuf() = default;
+  PinnedBuf(const PinnedBuf&) = delete;
+  PinnedBuf& operator=(const PinnedBuf&) = delete;
+  ~PinnedBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  hipError_t ensure(size_t n) {
+    if (n <= bytes) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+    size_t want = 4096;
+    while (want < n) want *= 2;
+    const hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) bytes = want;
+    return e;
+  }
+};
+
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
@@ -270,6 +293,8 @@ struct mq_ctx {
   DevBuf prof;   // G profile build (kQsaProfBytes > 0): per-kind (cycles, count), mq_qsa_profile
   DevBuf prof_sink;   // ... the launches MQ_PROF_LEVEL leaves out write here
   DevBuf verdict_buf;
+  PinnedBuf verdict_host;   // verdict bytes read back (batches up to kPinnedVerdictBytes)
+  PinnedBuf readback_host;  // a first-hit launch's counter slots and first hits
   // assembly interpreters (qsa.hip): handler byte offsets read back at context creation;
   // k = 0 the P kernel (preloaded variables), k = 1 the G kernel (general)
   bool qsa_ready = false;
@@ -4273,19 +4298,31 @@ int mq_eval_tapes_first_hit(mq_ctx* c, mq_tapes* T, int32_t* out, mq_stats* stat
   HIPCHK(hipEventRecord(c->ev1, c->stream));
   rc = mq_finalize_first_hit(c, T, c->best_tmp.as<int32_t>(), c->stream);
   if (rc) return rc;
-  HIPCHK(hipMemcpyAsync(out, c->best_tmp.p, sizeof(int32_t) * T->n_tapes, hipMemcpyDeviceToHost, c->stream));
+  // both readbacks through pinned staging: [counter slots | first hits]
+  const size_t best_bytes = sizeof(int32_t) * T->n_tapes;
+  const bool pinned = c->readback_host.ensure(kCounterBytes + best_bytes) == hipSuccess;
+  uint8_t* stage = pinned ? (uint8_t*)c->readback_host.p : nullptr;
+  HIPCHK(hipMemcpyAsync(pinned ? (void*)(stage + kCounterBytes) : (void*)out, c->best_tmp.p, best_bytes,
+                        hipMemcpyDeviceToHost, c->stream));
   unsigned long long total[3] = {0, 0, 0};
   for (mq_ctx* d : devs) {
     HIPCHK(hipSetDevice(d->device));
     std::vector<unsigned long long> raw(kCounterBytes / sizeof(unsigned long long));
-    HIPCHK(hipMemcpyAsync(raw.data(), d->counters.p, kCounterBytes, hipMemcpyDeviceToHost, d->stream));
-    HIPCHK(hipStreamSynchronize(d->stream));
+    if (d == c && pinned) {
+      HIPCHK(hipMemcpyAsync(stage, d->counters.p, kCounterBytes, hipMemcpyDeviceToHost, d->stream));
+      HIPCHK(hipStreamSynchronize(d->stream));
+      std::memcpy(raw.data(), stage, kCounterBytes);
+    } else {
+      HIPCHK(hipMemcpyAsync(raw.data(), d->counters.p, kCounterBytes, hipMemcpyDeviceToHost, d->stream));
+      HIPCHK(hipStreamSynchronize(d->stream));
+    }
     unsigned long long cnt[3];
     sum_counter_slots(raw, cnt);
     for (int i = 0; i < 3; i++) total[i] += cnt[i];
   }
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
+  if (pinned) std::memcpy(out, stage + kCounterBytes, best_bytes);
   if (stats) {
     float ms = 0;
     // lead stream: from before the first launch to after the RCCL reduce (all devices)
@@ -4331,7 +4368,15 @@ static int verdict_bytes_one(mq_ctx* c, mq_tapes* T, std::vector<uint8_t>& host)
   HIPCHK(hipMemsetAsync(c->verdict_buf.p, 0, std::max<size_t>(nbytes, 1), c->stream));
   const int rc = launch_all(c, T, nullptr, c->verdict_buf.as<uint8_t>(), c->stream);
   if (rc) return rc;
-  host.assign(nbytes, 0);
+  host.resize(nbytes);
+  // small batches (the drop-in path) through pinned memory; large ones straight into the vector
+  constexpr size_t kPinnedVerdictBytes = size_t(8) << 20;
+  if (nbytes && nbytes <= kPinnedVerdictBytes && c->verdict_host.ensure(nbytes) == hipSuccess) {
+    HIPCHK(hipMemcpyAsync(c->verdict_host.p, c->verdict_buf.p, nbytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    std::memcpy(host.data(), c->verdict_host.p, nbytes);
+    return MQ_OK;
+  }
   if (nbytes) HIPCHK(hipMemcpyAsync(host.data(), c->verdict_buf.p, nbytes, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return MQ_OK;
