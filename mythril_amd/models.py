@@ -44,7 +44,8 @@ class ModelBatch:
                  index_base: int = 0):
         self.var_widths = np.asarray(var_widths, dtype=np.uint16)
         self.var_words = np.ascontiguousarray(var_words, dtype=np.uint32)
-        n_rows = int(sum(limbs(int(w)) for w in self.var_widths))
+        # limbs(w) per variable (Bool -> 1), vectorised: the drop-in path builds a batch per launch
+        n_rows = int(np.maximum((self.var_widths.astype(np.int64) + 31) // 32, 1).sum())
         if self.var_words.ndim != 2 or self.var_words.shape[0] != n_rows:
             raise ValueError(f"var_words must be [{n_rows}, M], got {self.var_words.shape}")
         self.n_models = int(self.var_words.shape[1])
