@@ -81,7 +81,7 @@ PROF = os.environ.get("QSA_PROF") == "1"
 PROF_VGPR = "v70"     # G: LDS address of this wave's profile table
 # profile entries past the handler kinds: the tape frame split at its waits (tape header load,
 # early-exit check, window / run start) and the tape end bookkeeping
-PROF_EXTRA = ("FRAME", "FRAME_LD", "FRAME3", "FRAME3_LD", "F_HDR", "F_EE", "F_END", "PRELOAD", "STAGE")
+PROF_EXTRA = ("FRAME", "FRAME_LD", "FRAME3", "FRAME3_LD", "F_HDR", "F_EE", "F_ENDW", "F_END", "PRELOAD", "STAGE")
 
 
 def prof_point(kind):
@@ -1984,6 +1984,7 @@ def frame(variant, pfx, handlers, subs):
     ] + NEXT_P) + [
         f"{pfx}_tape_end:",
         "s_waitcnt lgkmcnt(0)",
+    ] + (prof_point("F_ENDW") if G else []) + [
         "s_and_b64 s[34:35], s[48:49], s[62:63]",
         # counters per wave: tapes run, their node counts and algorithmic ops; multiplied by the
         # tile's valid lanes once, when the wave's tapes are done
