@@ -1920,11 +1920,11 @@ def frame(variant, pfx, handlers, subs):
         f"{pfx}_tape_loop:",
         "s_cmp_ge_u32 s24, s25",
         f"s_cbranch_scc1 {pfx}_tapes_done",
+        f"{pfx}_tape_body:",
     ] + [
+        # descriptor s24 (32 bytes) through the load's SGPR offset
         "s_lshl_b32 s34, s24, 5",
-        "s_add_u32 s34, s22, s34",
-        "s_addc_u32 s35, s23, 0",
-        "s_load_dwordx8 s[80:87], s[34:35], 0x0",
+        "s_load_dwordx8 s[80:87], s[22:23], s34",
         "s_waitcnt lgkmcnt(0)",
     ] + (prof_point("F_HDR") if G else []) + ([] if G else [
         # P: &best[tape] (G computes it on a hit only; handlers never touch s72-s73, s80-s87)
@@ -2032,7 +2032,8 @@ def frame(variant, pfx, handlers, subs):
         f"{pfx}_next_tape:",
     ] + (prof_point("F_END") if G else []) + [
         "s_add_u32 s24, s24, 1",
-        f"s_branch {pfx}_tape_loop",
+        "s_cmp_lt_u32 s24, s25",
+        f"s_cbranch_scc1 {pfx}_tape_body",
         f"{pfx}_tapes_done:",
     ] + ([
         "v_mbcnt_lo_u32_b32 v6, -1, 0", "v_mbcnt_hi_u32_b32 v6, -1, v6", "v_lshlrev_b32 v6, 3, v6",
