@@ -334,72 +334,7 @@ struct mq_ctx {
   std::vector<ncclComm_t> comms;
   std::vector<int64_t> shard_lo;
   int64_t M_total = 0;
-  // small host-to-device uploads on `stream` go through a pinned ring (stage_upload): the copy
-  // is asynchronous and the caller's host memory may be freed at once; `ustage_ev` follows the
-  // last staged copy, and the ring restarts from 0 only after it completed
-  PinnedBuf ustage;
-  size_t ustage_used = 0;
-  hipEvent_t ustage_ev = nullptr;
-  bool ustage_pending = false;
 };
-
-// Upload count T's to dst on stream st: through the context's pinned ring when st is the
-// context stream and the block is small, else as a plain (pageable) async copy.
-template <class T>
-static hipError_t stage_upload(mq_ctx* c, DevBuf& dst, const T* src, size_t count, hipStream_t st) {
-  constexpr size_t kStageMax = size_t(1) << 20, kStageBytes = size_t(4) << 20;
-  const size_t bytes = sizeof(T) * count;
-  hipError_t e = dst.ensure(bytes);
-  if (e != hipSuccess || count == 0) return e;
-  if (bytes > kStageMax || st != c->stream || !c->ustage_ev)
-    return hipMemcpyAsync(dst.p, src, bytes, hipMemcpyHostToDevice, st);
-  size_t off = (c->ustage_used + 255) & ~size_t(255);
-  if (off + bytes > c->ustage.bytes) {
-    if (c->ustage_pending) {
-      e = hipEventSynchronize(c->ustage_ev);
-      if (e != hipSuccess) return e;
-      c->ustage_pending = false;
-    }
-    off = 0;
-    if (c->ustage.ensure(kStageBytes) != hipSuccess) return hipMemcpyAsync(dst.p, src, bytes, hipMemcpyHostToDevice, st);
-  }
-  std::memcpy((char*)c->ustage.p + off, src, bytes);
-  e = hipMemcpyAsync(dst.p, (char*)c->ustage.p + off, bytes, hipMemcpyHostToDevice, st);
-  if (e != hipSuccess) return e;
-  c->ustage_used = off + bytes;
-  e = hipEventRecord(c->ustage_ev, st);
-  c->ustage_pending = e == hipSuccess;
-  return e;
-}
-
-// Copy one host object to dev (a device pointer of at least sizeof(T)) the same way.
-template <class T>
-static hipError_t stage_upload_to(mq_ctx* c, void* dev, const T& src, hipStream_t st) {
-  if (st != c->stream || !c->ustage_ev) {
-    hipError_t e = hipMemcpyAsync(dev, &src, sizeof(T), hipMemcpyHostToDevice, st);
-    return e != hipSuccess ? e : hipStreamSynchronize(st);   // (src is the caller's host memory)
-  }
-  size_t off = (c->ustage_used + 255) & ~size_t(255);
-  if (off + sizeof(T) > c->ustage.bytes) {
-    if (c->ustage_pending) {
-      hipError_t e = hipEventSynchronize(c->ustage_ev);
-      if (e != hipSuccess) return e;
-      c->ustage_pending = false;
-    }
-    off = 0;
-    if (c->ustage.ensure(size_t(4) << 20) != hipSuccess) {
-      hipError_t e = hipMemcpyAsync(dev, &src, sizeof(T), hipMemcpyHostToDevice, st);
-      return e != hipSuccess ? e : hipStreamSynchronize(st);
-    }
-  }
-  std::memcpy((char*)c->ustage.p + off, &src, sizeof(T));
-  hipError_t e = hipMemcpyAsync(dev, (char*)c->ustage.p + off, sizeof(T), hipMemcpyHostToDevice, st);
-  if (e != hipSuccess) return e;
-  c->ustage_used = off + sizeof(T);
-  e = hipEventRecord(c->ustage_ev, st);
-  c->ustage_pending = e == hipSuccess;
-  return e;
-}
 
 struct FcaPlanSeg {   // one fca_kernel launch (fca_plan)
   int atom_off, n_atoms, group_off, n_groups, tape_first, n_tapes, chunk_first, smask_off, n_smask;
@@ -830,8 +765,7 @@ static int create_one(int dev, mq_ctx** out) {
       hipStreamCreateWithFlags(&c->aux[1], hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->join_ev[0], hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->join_ev[1], hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ustage_ev, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->join_ev[1], hipEventDisableTiming) != hipSuccess) {
     mq_ctx_destroy(c);
     return MQ_ERR_HIP;
   }
@@ -919,10 +853,6 @@ void mq_ctx_destroy(mq_ctx* c) {
       DevPool::get().unregister_stream(c->device, a);
     }
   if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
-  if (c->ustage_ev) {
-    (void)hipEventSynchronize(c->ustage_ev);   // (the ring is freed with the context)
-    (void)hipEventDestroy(c->ustage_ev);
-  }
   for (hipEvent_t e : c->join_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -2001,17 +1931,15 @@ static int tapes_upload_one(mq_ctx* c, int32_t n_tapes, std::vector<CompiledTape
   consts.resize(consts.size() + 16, 0);
   prog.push_back(gword(G_END, 0, 0));
   if (descs.empty()) descs.push_back(GDesc{});
-  HIPCHK(stage_upload(c, T->descs, descs.data(), descs.size(), c->stream));
+  HIPCHK(T->descs.upload(descs.data(), descs.size(), c->stream));
   HIPCHK(T->qargs[0].ensure(sizeof(QArgs)));
   HIPCHK(T->qargs[1].ensure(sizeof(QArgs)));
-  HIPCHK(stage_upload(c, T->prog, prog.data(), prog.size(), c->stream));
+  HIPCHK(T->prog.upload(prog.data(), prog.size(), c->stream));
   // P's constant prefetch reads 8 words at a tape's constants + 0 even for a tape without any
   consts.insert(consts.end(), 8, 0u);
-  HIPCHK(stage_upload(c, T->consts, consts.data(), consts.size(), c->stream));
-  HIPCHK(stage_upload(c, T->unsup_dev, T->unsupported.data(), T->unsupported.size(), c->stream));
-  // (blocks past the pinned ring's limit were plain async copies of these local vectors)
-  if (std::max({descs.size() * sizeof(GDesc), prog.size() * 4, consts.size() * 4}) > (size_t(1) << 20))
-    HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(T->consts.upload(consts.data(), consts.size(), c->stream));
+  HIPCHK(T->unsup_dev.upload(T->unsupported.data(), T->unsupported.size(), c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
   T->unsupported_base = T->unsupported;
   *out = T.release();
   return MQ_OK;
@@ -3464,8 +3392,8 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
     T->q_temps[k] = temps[k];
   }
   if (descs.empty()) descs.push_back(GDesc{});
-  HIPCHK(stage_upload(c, T->qdescs, descs.data(), descs.size(), c->stream));
-  HIPCHK(stage_upload(c, T->qprog, prog.data(), prog.size(), c->stream));
+  HIPCHK(T->qdescs.upload(descs.data(), descs.size(), c->stream));
+  HIPCHK(T->qprog.upload(prog.data(), prog.size(), c->stream));
   if (T->fca) {
     T->fc_count = (int)fap.tape_out.size();
     T->fca_atoms = (int)fap.atoms.size();
@@ -4058,7 +3986,8 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       QArgs* dq = T->cqargs.as<QArgs>() + li;
       if (std::memcmp(&T->cqargs_host[li], &q, sizeof(QArgs)) != 0) {
         PhaseTimer pq(&c->host_t[6]);
-        HIPCHK(stage_upload_to(c, dq, q, st));
+        HIPCHK(hipMemcpyAsync(dq, &q, sizeof(QArgs), hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));  // q is host memory
         T->cqargs_host[li] = q;
       }
       const int64_t groups = T->cq_lvl_groups[li];
@@ -4147,7 +4076,8 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     // the argument block only changes with the output buffer / mode / models: re-upload then
     if (!T->qargs_valid[k] || std::memcmp(&T->qargs_dev_copy[k], &q, sizeof(QArgs)) != 0) {
       PhaseTimer pq(&c->host_t[6]);
-      HIPCHK(stage_upload_to(c, T->qargs[k].p, q, st));
+      HIPCHK(hipMemcpyAsync(T->qargs[k].p, &q, sizeof(QArgs), hipMemcpyHostToDevice, st));
+      HIPCHK(hipStreamSynchronize(st));  // q is host memory
       T->qargs_dev_copy[k] = q;
       T->qargs_valid[k] = true;
     }
