@@ -556,3 +556,28 @@ def test_solver_worker_is_reused_and_replaced_after_a_failure(fresh):
     with pytest.raises(UnsatError):
         sp.get_model(sp.Constraints([x == 94]))
     assert sp._solver_pool is not None and sp._solver_pool is not pool   # a new worker
+
+
+def test_conjunct_row_numbering_and_query_reduction():
+    """ConjunctRows.rows_for numbers new conjunct nodes in order of first appearance (duplicates
+    share a row, the table grows past its first capacity), and the drop-in rows of a batch with an
+    empty conjunction (And() of nothing: true), a failing query and repeated conjuncts equal the
+    reference loop's per-model verdicts."""
+    rows = sp.ConjunctRows()
+    r = rows.rows_for(np.array([7, 3, 7, 2000, 3], np.int64), 4)
+    assert r.tolist() == [0, 1, 0, 2, 1] and rows.n_rows == 3
+    r2 = rows.rows_for(np.array([5000, 2000, 9], np.int64), 300)
+    assert r2.tolist() == [3, 2, 4] and rows.R.shape[1] >= 300 and len(rows.row_of) > 5000
+    x, y = S.BitVecSym("x", 256), S.BitVecSym("y", 256)
+    g = S.Function("g3", [8, 8, 8], 8)
+    v = S.BitVecSym("v", 8)
+    ms = [Model({"x": i, "y": 7 - i, "v": i}) for i in range(8)]
+    c1, c2 = S.ULT(x, S.BitVecVal(5, 256)), S.UGT(y, S.BitVecVal(2, 256))
+    qs = [S.And(c1, c2), S.And(), S.And(c1, g(v, v, v) == 0), S.And(c2, c1, c2), S.And(c1)]
+    eng = OracleEngine()
+    got = eng.rows(qs, ms)
+    assert got[2] is None
+    for q, row in zip(qs, got):
+        if row is None:
+            continue
+        assert row.tolist() == [eval_under(q, m) for m in ms]
