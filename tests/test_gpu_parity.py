@@ -1414,3 +1414,18 @@ def test_c4_tapes_on_the_flat_kernel(evaluator, monkeypatch):
     monkeypatch.setenv("MQ_NO_FLAT", "1")
     ct2 = evaluator.compile(tb)
     assert (evaluator.first_hit(ct2) == ref).all() and ct2.flat_split() == (0, 0)
+
+
+@pytest.mark.parametrize("n_tapes,n_models", [(48, 3000), (90, 100_000)])
+def test_verdict_matrix_readback_small_and_large(evaluator, n_tapes, n_models):
+    """Verdict matrices read back through the pinned staging buffer (up to 8 MB of verdict
+    bytes) and straight into host memory (past it: 90 x 10^5 = 9 MB), bit-exact against the
+    oracle, with first hits consistent with each row."""
+    tb, mb, expected = c2_workload(n_tapes, n_models, seed=11)
+    evaluator.upload_models(mb)
+    v, fh = evaluator.verdicts(tb)
+    ref = cref.verdicts(tb, mb)
+    assert v.shape == ref.shape and (v == ref).all()
+    first = np.where(v.any(axis=1), v.argmax(axis=1), -1)
+    assert (fh == first).all()
+    assert all(fh[t] == p for t, p in enumerate(expected) if p >= 0)
