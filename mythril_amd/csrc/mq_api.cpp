@@ -4034,11 +4034,14 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
   for (int k = 0; use_qsa && k < 2; k++) {
     const int n = T->q_count[k];
     if (n <= 0) continue;
-    // P: grid = (256-model tiles) x (tape groups), groups sized for ~8k workgroups.
+    // P: grid = (256-model tiles) x (tape groups), groups sized for ~32k workgroups (C2: 120
+    //    tapes a group; 8k / 16k / 24k / 32k / 64k: 23.75 / 23.15 / 22.88 / 22.87 / 22.87 ms,
+    //    profiles/r05bf, r05bg — finer groups shorten the last wave of workgroups; the model rows
+    //    are re-read once per group, ~2 GB per launch, far from the HBM bound of a VALU-bound kernel)
     // G: 64-model tiles, 4 tape groups per workgroup (one per wave), XCD-interleaved grid
     //    (qsa.hip); groups of g_tapes_per_group() tapes.
     const int64_t tiles256 = (c->M + 255) / 256;
-    int64_t p_wg = 8192;   // P: target workgroup count (MQ_P_WG overrides)
+    int64_t p_wg = 32768;   // P: target workgroup count (MQ_P_WG overrides)
     if (const char* e = std::getenv("MQ_P_WG")) p_wg = std::max(256L, std::atol(e));
     int64_t tpg = k == 0 ? (int64_t(n) * tiles256 + p_wg - 1) / p_wg : latency ? 1 : g_tapes_per_group(n, c->M);
     tpg = std::max<int64_t>(1, std::min<int64_t>(tpg, n));
@@ -4081,6 +4084,9 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       T->qargs_dev_copy[k] = q;
       T->qargs_valid[k] = true;
     }
+    // P: tiles fastest, so the workgroups running together share a tape group's program and
+    // constants in the scalar caches (the XCD-interleaved order G uses measured 22.8 -> 26.4 ms
+    // on C2, profiles/r05bi: P's program reads are scalar, its model rows preloaded once)
     unsigned gx = (unsigned)tiles256;
     unsigned gy = (unsigned)((n + tpg - 1) / tpg);
     if (k == 1) {
