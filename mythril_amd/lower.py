@@ -265,6 +265,11 @@ def _lower_one(t: S.Term, a: List[int], tp: Tape, syms: SymbolTable, node: Dict[
     if k == S.SEXT:
         return tp.sext(t.params[0], a[0])
     if k == S.ITE:
+        if t.sort == "array":
+            # an array-valued ite (the state-merge plugin's If(c, balances1, balances2),
+            # merge_states.py:27-29,95-107) is never a value of its own: every select reads
+            # through it (_select_merged), so it has no tape node
+            return -1
         return tp.ite(a[0], a[1], a[2])
     if k == S.ARRAY_SYM:
         return -1  # materialised at its first table use (a symbol only read at constant indices
@@ -272,9 +277,13 @@ def _lower_one(t: S.Term, a: List[int], tp: Tape, syms: SymbolTable, node: Dict[
     if k == S.CONST_ARRAY:
         return tp.const_array(a[0])
     if k == S.STORE:
+        if _merged_array(t.args[0]):
+            return -1   # a store over a merged array: read through by _select_merged as well
         return tp.store(arr_node(t.args[0], a[0]), a[1], a[2])
     if k == S.SELECT:
         arr, idx = t.args
+        if _merged_array(arr):
+            return _select_merged(arr, idx, a[1], tp, syms, node, arr_node)
         if syms.derive and arr.kind == S.ARRAY_SYM and idx.kind == S.VAL:
             return tp.var(syms.derived_var(arr.params[0], (idx.params[0],), _w(t)), _w(t))
         return tp.select(arr_node(arr, a[0]), a[1])
@@ -307,6 +316,38 @@ def _lower_one(t: S.Term, a: List[int], tp: Tape, syms: SymbolTable, node: Dict[
             return tp.uf_wide(fid, t.width, chunks)
         return tp.uf(fid, t.width, *a)
     raise LoweringError(f"term kind {k!r} not in the tape vocabulary")
+
+
+def _merged_array(arr: S.Term) -> bool:
+    """Whether the array term is an array-valued ite, or a store chain over one."""
+    while arr.kind == S.STORE:
+        arr = arr.args[0]
+    return arr.kind == S.ITE
+
+
+def _select_merged(arr: S.Term, idx: S.Term, i: int, tp: Tape, syms: SymbolTable, node: Dict[int, int],
+                   arr_node) -> int:
+    """``select(arr, idx)`` (tape node ``i`` = the index) pushed through array-valued ites and
+    the stores above them — ``select(ite(c, A, B), i) = ite(c, select(A, i), select(B, i))`` and
+    ``select(store(A, k, v), i) = ite(i == k, v, select(A, i))`` (SMT-LIB ArraysEx) — down to
+    plain arrays, read as usual.  Iterative over the store chains; the ite branches recurse
+    (merge depth)."""
+    chain = []   # (key node, value node) of the stores above the next ite / plain array, outermost first
+    while arr.kind == S.STORE:
+        base, kt, vt = arr.args
+        chain.append((node[id(kt)], node[id(vt)]))
+        arr = base
+    if arr.kind == S.ITE:
+        c, x, y = arr.args
+        r = tp.ite(node[id(c)], _select_merged(x, idx, i, tp, syms, node, arr_node),
+                   _select_merged(y, idx, i, tp, syms, node, arr_node))
+    elif syms.derive and arr.kind == S.ARRAY_SYM and idx.kind == S.VAL:
+        r = tp.var(syms.derived_var(arr.params[0], (idx.params[0],), _w(arr)), _w(arr))
+    else:
+        r = tp.select(arr_node(arr, node.get(id(arr), -1)), i)
+    for kn, vn in reversed(chain):   # the outermost store decides first
+        r = tp.ite(tp.eq(i, kn), vn, r)
+    return r
 
 
 def _chunk(t: S.Term, lo: int, hi: int, tp: Tape, syms: SymbolTable, node: Dict[int, int],
@@ -1078,6 +1119,9 @@ class IncrementalLowering:
     def _reset_models(self) -> None:
         self._slot: Dict[int, int] = {}      # id(model) -> slot
         self._slot_model: List[object] = []  # slot -> model (kept alive: the id stays valid)
+        # slot -> its record (smt_model.Model): a z3 model is read ONCE, without completion
+        # (lower_z3.model_record), when it gets its slot, not per variable / function / call
+        self._slot_rec: List[Model] = []
         self._ftabs: List[Dict[int, Tuple[np.ndarray, np.ndarray]]] = []   # slot -> {f: table}
         self._ser_nv = 0                     # variables serialized so far
         self._words = np.zeros((0, 64), np.uint32)
@@ -1128,9 +1172,11 @@ class IncrementalLowering:
         for mod in models:
             s = self._slot.get(id(mod))
             if s is None or self._slot_model[s] is not mod:
+                rec = as_record(mod)   # (raises LoweringError for an unreadable z3 model: no slot)
                 s = len(self._slot_model)
                 self._slot[id(mod)] = s
                 self._slot_model.append(mod)
+                self._slot_rec.append(rec)
                 self._ftabs.append({})
                 new.append(s)
             out.append(s)
@@ -1140,9 +1186,9 @@ class IncrementalLowering:
             grow[:, :self._words.shape[1]] = self._words
             self._words = grow
         if new and self._ser_nv:
-            self._words[:, new] = self._rows_of([as_record(self._slot_model[s]) for s in new], 0, self._ser_nv)
+            self._words[:, new] = self._rows_of([self._slot_rec[s] for s in new], 0, self._ser_nv)
         if nv > self._ser_nv:
-            recs = [as_record(m) for m in self._slot_model]
+            recs = self._slot_rec
             add = self._rows_of(recs, self._ser_nv, nv)
             rows = np.zeros((add.shape[0], self._words.shape[1]), np.uint32)
             rows[:, :n] = add
@@ -1160,7 +1206,7 @@ class IncrementalLowering:
         rnb, rmask = fields[-1]
         buf, ebuf, counts = bytearray(), bytearray(), []
         for s in slots:
-            interp = function_interp(as_record(self._slot_model[s]), name)
+            interp = function_interp(self._slot_rec[s], name)
             if interp is None:
                 counts.append(0)
                 ebuf += bytes(rnb)

@@ -286,7 +286,11 @@ def If(c, a, b) -> Term:
     a = a if isinstance(a, Term) else BitVecVal(int(a), w)
     b = b if isinstance(b, Term) else BitVecVal(int(b), w)
     if a.sort == "array" or b.sort == "array":
-        raise TypeError("array-sorted If is not in the evaluator's vocabulary (lowering fails closed)")
+        # an array-valued If (the state-merge plugin: If(cond, state1.balances, state2.balances),
+        # merge_states.py:27-29): the lowering pushes every select through it
+        if a.sort != b.sort or a.width != b.width or a.domain != b.domain:
+            raise TypeError("If over arrays of different sorts")
+        return Term(ITE, "array", a.width, (c, a, b), (), a.domain)
     return Term(ITE, "bv", _same(a, b), (c, a, b))
 
 

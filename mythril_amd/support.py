@@ -47,8 +47,9 @@ from typing import Callable, Dict, Iterable, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import smt as S
-from .exceptions import SolverTimeOutException, UnsatError, fail_closed  # noqa: F401 (fail_closed: queries
-#   routed to z3 because a conjunct did not lower, by reason -- array-valued ite, array equality, ...)
+from .exceptions import LoweringError, SolverTimeOutException, UnsatError, fail_closed  # noqa: F401
+#   (fail_closed: queries routed to z3 because a conjunct did not lower, by reason -- array equality, ...)
+from .exceptions import note_fail_closed as fail_closed_note
 from .lower import DagBatch
 from .smt_model import Model, as_record
 
@@ -203,9 +204,9 @@ class VerdictEngine:
 
     ``rows(exprs, models)`` -> one ``bool[len(models)]`` verdict row per expression (``None`` =
     unsupported: fail closed).  Works on z3-free terms (:mod:`mythril_amd.smt`) and, on a z3 host,
-    on z3 ``BoolRef`` (lowered by :mod:`mythril_amd.lower_z3`).
+    on z3 ``BoolRef``, translated once per AST into the same terms (:meth:`_rows_z3`).
 
-    The drop-in path (z3-free terms, the LRU's <= 100 models) keeps three things across calls:
+    The drop-in path (the LRU's <= 100 models) keeps three things across calls:
     the hash-consed DAG of every lowered term, the candidate models' serialized rows (resident on
     the device in slot order, so an LRU bump re-uploads nothing), and per-conjunct verdict rows
     (:class:`ConjunctRows`).  A call evaluates only the conjuncts not yet known under the current
@@ -255,6 +256,8 @@ class VerdictEngine:
         # that compiled batch is launched again (all of it: the extra rows are cached too) instead
         # of compiling the subset (~4 ms per fill on the fork stream, profiles/r04k)
         self._conj_ct = None
+        self._owner = threading.get_ident()   # the thread whose HIP context owns _conj_ct
+        self._z3 = None   # lower_z3.Z3Terms of the z3 queries seen (created on the first one)
 
     @property
     def evaluator(self):
@@ -264,14 +267,15 @@ class VerdictEngine:
         return self._ev
 
     def _lower(self, exprs, models, hoist: bool):
+        """``(tapes, models, supported mask)`` of z3-free terms, for a whole-batch launch."""
         clock = time.perf_counter
         t0 = clock()
-        if all(isinstance(e, S.Term) for e in exprs) and not hoist:
+        if not hoist:
             inc = self.incremental
             tb, ok = inc.lower(exprs)
             t1 = clock()
             mb = inc.serialize(models)
-        elif all(isinstance(e, S.Term) for e in exprs):
+        else:
             from .lower import lower_batch, serialize_models
             # states forked from a common parent share constraint prefixes: hoist what a batch
             # shares into once-per-model columns (lower.py lower_batch)
@@ -279,13 +283,44 @@ class VerdictEngine:
             tb, syms, ok = lower_batch(exprs, hoist=hoist)
             t1 = clock()
             mb = serialize_models(records, syms)
-        else:
-            from .lower_z3 import lower_batch_z3
-            tb, mb, ok = lower_batch_z3(exprs, models)
-            t1 = clock()
         self.timing["lower"] += t1 - t0
         self.timing["serialize"] += clock() - t1
         return tb, mb, ok
+
+    def _rows_z3(self, exprs: Sequence, models: Sequence) -> List[Optional[np.ndarray]]:
+        """z3 ``BoolRef`` queries (model.py:101 hands quick-sat ``simplify(And(*c)).raw``): each is
+        translated into interned terms (:class:`mythril_amd.lower_z3.Z3Terms`, memoized by z3 AST
+        id, so only ASTs never seen before are walked) and then takes the z3-free path — the
+        persistent DAG, the resident model rows (each z3 model read once, when it gets its slot)
+        and the per-conjunct verdict rows: the top-level ``And``'s children are the conjuncts, so
+        a forked state's parent conjuncts and the keccak axioms are answered from cached rows.
+        A query that does not translate is unsupported (``None``: the z3 loop answers it); a
+        cached model whose interpretation is not literal makes the whole batch unsupported."""
+        t0 = time.perf_counter()
+        if self._z3 is None:
+            from .lower_z3 import Z3Terms
+            self._z3 = Z3Terms()
+        out: List[Optional[np.ndarray]] = [None] * len(exprs)
+        terms, idx = [], []
+        for i, e in enumerate(exprs):
+            if isinstance(e, S.Term):
+                terms.append(e)
+                idx.append(i)
+                continue
+            try:
+                terms.append(self._z3.term(e))
+                idx.append(i)
+            except LoweringError as err:
+                fail_closed_note(err)
+        self.timing["lower"] += time.perf_counter() - t0
+        if terms:
+            try:
+                rows = self.rows(terms, models)
+            except LoweringError:
+                return out
+            for i, r in zip(idx, rows):
+                out[i] = r
+        return out
 
     @staticmethod
     def _latency_mode(ev, waves: Optional[int]) -> Optional[int]:
@@ -315,10 +350,32 @@ class VerdictEngine:
             self._free(prev[2])
 
     def __del__(self):
-        try:
-            self.close()
-        except Exception:   # (interpreter shutdown: the library may be gone)
-            pass
+        # libmq context calls are not thread-safe and the HIP device is per thread: a finalizer
+        # run by another thread (a GC pass on the solver worker) only queues the buffer, which
+        # the next engine call on the owning thread frees
+        prev = getattr(self, "_conj_ct", None)
+        if prev is None:
+            return
+        self._conj_ct = None
+        if threading.get_ident() == getattr(self, "_owner", None):
+            try:
+                self._free(prev[2])
+            except Exception:   # (interpreter shutdown: the library may be gone)
+                pass
+        else:
+            _DEFERRED_FREES.append((self._owner, prev[2]))
+
+    def _drain_deferred(self) -> None:
+        if _DEFERRED_FREES:
+            me = threading.get_ident()
+            keep = []
+            while _DEFERRED_FREES:
+                owner, ct = _DEFERRED_FREES.pop()
+                if owner == me:
+                    self._free(ct)
+                else:
+                    keep.append((owner, ct))
+            _DEFERRED_FREES.extend(keep)
 
     def _evaluate(self, tb, mb, upload: bool = True):
         """Device hook: (verdicts [n_tapes, M], first hits) of ``tb`` over ``mb``; ``upload``
@@ -404,6 +461,9 @@ class VerdictEngine:
             return []
         if not models:
             return [np.zeros(0, bool) for _ in exprs]
+        self._drain_deferred()
+        if not all(isinstance(e, S.Term) for e in exprs):
+            return self._rows_z3(exprs, models)
         hoist = len(exprs) >= self.hoist_min_batch and len(models) >= self.hoist_min_models
         if not hoist and all(isinstance(e, S.Term) for e in exprs):
             return self._rows_incremental(exprs, models)
@@ -508,6 +568,8 @@ class VerdictEngine:
 
 
 _UNSUPPORTED = object()
+# (owner thread, compiled batch) freed by the next engine call on that thread (VerdictEngine.__del__)
+_DEFERRED_FREES: List[Tuple[int, object]] = []
 
 
 # ---------------------------------------------------------------------------- ModelCache

@@ -828,3 +828,58 @@ def fork_children(parents: Sequence[S.Term], n_tx: int = 3, seed: int = 9) -> Li
         conj = list(p.args) if p.kind == S.AND else [p]
         out += [S.And(*(conj + [cond])), S.And(*(conj + [S.Not(cond)]))]
     return out
+
+
+def merge_workload(n_queries: int, n_models: int, seed: int = 31):
+    """The state-merge plugin's shapes (laser/plugin/plugins/state_merge/merge_states.py): two
+    world states joined under a merge condition, the balances as ``If(c, balances1, balances2)``
+    (:27-29) and an account's storage as an If of the two storages (:95-107), read and written
+    afterwards — selects through the merged arrays at symbolic and constant indices, stores over
+    them, nested merges.  Models interpret the arrays ``as-array`` (smt_model.Model functions)
+    with random tables.  Returns ``(exprs, records)``."""
+    from .smt_model import Model
+    rng = np.random.Generator(np.random.PCG64(seed))
+    cond = [S.BoolSym("merge_cond_1"), S.BitVecSym("call_value1", 256) == 0]
+    bal = [S.Array(f"balance_{i}", 256, 256) for i in range(3)]
+    sto = [S.Array(f"Storage_{i}", 256, 256) for i in range(2)]
+    addr = [S.BitVecSym(f"sender_{i}", 256) for i in range(1, 3)]
+    keys = [0, 1, 2, 3, 0xAFFE, 0xDEADBEEF]
+    cst = lambda v: S.BitVecVal(int(v), 256)  # noqa: E731
+    exprs = []
+    for _ in range(n_queries):
+        c = cond[int(rng.integers(2))]
+        merged = S.If(c, bal[0], bal[1])
+        if rng.random() < 0.4:   # a transfer after the merge: stores over the merged balances
+            a = addr[int(rng.integers(2))]
+            v = cst(rng.integers(1, 50))
+            merged = S.Store(S.Store(merged, a, merged[a] - v), cst(keys[int(rng.integers(6))]), merged[a] + v)
+        if rng.random() < 0.3:   # a second merge over the first (a three-way join)
+            merged = S.If(S.Not(cond[1] if c is cond[0] else cond[0]), merged, bal[2])
+        storage = S.If(S.ULT(addr[0], cst(0x10000)), S.Store(S.K(256, 256, 0), cst(7), cst(70)), sto[0])
+        if rng.random() < 0.5:
+            storage = S.Store(storage, cst(keys[int(rng.integers(6))]), addr[1])
+        conj = []
+        for _ in range(int(rng.integers(1, 4))):
+            kind = int(rng.integers(4))
+            idx = addr[int(rng.integers(2))] if rng.random() < 0.5 else cst(keys[int(rng.integers(6))])
+            if kind == 0:
+                conj.append(S.UGE(merged[idx], cst(rng.integers(0, 40))))
+            elif kind == 1:
+                conj.append(S.ULT(merged[idx], merged[cst(keys[int(rng.integers(6))])]))
+            elif kind == 2:
+                conj.append(storage[idx] == cst(rng.integers(0, 4) * 35))
+            else:
+                conj.append(S.Not(storage[idx] == merged[idx]))
+        exprs.append(S.And(*conj))
+    records = []
+    for _ in range(n_models):
+        asg = {"merge_cond_1": bool(rng.integers(2)), "call_value1": int(rng.integers(0, 2)),
+               "sender_1": keys[int(rng.integers(6))] if rng.random() < 0.8 else int(rng.integers(1 << 20)),
+               "sender_2": keys[int(rng.integers(6))]}
+        funcs = {}
+        for name in ("balance_0", "balance_1", "balance_2", "Storage_0"):
+            if rng.random() < 0.9:
+                funcs[name] = ({(k,): int(rng.integers(0, 80)) for k in keys if rng.random() < 0.6},
+                               int(rng.integers(0, 3)) * 35)
+        records.append(Model(asg, funcs))
+    return exprs, records

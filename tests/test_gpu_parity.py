@@ -1429,3 +1429,28 @@ def test_verdict_matrix_readback_small_and_large(evaluator, n_tapes, n_models):
     first = np.where(v.any(axis=1), v.argmax(axis=1), -1)
     assert (fh == first).all()
     assert all(fh[t] == p for t, p in enumerate(expected) if p >= 0)
+
+
+@pytest.mark.parametrize("hoist", [False, True])
+def test_state_merge_array_ite_matches_oracle(evaluator, hoist):
+    """The state-merge plugin's array-valued If (merge_states.py:27-29,95-107), lowered by
+    pushing selects through the merged arrays (lower.py _select_merged): GPU verdicts and first
+    hits against the oracle on the unhoisted lowering, and against the direct term evaluator."""
+    import term_eval
+    from mythril_amd.lower import lower_batch, serialize_models
+    from mythril_amd.synth_evm import merge_workload
+    exprs, recs = merge_workload(64, 300, seed=9)
+    tb, syms, ok = lower_batch(exprs, hoist=hoist)
+    assert ok.all()
+    mb = serialize_models(recs, syms)
+    tb0, syms0, _ = lower_batch(exprs)
+    mb0 = serialize_models(recs, syms0)
+    evaluator.upload_models(mb)
+    v, fh = evaluator.verdicts(tb)
+    assert (fh != -2).all()
+    v_ref = cref.verdicts(tb0, mb0)
+    assert (v == v_ref).all()
+    assert (fh == cref.first_hit(tb0, mb0)[0]).all()
+    direct = np.array([[term_eval.is_true(e, m) for m in recs[:40]] for e in exprs])
+    assert (v[:, :40] == direct).all()
+    assert v.any() and (~v).any()

@@ -285,7 +285,6 @@ def exercise_fail_closed(lz3):
     rej = [
         Z.ForAll(good),                                                     # quantifier
         Z.Eq(a1, a2),                                                       # array equality
-        Z.Eq(Z.Select(Z.If(good, a1, a2), x), x),                           # array-valued ite
         Z.Eq(Z._mk(C.Z3_OP_ROTATE_LEFT, bv(256), (x,), params=(3,)), x),    # kind outside the set
         Z.Eq(Z.Select(barr, Z.BoolVal(True)), Z.BitVecVal(0, 8)),           # array over a Bool domain
         Z.Eq(Z.Int("i"), Z.Int("j")),                                       # an Int sort
@@ -301,7 +300,7 @@ def exercise_fail_closed(lz3):
     # each rejected query is counted under its reason (the state-merge shapes by name)
     new = {k: fail_closed[k] - before.get(k, 0) for k in fail_closed if fail_closed[k] != before.get(k, 0)}
     assert sum(new.values()) == len(rej), new
-    assert new.get("array equality") == 1 and new.get("array-valued ite") == 1, new
+    assert new.get("array equality") == 1, new
     v = cref.verdicts(tb, mb)
     assert v[0, 0] and v[-1, 0]
     # a model whose interpretation cannot be read routes the whole batch to the z3 loop
@@ -359,11 +358,16 @@ def exercise_adapter(lz3):
     exprs = [g.bool(3) for _ in range(6)]
     models = [wrap(g.model()) for _ in range(5)]
     eng = sp.VerdictEngine(evaluator=object())
-    tb, mb, ok = eng._lower(exprs, models, hoist=False)
+    tb, mb, ok = lz3.lower_batch_z3(exprs, models)
     assert ok.all() and tb.n_tapes == 6 and mb.n_models == 5
     raw = [m.raw[0] for m in models]
     exp = fake_rows(exprs, raw)
     assert (cref.verdicts(tb, mb) == exp).all()
+    # hoisted form (the generated-candidates batch shape): same verdicts
+    tbh, mbh, okh = lz3.lower_batch_z3(exprs, models, hoist=True)
+    assert okh.all()
+    from oracle_engine import apply_columns
+    assert (cref.verdicts(tbh, apply_columns(tbh, mbh) if tbh.columns is not None else mbh) == exp).all()
     mc = sp.ModelCache(eng)
     for m in models:
         mc.put(m, 1)
@@ -463,3 +467,115 @@ def test_gpu_model_cache_on_z3_terms_matches_reference_loop(lz3, evaluator):
             ref_order.insert(0, want)
     assert list(reversed(mc.model_cache.lru_cache.keys())) == ref_order
     assert any(a is not False for a in got) and any(a is False for a in got)
+
+
+# ----------------------------------------------------------------------------- the incremental z3 path
+def _z3_fork_stream(n_parents=8, n_models=24, seed=11):
+    """Parents (EVM-shaped paths) and their JUMPI children (svm.py:351-358) as stand-in z3 ASTs,
+    the cached models as stand-in ModelRefs (the MRU-first LRU order)."""
+    import z3_bridge as B
+    from mythril_amd.synth_evm import dropin_workload, fork_children
+    exprs, recs, _ = dropin_workload(n_parents, n_models, seed=seed)
+    kids = fork_children(exprs)
+    sig = B.signature(exprs + kids)
+    to = B.ToZ3()
+    return [to(e) for e in exprs], [to(e) for e in kids], [B.model_to_z3(r, sig) for r in recs]
+
+
+def _run_z3_stream(lz3, engine, parents, kids, models):
+    """check_quick_sat over the parents, then the children, through ModelCache on z3 ASTs; the
+    answers and final LRU order against the reference loop replayed on the stand-in evaluator."""
+    import z3_bridge as B
+    from mythril_amd import support as sp
+    mc = sp.ModelCache(engine)
+    for m in reversed(models):
+        mc.put(m, 1)
+    got = mc.check_quick_sat_batch(parents)
+    evaluated = engine.stats["conjuncts_evaluated"]
+    translated = engine._z3.translated
+    got += mc.check_quick_sat_batch(kids)
+    want, order = B.reference_replay(parents + kids, models, lz3)
+    assert all(a is b for a, b in zip(got, want)), [(a is b) for a, b in zip(got, want)]
+    assert list(reversed(mc.model_cache.lru_cache.keys())) == order
+    assert any(a is not False for a in got) and any(a is False for a in got)
+    return got, evaluated, translated
+
+
+def test_z3_fork_stream_takes_the_incremental_path(lz3):
+    """model.py:101 hands quick-sat a z3 BoolRef.  A fork stream of such queries is translated
+    once per AST into the persistent DAG: the children's parent conjuncts are answered from
+    cached per-conjunct rows (conjuncts_cached > 0), only their new branch conditions reach the
+    device, the z3 models are read once, and the answers and LRU order are the reference
+    loop's (z3_quick_sat_loop, the stand-in's own evaluator)."""
+    from oracle_engine import OracleEngine
+    parents, kids, models = _z3_fork_stream()
+    eng = OracleEngine()
+    reads = []
+    real = lz3.model_record
+
+    def counting(m):
+        reads.append(id(m))
+        return real(m)
+    lz3.model_record = counting
+    try:
+        _, evaluated, translated = _run_z3_stream(lz3, eng, parents, kids, models)
+    finally:
+        lz3.model_record = real
+    st = eng.stats
+    assert st["conjuncts_cached"] > 0
+    # each child pair adds one branch condition and its negation: 2 new conjuncts per parent
+    assert st["conjuncts_evaluated"] - evaluated <= 2 * len(parents)
+    # the children's new ASTs: cond, Not(cond), two And roots and the condition's few sub-terms
+    assert eng._z3.translated - translated <= 16 * len(parents)
+    assert len(reads) == len(set(reads)) == len(models)   # every z3 model read once
+
+
+def test_z3_state_merge_shapes_lower(lz3):
+    """The state-merge plugin's array-valued If (merge_states.py:27-29,95-107) through the z3 side:
+    selects read through the merged balances / storage, stores over the merge included."""
+    bv = Z.BitVecSort
+    c = Z.Bool("merge_cond")
+    b1, b2 = Z.Array("balance_1", bv(256), bv(256)), Z.Array("balance_2", bv(256), bv(256))
+    s1 = Z.Store(Z.K(bv(256), Z.BitVecVal(0, 256)), Z.BitVecVal(7, 256), Z.BitVecVal(70, 256))
+    s2 = Z.Array("Storage_2", bv(256), bv(256))
+    x = Z.BitVec("x", 256)
+    merged_bal = Z.If(c, b1, b2)
+    merged_st = Z.Store(Z.If(Z.bool_op(C.Z3_OP_ULT, x, Z.BitVecVal(9, 256)), s1, s2), Z.BitVecVal(3, 256), x)
+    nested = Z.If(Z.Not(c), merged_bal, Z.Store(b1, x, Z.BitVecVal(1, 256)))
+    exprs = [Z.bool_op(C.Z3_OP_UGEQ, Z.Select(merged_bal, x), Z.BitVecVal(5, 256)),
+             Z.Eq(Z.Select(merged_st, Z.BitVecVal(7, 256)), Z.BitVecVal(70, 256)),
+             Z.Eq(Z.Select(merged_st, Z.BitVecVal(3, 256)), Z.BitVecVal(2, 256)),
+             Z.Eq(Z.Select(merged_st, x), Z.BitVecVal(0, 256)),
+             Z.bool_op(C.Z3_OP_ULT, Z.Select(nested, Z.BitVecVal(2, 256)), Z.Select(merged_bal, Z.BitVecVal(2, 256)))]
+    g = Gen(21)
+    models = []
+    for i in range(24):
+        m = Z.ModelRef()
+        if i % 3:
+            m.set(c.decl(), Z.BoolVal(bool(i % 2)))
+        m.set(x.decl(), Z.BitVecVal([0, 2, 3, 7, 8, 11][i % 6], 256))
+        for a in (b1, b2, s2):
+            f = Z.FuncDeclRef(f"{a.decl().name()}!as", C.Z3_OP_UNINTERPRETED, (), (bv(256),), bv(256))
+            ents = [Z.FuncEntry([Z.BitVecVal(k, 256)], Z.BitVecVal(int(g.rng.integers(0, 12)), 256)) for k in (0, 2, 3, 7, 8, 11)
+                    if g.r(2)]
+            m.set(f, Z.FuncInterp(1, ents, Z.BitVecVal(g.r(3), 256)))
+            m.set(a.decl(), Z.AsArray(f))
+        models.append(m)
+    tb, mb, ok = lz3.lower_batch_z3(exprs, [wrap(m) for m in models])
+    assert ok.all()
+    exp = fake_rows(exprs, models)
+    assert (cref.verdicts(tb, mb) == exp).all()
+    assert exp.any(axis=1).all() and (~exp).any(axis=1).all()   # every query splits the models
+
+
+@pytest.mark.gpu
+def test_gpu_z3_fork_stream_takes_the_incremental_path(lz3, evaluator):
+    """The same z3 fork stream on the GPU through libmq: answers and LRU order equal the
+    reference loop's; the children reuse their parents' conjunct rows."""
+    from mythril_amd import support as sp
+    parents, kids, models = _z3_fork_stream(n_parents=16, n_models=40, seed=13)
+    eng = sp.VerdictEngine(evaluator)
+    _, evaluated, _ = _run_z3_stream(lz3, eng, parents, kids, models)
+    assert eng.stats["conjuncts_cached"] > 0
+    assert eng.stats["conjuncts_evaluated"] - evaluated <= 2 * len(parents)
+    eng.close()

@@ -442,3 +442,32 @@ def test_constant_keccaks_fold_at_lowering():
     mb = serialize_models(models, syms1)
     v = cref.verdicts(tb, apply_columns(tb, mb) if tb.columns is not None else mb)
     assert (v == cref.verdicts(tb0, serialize_models(models, syms0))).all()
+
+
+def test_state_merge_array_ite_lowers_and_agrees_with_term_evaluation():
+    """Array-valued If (the state-merge plugin, merge_states.py:27-29,95-107): every select is
+    pushed through the merged arrays and the stores above them (lower.py _select_merged).  Both
+    product lowerings — batch (hoisted and not) and the drop-in DAG — agree with the direct term
+    evaluator (tests/term_eval.py evaluates the array If itself, no rewrite)."""
+    import term_eval
+    from mythril_amd.lower import IncrementalLowering
+    from mythril_amd.synth_evm import merge_workload
+    from oracle_engine import apply_columns
+    exprs, recs = merge_workload(60, 40, seed=5)
+    direct = np.array([[term_eval.is_true(e, m) for m in recs] for e in exprs])
+    assert direct.any() and (~direct).any()
+    tb, syms, ok = lower_batch(exprs)
+    assert ok.all()
+    assert (cref.verdicts(tb, serialize_models(recs, syms)) == direct).all()
+    tbh, symsh, okh = lower_batch(exprs, hoist=True)
+    assert okh.all()
+    mbh = serialize_models(recs, symsh)
+    assert (cref.verdicts(tbh, apply_columns(tbh, mbh) if tbh.columns is not None else mbh) == direct).all()
+    inc = IncrementalLowering()
+    db, ok = inc.lower(exprs)
+    assert ok.all()
+    assert (cref.verdicts(db.to_tapes(), inc.serialize(recs)) == direct).all()
+    # array equality stays outside the vocabulary (fail closed)
+    a, b = S.Array("A", 256, 256), S.Array("B", 256, 256)
+    _, _, ok = lower_batch([S.Term(S.EQ, "bool", 0, (a, b)), exprs[0]])
+    assert ok.tolist() == [False, True]
