@@ -290,6 +290,62 @@ def dropin_stream_leg(ev, grid=((1, 16), (1, 100), (16, 100), (128, 100)), seed:
     return out
 
 
+def dropin_stream_z3stub_leg(ev, grid=((1, 16), (1, 100), (16, 100), (128, 100)), seed: int = 7):
+    """``dropin_stream`` on the path a Mythril install takes: the queries are z3 ``BoolRef`` ASTs
+    (model.py:101) and the cached models ``z3.ModelRef``s wrapped like mythril ``Model``s — here
+    built in the z3 STAND-IN (tests/fake_z3.py; no z3 on the box) from the same workload
+    (tests/z3_bridge.py).  Times are stand-in timings: the stand-in's AST accessors are plain
+    Python calls, z3py's go through ctypes.  Per cell: the same stage split as dropin_stream, the
+    z3 ASTs the engine translated for the timed children (only new ones are walked), and the
+    answers against the reference loop replayed on the stand-in's own evaluator
+    (z3_quick_sat_loop, support_utils.py:62-66)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import fake_z3  # z3 stand-in: bench leg only
+    saved = fake_z3.install()
+    try:
+        import z3_bridge as B
+        import mythril_amd.lower_z3 as lz3
+        from mythril_amd import support as sp
+        from mythril_amd.synth_evm import dropin_workload, fork_children
+        out = []
+        for n, m in grid:
+            warm_t, recs, _ = dropin_workload(n, m, seed=seed)
+            kids_t = fork_children(warm_t, seed=seed + n)
+            sig, to = B.signature(warm_t + kids_t), B.ToZ3()
+            warm, kids = [to(e) for e in warm_t], [to(e) for e in kids_t]
+            models = [B.model_to_z3(r, sig) for r in recs]
+            eng = sp.VerdictEngine(ev)
+            cache = sp.ModelCache(eng)
+            for r in reversed(models):
+                cache.put(r, 1)
+            cache.check_quick_sat_batch(warm)
+            order_before = list(reversed(cache.model_cache.lru_cache.keys()))
+            before, st0, tr0 = dict(eng.timing), dict(eng.stats), eng._z3.translated
+            ev.time_kernels(True)
+            ev.host_times(reset=True)
+            t0 = time.perf_counter()
+            answers = cache.check_quick_sat_batch(kids)
+            wall = time.perf_counter() - t0
+            kt = ev.kernel_times(reset=True)
+            ev.time_kernels(False)
+            stages = {k: (eng.timing[k] - before[k]) * 1e3 for k in eng.timing}
+            lib_ms = {k: v * 1e3 for k, v in ev.host_times(reset=True).items()}
+            ref, _ = B.reference_replay(kids, order_before, lz3)
+            out.append({"n_parents": n, "n_queries": len(kids), "n_models": m, "ms_per_batch": wall * 1e3,
+                        "ms_per_query": wall * 1e3 / len(kids), "stage_ms": stages, "library_phase_ms": lib_ms,
+                        "kernel_ms": float(sum(kt)),
+                        "z3_asts_translated": eng._z3.translated - tr0,
+                        "conjuncts_evaluated": eng.stats["conjuncts_evaluated"] - st0["conjuncts_evaluated"],
+                        "conjuncts_cached": eng.stats["conjuncts_cached"] - st0["conjuncts_cached"],
+                        "hits": int(sum(a is not False for a in answers)),
+                        "answers_match_reference_loop": bool(all(a is b for a, b in zip(answers, ref))),
+                        "timing": "z3 stand-in (tests/fake_z3.py), not real z3"})
+            eng.close()
+        return out
+    finally:
+        fake_z3.uninstall(saved)
+
+
 def calls_avoided_leg(ev, n_forks: int = 256, n_models: int = 100, seed: int = 21, budget: int = 100_000):
     """"z3 solver calls avoided", counted where SURVEY Appendix E says: at ``get_model``
     (``support.counters``: calls, answers from quick-sat at model.py:101-103, answers from
@@ -420,25 +476,44 @@ class OracleRehearsal:
 
     rccl_active = False
 
-    def __init__(self):
+    def __init__(self, n_devices: int = 1):
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import cref  # oracle: rehearsal only
         self.cref = cref
         self.mb = None
+        self.n_devices = n_devices   # a one-process context over n "devices": contiguous model shards
         self._counts = [0.0, 0.0, 0.0]
         self._times = []
+        self._dev_times = [[] for _ in range(n_devices)]
+        self._launch = ([], [], [])
 
     def upload_models(self, mb):
+        from mythril_amd.dist import shard_bounds
         self.mb = mb
+        self.shards = [mb.shard(*shard_bounds(mb.n_models, g, self.n_devices)) for g in range(self.n_devices)]
 
     def compile(self, tb):
         from mythril_amd.evaluator import tape_alg_ops
         self.tb, self.alg = tb, np.array([tape_alg_ops(tb, t) for t in range(tb.n_tapes)])
 
     def launch_first_hit(self, best):
+        # each "device" evaluates its shard (global indices), then the MIN over devices: the
+        # in-library protocol of mq_launch_first_hit on a multi-device context
         t0 = time.perf_counter()
-        fh, pairs = self.cref.first_hit(self.tb, self.mb)
-        self._times.append((time.perf_counter() - t0) * 1e3)
+        enc = []
+        for g, sb in enumerate(self.shards):
+            t = time.perf_counter()
+            f, _ = self.cref.first_hit(self.tb, sb)
+            self._dev_times[g].append((time.perf_counter() - t) * 1e3)
+            enc.append(np.where(f < 0, np.iinfo(np.int32).max, f).astype(np.int32))
+        t1 = time.perf_counter()
+        fh = np.minimum.reduce(enc)
+        t2 = time.perf_counter()
+        self._times.append((t2 - t0) * 1e3)
+        self._launch[0].append((t2 - t1) * 1e3)
+        self._launch[1].append((t2 - t0) * 1e3)
+        self._launch[2].append((t1 - t0) * 1e3 - self._dev_times[0][-1])
+        fh = np.where(fh == np.iinfo(np.int32).max, -1, fh)
         best.copy_(torch_tensor(np.where(fh < 0, np.iinfo(np.int32).max, fh).astype(np.int32)))
         sizes = self.tb.sizes()
         evals = np.where(fh < 0, self.mb.n_models, fh - self.mb.index_base + 1).astype(np.float64)
@@ -464,6 +539,20 @@ class OracleRehearsal:
 
     def time_kernels(self, on=True):
         self._times = []
+        self._dev_times = [[] for _ in range(self.n_devices)]
+        self._launch = ([], [], [])
+
+    def kernel_times_device(self, g, reset=False):
+        t = list(self._dev_times[g])
+        if reset:
+            self._dev_times[g] = []
+        return t
+
+    def launch_times(self, reset=True):
+        t = tuple(list(x) for x in self._launch)
+        if reset:
+            self._launch = ([], [], [])
+        return t
 
 
 def torch_tensor(a):
@@ -487,6 +576,8 @@ def launch_mode(args):
             raise SystemExit(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world}")
         return "torchrun", world
     if args.gpus > 1 or getattr(args, "context", False):
+        if getattr(args, "engine", "gpu") == "oracle":
+            return "context", args.gpus   # (the CPU rehearsal: shards stand in for devices)
         import torch
         have = torch.cuda.device_count()   # does not initialise the GPU
         if have < args.gpus:
@@ -544,7 +635,7 @@ def main():
     t_gen = time.perf_counter() - t_gen
 
     if oracle:
-        ev = OracleRehearsal()
+        ev = OracleRehearsal(n_gpus if mode == "context" else 1)
         ev.upload_models(mb)
         ev.compile(tb)
         ct = None
@@ -644,6 +735,13 @@ def main():
     t_end = time.perf_counter()
     elapsed = t_end - t0
     pairs, node_evals, alg_ops = ev.counters(reset=True)
+    ctx_attr = None
+    if mode == "context":
+        # one process, N devices: each device's own kernel events, then the in-library reduce
+        # (events on the lead stream around the ncclGroup) and the host time spent issuing
+        dev_ms = [float(np.mean(ev.kernel_times_device(g, reset=False) or [0.0])) for g in range(n_gpus)]
+        red_l, iss_l, peer_l = ev.launch_times(reset=True)
+        ctx_attr = (dev_ms, red_l, iss_l, peer_l)
     ktimes = ev.kernel_times(reset=True)
     ev.time_kernels(False)
     assert len(ktimes) == args.steps, ktimes
@@ -669,6 +767,16 @@ def main():
                     for j, k in ((4, "kernel_ms"), (5, "allreduce_ms"), (6, "barrier_wait_ms"))}
         per_rank["allreduce_timer"] = "hip events on the launch stream (RCCL)" if red_ev is not None else \
             "host clock around the gloo all_reduce"
+    elif ctx_attr is not None:
+        dev_ms, red_l, iss_l, peer_l = ctx_attr
+        mean = lambda x: float(np.mean(x)) if x else 0.0  # noqa: E731
+        per_rank = {"kernel_ms": {"min": min(dev_ms), "max": max(dev_ms)},
+                    "kernel_ms_per_device": dev_ms,
+                    "allreduce_ms": {"min": mean(red_l), "max": mean(red_l)},
+                    "issue_ms": mean(iss_l), "peer_issue_ms": mean(peer_l),
+                    "barrier_wait_ms": None,
+                    "allreduce_timer": ("host clock around the MIN over shards (oracle rehearsal)" if oracle else
+                                        "hip events on the lead stream around the in-library ncclGroup")}
     hits = int((got >= 0).sum())
 
     if rank == 0:
@@ -742,6 +850,7 @@ def main():
         if n_gpus == 1 and not args.no_dropin and not oracle:
             out["dropin"] = dropin_leg(ev)
             out["dropin_stream"] = dropin_stream_leg(ev)
+            out["dropin_stream_z3stub"] = dropin_stream_z3stub_leg(ev)
             out["z3_calls_avoided"] = calls_avoided_leg(ev)
             out["keccak_service"] = keccak_leg(ev)
         print(json.dumps(out), flush=True)

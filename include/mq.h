@@ -325,6 +325,21 @@ int mq_ctx_set_option(mq_ctx* ctx, int option, int value);
    (may exceed max_out; only max_out are written).  reset != 0 forgets them. */
 int mq_kernel_times(mq_ctx* ctx, float* out_ms, int32_t max_out, int32_t* n_out, int reset);
 
+/* The same for ONE device of a multi-device context (device_index 0 = the lead, i = dev_ids[i]),
+   so a one-process N-GPU launch is attributable per device.  reset != 0 forgets that device's
+   records only.  No reference counterpart (SURVEY §8(e) measurement). */
+int mq_kernel_times_device(mq_ctx* ctx, int32_t device_index, float* out_ms, int32_t max_out, int32_t* n_out,
+                           int reset);
+
+/* Per mq_launch_first_hit since the last reset, on a context that reduces in-library
+   (MQ_OPT_USE_RCCL) with MQ_OPT_TIME_KERNELS on: reduce_ms[i] = HIP events on the lead stream
+   around the ncclGroup of the MIN all-reduce; issue_ms[i] = host milliseconds the call spent
+   issuing every device's kernels and the reduce; peer_issue_ms[i] = the peers' share of it (their
+   launches are issued one after another from the calling thread).  Waits for the reduce events.
+   *n_out = number recorded (only max_out written).  No reference counterpart. */
+int mq_launch_times(mq_ctx* ctx, float* reduce_ms, double* issue_ms, double* peer_issue_ms, int32_t max_out,
+                    int32_t* n_out, int reset);
+
 /* Diagnostic: host seconds this context spent per phase since the last reset (out[i], i <
    MQ_HOST_PHASES; *n_out = MQ_HOST_PHASES): 0 DAG expansion + tape compilation, 1 structural
    P/G translation at upload, 2 tape upload, 3 P translation at launch, 4 G translation at

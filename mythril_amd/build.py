@@ -82,6 +82,9 @@ def build_lowerwalk(force: bool = False) -> str:
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
+    # the host-only lowering walk first: it needs no ROCm toolchain, and lower.py uses it whether
+    # or not the HIP build below succeeds
+    build_lowerwalk(force)
     hipcc = _hipcc()
     if force or not _generated_current():
         subprocess.check_call([sys.executable, os.path.join(CSRC, "gen_qsa.py")])
@@ -108,7 +111,6 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if res.returncode:
             sys.stderr.write(res.stderr)
             raise RuntimeError("link failed")
-    build_lowerwalk(force)
     tool = os.path.join(HERE, "valu_peak")
     tsrc = os.path.join(CSRC, "valu_peak.hip")
     if force or not os.path.exists(tool) or os.path.getmtime(tool) < os.path.getmtime(tsrc):

@@ -347,18 +347,13 @@ __global__ __launch_bounds__(256) void fca_kernel(const FcaGroup* __restrict__ g
       run_nodes += tape_metric[2 * t];
       run_ops += tape_metric[2 * t + 1];
       if (MODE == 3) {
-        // a Bool column: its tiles' lane masks, and its 0/1 row where a HIP C++ kernel reads rows
-        // or it has no mask index (one lane per column: these row stores do not coalesce; the
-        // assembly-only launches C4 / C3 / C5 make need none)
+        // a Bool column: its tiles' lane masks (its 0/1 row, where one is needed, below)
         const int32_t mo = r.col_mask[t];
+        if (mo >= 0) {
 #pragma unroll
-        for (int j = 0; j < FC_TILES; j++) {
-          const int64_t mt = m0 + 64 * j;
-          if (mt >= r.M) break;
-          if (mo >= 0) r.bool_masks_out[(tile0 + j) * (int64_t)r.n_bool_masks + mo] = acc[j];
-          if (r.bool_rows || mo < 0) {
-            const int lim = (int)min<int64_t>(64, r.M - mt);
-            for (int q = 0; q < lim; q++) r.vars_out[(int64_t)row * r.M + mt + q] = (uint32_t)((acc[j] >> q) & 1u);
+          for (int j = 0; j < FC_TILES; j++) {
+            if (m0 + 64 * j >= r.M) break;
+            r.bool_masks_out[(tile0 + j) * (int64_t)r.n_bool_masks + mo] = acc[j];
           }
         }
       } else if (MODE == 0) {
@@ -384,6 +379,26 @@ __global__ __launch_bounds__(256) void fca_kernel(const FcaGroup* __restrict__ g
             const int lim = (int)min<int64_t>(64, r.M - mt);
             for (int q = 0; q < lim; q++) vrow[q] = (uint8_t)((acc[j] >> q) & 1u);
           }
+        }
+      }
+    }
+    if (MODE == 3) {
+      // 0/1 rows of the chunk's Bool columns that need one (a HIP C++ kernel reads rows, or the
+      // column has no mask index): the wave writes them one column at a time, lane l storing model
+      // mt + l of the column's lane mask (broadcast from its lane), so every store is a coalesced
+      // 256-byte row segment instead of 64 serial stores by the column's own lane
+      uint64_t pend = __ballot(run && (r.bool_rows || r.col_mask[live ? t : 0] < 0));
+      while (pend) {
+        const int q = __builtin_ctzll(pend);
+        pend &= pend - 1;
+        const int64_t rq = (int64_t)__shfl((int)row, q);
+#pragma unroll
+        for (int j = 0; j < FC_TILES; j++) {
+          const int64_t mt = m0 + 64 * j;
+          if (mt >= r.M) break;
+          const uint64_t aq = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(acc[j] >> 32), q) << 32) |
+                              (uint32_t)__shfl((int)(uint32_t)acc[j], q);
+          if (mt + lane < r.M) r.vars_out[rq * r.M + mt + lane] = (uint32_t)((aq >> lane) & 1u);
         }
       }
     }

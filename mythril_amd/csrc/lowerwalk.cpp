@@ -19,6 +19,48 @@
 #include <cstring>
 #include <vector>
 
+// Non-negative int that fits in w bits / its little-endian bytes.  CPython's private long API
+// (_PyLong_Sign, _PyLong_NumBits, _PyLong_AsByteArray) changed in 3.13 (_PyLong_AsByteArray gained
+// a with_exceptions argument): from 3.13 on the public PyLong_AsNativeBytes is used instead.
+static bool long_fits_unsigned(PyObject* v, long w) {
+#if PY_VERSION_HEX >= 0x030D0000
+  const int neg = PyObject_RichCompareBool(v, Py_False, Py_LT);   // (False == 0)
+  if (neg != 0) {
+    if (neg < 0) PyErr_Clear();
+    return false;
+  }
+  PyObject* wo = PyLong_FromLong(w);
+  PyObject* hi = wo ? PyNumber_Rshift(v, wo) : nullptr;
+  Py_XDECREF(wo);
+  if (!hi) {
+    PyErr_Clear();
+    return false;
+  }
+  const int nz = PyObject_IsTrue(hi);
+  Py_DECREF(hi);
+  if (nz < 0) PyErr_Clear();
+  return nz == 0;
+#else
+  return _PyLong_Sign(v) >= 0 && _PyLong_NumBits(v) <= (size_t)w;
+#endif
+}
+
+// v >= 0 into n little-endian bytes (v fits: masked by the caller); 0 on success, -1 on error
+static int long_le_bytes(PyObject* v, unsigned char* buf, size_t n) {
+#if PY_VERSION_HEX >= 0x030D0000
+  const Py_ssize_t need = PyLong_AsNativeBytes(v, buf, (Py_ssize_t)n,
+                                               Py_ASNATIVEBYTES_LITTLE_ENDIAN | Py_ASNATIVEBYTES_UNSIGNED_BUFFER);
+  if (need < 0) return -1;
+  if ((size_t)need > n) {
+    PyErr_SetString(PyExc_OverflowError, "lowerwalk: constant wider than its width");
+    return -1;
+  }
+  return 0;
+#else
+  return _PyLong_AsByteArray((PyLongObject*)v, buf, n, 1, 0);
+#endif
+}
+
 namespace {
 
 struct State {
@@ -111,7 +153,7 @@ PyObject* fast_node(const State& s, PyObject* t, long code, PyObject* k, const l
     // v = params[0] & ((1 << w) - 1)
     PyObject* p0 = PyTuple_GET_ITEM(params, 0);
     PyObject* v;
-    if (PyLong_CheckExact(p0) && _PyLong_Sign(p0) >= 0 && _PyLong_NumBits(p0) <= (size_t)w) {
+    if (PyLong_CheckExact(p0) && long_fits_unsigned(p0, w)) {
       Py_INCREF(p0);
       v = p0;
     } else {
@@ -137,7 +179,7 @@ PyObject* fast_node(const State& s, PyObject* t, long code, PyObject* k, const l
       off = PyLong_FromSsize_t(PyList_GET_SIZE(s.consts));
       const size_t nw = (size_t)(w + 31) / 32;
       std::vector<unsigned char> buf(nw * 4);
-      int rc = off ? _PyLong_AsByteArray((PyLongObject*)v, buf.data(), buf.size(), 1, 0) : -1;
+      int rc = off ? long_le_bytes(v, buf.data(), buf.size()) : -1;
       for (size_t i = 0; rc == 0 && i < nw; i++) {
         const unsigned long x = (unsigned long)buf[4 * i] | ((unsigned long)buf[4 * i + 1] << 8) |
                                 ((unsigned long)buf[4 * i + 2] << 16) | ((unsigned long)buf[4 * i + 3] << 24);

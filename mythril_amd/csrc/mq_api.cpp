@@ -325,6 +325,13 @@ struct mq_ctx {
   int time_kernels = 0;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> kev;
   size_t kev_used = 0;
+  // ... and, on a context that reduces in-library (comms), per launch: the event pair around the
+  // ncclGroup of the MIN all-reduce on the lead stream, the host milliseconds the launch call
+  // spent issuing every device's kernels and the reduce, and those of the peers' launch loop
+  // (mq_launch_times)
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> rev;
+  size_t rev_used = 0;
+  std::vector<double> issue_ms, peer_issue_ms;
   // Several devices from one process (mq_ctx_create(n_dev > 1)): this context is
   // the lead (dev_ids[0]); peers[i] is a single-device context on dev_ids[i + 1].  The candidate
   // axis is split contiguously over [lead, peers...] (shard_lo[g] = first local model of device
@@ -858,6 +865,10 @@ void mq_ctx_destroy(mq_ctx* c) {
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   for (auto& e : c->kev) {
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  for (auto& e : c->rev) {
     (void)hipEventDestroy(e.first);
     (void)hipEventDestroy(e.second);
   }
@@ -4191,6 +4202,45 @@ static int kernel_times_one(mq_ctx* c, std::vector<float>& ms_out, int reset) {
   return MQ_OK;
 }
 
+int mq_kernel_times_device(mq_ctx* c, int32_t device_index, float* out_ms, int32_t max_out, int32_t* n_out,
+                           int reset) {
+  if (!c || (max_out > 0 && !out_ms)) return MQ_ERR_ARG;
+  const std::vector<mq_ctx*> devs = devices_of(c);
+  if (device_index < 0 || device_index >= (int32_t)devs.size()) return MQ_ERR_ARG;
+  std::vector<float> one;
+  const int rc = kernel_times_one(devs[device_index], one, reset);
+  HIPCHK(hipSetDevice(c->device));
+  if (rc) return rc;
+  const int32_t n = (int32_t)one.size();
+  for (int32_t i = 0; i < n && i < max_out; i++) out_ms[i] = one[i];
+  if (n_out) *n_out = n;
+  return MQ_OK;
+}
+
+int mq_launch_times(mq_ctx* c, float* reduce_ms, double* issue_ms, double* peer_issue_ms, int32_t max_out,
+                    int32_t* n_out, int reset) {
+  if (!c || !n_out || (max_out > 0 && (!reduce_ms || !issue_ms || !peer_issue_ms))) return MQ_ERR_ARG;
+  HIPCHK(hipSetDevice(c->device));
+  const int32_t n = (int32_t)c->issue_ms.size();
+  for (int32_t i = 0; i < n && i < max_out; i++) {
+    float ms = 0.f;
+    if ((size_t)i < c->rev_used) {
+      HIPCHK(hipEventSynchronize(c->rev[i].second));
+      HIPCHK(hipEventElapsedTime(&ms, c->rev[i].first, c->rev[i].second));
+    }
+    reduce_ms[i] = ms;
+    issue_ms[i] = c->issue_ms[i];
+    peer_issue_ms[i] = c->peer_issue_ms[i];
+  }
+  *n_out = n;
+  if (reset) {
+    c->rev_used = 0;
+    c->issue_ms.clear();
+    c->peer_issue_ms.clear();
+  }
+  return MQ_OK;
+}
+
 int mq_kernel_times(mq_ctx* c, float* out_ms, int32_t max_out, int32_t* n_out, int reset) {
   if (!c || (max_out > 0 && !out_ms)) return MQ_ERR_ARG;
   // several devices: launch i took as long as its slowest device
@@ -4221,6 +4271,8 @@ int mq_launch_first_hit(mq_ctx* c, mq_tapes* T, int32_t* d_best, void* stream) {
   if (T->ctx != c || T->peers.size() != c->peers.size()) return MQ_ERR_STATE;
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
   if (st != c->stream) DevPool::get().mark_foreign(c->device);
+  using clk = std::chrono::steady_clock;
+  const clk::time_point t0 = clk::now();
   int rc = launch_one(c, T, d_best, st);
   if (rc || c->comms.empty()) return rc;
   // every device evaluates its contiguous shard of candidates (global indices), then ONE RCCL
@@ -4228,6 +4280,7 @@ int mq_launch_first_hit(mq_ctx* c, mq_tapes* T, int32_t* d_best, void* stream) {
   std::vector<mq_ctx*> devs = devices_of(c);
   std::vector<int32_t*> bufs{d_best};
   std::vector<hipStream_t> streams{st};
+  const clk::time_point t1 = clk::now();
   for (size_t i = 0; i < c->peers.size(); i++) {
     mq_ctx* p = c->peers[i];
     HIPCHK(hipSetDevice(p->device));
@@ -4236,6 +4289,19 @@ int mq_launch_first_hit(mq_ctx* c, mq_tapes* T, int32_t* d_best, void* stream) {
     if (rc) return rc;
     bufs.push_back(p->best_tmp.as<int32_t>());
     streams.push_back(p->stream);
+  }
+  const clk::time_point t2 = clk::now();
+  std::pair<hipEvent_t, hipEvent_t>* re = nullptr;
+  if (c->time_kernels) {
+    HIPCHK(hipSetDevice(c->device));
+    if (c->rev_used == c->rev.size()) {
+      std::pair<hipEvent_t, hipEvent_t> e{};
+      HIPCHK(hipEventCreate(&e.first));
+      HIPCHK(hipEventCreate(&e.second));
+      c->rev.push_back(e);
+    }
+    re = &c->rev[c->rev_used++];
+    HIPCHK(hipEventRecord(re->first, st));
   }
   if (T->n_tapes > 0) {
     ncclResult_t r = ncclGroupStart();
@@ -4246,6 +4312,12 @@ int mq_launch_first_hit(mq_ctx* c, mq_tapes* T, int32_t* d_best, void* stream) {
     if (r2 != ncclSuccess) return rccl_fail(r2, "ncclGroupEnd");
   }
   HIPCHK(hipSetDevice(c->device));
+  if (re) {
+    HIPCHK(hipEventRecord(re->second, st));
+    const clk::time_point t3 = clk::now();
+    c->issue_ms.push_back(std::chrono::duration<double, std::milli>(t3 - t0).count());
+    c->peer_issue_ms.push_back(std::chrono::duration<double, std::milli>(t2 - t1).count());
+  }
   return MQ_OK;
 }
 
@@ -4442,6 +4514,9 @@ int mq_ctx_set_option(mq_ctx* c, int option, int value) {
     case MQ_OPT_TIME_KERNELS:
       c->time_kernels = value ? 1 : 0;
       c->kev_used = 0;
+      c->rev_used = 0;
+      c->issue_ms.clear();
+      c->peer_issue_ms.clear();
       return MQ_OK;
     default: return MQ_ERR_ARG;
   }

@@ -59,6 +59,10 @@ def load_library(path: str = LIB_PATH):
         L.mq_counters.argtypes = [P, C.POINTER(C.c_double), C.c_int]
         L.mq_ctx_set_option.argtypes = [P, C.c_int, C.c_int]
         L.mq_kernel_times.argtypes = [P, C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_int32), C.c_int]
+        L.mq_kernel_times_device.argtypes = [P, C.c_int32, C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_int32),
+                                             C.c_int]
+        L.mq_launch_times.argtypes = [P, C.POINTER(C.c_float), C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                      C.c_int32, C.POINTER(C.c_int32), C.c_int]
         L.mq_host_times.argtypes = [P, C.POINTER(C.c_double), C.c_int32, C.POINTER(C.c_int32), C.c_int]
         L.mq_tapes_info.argtypes = [P] + [C.POINTER(C.c_int32)] * 3
         L.mq_tapes_qsa_split.argtypes = [P] + [C.POINTER(C.c_int32)] * 3
@@ -452,6 +456,31 @@ class Evaluator:
         buf = (C.c_float * max(n.value, 1))()
         _check(self.lib.mq_kernel_times(self.ctx, buf, n.value, C.byref(n), 1 if reset else 0), "mq_kernel_times")
         return [float(buf[i]) for i in range(n.value)]
+
+    def kernel_times_device(self, device_index: int, reset: bool = False) -> List[float]:
+        """``kernel_times`` of one device of a multi-device context (0 = the lead)."""
+        n = C.c_int32()
+        f = self.lib.mq_kernel_times_device
+        _check(f(self.ctx, device_index, None, 0, C.byref(n), 0), "mq_kernel_times_device")
+        buf = (C.c_float * max(n.value, 1))()
+        _check(f(self.ctx, device_index, buf, n.value, C.byref(n), 1 if reset else 0), "mq_kernel_times_device")
+        return [float(buf[i]) for i in range(n.value)]
+
+    def launch_times(self, reset: bool = True):
+        """Per launch on an in-library-reducing context (mq_launch_times): (reduce ms on the lead
+        stream, host issue ms of the whole launch call, host issue ms of the peers' loop)."""
+        n = C.c_int32()
+        f = self.lib.mq_launch_times
+        _check(f(self.ctx, None, None, None, 0, C.byref(n), 0), "mq_launch_times")
+        k = max(n.value, 1)
+        red, iss, peer = (C.c_float * k)(), (C.c_double * k)(), (C.c_double * k)()
+        _check(f(self.ctx, red, iss, peer, n.value, C.byref(n), 1 if reset else 0), "mq_launch_times")
+        return [float(red[i]) for i in range(n.value)], [float(iss[i]) for i in range(n.value)], \
+            [float(peer[i]) for i in range(n.value)]
+
+    @property
+    def n_devices(self) -> int:
+        return len(self.devices)
 
     HOST_PHASES = ("compile", "translate_upload", "tape_upload", "translate_p", "translate_g", "program_upload",
                    "args_upload", "launch_readback", "model_upload", "tape_free")

@@ -738,18 +738,21 @@ _WALKER = []
 
 
 def _walker():
-    """The C++ term walk (csrc/lowerwalk.cpp, built by build.py next to this file).  Required:
-    MQ_PY_LOWER=1 selects the Python loop of IncrementalLowering._lower instead (the tests
-    compare the two)."""
+    """The C++ term walk (csrc/lowerwalk.cpp, built by build.py next to this file), or None: the
+    Python loop of IncrementalLowering._lower, which builds the same DAG (the tests compare the
+    two) — selected by MQ_PY_LOWER=1, and the fallback (with one warning) where the extension is
+    not built."""
     if os.environ.get("MQ_PY_LOWER") == "1":
         return None
     if not _WALKER:
         try:
             from . import _lowerwalk
+            _lowerwalk.bind(S.Term)
         except ImportError as e:
-            raise ImportError("mythril_amd._lowerwalk is not built (python -m mythril_amd.build); "
-                              "MQ_PY_LOWER=1 runs the Python lowering walk instead") from e
-        _lowerwalk.bind(S.Term)
+            import warnings
+            warnings.warn(f"mythril_amd._lowerwalk is not built ({e}; python -m mythril_amd.build): "
+                          "the drop-in lowering uses the slower Python walk", RuntimeWarning)
+            _lowerwalk = None
         _WALKER.append(_lowerwalk)
     return _WALKER[0]
 

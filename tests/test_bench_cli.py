@@ -85,3 +85,26 @@ def test_two_rank_line_under_gloo_with_the_oracle_engine():
     for k in ("kernel_ms", "allreduce_ms", "barrier_wait_ms"):
         assert 0 <= pr[k]["min"] <= pr[k]["max"], (k, pr[k])
     assert line["engine"].startswith("oracle")
+
+
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_context_mode_line_is_attributable_with_the_oracle_engine(gpus):
+    """One process driving N devices (--context, the way single-process Mythril would,
+    mythril_analyzer.py:136-185), rehearsed on CPU with the oracle answering per model shard:
+    the line carries each device's kernel time, the reduce and the host issue time."""
+    import json
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--context",
+                        "--engine", "oracle", "--config", "c2", "--tapes", "40", "--models", "64", "--steps", "2",
+                        "--warmup", "1", "--no-dropin", "--no-cpu-baseline"],
+                       capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == gpus and line["parity_ok"] is True
+    assert line["config"]["models_total"] == 64 * gpus
+    pr = line["per_rank"]
+    assert len(pr["kernel_ms_per_device"]) == gpus
+    assert 0 <= pr["kernel_ms"]["min"] <= pr["kernel_ms"]["max"]
+    assert pr["kernel_ms"]["max"] == max(pr["kernel_ms_per_device"])
+    assert pr["allreduce_ms"]["min"] >= 0 and pr["issue_ms"] >= pr["peer_issue_ms"] >= 0
+    assert "oracle" in pr["allreduce_timer"]

@@ -1454,3 +1454,45 @@ def test_state_merge_array_ite_matches_oracle(evaluator, hoist):
     direct = np.array([[term_eval.is_true(e, m) for m in recs[:40]] for e in exprs])
     assert (v[:, :40] == direct).all()
     assert v.any() and (~v).any()
+
+
+def test_p_section_lengths_every_residue_with_packed_g_columns(evaluator):
+    """The r05ak fault class (packed column programs): G's program windows are the
+    buffer's aligned 64-word blocks and the G section follows the P section, so a P section of any
+    length mod 64 must leave G's programs (and the packed column programs, which start mid-block)
+    decoding their own words.  One mixed batch per P-section length — EVM-shaped paths (G tapes,
+    hoisted columns on G / the gather / flat kernels) plus P tapes whose handler count steps by
+    one — over every residue mod 64, verdicts against the oracle on the unhoisted lowering."""
+    from mythril_amd import smt as S
+    from mythril_amd.lower import lower_batch, serialize_models
+    from mythril_amd.smt_model import Model
+    from mythril_amd.synth_evm import dropin_workload
+    paths, recs, _ = dropin_workload(12, 200, seed=17, planted_frac=0.5)
+    p = [S.BitVecSym(f"p{i}", 256) for i in range(3)]
+    rng = np.random.default_rng(3)
+    recs = [Model({**r.assignment, **{f"p{i}": int(rng.integers(0, 1 << 20)) for i in range(3)}}, r.functions)
+            for r in recs]
+    residues = set()
+    for k in range(64):
+        acc = p[0] * p[1]
+        for j in range(k):
+            acc = acc + S.BitVecVal(int(rng.integers(1, 1 << 30)), 256)
+        ptapes = [S.ULT(acc, p[2] * S.BitVecVal(1 << 20, 256)), S.ULT(p[1] + p[2], acc)]
+        roots = ptapes + paths
+        tb, syms, ok = lower_batch(roots, hoist=True)
+        assert ok.all() and tb.columns is not None and tb.columns.n > 0
+        mb = serialize_models(recs, syms)
+        tb0, syms0, _ = lower_batch(roots)
+        mb0 = serialize_models(recs, syms0)
+        evaluator.upload_models(mb)
+        ct = evaluator.compile(tb)
+        v, fh = evaluator.verdicts(ct)
+        n_p, n_g, live = ct.asm_split()
+        assert live and n_p >= 2 and n_g > 0, (n_p, n_g, live)
+        assert ct.column_asm_split()[0] > 0
+        residues.add(int(sum(ct.handler_histogram(0).values())) % 64)
+        vref = cref.verdicts(tb0, mb0)
+        assert (v == vref).all(), (k, np.argwhere(v != vref)[:5])
+        assert (fh == cref.first_hit(tb0, mb0)[0]).all()
+        ct.free()
+    assert len(residues) == 64, sorted(set(range(64)) - residues)

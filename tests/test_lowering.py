@@ -471,3 +471,20 @@ def test_state_merge_array_ite_lowers_and_agrees_with_term_evaluation():
     a, b = S.Array("A", 256, 256), S.Array("B", 256, 256)
     _, _, ok = lower_batch([S.Term(S.EQ, "bool", 0, (a, b)), exprs[0]])
     assert ok.tolist() == [False, True]
+
+
+def test_missing_native_walk_falls_back_to_the_python_walk(monkeypatch):
+    """Without the built extension (mythril_amd._lowerwalk) the drop-in lowering warns once and
+    uses the Python walk, which builds the same DAG."""
+    import sys
+    from mythril_amd import lower as L
+    from mythril_amd.synth_evm import dropin_workload
+    exprs, recs, _ = dropin_workload(4, 6, seed=2)
+    want = L.IncrementalLowering().lower(exprs)[0]
+    monkeypatch.setattr(L, "_WALKER", [])
+    monkeypatch.setitem(sys.modules, "mythril_amd._lowerwalk", None)   # import -> ImportError
+    monkeypatch.delattr(sys.modules["mythril_amd"], "_lowerwalk", raising=False)
+    with pytest.warns(RuntimeWarning, match="Python walk"):
+        assert L._walker() is None
+    got = L.IncrementalLowering().lower(exprs)[0]
+    assert (got.nodes == want.nodes).all() and (got.roots == want.roots).all()
