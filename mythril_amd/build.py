@@ -72,7 +72,7 @@ def build_lowerwalk(force: bool = False) -> str:
     src = os.path.join(CSRC, "lowerwalk.cpp")
     out = os.path.join(HERE, "_lowerwalk" + sysconfig.get_config_var("EXT_SUFFIX"))
     if force or not os.path.exists(out) or os.path.getmtime(out) < os.path.getmtime(src):
-        cmd = [os.environ.get("CXX", "g++"), "-O2", "-shared", "-fPIC", "-std=c++17", "-Wall",
+        cmd = [os.environ.get("CXX", "g++"), "-O2", "-shared", "-fPIC", "-std=c++17", "-Wall", "-pthread",
                f"-I{sysconfig.get_paths()['include']}", src, "-o", out]
         res = subprocess.run(cmd, capture_output=True, text=True)
         if res.returncode:

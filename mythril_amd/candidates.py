@@ -30,6 +30,7 @@ callers (``Constraints.is_possible``), never for callers that read model content
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -153,6 +154,98 @@ def _wanted(op: int, const_left: bool, c: int, w: int, positive: Optional[bool])
         return [lo_side, 0] if positive else [c if strict else (c + 1) & m]
     hi_side = (c + 1) & m if strict else c
     return [hi_side, m >> (1 if op in (_SLT, _SLE) else 0)] if positive else [c if strict else (c - 1) & m]
+
+
+def _candidate_rows(lru: ModelBatch, src: np.ndarray, starts: np.ndarray, sizes: np.ndarray,
+                    blocks: List[Tuple[Tuple, np.ndarray]], syms, off: np.ndarray, K: int) -> np.ndarray:
+    """The whole batch's variable rows [rows, n_lru + K]: the LRU's, then each generated
+    candidate's base LRU row with its block's patch applied — value assignments in patch order
+    (the last assignment of a bit wins), then the size floors.  The host extension's loop
+    (csrc/lowerwalk.cpp candidate_rows, writing the candidates' columns in place); the numpy form
+    below where it is not built (the tests compare the two)."""
+    from .lower import _walker
+    n_lru = lru.n_models
+    walker = _walker()
+    if walker is not None and n_lru and K and os.environ.get("MQ_PY_CANDIDATES") != "1":
+        words = np.empty((int(off[-1]), n_lru + K), np.uint32)
+        words[:, :n_lru] = lru.var_words
+        gen = words[:, n_lru:]
+        widths = syms.var_widths
+        walker.candidate_rows(gen, np.ascontiguousarray(lru.var_words, np.uint32), np.ascontiguousarray(src, np.int64),
+                              np.ascontiguousarray(starts, np.int64), [p for p, _ in blocks],
+                              np.ascontiguousarray(off[:-1], np.int64),
+                              np.asarray([limbs(w) for w in widths], np.int64))
+        return words
+    gen = lru.var_words[:, src].copy() if n_lru else np.zeros((int(off[-1]), K), np.uint32)
+    # each block's patch over its candidate range.  Per (limb row, block) the composed update
+    # (mask, bits) of the block's value assignments, in patch order (the last assignment of a
+    # bit wins); the limb updates of a patch element are computed once (elements recur in many
+    # blocks: the random mixes reuse the directed singles).  Then ONE vectorised update per
+    # row over every block that patches it, and the size floors (applied after the values of
+    # their block) per variable
+    widths = syms.var_widths
+    cache: Dict[Tuple, List[Tuple[int, int, int]]] = {}
+    row_ops: Dict[int, Dict[int, List[int]]] = {}
+    floor_ops: Dict[int, Dict[int, int]] = {}
+    for j, (patch, _) in enumerate(blocks):
+        for el in patch:
+            v, lo, n, bits = el
+            if lo < 0:   # size >= minimum (values < 2^32 in their low limb)
+                fj = floor_ops.setdefault(v, {})
+                fj[j] = max(fj.get(j, 0), bits)
+                continue
+            ups = cache.get(el)
+            if ups is None:
+                ups = []
+                o = int(off[v])
+                for i in range(lo // 32, (lo + n - 1) // 32 + 1):
+                    blo = 32 * i
+                    a, b2 = max(lo, blo), min(lo + n, blo + 32)
+                    mask = ((1 << (b2 - a)) - 1) << (a - blo)
+                    ups.append((o + i, mask, ((bits >> (a - lo)) << (a - blo)) & mask))
+                cache[el] = ups
+            for row, mask, val in ups:
+                d = row_ops.get(row)
+                if d is None:
+                    d = row_ops[row] = {}
+                c = d.get(j)
+                if c is None:
+                    d[j] = [mask, val]
+                else:
+                    c[1] = (c[1] & ~mask) | val
+                    c[0] |= mask
+    nb = int(sizes.max()) if len(sizes) else 0
+    ar = np.arange(nb, dtype=np.int64)
+
+    def cols_of(js: np.ndarray):
+        """(block columns [k, nb] of the full-size blocks among js, their positions in js, the others)."""
+        full = sizes[js] == nb
+        return starts[js[full]][:, None] + ar[None, :], np.flatnonzero(full), np.flatnonzero(~full)
+
+    for row, d in row_ops.items():
+        js = np.fromiter(d.keys(), np.int64, len(d))
+        mv = np.asarray(list(d.values()), np.uint64).astype(np.uint32).reshape(-1, 2)
+        keep, val = ~mv[:, 0], mv[:, 1]
+        cols, fi, pi = cols_of(js)
+        if len(fi):
+            gen[row, cols] = (gen[row, cols] & keep[fi][:, None]) | val[fi][:, None]
+        for k in pi:   # (a partial block: the budget's last random block)
+            sl = slice(int(starts[js[k]]), int(starts[js[k] + 1]))
+            gen[row, sl] = (gen[row, sl] & keep[k]) | val[k]
+    for v, fj in floor_ops.items():
+        r0, nl = int(off[v]), limbs(widths[v])
+        js = np.fromiter(fj.keys(), np.int64, len(fj))
+        mins = np.fromiter(fj.values(), np.int64, len(fj)).astype(np.uint32)
+        cols, fi, pi = cols_of(js)
+        groups = [(cols, mins[fi][:, None])] + [(np.arange(int(starts[js[k]]), int(starts[js[k] + 1]))[None, :],
+                                                 mins[k:k + 1][:, None]) for k in pi]
+        for cc, mn in groups:
+            if not cc.size:
+                continue
+            x = gen[r0, cc]
+            small = ~gen[r0 + 1:r0 + nl][:, cc].any(axis=0) if nl > 1 else np.ones(x.shape, bool)
+            gen[r0, cc] = np.where(small & (x < mn), mn, x)
+    return np.concatenate([lru.var_words, gen], axis=1)
 
 
 class CandidateSet:
@@ -354,27 +447,7 @@ class CandidateGenerator:
         starts = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
         off = lru.var_word_offsets()
         src = np.where(base >= 0, base, 0)
-        gen = lru.var_words[:, src].copy() if n_lru else np.zeros((int(off[-1]), K), np.uint32)
-        # each block's patch over its candidate range: value assignments, then size floors
-        for j, (patch, _) in enumerate(blocks):
-            sl = slice(int(starts[j]), int(starts[j + 1]))
-            for v, lo, n, bits in sorted(patch, key=lambda p: p[1] < 0):
-                if lo < 0:   # size >= minimum (values < 2^32 in their low limb)
-                    r0, nl = int(off[v]), limbs(syms.var_widths[v])
-                    small = ~gen[r0 + 1:r0 + nl, sl].any(axis=0) if nl > 1 else np.ones(sl.stop - sl.start, bool)
-                    low = small & (gen[r0, sl] < np.uint32(bits))
-                    gen[r0, sl][low] = np.uint32(bits)
-                    continue
-                for i in range(limbs(syms.var_widths[v])):
-                    blo, bhi = 32 * i, 32 * i + 32
-                    a, b2 = max(lo, blo), min(lo + n, bhi)
-                    if a >= b2:
-                        continue
-                    mask = ((1 << (b2 - a)) - 1) << (a - blo)
-                    val = ((bits >> (a - lo)) << (a - blo)) & mask
-                    row = int(off[v]) + i
-                    gen[row, sl] = (gen[row, sl] & np.uint32(~mask & 0xFFFFFFFF)) | np.uint32(val)
-        words = np.concatenate([lru.var_words, gen], axis=1)
+        words = _candidate_rows(lru, src, starts, sizes, blocks, syms, off, K)
         M = n_lru + K
         if not lru.funcs:
             return CandidateSet(ModelBatch(lru.var_widths, words), n_lru, base, block_of,

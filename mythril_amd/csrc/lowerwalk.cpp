@@ -16,6 +16,8 @@
 #include <structmember.h>
 
 #include <cstdint>
+#include <algorithm>
+#include <thread>
 #include <cstring>
 #include <vector>
 
@@ -502,7 +504,172 @@ PyObject* py_pack_nodes(PyObject*, PyObject* a) {
   Py_RETURN_NONE;
 }
 
+// candidate_rows(gen, lru, src, starts, patches, var_off, var_limbs): the generated candidates'
+// variable rows (candidates.py CandidateGenerator._serialize).  gen: writable u32 [R, K] (rows may
+// be strided: the candidates' columns of the whole batch's rows); lru: u32
+// [R, n_lru] (the LRU's rows); src: i64 [K] base model of each candidate; starts: i64 [B + 1]
+// block column ranges; patches: B tuples of (var, lo, n_bits, bits) applied in order over their
+// block (value assignments; lo < 0: a size floor "var >= bits when var < 2^32", applied after the
+// block's values); var_off / var_limbs: i64 [V] first row and limb count of each variable.
+struct Buf {
+  Py_buffer b{};
+  bool ok = false;
+  ~Buf() { if (ok) PyBuffer_Release(&b); }
+};
+
+static bool get_buf(PyObject* o, Buf& out, bool writable, Py_ssize_t itemsize, const char* what, bool strided = false) {
+  const int flags = (writable ? PyBUF_WRITABLE : 0) | (strided ? PyBUF_STRIDES : PyBUF_C_CONTIGUOUS) | PyBUF_FORMAT;
+  if (PyObject_GetBuffer(o, &out.b, flags) < 0) return false;
+  out.ok = true;
+  if (out.b.itemsize != itemsize) {
+    PyErr_Format(PyExc_TypeError, "candidate_rows: %s has item size %zd, not %zd", what, out.b.itemsize, itemsize);
+    return false;
+  }
+  return true;
+}
+
+// bits [b0, b0 + n) (n <= 32) of the little-endian word array w
+static inline uint32_t bits_at(const std::vector<uint32_t>& w, int64_t b0, int n) {
+  const size_t i = (size_t)(b0 >> 5);
+  const int sh = (int)(b0 & 31);
+  uint64_t x = i < w.size() ? w[i] : 0;
+  if (i + 1 < w.size()) x |= (uint64_t)w[i + 1] << 32;
+  x >>= sh;
+  return (uint32_t)(x & (n >= 32 ? 0xFFFFFFFFull : ((1ull << n) - 1)));
+}
+
+PyObject* py_candidate_rows(PyObject*, PyObject* a) {
+  PyObject *o_gen, *o_lru, *o_src, *o_starts, *patches, *o_off, *o_nl;
+  if (!PyArg_ParseTuple(a, "OOOOOOO", &o_gen, &o_lru, &o_src, &o_starts, &patches, &o_off, &o_nl)) return nullptr;
+  Buf gen, lru, src, starts, off, nl;
+  if (!get_buf(o_gen, gen, true, 4, "gen", true) || !get_buf(o_lru, lru, false, 4, "lru") ||
+      !get_buf(o_src, src, false, 8, "src") || !get_buf(o_starts, starts, false, 8, "starts") ||
+      !get_buf(o_off, off, false, 8, "var_off") || !get_buf(o_nl, nl, false, 8, "var_limbs"))
+    return nullptr;
+  if (gen.b.ndim != 2 || lru.b.ndim != 2 || gen.b.shape[0] != lru.b.shape[0] || !PyList_Check(patches) ||
+      gen.b.strides[1] != 4 || gen.b.strides[0] % 4 != 0 || gen.b.strides[0] < 4 * gen.b.shape[1]) {
+    PyErr_SetString(PyExc_ValueError, "candidate_rows: shapes");
+    return nullptr;
+  }
+  uint32_t* G = (uint32_t*)gen.b.buf;
+  const uint32_t* L = (const uint32_t*)lru.b.buf;
+  const int64_t* S = (const int64_t*)src.b.buf;
+  const int64_t* ST = (const int64_t*)starts.b.buf;
+  const int64_t* VO = (const int64_t*)off.b.buf;
+  const int64_t* VL = (const int64_t*)nl.b.buf;
+  const Py_ssize_t R = gen.b.shape[0], K = gen.b.shape[1], NL = lru.b.shape[1], GS = gen.b.strides[0] / 4;
+  const Py_ssize_t B = PyList_GET_SIZE(patches), V = off.b.len / 8;
+  if (src.b.len / 8 != K || starts.b.len / 8 != B + 1 || nl.b.len / 8 != V || (NL == 0 && K > 0 && R > 0)) {
+    PyErr_SetString(PyExc_ValueError, "candidate_rows: sizes");
+    return nullptr;
+  }
+  for (Py_ssize_t k = 0; k < K; k++)
+    if (S[k] < 0 || S[k] >= NL) {
+      PyErr_SetString(PyExc_ValueError, "candidate_rows: base index out of range");
+      return nullptr;
+    }
+  // pass 1 (holding the GIL): every block's updates as plain records — (row, keep mask, bits) for
+  // the value assignments, (first row, limbs, minimum) for the floors
+  struct Up { int64_t row; uint32_t mask, val; };
+  struct Fl { int64_t r0, nl; uint32_t mn; };
+  std::vector<int64_t> up_off(B + 1, 0), fl_off(B + 1, 0);
+  std::vector<Up> ups;
+  std::vector<Fl> fls;
+  std::vector<uint32_t> words;
+  for (Py_ssize_t j = 0; j < B; j++) {
+    const int64_t c0 = ST[j], c1 = ST[j + 1];
+    if (c0 < 0 || c1 > K || c0 > c1) {
+      PyErr_SetString(PyExc_ValueError, "candidate_rows: block range");
+      return nullptr;
+    }
+    PyObject* patch = PyList_GET_ITEM(patches, j);
+    if (!PyTuple_Check(patch)) {
+      PyErr_SetString(PyExc_TypeError, "candidate_rows: a patch is not a tuple");
+      return nullptr;
+    }
+    for (Py_ssize_t e = 0; e < PyTuple_GET_SIZE(patch); e++) {
+      PyObject* el = PyTuple_GET_ITEM(patch, e);
+      if (!PyTuple_Check(el) || PyTuple_GET_SIZE(el) != 4) {
+        PyErr_SetString(PyExc_TypeError, "candidate_rows: a patch element is not a 4-tuple");
+        return nullptr;
+      }
+      const long v = PyLong_AsLong(PyTuple_GET_ITEM(el, 0));
+      const long lo = PyLong_AsLong(PyTuple_GET_ITEM(el, 1));
+      const long n = PyLong_AsLong(PyTuple_GET_ITEM(el, 2));
+      if (PyErr_Occurred()) return nullptr;
+      if (v < 0 || v >= V || VO[v] < 0 || VO[v] + VL[v] > R) {
+        PyErr_SetString(PyExc_ValueError, "candidate_rows: variable out of range");
+        return nullptr;
+      }
+      PyObject* bits = PyTuple_GET_ITEM(el, 3);
+      if (lo < 0) {   // size >= minimum (values < 2^32 in their low limb)
+        const unsigned long mn = PyLong_AsUnsignedLongMask(bits);
+        if (PyErr_Occurred()) return nullptr;
+        fls.push_back(Fl{VO[v], VL[v], (uint32_t)mn});
+        continue;
+      }
+      if (n <= 0) continue;
+      if (!PyLong_Check(bits) || !long_fits_unsigned(bits, n)) {
+        PyErr_SetString(PyExc_ValueError, "candidate_rows: assignment bits wider than the field");
+        return nullptr;
+      }
+      words.assign((size_t)(n + 31) / 32 + 1, 0u);
+      if (long_le_bytes(bits, (unsigned char*)words.data(), words.size() * 4) < 0) return nullptr;
+      for (long i = lo / 32; i <= (lo + n - 1) / 32 && i < VL[v]; i++) {
+        const long blo = 32 * i, aa = std::max(lo, blo), bb = std::min(lo + n, blo + 32);
+        if (aa >= bb) continue;
+        const uint32_t mask = (uint32_t)((bb - aa >= 32 ? 0xFFFFFFFFull : ((1ull << (bb - aa)) - 1)) << (aa - blo));
+        ups.push_back(Up{VO[v] + i, ~mask, (bits_at(words, aa - lo, (int)(bb - aa)) << (aa - blo)) & mask});
+      }
+    }
+    up_off[j + 1] = (int64_t)ups.size();
+    fl_off[j + 1] = (int64_t)fls.size();
+  }
+  // pass 2 (GIL released): blocks are disjoint column ranges, so threads take ranges of blocks;
+  // each copies its candidates' base rows, then applies its blocks' values, then their floors
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const int64_t work = (int64_t)R * K;
+  const int nt = (int)std::min<int64_t>({(int64_t)std::min(8u, hw), std::max<int64_t>(1, work / (1 << 20)), std::max<Py_ssize_t>(B, 1)});
+  auto run = [&](int64_t b0, int64_t b1) {
+    if (b0 >= b1) return;
+    const int64_t k0 = ST[b0], k1 = ST[b1];
+    for (Py_ssize_t r = 0; r < R; r++) {
+      uint32_t* g = G + r * GS;
+      const uint32_t* l = L + r * NL;
+      for (int64_t k = k0; k < k1; k++) g[k] = l[S[k]];
+    }
+    for (int64_t j = b0; j < b1; j++) {
+      const int64_t c0 = ST[j], c1 = ST[j + 1];
+      for (int64_t u = up_off[j]; u < up_off[j + 1]; u++) {
+        uint32_t* g = G + ups[u].row * GS;
+        const uint32_t keep = ups[u].mask, val = ups[u].val;
+        for (int64_t k = c0; k < c1; k++) g[k] = (g[k] & keep) | val;
+      }
+      for (int64_t f = fl_off[j]; f < fl_off[j + 1]; f++) {
+        uint32_t* g0 = G + fls[f].r0 * GS;
+        for (int64_t k = c0; k < c1; k++) {
+          bool small = true;
+          for (int64_t q = 1; q < fls[f].nl && small; q++) small = G[(fls[f].r0 + q) * GS + k] == 0;
+          if (small && g0[k] < fls[f].mn) g0[k] = fls[f].mn;
+        }
+      }
+    }
+  };
+  Py_BEGIN_ALLOW_THREADS
+  if (nt <= 1) {
+    run(0, B);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; t++) th.emplace_back(run, (int64_t)B * t / nt, (int64_t)B * (t + 1) / nt);
+    for (auto& x : th) x.join();
+  }
+  Py_END_ALLOW_THREADS
+  Py_RETURN_NONE;
+}
+
 PyMethodDef methods[] = {
+    {"candidate_rows", py_candidate_rows, METH_VARARGS,
+     "candidate_rows(gen, lru, src, starts, patches, var_off, var_limbs): generated candidates' rows"},
     {"pack_nodes", py_pack_nodes, METH_VARARGS, "pack_nodes(nodes, start, end, out): node tuples -> NODE_DTYPE records"},
     {"bind", py_bind, METH_O, "bind(Term): read the term class's slot offsets"},
     {"lower_roots", py_lower_roots, METH_VARARGS, "lower_roots(roots, state) -> per root: node list or exception"},
