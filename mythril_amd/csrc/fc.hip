@@ -208,6 +208,186 @@ __global__ __launch_bounds__(256) void fc_kernel(const FcTape* __restrict__ tape
   }
 }
 
+// ---- unary atoms: the transform of an 8-limb value (w uniform, bits above w zero) --------------
+__device__ __forceinline__ void fx_mask(uint32_t y[8], uint32_t w) {
+#pragma unroll
+  for (int l = 0; l < 8; l++) {
+    const uint32_t lo = 32u * l;
+    if (w <= lo) y[l] = 0u;
+    else if (w < lo + 32u) y[l] &= (1u << (w - lo)) - 1u;
+  }
+}
+// bits [w_in, w_out) set (sign-fill) where s
+__device__ __forceinline__ void fx_fill(uint32_t y[8], uint32_t w_in, uint32_t w_out, bool s) {
+#pragma unroll
+  for (int l = 0; l < 8; l++) {
+    const uint32_t lo = 32u * l;
+    const uint32_t a = max(w_in, lo), b = min(w_out, lo + 32u);
+    if (a < b) {
+      const uint32_t m = (b - a == 32u ? 0xFFFFFFFFu : ((1u << (b - a)) - 1u)) << (a - lo);
+      if (s) y[l] |= m;
+    }
+  }
+}
+__device__ __forceinline__ bool fx_sign(const uint32_t y[8], uint32_t w) {
+  const uint32_t li = (w - 1u) >> 5, bi = (w - 1u) & 31u;
+  uint32_t t = 0;
+#pragma unroll
+  for (int l = 0; l < 8; l++)
+    if ((uint32_t)l == li) t = y[l];
+  return (t >> bi) & 1u;
+}
+// y >> k over 256 bits, `top` shifted in from above (0 or all ones)
+__device__ __forceinline__ void fx_shr(uint32_t y[8], uint32_t k, uint32_t top) {
+  if (k >= 256u) {
+#pragma unroll
+    for (int l = 0; l < 8; l++) y[l] = top;
+    return;
+  }
+  const uint32_t q = k >> 5, r = k & 31u;
+  if (q & 4u) {
+#pragma unroll
+    for (int l = 0; l < 8; l++) y[l] = l + 4 < 8 ? y[l + 4] : top;
+  }
+  if (q & 2u) {
+#pragma unroll
+    for (int l = 0; l < 8; l++) y[l] = l + 2 < 8 ? y[l + 2] : top;
+  }
+  if (q & 1u) {
+#pragma unroll
+    for (int l = 0; l < 8; l++) y[l] = l + 1 < 8 ? y[l + 1] : top;
+  }
+  if (r) {
+#pragma unroll
+    for (int l = 0; l < 8; l++) {
+      const uint32_t hi = l + 1 < 8 ? y[l + 1] : top;
+      y[l] = (uint32_t)((((uint64_t)hi << 32) | y[l]) >> r);
+    }
+  }
+}
+__device__ __forceinline__ void fx_shl(uint32_t y[8], uint32_t k) {
+  if (k >= 256u) {
+#pragma unroll
+    for (int l = 0; l < 8; l++) y[l] = 0u;
+    return;
+  }
+  const uint32_t q = k >> 5, r = k & 31u;
+  if (q & 4u) {
+#pragma unroll
+    for (int l = 7; l >= 0; l--) y[l] = l >= 4 ? y[l - 4] : 0u;
+  }
+  if (q & 2u) {
+#pragma unroll
+    for (int l = 7; l >= 0; l--) y[l] = l >= 2 ? y[l - 2] : 0u;
+  }
+  if (q & 1u) {
+#pragma unroll
+    for (int l = 7; l >= 0; l--) y[l] = l >= 1 ? y[l - 1] : 0u;
+  }
+  if (r) {
+#pragma unroll
+    for (int l = 7; l >= 0; l--) {
+      const uint32_t lo = l >= 1 ? y[l - 1] : 0u;
+      y[l] = (uint32_t)((((uint64_t)y[l] << 32) | lo) >> (32u - r));
+    }
+  }
+}
+// two's complement negation at width w
+__device__ __forceinline__ void fx_neg(uint32_t y[8], uint32_t w) {
+  uint64_t cy = 1;
+#pragma unroll
+  for (int l = 0; l < 8; l++) {
+    const uint64_t t = (uint64_t)(~y[l]) + cy;
+    y[l] = (uint32_t)t;
+    cy = t >> 32;
+  }
+  fx_mask(y, w);
+}
+// y = y / d (quotient limbs), returns y mod d; 0 < d < 2^21: each step's dividend r * 2^32 + limb
+// is below 2^53, so the fp64 estimate of its quotient is exact up to one unit either way
+__device__ __forceinline__ uint32_t fx_divmod(uint32_t y[8], uint32_t d) {
+  const double inv = 1.0 / (double)d;
+  uint32_t r = 0;
+#pragma unroll
+  for (int l = 7; l >= 0; l--) {
+    const uint64_t v = ((uint64_t)r << 32) | y[l];
+    uint32_t q = (uint32_t)((double)v * inv);
+    int64_t rem = (int64_t)(v - (uint64_t)q * d);
+    if (rem < 0) {
+      q--;
+      rem += d;
+    } else if (rem >= (int64_t)d) {
+      q++;
+      rem -= d;
+    }
+    y[l] = q;
+    r = (uint32_t)rem;
+  }
+  return r;
+}
+__device__ __forceinline__ void fx_apply(uint32_t y[8], const FcXf& X) {
+  for (uint32_t k = 0; k < X.n; k++) {
+    const FcXop o = X.op[k];
+    const uint32_t code = o.code & 0xFFu, w = o.code >> 8;
+    if (code == FX_SEXT) {
+      fx_fill(y, w, o.p0, fx_sign(y, w));
+    } else if (code == FX_EXTRACT) {
+      fx_shr(y, o.p0, 0u);
+      fx_mask(y, o.p1);
+    } else if (code == FX_LSHR) {
+      fx_shr(y, o.p0 >= w ? 256u : o.p0, 0u);
+    } else if (code == FX_SHL) {
+      fx_shl(y, o.p0 >= w ? 256u : o.p0);
+      fx_mask(y, w);
+    } else if (code == FX_ASHR) {
+      const bool s = fx_sign(y, w);
+      fx_fill(y, w, 256u, s);
+      fx_shr(y, min(o.p0, w - 1u), s ? 0xFFFFFFFFu : 0u);
+      fx_mask(y, w);
+    } else if (code == FX_UREM || code == FX_UDIV) {
+      const uint32_t r = fx_divmod(y, o.p0);
+      if (code == FX_UREM) {
+#pragma unroll
+        for (int l = 0; l < 8; l++) y[l] = l == 0 ? r : 0u;
+      }
+    } else {   // FX_SMOD / FX_SREM / FX_SDIV: on |y| and |d|, then the signs (SMT-LIB)
+      const bool neg = fx_sign(y, w), dneg = o.p1 != 0u;
+      if (neg) fx_neg(y, w);
+      const uint32_t r = fx_divmod(y, o.p0);
+      if (code == FX_SDIV) {
+        if (neg != dneg) fx_neg(y, w);
+      } else {
+#pragma unroll
+        for (int l = 0; l < 8; l++) y[l] = l == 0 ? r : 0u;
+        if (code == FX_SREM) {
+          if (neg) fx_neg(y, w);
+        } else if (r != 0u) {
+          // x >= 0, d > 0: r; x < 0, d > 0: |d| - r; x >= 0, d < 0: r - |d|; x < 0, d < 0: -r
+          if (neg != dneg) {
+            y[0] = o.p0 - r;
+            if (dneg) fx_neg(y, w);
+          } else if (neg) {
+            fx_neg(y, w);
+          }
+        }
+      }
+    }
+  }
+}
+// the accept bit of y (8 limbs, signed compares pre-flipped by f) against the atom's constant
+__device__ __forceinline__ uint32_t fx_case(const uint32_t y[8], const FcCmpHead& h, const FcCmpTail& t) {
+  const uint64_t x0 = (((uint64_t)y[1] << 32) | y[0]) ^ h.f01;
+  bool lt = x0 < h.c01, eq = x0 == h.c01;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const uint64_t xv = ((uint64_t)(y[2 * k + 3] ^ t.f[2 * k + 1]) << 32) | (y[2 * k + 2] ^ t.f[2 * k]);
+    const uint64_t c = ((uint64_t)t.c[2 * k + 1] << 32) | t.c[2 * k];
+    lt = xv < c || (xv == c && lt);
+    eq = xv == c && eq;
+  }
+  return lt ? 1u : (eq ? 2u : 4u);
+}
+
 // Two-phase form for tapes (FcaArgs).  fc_kernel pays a tape's scalar frame, mask reduction and
 // compares once per (tape, tile): ~110 instructions, and it can only compare variables staged in
 // LDS.  Here a workgroup of FC_TILES tiles first evaluates the launch's DISTINCT compares (C4: 647
@@ -221,6 +401,7 @@ __global__ __launch_bounds__(256) void fc_kernel(const FcTape* __restrict__ tape
 // verdict / column store code and its loop-invariant addresses)
 template <int MODE>
 __global__ __launch_bounds__(256) void fca_kernel(const FcaGroup* __restrict__ groups, const FcCmp* __restrict__ atoms,
+                                                  const FcXf* __restrict__ xfs,
                                                   const uint32_t* __restrict__ lists,
                                                   const uint32_t* __restrict__ chunk_off,
                                                   const uint32_t* __restrict__ tape_out,
@@ -282,6 +463,25 @@ __global__ __launch_bounds__(256) void fca_kernel(const FcaGroup* __restrict__ g
         const FcCmpHead h = atoms[a].h;
         const FcCmpTail t = atoms[a].t;
         uint64_t m[FC_TILES];
+        const uint32_t nx = xfs[a].n;
+        if (nx) {   // a unary atom: the transform of the variable, then the compare
+          const FcXf X = xfs[a];
+#pragma unroll
+          for (int j = 0; j < FC_TILES; j++) {
+            uint32_t y[8];
+#pragma unroll
+            for (int l = 0; l < 8; l++) y[l] = x[j][l];
+            fx_apply(y, X);
+            const uint64_t b = __ballot((h.accept & fx_case(y, h, t)) != 0u);
+            m[j] = b;
+          }
+          if (lane == 0) {
+            ulonglong2* p = reinterpret_cast<ulonglong2*>(tab + (abase + (int)a) * FC_TILES);
+            p[0] = make_ulonglong2(m[0], m[1]);
+            p[1] = make_ulonglong2(m[2], m[3]);
+          }
+          continue;
+        }
 #pragma unroll
         for (int j = 0; j < FC_TILES; j++) {
           const uint64_t x0 = (((uint64_t)x[j][1] << 32) | x[j][0]) ^ h.f01;
@@ -429,13 +629,13 @@ hipError_t launch_fca(const FcaArgs& a, hipStream_t st) {
   if (groups > 0x7FFFFFFF) return hipErrorInvalidValue;
   const size_t lds = (size_t)(1 + a.n_smask + a.n_atoms) * 8u * FC_TILES;
   if (a.mode == 0)
-    hipLaunchKernelGGL(fca_kernel<0>, dim3((unsigned)groups), dim3(256), lds, st, a.groups, a.atoms, a.lists,
+    hipLaunchKernelGGL(fca_kernel<0>, dim3((unsigned)groups), dim3(256), lds, st, a.groups, a.atoms, a.xfs, a.lists,
                        a.chunk_off, a.tape_out, a.tape_metric, a.vars, a.bool_masks, a.stage_masks, a);
   else if (a.mode == 1)
-    hipLaunchKernelGGL(fca_kernel<1>, dim3((unsigned)groups), dim3(256), lds, st, a.groups, a.atoms, a.lists,
+    hipLaunchKernelGGL(fca_kernel<1>, dim3((unsigned)groups), dim3(256), lds, st, a.groups, a.atoms, a.xfs, a.lists,
                        a.chunk_off, a.tape_out, a.tape_metric, a.vars, a.bool_masks, a.stage_masks, a);
   else if (a.mode == 3)
-    hipLaunchKernelGGL(fca_kernel<3>, dim3((unsigned)groups), dim3(256), lds, st, a.groups, a.atoms, a.lists,
+    hipLaunchKernelGGL(fca_kernel<3>, dim3((unsigned)groups), dim3(256), lds, st, a.groups, a.atoms, a.xfs, a.lists,
                        a.chunk_off, a.tape_out, a.tape_metric, a.vars, a.bool_masks, a.stage_masks, a);
   else
     return hipErrorInvalidValue;

@@ -479,13 +479,13 @@ struct mq_tapes {
   bool fca = false;
   int fca_atoms = 0;
   std::vector<FcaPlanSeg> fca_segs;
-  DevBuf fca_chunk_dev, fca_out_dev, fca_metric_dev, fca_group_dev;
+  DevBuf fca_chunk_dev, fca_out_dev, fca_metric_dev, fca_group_dev, fca_xf_dev;
   // the G-eligible Bool columns of a level that are flat (fc_match) run on fc_kernel, mode 3,
   // before the level's G launch (cq_prepare); the level's G descriptors are the others
   struct FcLevel {   // fca_kernel mode 3 (fca_plan per level)
     int count = 0;
     std::vector<FcaPlanSeg> segs;
-    DevBuf atoms, groups, lists, chunk, out, metric, smask, colmask;
+    DevBuf atoms, xfs, groups, lists, chunk, out, metric, smask, colmask;
   };
   std::vector<std::unique_ptr<FcLevel>> fc_lvl;
   std::vector<int> cq_lvl_desc_off, cq_lvl_desc_n;
@@ -2830,6 +2830,9 @@ static void plan_stage(const mq_ctx* c, const std::vector<int64_t>& pushes, cons
 struct FcCmpH {
   uint32_t row, nl, accept;
   uint32_t c[8], f[8];
+  uint32_t src_nl = 0;   // limbs of the compared variable's rows (0: nl; fewer when it was zero-extended)
+  uint32_t nx = 0;       // unary atoms (fca only): the variable's transform, nx steps
+  FcXop xf[kFcMaxXops] = {};
 };
 // accept masks: bit 0 x < c, bit 1 x == c, bit 2 x > c
 static constexpr uint32_t kAccEq = 2, kAccNe = 5, kAccLt = 1, kAccLe = 3, kAccGt = 4, kAccGe = 6;
@@ -2842,14 +2845,30 @@ static constexpr int kFcStageMasks = 256;
 // A program that is a flat conjunction of atoms (Bool variables, variable-constant compares),
 // or the negation of one: ORs of atoms and of negated conjunctions are taken by De Morgan
 // (OR(a, b) = NOT(AND(NOT a, NOT b))), the result negation returned in *neg.
+// With `unary` (the two-phase kernel only) an atom may also compare a constant with a unary
+// function of its variable: zero extension (free: values are canonical), sign extension, extract,
+// shifts by constants, and division / remainder by small constants (FcXop, fc.hip fx_apply).
 static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_t>& masks, std::vector<FcCmpH>& cmps,
-                     bool* neg = nullptr) {
+                     bool* neg = nullptr, bool unary = false) {
   struct Item {
-    int kind = 0;   // 0 model variable (BV), 1 constant, 2 conjunction (negated when neg)
+    int kind = 0;   // 0 model variable (BV, through xf), 1 constant, 2 conjunction (negated when neg)
     uint32_t v = 0;
+    uint32_t w = 0;   // kind 0: the width of its current value
     bool neg = false;
     std::vector<uint32_t> m;
     std::vector<FcCmpH> q;
+    std::vector<FcXop> xf;
+  };
+  // the 256-bit constant at word offset k of the tape's pool, limb by limb (8 limbs, zero padded)
+  auto const_limbs = [&](uint32_t k, uint32_t out[8]) {
+    for (int i = 0; i < 8; i++) out[i] = x.consts[k + i];
+  };
+  // value (< 2^32 or saturated) of a constant of width w: its limbs above 0 are zero?
+  auto small_value = [&](const uint32_t l[8], uint64_t* v) {
+    for (int i = 2; i < 8; i++)
+      if (l[i]) return false;
+    *v = (uint64_t)l[0] | ((uint64_t)l[1] << 32);
+    return true;
   };
   // NOT of an item as a plain conjunction: a single atom negated, or a negated conjunction's body
   auto negate_to_conj = [](Item& a) -> bool {
@@ -2880,6 +2899,21 @@ static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_
   for (size_t pc = 0; pc < pr.size(); pc++) {
     const uint32_t w = pr[pc], op = w & 0xFFu, imm = w >> 12;
     if (op == G_END) break;
+    if (unary && (op == G_EXTRACT || op == G_SEXT) && pc + 1 < pr.size()) {
+      // (the two ops with a second word: the result width)
+      const uint32_t w2 = pr[++pc];
+      if (st.empty() || st.back().kind != 0 || st.back().xf.size() >= (size_t)kFcMaxXops) return false;
+      Item& a = st.back();
+      if (op == G_EXTRACT) {
+        if (imm + w2 > a.w || w2 == 0) return false;
+        a.xf.push_back(FcXop{FX_EXTRACT | (a.w << 8), imm, w2, 0});
+      } else {
+        if (imm != a.w || w2 <= a.w || w2 > 256) return false;
+        a.xf.push_back(FcXop{FX_SEXT | (a.w << 8), w2, 0, 0});
+      }
+      a.w = w2;
+      continue;
+    }
     if (has_imm2(op)) return false;
     Item it;
     switch (op) {
@@ -2887,8 +2921,52 @@ static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_
         if (imm >= c->var_nl_h.size() || c->var_width[imm] == 0 || c->var_nl_h[imm] > 8) return false;
         it.kind = 0;
         it.v = imm;
+        it.w = c->var_width[imm];
         st.push_back(std::move(it));
         break;
+      case G_LSHR: case G_SHL: case G_ASHR: case G_UREM: case G_UDIV: case G_SMOD: case G_SREM: case G_SDIV: {
+        // a unary step: the variable (through its steps so far) OP a constant
+        if (!unary || st.size() < 2 || st.back().kind != 1 || st[st.size() - 2].kind != 0) return false;
+        const uint32_t kc = st.back().v;
+        st.pop_back();
+        Item& a = st.back();
+        const uint32_t w = a.w;
+        if (imm != w || w == 0 || w > 256 || a.xf.size() >= (size_t)kFcMaxXops) return false;
+        uint32_t l[8];
+        const_limbs(kc, l);
+        uint64_t k = 0;
+        const bool small = small_value(l, &k);
+        if (op == G_LSHR || op == G_SHL || op == G_ASHR) {
+          const uint32_t sh = (!small || k >= w) ? w : (uint32_t)k;   // (>= w: the kernel's saturation)
+          a.xf.push_back(FcXop{(op == G_LSHR ? FX_LSHR : op == G_SHL ? FX_SHL : FX_ASHR) | (w << 8), sh, 0, 0});
+        } else if (op == G_UREM || op == G_UDIV) {
+          if (!small || k == 0 || k >= (1u << 21)) return false;
+          a.xf.push_back(FcXop{(op == G_UREM ? FX_UREM : FX_UDIV) | (w << 8), (uint32_t)k, 0, 0});
+        } else {
+          // signed divisor: |d| and its sign at width w (two's complement of the w-bit constant)
+          bool dneg = ((l[(w - 1) / 32] >> ((w - 1) % 32)) & 1u) != 0;
+          uint32_t m[8];
+          for (int i = 0; i < 8; i++) m[i] = l[i];
+          if (dneg) {   // |d| = -d mod 2^w
+            uint64_t cy = 1;
+            for (int i = 0; i < 8; i++) {
+              const uint64_t t = (uint64_t)(~m[i]) + cy;
+              m[i] = (uint32_t)t;
+              cy = t >> 32;
+            }
+            for (int i = 0; i < 8; i++) {
+              const uint32_t lo = 32u * i;
+              if (w <= lo) m[i] = 0;
+              else if (w < lo + 32) m[i] &= (1u << (w - lo)) - 1u;
+            }
+          }
+          uint64_t ad = 0;
+          if (!small_value(m, &ad) || ad == 0 || ad >= (1u << 21)) return false;
+          const uint32_t code = op == G_SMOD ? FX_SMOD : op == G_SREM ? FX_SREM : FX_SDIV;
+          a.xf.push_back(FcXop{code | (w << 8), (uint32_t)ad, dneg ? 1u : 0u, 0});
+        }
+        break;
+      }
       case G_PUSH_VAR_B:
         if (imm >= c->var_nl_h.size() || c->var_width[imm] != 0) return false;
         bool_item(imm, it);
@@ -2940,10 +3018,14 @@ static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_
         const Item& var = swap ? r : l;
         const Item& cst = swap ? l : r;
         const uint32_t wdt = imm;
-        if (wdt == 0 || c->var_width[var.v] != wdt) return false;
+        // (a narrower value compared at a wider width: a zero-extended column read, free)
+        if (wdt == 0 || wdt > 256 || var.w > wdt || (!unary && (var.w != wdt || !var.xf.empty()))) return false;
         FcCmpH q{};
         q.row = c->var_off_h[var.v];
-        q.nl = c->var_nl_h[var.v];
+        q.nl = (wdt + 31) / 32;
+        q.src_nl = c->var_nl_h[var.v];
+        q.nx = (uint32_t)var.xf.size();
+        for (size_t k = 0; k < var.xf.size(); k++) q.xf[k] = var.xf[k];
         for (uint32_t i = 0; i < q.nl; i++) q.c[i] = x.consts[cst.v + i];
         // x OP c with the variable on the left; a constant on the left mirrors the order
         switch (op) {
@@ -3068,6 +3150,7 @@ static void fc_plan(const mq_ctx* c, const std::vector<std::vector<uint32_t>>& f
 // the variable they read (one group per variable: its limbs are loaded once per tile).
 struct FcaPlan {
   std::vector<FcCmp> atoms;
+  std::vector<FcXf> xfs;   // parallel to atoms
   std::vector<FcaGroup> groups;
   std::vector<uint32_t> lists, chunk_off, tape_out, metric, stage_masks;
   std::vector<int32_t> col_mask;   // (columns: per kept column its lane-mask index)
@@ -3080,12 +3163,23 @@ static void fca_plan(const mq_ctx* c, const std::vector<std::vector<uint32_t>>& 
                      const std::function<std::pair<uint32_t, uint32_t>(size_t)>& nodes_ops, FcaPlan& P,
                      const std::function<int32_t(size_t)>& mask_out = nullptr) {
   const uint32_t zero_row = (uint32_t)(c->var_off_h.empty() ? 0 : c->var_off_h.back() + c->var_nl_h.back());
+  // key: row, source limbs, path (1: the 8-limb path — wide compares, zero-extended reads wider
+  // than 64 bits, unary atoms), accept, compare limbs, then the constant / flip limbs and the
+  // transform steps (atoms of one (row, source limbs, path) form groups)
   auto atom_key = [](const FcCmpH& h, bool* ng) {
     *ng = h.accept >= 4;
-    std::vector<uint32_t> key{h.row, h.nl, *ng ? (h.accept ^ 7u) : h.accept};
+    const uint32_t src = h.src_nl ? h.src_nl : h.nl;
+    const uint32_t general = (h.nx > 0 || h.nl > 2 || src > 2) ? 1u : 0u;
+    std::vector<uint32_t> key{h.row, src, general, *ng ? (h.accept ^ 7u) : h.accept, h.nl, h.nx};
     for (uint32_t l = 0; l < h.nl; l++) {
       key.push_back(h.c[l]);
       key.push_back(h.f[l]);
+    }
+    for (uint32_t k = 0; k < h.nx; k++) {
+      key.push_back(h.xf[k].code);
+      key.push_back(h.xf[k].p0);
+      key.push_back(h.xf[k].p1);
+      key.push_back(h.xf[k].p2);
     }
     return key;
   };
@@ -3117,7 +3211,9 @@ static void fca_plan(const mq_ctx* c, const std::vector<std::vector<uint32_t>>& 
     std::vector<uint32_t> ord(akeys.size());
     for (size_t i = 0; i < ord.size(); i++) ord[i] = (uint32_t)i;
     std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
-      return akeys[x][0] != akeys[y][0] ? akeys[x][0] < akeys[y][0] : akeys[x][1] < akeys[y][1];
+      for (int f = 0; f < 3; f++)
+        if (akeys[x][f] != akeys[y][f]) return akeys[x][f] < akeys[y][f];
+      return false;
     });
     static const uint32_t group_atoms = [] {
       const char* e = std::getenv("MQ_FCA_GROUP_ATOMS");
@@ -3130,24 +3226,32 @@ static void fca_plan(const mq_ctx* c, const std::vector<std::vector<uint32_t>>& 
       // (a group holds at most kFcaGroupAtoms atoms: the 4 waves take every fourth group, so one
       // variable's many compares must not land on one wave)
       if (r == 0 || akeys[ord[r - 1]][0] != key[0] || akeys[ord[r - 1]][1] != key[1] ||
-          P.groups.back().count >= group_atoms) {
+          akeys[ord[r - 1]][2] != key[2] || P.groups.back().count >= group_atoms) {
         FcaGroup g{};
         const uint32_t nl = key[1];
         for (uint32_t l = 0; l < 8; l++) g.rows[l] = l < nl ? key[0] + l : zero_row;
         g.first = (uint32_t)r;
-        g.nl = nl;
+        g.nl = key[2] ? 8u : nl;   // (the kernel's 8-limb path for nl > 2)
         P.groups.push_back(g);
       }
       P.groups.back().count++;
       FcCmp q{};
       q.h.slot = 0;
-      q.h.nl = key[1];
-      q.h.accept = key[2];
+      const uint32_t cnl = key[4], nx = key[5];
+      q.h.nl = cnl;
+      q.h.accept = key[3];
       uint32_t cc[8] = {0}, ff[8] = {0};
-      for (uint32_t l = 0; l < key[1]; l++) {
-        cc[l] = key[3 + 2 * l];
-        ff[l] = key[4 + 2 * l];
+      for (uint32_t l = 0; l < cnl; l++) {
+        cc[l] = key[6 + 2 * l];
+        ff[l] = key[7 + 2 * l];
       }
+      FcXf xf{};
+      xf.n = nx;
+      for (uint32_t k = 0; k < nx; k++) {
+        const size_t o = 6 + 2 * cnl + 4 * k;
+        xf.op[k] = FcXop{key[o], key[o + 1], key[o + 2], key[o + 3]};
+      }
+      P.xfs.push_back(xf);
       q.h.c01 = (uint64_t)cc[0] | ((uint64_t)cc[1] << 32);
       q.h.f01 = (uint64_t)ff[0] | ((uint64_t)ff[1] << 32);
       for (int l = 0; l < 6; l++) {
@@ -3264,17 +3368,19 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
   std::vector<std::vector<uint32_t>> fc_m(nq);
   std::vector<std::vector<FcCmpH>> fc_q(nq);
   std::vector<char> fc_neg(nq, 0);
+  T->fca = std::getenv("MQ_FC_ONEPHASE") == nullptr;
+  // unary atoms (fca only; MQ_FC_NO_UNARY=1 keeps the plain variable-constant atoms)
+  static const bool no_unary = std::getenv("MQ_FC_NO_UNARY") != nullptr;
   if (!no_flat)
     parallel_for(nq, 32, [&](int, int64_t b, int64_t e) {
       for (int64_t i = b; i < e; i++) {
         bool ng = false;
-        on_fc[i] = fc_match(c, T->qct[i], fc_m[i], fc_q[i], &ng) ? 1 : 0;
+        on_fc[i] = fc_match(c, T->qct[i], fc_m[i], fc_q[i], &ng, T->fca && !no_unary) ? 1 : 0;
         fc_neg[i] = ng ? 1 : 0;
       }
     });
   FcPlan fcp;
   FcaPlan fap;
-  T->fca = std::getenv("MQ_FC_ONEPHASE") == nullptr;
   if (T->fca)
     fca_plan(c, fc_m, fc_q, fc_neg, on_fc, [&](size_t i) { return T->qbase[i].tape; },
              [&](size_t i) { return std::make_pair(T->qbase[i].n_nodes, T->qbase[i].alg_ops); }, fap);
@@ -3412,9 +3518,11 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
     if (T->fc_count > 0) {
       if (fap.stage_masks.empty()) fap.stage_masks.push_back(0);
       if (fap.atoms.empty()) fap.atoms.push_back(FcCmp{});
+      if (fap.xfs.empty()) fap.xfs.push_back(FcXf{});
       if (fap.groups.empty()) fap.groups.push_back(FcaGroup{});
       if (fap.lists.empty()) fap.lists.push_back(0);
       HIPCHK(T->fc_cmp_dev.upload(fap.atoms.data(), fap.atoms.size(), c->stream));
+      HIPCHK(T->fca_xf_dev.upload(fap.xfs.data(), fap.xfs.size(), c->stream));
       HIPCHK(T->fca_group_dev.upload(fap.groups.data(), fap.groups.size(), c->stream));
       HIPCHK(T->fc_mask_dev.upload(fap.lists.data(), fap.lists.size(), c->stream));
       HIPCHK(T->fca_chunk_dev.upload(fap.chunk_off.data(), fap.chunk_off.size(), c->stream));
@@ -3554,9 +3662,11 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
     if (fl.count > 0) {
       if (fap.stage_masks.empty()) fap.stage_masks.push_back(0);
       if (fap.atoms.empty()) fap.atoms.push_back(FcCmp{});
+      if (fap.xfs.empty()) fap.xfs.push_back(FcXf{});
       if (fap.groups.empty()) fap.groups.push_back(FcaGroup{});
       if (fap.lists.empty()) fap.lists.push_back(0);
       HIPCHK(fl.atoms.upload(fap.atoms.data(), fap.atoms.size(), c->stream));
+      HIPCHK(fl.xfs.upload(fap.xfs.data(), fap.xfs.size(), c->stream));
       HIPCHK(fl.groups.upload(fap.groups.data(), fap.groups.size(), c->stream));
       HIPCHK(fl.lists.upload(fap.lists.data(), fap.lists.size(), c->stream));
       HIPCHK(fl.chunk.upload(fap.chunk_off.data(), fap.chunk_off.size(), c->stream));
@@ -3936,6 +4046,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
         f.n_groups = sg.n_groups;
         f.groups = fl.groups.as<FcaGroup>() + sg.group_off;
         f.atoms = fl.atoms.as<FcCmp>() + sg.atom_off;
+        f.xfs = fl.xfs.as<FcXf>() + sg.atom_off;
         f.lists = fl.lists.as<uint32_t>();
         f.chunk_off = fl.chunk.as<uint32_t>() + sg.chunk_first;
         f.tape_out = fl.out.as<uint32_t>() + sg.tape_first;
@@ -4120,6 +4231,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     f.n_groups = sg.n_groups;
     f.groups = T->fca_group_dev.as<FcaGroup>() + sg.group_off;
     f.atoms = T->fc_cmp_dev.as<FcCmp>() + sg.atom_off;
+    f.xfs = T->fca_xf_dev.as<FcXf>() + sg.atom_off;
     f.lists = T->fc_mask_dev.as<uint32_t>();
     f.chunk_off = T->fca_chunk_dev.as<uint32_t>() + sg.chunk_first;
     f.tape_out = T->fca_out_dev.as<uint32_t>() + sg.tape_first;

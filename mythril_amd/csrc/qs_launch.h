@@ -256,6 +256,31 @@ hipError_t launch_fc(const FcArgs& a, hipStream_t st);
 // ANDs its atoms' and Bool variables' masks with one lane per tape.  A workgroup's LDS table per
 // tile: entry 0 all ones, 1 .. n_smask the Bool masks, then the atoms; a list entry is a table
 // index | negated << 31.
+// Unary atoms (round 6): an atom may compare a constant with a UNARY function of its variable —
+// a chain of at most kFcMaxXops constant-operand steps (the narrow / sign-extended column reads,
+// shifts, extracts and divisions by small constants of C3's path conditions, instructions.py:
+// 510-573).  Step k transforms the 8-limb value of width w_in (bits above it zero).
+enum FcXcode : uint32_t {
+  FX_SEXT = 1,     // p0 = result width
+  FX_EXTRACT = 2,  // p0 = lo, p1 = result width
+  FX_LSHR = 3,     // p0 = shift (>= w_in: 0)
+  FX_SHL = 4,      // p0 = shift (>= w_in: 0)
+  FX_ASHR = 5,     // p0 = shift (clamped to w_in - 1)
+  FX_UREM = 6,     // p0 = divisor, 0 < d < 2^21
+  FX_UDIV = 7,     // p0 = divisor
+  FX_SMOD = 8,     // p0 = |divisor|, p1 = divisor negative (SMT-LIB bvsmod)
+  FX_SREM = 9,     // p0 = |divisor|, p1 = divisor negative (bvsrem)
+  FX_SDIV = 10     // p0 = |divisor|, p1 = divisor negative (bvsdiv)
+};
+constexpr int kFcMaxXops = 3;
+struct FcXop {
+  uint32_t code;   // FcXcode | w_in << 8
+  uint32_t p0, p1, p2;
+};
+struct FcXf {      // per atom (FcaArgs.xfs, parallel to atoms); n = 0: the variable itself
+  uint32_t n, pad[3];
+  FcXop op[kFcMaxXops];
+};
 struct FcaGroup {
   uint32_t rows[8];   // the variable's limb rows (nl <= 2: rows[0..1]; else 8, the zero row past nl)
   uint32_t first;     // its atoms: atoms[first .. first + count)
@@ -269,6 +294,7 @@ struct FcaArgs {
   int n_groups;
   const FcaGroup* groups;
   const FcCmp* atoms;             // accept in {1, 2, 3} (x < c, x == c, x <= c); negations in the lists
+  const FcXf* xfs;                // per atom: its unary transform (n = 0: none); groups with one have nl = 8
   const uint32_t* lists;          // chunk c of 64 tapes: kmax(c) entries x 64 lanes, k-major, from chunk_off[c]
   const uint32_t* chunk_off;      // [n_chunks + 1]: kmax(c) = (chunk_off[c + 1] - chunk_off[c]) / 64
   const uint32_t* tape_out;       // per tape: its best / verdict row | negated result << 31

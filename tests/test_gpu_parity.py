@@ -1496,3 +1496,104 @@ def test_p_section_lengths_every_residue_with_packed_g_columns(evaluator):
         assert (fh == cref.first_hit(tb0, mb0)[0]).all()
         ct.free()
     assert len(residues) == 64, sorted(set(range(64)) - residues)
+
+
+def _unary_atom_workload(seed, n_tapes=160, M=700):
+    """Tapes that are ANDs / ORs of compares of a constant with a UNARY function of one variable
+    (zero / sign extension, extract, shifts by constants — 0, mid, >= the width — and division /
+    remainder by small constants, signed ones negative too; chains of two or three steps), the
+    constants drawn from the functions' values under the models so the verdicts split."""
+    import term_eval
+    from mythril_amd import smt as S
+    from mythril_amd.lower import lower_batch, serialize_models
+    from mythril_amd.smt_model import Model
+    rng = np.random.default_rng(seed)
+    widths = (8, 64, 160, 256)
+    xs = {w: [S.BitVecSym(f"u{w}_{i}", w) for i in range(2)] for w in widths}
+    bools = [S.BoolSym(f"ub{i}") for i in range(2)]
+
+    def val(w):
+        k = int(rng.integers(6))
+        if k == 0:
+            return int(rng.integers(0, 4))
+        if k == 1:
+            return (1 << w) - 1 - int(rng.integers(0, 3))
+        if k == 2:
+            return (1 << (w - 1)) + int(rng.integers(-2, 3)) % (1 << w)
+        return int.from_bytes(rng.bytes(32), "little") & ((1 << w) - 1)
+
+    models = []
+    for _ in range(M):
+        asg = {f"u{w}_{i}": val(w) for w in widths for i in range(2) if rng.random() < 0.95}
+        asg.update({f"ub{i}": bool(rng.integers(2)) for i in range(2)})
+        models.append(Model(asg))
+
+    def step(t):
+        w = t.width
+        k = int(rng.integers(11))
+        if k == 0:
+            return S.SignExt(int(rng.integers(1, 257 - w)), t) if w < 256 else t
+        if k == 1 and w > 1:
+            lo = int(rng.integers(0, w))
+            hi = int(rng.integers(lo, w))
+            return S.Extract(hi, lo, t)
+        if k in (2, 3, 4):
+            sh = int(rng.choice([0, 1, 7, 31, 32, 33, w - 1, w, w + 5, 1 << 40])) % (1 << w) if w < 64 else \
+                int(rng.choice([0, 1, 7, 31, 32, 33, w - 1, w, w + 5, 1 << 40]))
+            c = S.BitVecVal(sh, w)
+            return [S.LShR(t, c), t << c, t >> c][k - 2]
+        if k in (5, 6, 7, 8, 9):
+            d = int(rng.choice([1, 2, 3, 7, 10, 255, 256, 1000, (1 << 21) - 1, (1 << 20) + 3]))
+            d = d % (1 << w) or 1
+            if k >= 7 and rng.random() < 0.5 and w > 1:
+                d = (-d) % (1 << w)   # a negative signed divisor
+            c = S.BitVecVal(d, w)
+            return [S.URem(t, c), S.UDiv(t, c), S.SMod(t, c), S.SRem(t, c), t / c][k - 5]
+        return S.ZeroExt(int(rng.integers(1, 257 - w)), t) if w < 256 else t
+
+    def atom():
+        w = widths[int(rng.integers(4))]
+        t = xs[w][int(rng.integers(2))]
+        for _ in range(int(rng.integers(1, 4))):
+            t = step(t)
+        w = t.width
+        base = term_eval.evaluate(t, models[int(rng.integers(M))])
+        c = S.BitVecVal((base + int(rng.choice([0, 0, 1, -1]))) % (1 << w), w)
+        k = int(rng.integers(6))
+        e = [t == c, S.ULT(t, c), S.Not(S.ULT(c, t)), t < c, t <= c, S.UGT(t, c)][k]
+        return S.Not(e) if rng.random() < 0.2 else e
+
+    exprs = []
+    for _ in range(n_tapes):
+        parts = [atom() for _ in range(int(rng.integers(1, 5)))]
+        if rng.random() < 0.3:
+            parts.append(bools[int(rng.integers(2))])
+        e = S.And(*parts) if rng.random() < 0.75 else S.Or(*parts)
+        exprs.append(e)
+    tb, syms, ok = lower_batch(exprs)
+    assert ok.all()
+    return exprs, models, tb, serialize_models(models, syms)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_flat_unary_atoms_match_oracle(evaluator, monkeypatch, seed):
+    """fca_kernel's unary atoms (fc.hip fx_apply; mq_api.cpp fc_match with unary steps): the
+    workload's tapes run on the flat kernel, and their verdicts and first hits are the oracle's
+    (and the direct term evaluator's)."""
+    import term_eval
+    exprs, models, tb, mb = _unary_atom_workload(seed)
+    evaluator.upload_models(mb)
+    ct = evaluator.compile(tb)
+    v, fh = evaluator.verdicts(ct)
+    n_flat = ct.flat_split()[0]
+    vref = cref.verdicts(tb, mb)
+    bad = np.argwhere(v != vref)
+    assert len(bad) == 0, (len(bad), bad[:5], [repr(exprs[i]) for i in sorted(set(bad[:3, 0]))])
+    assert (fh == cref.first_hit(tb, mb)[0]).all()
+    fh1 = evaluator.first_hit(ct)
+    assert (fh1 == cref.first_hit(tb, mb)[0]).all()
+    assert n_flat >= 0.9 * tb.n_tapes, n_flat
+    assert v.any() and (~v).any()
+    direct = np.array([[term_eval.is_true(e, m) for m in models[:50]] for e in exprs])
+    assert (v[:, :50] == direct).all()
+    ct.free()
