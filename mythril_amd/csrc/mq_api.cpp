@@ -2899,6 +2899,20 @@ static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_
   for (size_t pc = 0; pc < pr.size(); pc++) {
     const uint32_t w = pr[pc], op = w & 0xFFu, imm = w >> 12;
     if (op == G_END) break;
+    if (unary && op == G_CONCAT && pc + 1 < pr.size()) {
+      // Concat(0, x): a zero extension (bitvec.py:16-22 pads a narrower operand so; EVM BYTE)
+      const uint32_t w2 = pr[++pc];
+      if (st.size() < 2 || st.back().kind != 0 || st[st.size() - 2].kind != 1 || st.back().w != imm || w2 > 256) return false;
+      uint32_t hl[8];
+      const_limbs(st[st.size() - 2].v, hl);
+      for (int i = 0; i < 8; i++)
+        if (hl[i]) return false;
+      Item v = std::move(st.back());
+      st.pop_back();
+      st.back() = std::move(v);
+      st.back().w = w2;
+      continue;
+    }
     if (unary && (op == G_EXTRACT || op == G_SEXT) && pc + 1 < pr.size()) {
       // (the two ops with a second word: the result width)
       const uint32_t w2 = pr[++pc];
@@ -3014,7 +3028,39 @@ static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_
         bool swap;
         if (l.kind == 0 && r.kind == 1) swap = false;
         else if (l.kind == 1 && r.kind == 0) swap = true;
-        else return false;
+        else if (unary && l.kind == 1 && r.kind == 1 && imm > 0 && imm <= 256 && !c->var_off_h.empty()) {
+          // two constants (an unfolded compare): its truth value — TRUE is the empty
+          // conjunction, FALSE an atom that accepts nothing
+          uint32_t a[8], b[8];
+          const_limbs(l.v, a);
+          const_limbs(r.v, b);
+          if (op >= G_SLT) {
+            a[(imm - 1) / 32] ^= 1u << ((imm - 1) % 32);
+            b[(imm - 1) / 32] ^= 1u << ((imm - 1) % 32);
+          }
+          int cmp = 0;
+          for (int i = 7; i >= 0 && !cmp; i--) cmp = a[i] < b[i] ? -1 : (a[i] > b[i] ? 1 : 0);
+          bool t;
+          switch (op) {
+            case G_EQ: t = cmp == 0; break;
+            case G_ULT: case G_SLT: t = cmp < 0; break;
+            case G_ULE: case G_SLE: t = cmp <= 0; break;
+            case G_UGT: case G_SGT: t = cmp > 0; break;
+            default: t = cmp >= 0; break;
+          }
+          it.kind = 2;
+          if (!t) {
+            FcCmpH q{};
+            q.row = c->var_off_h[0];
+            q.nl = 1;
+            q.accept = 0;
+            it.q.push_back(q);
+          }
+          st.push_back(std::move(it));
+          break;
+        } else {
+          return false;
+        }
         const Item& var = swap ? r : l;
         const Item& cst = swap ? l : r;
         const uint32_t wdt = imm;

@@ -720,13 +720,17 @@ def test_asm_const_ops_and_lookups_match_oracle(evaluator, seed):
 
 
 def test_c3_tapes_run_on_general_asm_kernel(evaluator):
+    """C3's hoisted tapes run without the HIP C++ interpreter: on the flat kernel (unary atoms:
+    most of them) or the assembly interpreters (those reading an ite)."""
     from mythril_amd import synth_evm
     tb, mb, exp, _ = synth_evm.c3_workload(60, 3000, seed=9, hoist=True)
     evaluator.upload_models(mb)
     ct = evaluator.compile(tb)
     fh = evaluator.first_hit(ct)
     n_p, n_g, live = ct.asm_split()
-    assert live and n_p + n_g >= 0.8 * tb.n_tapes, (n_p, n_g, ct.split())
+    n_flat = ct.flat_split()[0]
+    assert live and n_p + n_g + n_flat >= 0.8 * tb.n_tapes, (n_p, n_g, n_flat, ct.split())
+    assert n_flat >= 0.5 * tb.n_tapes and n_g > 0, (n_p, n_g, n_flat)
     assert (fh == exp).all()
     evaluator.use_asm(False)
     try:

@@ -145,5 +145,45 @@ def distinct(cfg, n):
     print(f"compare atoms {total}, distinct {len(seen)}; divisor bit lengths {sorted(divs.items())}")
 
 
-if __name__ == "__main__" and len(sys.argv) > 3:
+if __name__ == "__main__" and len(sys.argv) > 3 and sys.argv[3] != "why":
     distinct(sys.argv[1], int(sys.argv[2]))
+
+
+def why_not(cfg, n):
+    """For tapes that are not flat: the kinds of the conjuncts that break it."""
+    if cfg == "c3":
+        tb = synth_evm.c3_workload(n, 64, hoist=True)[0]
+    else:
+        tb = synth_evm.c3_workload(n, 64, seed=5, n_tx=5, checks_per_tx=(18, 24), n_args=5, hoist=True)[0]
+    bad = collections.Counter()
+    per_tape = []
+    for t in range(tb.n_tapes):
+        nd = tb.tape_nodes(t)
+        stack, nb = [len(nd) - 1], 0
+        while stack:
+            i = stack.pop()
+            op = Op(int(nd[i]["op"]))
+            if op == Op.AND:
+                stack += [int(nd[i]["a"]), int(nd[i]["b"])]
+                continue
+            out = []
+            if not atoms(nd, i, out):
+                nb += 1
+                sub = []
+                j = i
+                while len(sub) < 4:
+                    o = Op(int(nd[j]["op"]))
+                    sub.append(o.name)
+                    if o in (Op.VAR, Op.CONST):
+                        break
+                    j = int(nd[j]["a"])
+                a, b = int(nd[i]["a"]), int(nd[i]["b"])
+                kid = (Op(int(nd[a]["op"])).name, Op(int(nd[b]["op"])).name) if op in PRED else ()
+                bad[(op.name, kid)] += 1
+        per_tape.append(nb)
+    print("non-flat conjuncts:", bad.most_common(12))
+    print("per tape non-flat conjuncts:", collections.Counter(per_tape).most_common(8))
+
+
+if __name__ == "__main__" and len(sys.argv) > 3 and sys.argv[3] == "why":
+    why_not(sys.argv[1], int(sys.argv[2]))
