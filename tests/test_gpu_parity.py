@@ -1481,9 +1481,15 @@ def test_p_section_lengths_every_residue_with_packed_g_columns(evaluator):
         acc = p[0] * p[1]
         for j in range(k):
             acc = acc + S.BitVecVal(int(rng.integers(1, 1 << 30)), 256)
-        ptapes = [S.ULT(acc, p[2] * S.BitVecVal(1 << 20, 256)), S.ULT(p[1] + p[2], acc)]
+        # (two P tapes that share no sub-term: nothing of them is hoisted into a column)
+        ptapes = [S.ULT(acc, p[2] * S.BitVecVal(1 << 20, 256)), S.ULT(p[1] + p[2], p[0] * S.BitVecVal(3, 256))]
         roots = ptapes + paths
-        tb, syms, ok = lower_batch(roots, hoist=True)
+        # (p0..p2 first in the symbol table: P preloads variables 0-7)
+        from mythril_amd.lower import SymbolTable
+        syms = SymbolTable()
+        for i in range(3):
+            syms.var(f"p{i}", 256)
+        tb, syms, ok = lower_batch(roots, syms=syms, hoist=True)
         assert ok.all() and tb.columns is not None and tb.columns.n > 0
         mb = serialize_models(recs, syms)
         tb0, syms0, _ = lower_batch(roots)
@@ -1492,7 +1498,7 @@ def test_p_section_lengths_every_residue_with_packed_g_columns(evaluator):
         ct = evaluator.compile(tb)
         v, fh = evaluator.verdicts(ct)
         n_p, n_g, live = ct.asm_split()
-        assert live and n_p >= 2 and n_g > 0, (n_p, n_g, live)
+        assert live and n_p >= 1 and n_g > 0, (n_p, n_g, live)
         assert ct.column_asm_split()[0] > 0
         residues.add(int(sum(ct.handler_histogram(0).values())) % 64)
         vref = cref.verdicts(tb0, mb0)

@@ -64,7 +64,7 @@ def main():
         for kids in batches[40:]:
             cache.check_quick_sat_batch(kids)
         pr.disable()
-        pstats.Stats(pr).sort_stats("cumulative").print_stats(30)
+        pstats.Stats(pr).sort_stats(sys.argv[4] if len(sys.argv) > 4 else "cumulative").print_stats(40)
 
 
 if __name__ == "__main__":
