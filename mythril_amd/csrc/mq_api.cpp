@@ -2902,7 +2902,7 @@ static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_
     if (unary && op == G_CONCAT && pc + 1 < pr.size()) {
       // Concat(0, x): a zero extension (bitvec.py:16-22 pads a narrower operand so; EVM BYTE)
       const uint32_t w2 = pr[++pc];
-      if (st.size() < 2 || st.back().kind != 0 || st[st.size() - 2].kind != 1 || st.back().w != imm || w2 > 256) return false;
+      if (st.size() < 2 || st.back().kind != 0 || st[st.size() - 2].kind != 1 || st.back().w > imm || w2 > 256) return false;
       uint32_t hl[8];
       const_limbs(st[st.size() - 2].v, hl);
       for (int i = 0; i < 8; i++)
@@ -2918,12 +2918,14 @@ static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_
       const uint32_t w2 = pr[++pc];
       if (st.empty() || st.back().kind != 0 || st.back().xf.size() >= (size_t)kFcMaxXops) return false;
       Item& a = st.back();
+      // (a value narrower than the op's operand was zero-extended: canonical values are, so the
+      // op reads it at the wider width as is)
       if (op == G_EXTRACT) {
-        if (imm + w2 > a.w || w2 == 0) return false;
-        a.xf.push_back(FcXop{FX_EXTRACT | (a.w << 8), imm, w2, 0});
+        if (imm + w2 > 256 || w2 == 0) return false;
+        a.xf.push_back(FcXop{FX_EXTRACT | (std::max(a.w, imm + w2) << 8), imm, w2, 0});
       } else {
-        if (imm != a.w || w2 <= a.w || w2 > 256) return false;
-        a.xf.push_back(FcXop{FX_SEXT | (a.w << 8), w2, 0, 0});
+        if (imm < a.w || w2 <= imm || w2 > 256) return false;
+        a.xf.push_back(FcXop{FX_SEXT | (imm << 8), w2, 0, 0});
       }
       a.w = w2;
       continue;
@@ -2944,8 +2946,8 @@ static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_
         const uint32_t kc = st.back().v;
         st.pop_back();
         Item& a = st.back();
-        const uint32_t w = a.w;
-        if (imm != w || w == 0 || w > 256 || a.xf.size() >= (size_t)kFcMaxXops) return false;
+        const uint32_t w = imm;   // (>= the value's width: a zero-extended value, read as is)
+        if (imm < a.w || w == 0 || w > 256 || a.xf.size() >= (size_t)kFcMaxXops) return false;
         uint32_t l[8];
         const_limbs(kc, l);
         uint64_t k = 0;
@@ -2979,6 +2981,7 @@ static bool fc_match(const mq_ctx* c, const CompiledTape& x, std::vector<uint32_
           const uint32_t code = op == G_SMOD ? FX_SMOD : op == G_SREM ? FX_SREM : FX_SDIV;
           a.xf.push_back(FcXop{code | (w << 8), (uint32_t)ad, dneg ? 1u : 0u, 0});
         }
+        a.w = w;
         break;
       }
       case G_PUSH_VAR_B:
