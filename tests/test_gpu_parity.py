@@ -1605,10 +1605,11 @@ def test_flat_unary_atoms_match_oracle(evaluator, monkeypatch, seed):
     assert (fh == cref.first_hit(tb, mb)[0]).all()
     fh1 = evaluator.first_hit(ct)
     assert (fh1 == cref.first_hit(tb, mb)[0]).all()
-    # every tape the assembly path takes is flat (the others — signed division below 256 bits
-    # and the like — run on the HIP C++ kernel, which the flat path does not take from)
+    # (nearly) every tape the assembly path takes is flat — not one whose sub-term is used twice
+    # (a temp); the others (signed division below 256 bits and the like) run on the HIP C++ kernel,
+    # which the flat path does not take from
     n_asm = ct.split()[0]
-    assert n_flat == n_asm and n_flat >= 0.4 * tb.n_tapes, (n_flat, ct.split(), ct.asm_split())
+    assert n_flat >= 0.9 * n_asm and n_flat >= 0.4 * tb.n_tapes, (n_flat, ct.split(), ct.asm_split())
     assert v.any() and (~v).any()
     direct = np.array([[term_eval.is_true(e, m) for m in models[:50]] for e in exprs])
     assert (v[:, :50] == direct).all()
