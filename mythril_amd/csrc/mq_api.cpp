@@ -3418,13 +3418,16 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
   std::vector<std::vector<FcCmpH>> fc_q(nq);
   std::vector<char> fc_neg(nq, 0);
   T->fca = std::getenv("MQ_FC_ONEPHASE") == nullptr;
-  // unary atoms (fca only; MQ_FC_NO_UNARY=1 keeps the plain variable-constant atoms)
-  static const bool no_unary = std::getenv("MQ_FC_NO_UNARY") != nullptr;
+  // unary atoms (fca only) are opt-in, MQ_FC_UNARY=1: they move C3's tapes off G (all 1 000 are
+  // flat with them) but measured slower there — C3 18.6 -> 40.9 ms, C5 49 -> 69 ms (profiles/r06c):
+  // C3's 8 854 compares are 8 442 distinct atoms, so the flat kernel's phase 1 does the tapes' work
+  // with no sharing to win, for every tile, while G's per-tape cost is no higher per atom
+  const bool unary = T->fca && std::getenv("MQ_FC_UNARY") != nullptr;
   if (!no_flat)
     parallel_for(nq, 32, [&](int, int64_t b, int64_t e) {
       for (int64_t i = b; i < e; i++) {
         bool ng = false;
-        on_fc[i] = fc_match(c, T->qct[i], fc_m[i], fc_q[i], &ng, T->fca && !no_unary) ? 1 : 0;
+        on_fc[i] = fc_match(c, T->qct[i], fc_m[i], fc_q[i], &ng, unary) ? 1 : 0;
         fc_neg[i] = ng ? 1 : 0;
       }
     });

@@ -720,8 +720,7 @@ def test_asm_const_ops_and_lookups_match_oracle(evaluator, seed):
 
 
 def test_c3_tapes_run_on_general_asm_kernel(evaluator):
-    """C3's hoisted tapes run without the HIP C++ interpreter: on the flat kernel (unary atoms:
-    most of them) or the assembly interpreters (those reading an ite)."""
+    """C3's hoisted tapes run without the HIP C++ interpreter (on the assembly interpreters)."""
     from mythril_amd import synth_evm
     tb, mb, exp, _ = synth_evm.c3_workload(60, 3000, seed=9, hoist=True)
     evaluator.upload_models(mb)
@@ -730,7 +729,6 @@ def test_c3_tapes_run_on_general_asm_kernel(evaluator):
     n_p, n_g, live = ct.asm_split()
     n_flat = ct.flat_split()[0]
     assert live and n_p + n_g + n_flat >= 0.8 * tb.n_tapes, (n_p, n_g, n_flat, ct.split())
-    assert n_flat >= 0.5 * tb.n_tapes and n_g > 0, (n_p, n_g, n_flat)
     assert (fh == exp).all()
     evaluator.use_asm(False)
     try:
@@ -1590,10 +1588,11 @@ def _unary_atom_workload(seed, n_tapes=160, M=700):
 
 @pytest.mark.parametrize("seed", range(4))
 def test_flat_unary_atoms_match_oracle(evaluator, monkeypatch, seed):
-    """fca_kernel's unary atoms (fc.hip fx_apply; mq_api.cpp fc_match with unary steps): the
-    workload's tapes run on the flat kernel, and their verdicts and first hits are the oracle's
-    (and the direct term evaluator's)."""
+    """fca_kernel's unary atoms (fc.hip fx_apply; mq_api.cpp fc_match with unary steps; opt-in
+    MQ_FC_UNARY=1): the workload's tapes run on the flat kernel, and their verdicts and first
+    hits are the oracle's (and the direct term evaluator's)."""
     import term_eval
+    monkeypatch.setenv("MQ_FC_UNARY", "1")   # (opt-in: read per compile)
     exprs, models, tb, mb = _unary_atom_workload(seed)
     evaluator.upload_models(mb)
     ct = evaluator.compile(tb)
