@@ -61,17 +61,23 @@ class _BitMaps:
         self.c = nodes["c"].astype(np.int64)
         self.consts = consts
         self.memo: Dict[int, Optional[Tuple[Segment, ...]]] = {}
+        self.cvals: Dict[int, int] = {}
         self.floors: Dict[int, Tuple[Tuple[int, int], ...]] = {}
 
     def const_value(self, n: int) -> Optional[int]:
         if self.op[n] != 1:
             return None
+        v = self.cvals.get(n)
+        if v is not None:
+            return v
         nl = limbs(int(self.w[n]))
         off = int(self.a[n])
         v = 0
         for i in range(nl):
             v |= int(self.consts[off + i]) << (32 * i)
-        return v & ((1 << int(self.w[n])) - 1)
+        v &= (1 << int(self.w[n])) - 1
+        self.cvals[n] = v
+        return v
 
     def map(self, n: int) -> Optional[Tuple[Segment, ...]]:
         if n in self.memo:
@@ -457,13 +463,21 @@ class CandidateGenerator:
         # match wins)
         F = len(lru.funcs)
         func_index = {name: f for f, name in enumerate(syms.func_names)}
-        changed = []   # per block: {f: sorted derived vars of f the patch assigns}
-        for patch, _ in blocks:
-            d: Dict[int, set] = {}
-            for v, lo, n, bits in patch:
-                if lo >= 0 and v in syms.derived and syms.derived[v][0] in func_index:
-                    d.setdefault(func_index[syms.derived[v][0]], set()).add(v)
-            changed.append({f: sorted(vs) for f, vs in d.items()})
+        dfunc = {v: func_index[fn] for v, (fn, _) in syms.derived.items() if fn in func_index}
+        # per function: (block, position among the block's changed derived vars of it, var) triples
+        per_f: Dict[int, Tuple[List[int], List[int], List[int]]] = {}
+        for j, (patch, _) in enumerate(blocks):
+            vs = {el[0] for el in patch if el[0] in dfunc and el[1] >= 0}
+            if not vs:
+                continue
+            pos: Dict[int, int] = {}
+            for v in sorted(vs):
+                f = dfunc[v]
+                t = per_f.setdefault(f, ([], [], []))
+                t[0].append(j)
+                t[1].append(pos.get(f, 0))
+                t[2].append(v)
+                pos[f] = pos.get(f, 0) + 1
         eptr = np.zeros((F, M + 1), np.int64)
         ew_chunks, el_chunks = [], []
         ebase = np.zeros(F, np.int64)
@@ -474,27 +488,34 @@ class CandidateGenerator:
             base_ptr = lru.entry_ptr[f]
             base_cnt = np.diff(base_ptr)                                   # [n_lru]
             cnt_gen = base_cnt[src] if n_lru else np.zeros(K, np.int64)
-            add_cnt = np.repeat(np.asarray([len(ch.get(f, ())) for ch in changed], np.int64), sizes) \
-                if blocks else np.zeros(0, np.int64)
+            trip = per_f.get(f)
+            if trip is not None:
+                tj, ti, tv = (np.asarray(x, np.int64) for x in trip)
+                add_cnt = np.repeat(np.bincount(tj, minlength=len(blocks)), sizes)
+            else:
+                add_cnt = np.zeros(K, np.int64)
             counts = np.concatenate([base_cnt, cnt_gen + add_cnt])
             eptr[f, 1:] = np.cumsum(counts)
             ent = lru.entry_words[int(lru.entry_base[f]):int(lru.entry_base[f]) + int(base_ptr[-1]) * s].reshape(-1, s)
             out = np.zeros((int(eptr[f, -1]), s), np.uint32)
             out[:int(base_ptr[-1])] = ent
             gstarts = eptr[f, n_lru:n_lru + K]
-            for j, ch in enumerate(changed):
-                vs = ch.get(f)
-                if not vs:
-                    continue
-                cols = np.arange(int(starts[j]), int(starts[j + 1]))
-                for i, v in enumerate(vs):
-                    key = []
-                    for aw, av in zip(spec.arg_widths, syms.derived[v][1]):
-                        key.extend(to_words(int(av), aw))
-                    nl = limbs(syms.var_widths[v])
-                    rows = gstarts[cols] + i
-                    out[rows, :len(key)] = np.asarray(key, np.uint32)
-                    out[rows, len(key):len(key) + nl] = words[int(off[v]):int(off[v]) + nl, n_lru + cols].T
+            if trip is not None:
+                # the changed derived vars' entries (key = their constant arguments, value = the
+                # candidate's patched column), one row per (triple, candidate of its block)
+                lens = sizes[tj]
+                rep = np.repeat(np.arange(len(tj)), lens)
+                within = np.arange(int(lens.sum())) - np.repeat(np.cumsum(lens) - lens, lens)
+                cols = starts[tj][rep] + within
+                rows = gstarts[cols] + ti[rep]
+                uv, vinv = np.unique(tv, return_inverse=True)
+                keys = np.asarray([[w for aw, av in zip(spec.arg_widths, syms.derived[int(v)][1])
+                                    for w in to_words(int(av), aw)] for v in uv], np.uint32)
+                klen = keys.shape[1]
+                nl = limbs(syms.var_widths[int(uv[0])])
+                out[rows, :klen] = keys[vinv[rep]]
+                vrow = off[uv][vinv[rep]]
+                out[rows, klen:klen + nl] = words[vrow[:, None] + np.arange(nl)[None, :], (n_lru + cols)[:, None]]
             if n_lru and K:
                 gstart = gstarts + add_cnt
                 rep = cnt_gen

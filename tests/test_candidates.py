@@ -63,3 +63,27 @@ def test_candidate_rows_native_numpy_and_literal_agree(monkeypatch, fill):
     mats = [cs.materialize(int(k)) for k in ks]
     ser = inc.serialize(mats)
     assert (ser.var_words == cs.batch.var_words[:, ks]).all()
+
+
+def test_candidate_function_tables_match_materialized_models():
+    """A generated candidate's function tables (its base model's entries plus the entries of the
+    derived calldata bytes its patch changed) read like its materialized model's: the oracle's
+    verdicts of the workload's tapes agree on both serializations."""
+    import cref
+    exprs, recs, _ = fork_workload(24, 40, seed=6)
+    inc = IncrementalLowering()
+    db, ok = inc.lower(exprs)
+    cs = C.CandidateGenerator(6000, seed=4, fill=True).generate(db, inc.syms, inc.serialize(recs), recs)
+    assert cs.batch.funcs
+    tb = db.to_tapes()
+    fh, _ = cref.first_hit(tb, cs.batch)
+    hits = [int(h) for h in fh if h >= cs.n_lru]
+    assert hits
+    ks = np.asarray(hits[:30] + list(np.random.default_rng(1).integers(cs.n_lru, cs.batch.n_models, 30)), np.int64)
+    mats = [cs.materialize(int(k)) for k in ks]
+    ser = inc.serialize(mats)
+    v_mat = cref.verdicts(tb, ser)
+    for i, k in enumerate(ks):
+        one = cs.batch.shard(int(k), int(k) + 1)
+        assert (cref.verdicts(tb, one)[:, 0] == v_mat[:, i]).all(), int(k)
+    assert v_mat.any()
