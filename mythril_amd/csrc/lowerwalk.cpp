@@ -667,7 +667,132 @@ PyObject* py_candidate_rows(PyObject*, PyObject* a) {
   Py_RETURN_NONE;
 }
 
+// conj_rows(roots, row_of, n_rows, R, slots, rows_out) -> (n_rows, todo): ConjunctRows' bookkeeping
+// for one query batch (support.py VerdictEngine._rows_incremental).  roots: u32 [n] conjunct DAG
+// nodes of the batch's queries, back to back; row_of: i64 [> max node] node -> row (-1: none),
+// new rows numbered in first-appearance order from n_rows; R: i8 [rows cap, slot cap] verdicts
+// (-1 unknown); slots: i64 [s] the candidate models' slots.  rows_out: i64 [n] each root's row.
+// todo: the distinct nodes (first-appearance order) with an unknown verdict under some slot.
+PyObject* py_conj_rows(PyObject*, PyObject* a) {
+  PyObject *o_roots, *o_row_of, *o_R, *o_slots, *o_out;
+  long long n_rows;
+  if (!PyArg_ParseTuple(a, "OOLOOO", &o_roots, &o_row_of, &n_rows, &o_R, &o_slots, &o_out)) return nullptr;
+  Buf roots, row_of, R, slots, out;
+  if (!get_buf(o_roots, roots, false, 4, "roots") || !get_buf(o_row_of, row_of, true, 8, "row_of") ||
+      !get_buf(o_R, R, true, 1, "R") || !get_buf(o_slots, slots, false, 8, "slots") ||
+      !get_buf(o_out, out, true, 8, "rows_out"))
+    return nullptr;
+  const Py_ssize_t n = roots.b.len / 4, nro = row_of.b.len / 8, ns = slots.b.len / 8;
+  if (R.b.ndim != 2 || out.b.len / 8 != n) {
+    PyErr_SetString(PyExc_ValueError, "conj_rows: shapes");
+    return nullptr;
+  }
+  const Py_ssize_t rcap = R.b.shape[0], scap = R.b.shape[1];
+  const uint32_t* rt = (const uint32_t*)roots.b.buf;
+  int64_t* ro = (int64_t*)row_of.b.buf;
+  int8_t* RR = (int8_t*)R.b.buf;
+  const int64_t* sl = (const int64_t*)slots.b.buf;
+  int64_t* rows = (int64_t*)out.b.buf;
+  for (Py_ssize_t j = 0; j < ns; j++)
+    if (sl[j] < 0 || sl[j] >= scap) {
+      PyErr_SetString(PyExc_ValueError, "conj_rows: slot beyond R");
+      return nullptr;
+    }
+  PyObject* todo = PyList_New(0);
+  if (!todo) return nullptr;
+  for (Py_ssize_t i = 0; i < n; i++) {
+    const uint32_t node = rt[i];
+    if ((Py_ssize_t)node >= nro) {
+      Py_DECREF(todo);
+      PyErr_SetString(PyExc_ValueError, "conj_rows: node beyond row_of");
+      return nullptr;
+    }
+    int64_t r = ro[node];
+    bool fresh = false;
+    if (r < 0) {
+      if (n_rows >= rcap) {
+        Py_DECREF(todo);
+        PyErr_SetString(PyExc_ValueError, "conj_rows: R has too few rows");
+        return nullptr;
+      }
+      r = ro[node] = n_rows++;
+      fresh = true;   // (a new row is all unknown; its node is listed once, here)
+    }
+    rows[i] = r;
+    bool unknown = fresh;
+    if (!fresh) {
+      // listed already when a row seen earlier in this batch was unknown: mark with -2 below
+      const int8_t* rr = RR + r * scap;
+      for (Py_ssize_t j = 0; j < ns && !unknown; j++) unknown = rr[sl[j]] < 0;
+      if (unknown && rr[sl[0]] == -2) unknown = false;
+    }
+    if (unknown) {
+      PyObject* o = PyLong_FromUnsignedLong(node);
+      if (!o || PyList_Append(todo, o) < 0) {
+        Py_XDECREF(o);
+        Py_DECREF(todo);
+        return nullptr;
+      }
+      Py_DECREF(o);
+      if (ns) RR[r * scap + sl[0]] = -2;   // (a transient "listed" mark: still unknown)
+    }
+  }
+  // clear the transient marks (they stay unknown, -1, until the caller writes the verdicts)
+  for (Py_ssize_t i = 0; i < n && ns; i++) {
+    int8_t* v = RR + rows[i] * scap + sl[0];
+    if (*v == -2) *v = -1;
+  }
+  return Py_BuildValue("(LN)", n_rows, todo);
+}
+
+// conj_answer(R, rows, offsets, slots, out): out[q, j] = AND over the conjuncts of query q
+// (rows[offsets[q] .. offsets[q + 1]]) of R[row, slots[j]] > 0 (And() of nothing: true)
+PyObject* py_conj_answer(PyObject*, PyObject* a) {
+  PyObject *o_R, *o_rows, *o_off, *o_slots, *o_out;
+  if (!PyArg_ParseTuple(a, "OOOOO", &o_R, &o_rows, &o_off, &o_slots, &o_out)) return nullptr;
+  Buf R, rows, off, slots, out;
+  if (!get_buf(o_R, R, false, 1, "R") || !get_buf(o_rows, rows, false, 8, "rows") ||
+      !get_buf(o_off, off, false, 8, "offsets") || !get_buf(o_slots, slots, false, 8, "slots") ||
+      !get_buf(o_out, out, true, 1, "out"))
+    return nullptr;
+  const Py_ssize_t nq = off.b.len / 8 - 1, ns = slots.b.len / 8, nr = rows.b.len / 8;
+  if (R.b.ndim != 2 || nq < 0 || out.b.len != nq * ns) {
+    PyErr_SetString(PyExc_ValueError, "conj_answer: shapes");
+    return nullptr;
+  }
+  const Py_ssize_t rcap = R.b.shape[0], scap = R.b.shape[1];
+  const int8_t* RR = (const int8_t*)R.b.buf;
+  const int64_t* rw = (const int64_t*)rows.b.buf;
+  const int64_t* of = (const int64_t*)off.b.buf;
+  const int64_t* sl = (const int64_t*)slots.b.buf;
+  uint8_t* o = (uint8_t*)out.b.buf;
+  for (Py_ssize_t j = 0; j < ns; j++)
+    if (sl[j] < 0 || sl[j] >= scap) {
+      PyErr_SetString(PyExc_ValueError, "conj_answer: slot beyond R");
+      return nullptr;
+    }
+  for (Py_ssize_t q = 0; q < nq; q++) {
+    if (of[q] < 0 || of[q + 1] > nr || of[q] > of[q + 1]) {
+      PyErr_SetString(PyExc_ValueError, "conj_answer: offsets");
+      return nullptr;
+    }
+    uint8_t* oq = o + q * ns;
+    for (Py_ssize_t j = 0; j < ns; j++) oq[j] = 1;
+    for (int64_t k = of[q]; k < of[q + 1]; k++) {
+      if (rw[k] < 0 || rw[k] >= rcap) {
+        PyErr_SetString(PyExc_ValueError, "conj_answer: row beyond R");
+        return nullptr;
+      }
+      const int8_t* rr = RR + rw[k] * scap;
+      for (Py_ssize_t j = 0; j < ns; j++) oq[j] &= rr[sl[j]] > 0 ? 1 : 0;
+    }
+  }
+  Py_RETURN_NONE;
+}
+
 PyMethodDef methods[] = {
+    {"conj_rows", py_conj_rows, METH_VARARGS, "conj_rows(roots, row_of, n_rows, R, slots, rows_out) -> (n_rows, todo)"},
+    {"conj_answer", py_conj_answer, METH_VARARGS, "conj_answer(R, rows, offsets, slots, out): per-query AND of conjunct rows"},
     {"candidate_rows", py_candidate_rows, METH_VARARGS,
      "candidate_rows(gen, lru, src, starts, patches, var_off, var_limbs): generated candidates' rows"},
     {"pack_nodes", py_pack_nodes, METH_VARARGS, "pack_nodes(nodes, start, end, out): node tuples -> NODE_DTYPE records"},
