@@ -220,8 +220,51 @@ struct DevBuf {
     if (e != hipSuccess || count == 0) return e;
     return hipMemcpyAsync(p, src, sizeof(T) * count, hipMemcpyHostToDevice, st);
   }
+  // the same through the staging ring (StageRing, defined below): the source may be freed at once
+  template <class T, class Ring>
+  hipError_t upload_staged(const T* src, size_t count, hipStream_t st, Ring& ring) {
+    hipError_t e = ensure(sizeof(T) * count);
+    if (e != hipSuccess || count == 0) return e;
+    const size_t n = sizeof(T) * count;
+    void* h = n <= Ring::kMaxStaged ? ring.put(src, n, st) : nullptr;
+    if (!h) {
+      e = hipMemcpyAsync(p, src, n, hipMemcpyHostToDevice, st);
+      return e != hipSuccess ? e : hipStreamSynchronize(st);
+    }
+    return hipMemcpyAsync(p, h, n, hipMemcpyHostToDevice, st);
+  }
   template <class T>
   T* as() const { return (T*)p; }
+};
+
+// Small host-to-device uploads of the drop-in path (tape tables, translated programs, argument
+// blocks: ~10 per query batch) through a page-locked ring: the copy is a DMA from pinned memory
+// that the host does not wait for, so the stream syncs that kept pageable sources alive until
+// their copy ran are gone (profiles/r06f: 10 pageable hipMemcpyAsync + ~6 stream syncs per batch,
+// ~0.14 ms of a 0.23 ms batch).  A source is staged at the ring's head; when the ring is full the
+// streams that copied out of it are drained and it starts over (every ~8 MB of uploads).
+struct StageRing {
+  static constexpr size_t kMaxStaged = size_t(256) << 10;   // larger uploads: pageable + a sync
+  static constexpr size_t kBytes = size_t(8) << 20;
+  PinnedBuf buf;
+  size_t head = 0;
+  std::vector<hipStream_t> used;
+  // pinned copy of src (n <= kMaxStaged) for an async copy on st; nullptr: stage failed
+  void* put(const void* src, size_t n, hipStream_t st) {
+    if (!buf.p && buf.ensure(kBytes) != hipSuccess) return nullptr;
+    const size_t a = (n + 255) & ~size_t(255);
+    if (head + a > buf.bytes) {
+      for (hipStream_t s : used)
+        if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
+      used.clear();
+      head = 0;
+    }
+    if (std::find(used.begin(), used.end(), st) == used.end()) used.push_back(st);
+    void* d = (char*)buf.p + head;
+    std::memcpy(d, src, n);
+    head += a;
+    return d;
+  }
 };
 
 }  // namespace
@@ -295,6 +338,8 @@ struct mq_ctx {
   DevBuf verdict_buf;
   PinnedBuf verdict_host;   // verdict bytes read back (batches up to kPinnedVerdictBytes)
   PinnedBuf readback_host;  // a first-hit launch's counter slots and first hits
+  StageRing stage;          // small uploads (DevBuf::upload_staged)
+  hipEvent_t stage_ev = nullptr;   // a launch on a caller's stream waits for the context stream's copies
   // assembly interpreters (qsa.hip): handler byte offsets read back at context creation;
   // k = 0 the P kernel (preloaded variables), k = 1 the G kernel (general)
   bool qsa_ready = false;
@@ -494,6 +539,7 @@ struct mq_tapes {
   DevBuf cq_group_dev;
   // multi-device context: the same batch compiled on each peer device (ctx->peers order)
   std::vector<mq_tapes*> peers;
+  bool in_flight = false;   // copies or launches the host has not waited for (mq_tapes_free)
   ~mq_tapes() {
     for (mq_tapes* p : peers) delete p;
     std::lock_guard<std::mutex> g(g_live_mu);
@@ -772,7 +818,8 @@ static int create_one(int dev, mq_ctx** out) {
       hipStreamCreateWithFlags(&c->aux[1], hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->join_ev[0], hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->join_ev[1], hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->join_ev[1], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->stage_ev, hipEventDisableTiming) != hipSuccess) {
     mq_ctx_destroy(c);
     return MQ_ERR_HIP;
   }
@@ -860,6 +907,7 @@ void mq_ctx_destroy(mq_ctx* c) {
       DevPool::get().unregister_stream(c->device, a);
     }
   if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+  if (c->stage_ev) (void)hipEventDestroy(c->stage_ev);
   for (hipEvent_t e : c->join_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1942,15 +1990,15 @@ static int tapes_upload_one(mq_ctx* c, int32_t n_tapes, std::vector<CompiledTape
   consts.resize(consts.size() + 16, 0);
   prog.push_back(gword(G_END, 0, 0));
   if (descs.empty()) descs.push_back(GDesc{});
-  HIPCHK(T->descs.upload(descs.data(), descs.size(), c->stream));
+  HIPCHK(T->descs.upload_staged(descs.data(), descs.size(), c->stream, c->stage));
   HIPCHK(T->qargs[0].ensure(sizeof(QArgs)));
   HIPCHK(T->qargs[1].ensure(sizeof(QArgs)));
-  HIPCHK(T->prog.upload(prog.data(), prog.size(), c->stream));
+  HIPCHK(T->prog.upload_staged(prog.data(), prog.size(), c->stream, c->stage));
   // P's constant prefetch reads 8 words at a tape's constants + 0 even for a tape without any
   consts.insert(consts.end(), 8, 0u);
-  HIPCHK(T->consts.upload(consts.data(), consts.size(), c->stream));
-  HIPCHK(T->unsup_dev.upload(T->unsupported.data(), T->unsupported.size(), c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(T->consts.upload_staged(consts.data(), consts.size(), c->stream, c->stage));
+  HIPCHK(T->unsup_dev.upload_staged(T->unsupported.data(), T->unsupported.size(), c->stream, c->stage));
+  T->in_flight = true;
   T->unsupported_base = T->unsupported;
   *out = T.release();
   return MQ_OK;
@@ -2177,7 +2225,9 @@ void mq_tapes_free(mq_tapes* t) {
   double* acc = t->ctx ? &t->ctx->host_t[9] : nullptr;
   double dummy = 0;
   PhaseTimer pt(acc ? acc : &dummy);
-  if (t->ctx && t->ctx->stream) (void)hipStreamSynchronize(t->ctx->stream);
+  // (a batch whose copies and launches the host has already waited for needs no sync: the
+  // drop-in path frees one per query batch)
+  if (t->ctx && t->ctx->stream && t->in_flight) (void)hipStreamSynchronize(t->ctx->stream);
   delete t;
 }
 
@@ -3561,8 +3611,8 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
     T->q_temps[k] = temps[k];
   }
   if (descs.empty()) descs.push_back(GDesc{});
-  HIPCHK(T->qdescs.upload(descs.data(), descs.size(), c->stream));
-  HIPCHK(T->qprog.upload(prog.data(), prog.size(), c->stream));
+  HIPCHK(T->qdescs.upload_staged(descs.data(), descs.size(), c->stream, c->stage));
+  HIPCHK(T->qprog.upload_staged(prog.data(), prog.size(), c->stream, c->stage));
   if (T->fca) {
     T->fc_count = (int)fap.tape_out.size();
     T->fca_atoms = (int)fap.atoms.size();
@@ -3573,14 +3623,14 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
       if (fap.xfs.empty()) fap.xfs.push_back(FcXf{});
       if (fap.groups.empty()) fap.groups.push_back(FcaGroup{});
       if (fap.lists.empty()) fap.lists.push_back(0);
-      HIPCHK(T->fc_cmp_dev.upload(fap.atoms.data(), fap.atoms.size(), c->stream));
-      HIPCHK(T->fca_xf_dev.upload(fap.xfs.data(), fap.xfs.size(), c->stream));
-      HIPCHK(T->fca_group_dev.upload(fap.groups.data(), fap.groups.size(), c->stream));
-      HIPCHK(T->fc_mask_dev.upload(fap.lists.data(), fap.lists.size(), c->stream));
-      HIPCHK(T->fca_chunk_dev.upload(fap.chunk_off.data(), fap.chunk_off.size(), c->stream));
-      HIPCHK(T->fca_out_dev.upload(fap.tape_out.data(), fap.tape_out.size(), c->stream));
-      HIPCHK(T->fca_metric_dev.upload(fap.metric.data(), fap.metric.size(), c->stream));
-      HIPCHK(T->fc_smask_dev.upload(fap.stage_masks.data(), fap.stage_masks.size(), c->stream));
+      HIPCHK(T->fc_cmp_dev.upload_staged(fap.atoms.data(), fap.atoms.size(), c->stream, c->stage));
+      HIPCHK(T->fca_xf_dev.upload_staged(fap.xfs.data(), fap.xfs.size(), c->stream, c->stage));
+      HIPCHK(T->fca_group_dev.upload_staged(fap.groups.data(), fap.groups.size(), c->stream, c->stage));
+      HIPCHK(T->fc_mask_dev.upload_staged(fap.lists.data(), fap.lists.size(), c->stream, c->stage));
+      HIPCHK(T->fca_chunk_dev.upload_staged(fap.chunk_off.data(), fap.chunk_off.size(), c->stream, c->stage));
+      HIPCHK(T->fca_out_dev.upload_staged(fap.tape_out.data(), fap.tape_out.size(), c->stream, c->stage));
+      HIPCHK(T->fca_metric_dev.upload_staged(fap.metric.data(), fap.metric.size(), c->stream, c->stage));
+      HIPCHK(T->fc_smask_dev.upload_staged(fap.stage_masks.data(), fap.stage_masks.size(), c->stream, c->stage));
     }
   } else {
     T->fc_count = (int)fcp.tapes.size();
@@ -3592,16 +3642,15 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
     if (fcp.stage_masks.empty()) fcp.stage_masks.push_back(0);
     if (fcp.mask_lds.empty()) fcp.mask_lds.push_back(0);
     if (fcp.cmps.empty()) fcp.cmps.push_back(FcCmp{});
-    HIPCHK(T->fc_tapes_dev.upload(fcp.tapes.data(), fcp.tapes.size(), c->stream));
-    HIPCHK(T->fc_mask_dev.upload(fcp.mask_lds.data(), fcp.mask_lds.size(), c->stream));
-    HIPCHK(T->fc_cmp_dev.upload(fcp.cmps.data(), fcp.cmps.size(), c->stream));
-    HIPCHK(T->fc_stage_dev.upload(fcp.stage_rows.data(), fcp.stage_rows.size(), c->stream));
-    HIPCHK(T->fc_smask_dev.upload(fcp.stage_masks.data(), fcp.stage_masks.size(), c->stream));
-    HIPCHK(T->fc_prefix_dev.upload(fcp.prefix.data(), fcp.prefix.size(), c->stream));
+    HIPCHK(T->fc_tapes_dev.upload_staged(fcp.tapes.data(), fcp.tapes.size(), c->stream, c->stage));
+    HIPCHK(T->fc_mask_dev.upload_staged(fcp.mask_lds.data(), fcp.mask_lds.size(), c->stream, c->stage));
+    HIPCHK(T->fc_cmp_dev.upload_staged(fcp.cmps.data(), fcp.cmps.size(), c->stream, c->stage));
+    HIPCHK(T->fc_stage_dev.upload_staged(fcp.stage_rows.data(), fcp.stage_rows.size(), c->stream, c->stage));
+    HIPCHK(T->fc_smask_dev.upload_staged(fcp.stage_masks.data(), fcp.stage_masks.size(), c->stream, c->stage));
+    HIPCHK(T->fc_prefix_dev.upload_staged(fcp.prefix.data(), fcp.prefix.size(), c->stream, c->stage));
   }
   if (T->stage_rows.empty()) HIPCHK(T->stage_dev.ensure(sizeof(uint32_t)));
-  else HIPCHK(T->stage_dev.upload(T->stage_rows.data(), T->stage_rows.size(), c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  else HIPCHK(T->stage_dev.upload_staged(T->stage_rows.data(), T->stage_rows.size(), c->stream, c->stage));
   T->qargs_valid[0] = T->qargs_valid[1] = false;
   T->qsa_live = true;
   return MQ_OK;
@@ -3846,12 +3895,12 @@ static int refresh_wide_unsupported(mq_ctx* c, mq_tapes* T, hipStream_t st) {
     n += T->unsupported[t];
   }
   T->n_unsupported = n;
-  HIPCHK(T->unsup_dev.upload(T->unsupported.data(), T->unsupported.size(), st));
-  HIPCHK(hipStreamSynchronize(st));
+  HIPCHK(T->unsup_dev.upload_staged(T->unsupported.data(), T->unsupported.size(), st, c->stage));
   return MQ_OK;
 }
 
 static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, hipStream_t st) {
+  T->in_flight = true;   // (cleared where the host waits for the launch: mq_tapes_free skips its sync)
   if (const int rc = refresh_wide_unsupported(c, T, st)) return rc;
   bool use_qsa = c->qsa_ready && c->use_asm && T->qsa.count > 0;
   // latency-bound launch (a few tapes over a few models): G runs one tape per wave instead of
@@ -3913,6 +3962,12 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
   } else {
     T->cq_live = false;   // (re-translated when the assembly path is enabled again)
     T->cq_gen = ~0ull;
+  }
+  if (st != c->stream) {
+    // the batch's tables were copied on the context stream (tape upload, translations): a
+    // launch on a caller's stream waits for them
+    HIPCHK(hipEventRecord(c->stage_ev, c->stream));
+    HIPCHK(hipStreamWaitEvent(st, c->stage_ev, 0));
   }
   const uint32_t zero_row = (uint32_t)(c->var_off_h.empty() ? 0 : c->var_off_h.back() + c->var_nl_h.back());
   if (T->bmask_gen != c->layout_gen) {
@@ -4160,8 +4215,9 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
       QArgs* dq = T->cqargs.as<QArgs>() + li;
       if (std::memcmp(&T->cqargs_host[li], &q, sizeof(QArgs)) != 0) {
         PhaseTimer pq(&c->host_t[6]);
-        HIPCHK(hipMemcpyAsync(dq, &q, sizeof(QArgs), hipMemcpyHostToDevice, st));
-        HIPCHK(hipStreamSynchronize(st));  // q is host memory
+        void* h = c->stage.put(&q, sizeof(QArgs), st);   // (q is on the stack: staged)
+        if (!h) return MQ_ERR_NOMEM;
+        HIPCHK(hipMemcpyAsync(dq, h, sizeof(QArgs), hipMemcpyHostToDevice, st));
         T->cqargs_host[li] = q;
       }
       const int64_t groups = T->cq_lvl_groups[li];
@@ -4253,8 +4309,9 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     // the argument block only changes with the output buffer / mode / models: re-upload then
     if (!T->qargs_valid[k] || std::memcmp(&T->qargs_dev_copy[k], &q, sizeof(QArgs)) != 0) {
       PhaseTimer pq(&c->host_t[6]);
-      HIPCHK(hipMemcpyAsync(T->qargs[k].p, &q, sizeof(QArgs), hipMemcpyHostToDevice, st));
-      HIPCHK(hipStreamSynchronize(st));  // q is host memory
+      void* h = c->stage.put(&q, sizeof(QArgs), st);   // (q is on the stack: staged)
+      if (!h) return MQ_ERR_NOMEM;
+      HIPCHK(hipMemcpyAsync(T->qargs[k].p, h, sizeof(QArgs), hipMemcpyHostToDevice, st));
       T->qargs_dev_copy[k] = q;
       T->qargs_valid[k] = true;
     }
@@ -4564,6 +4621,9 @@ int mq_eval_tapes_first_hit(mq_ctx* c, mq_tapes* T, int32_t* out, mq_stats* stat
   }
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
+  // (every device's stream was waited for above; the RCCL reduce runs on them)
+  T->in_flight = false;
+  for (mq_tapes* p : T->peers) p->in_flight = false;
   if (pinned) std::memcpy(out, stage + kCounterBytes, best_bytes);
   if (stats) {
     float ms = 0;
@@ -4616,11 +4676,13 @@ static int verdict_bytes_one(mq_ctx* c, mq_tapes* T, std::vector<uint8_t>& host)
   if (nbytes && nbytes <= kPinnedVerdictBytes && c->verdict_host.ensure(nbytes) == hipSuccess) {
     HIPCHK(hipMemcpyAsync(c->verdict_host.p, c->verdict_buf.p, nbytes, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    T->in_flight = false;
     std::memcpy(host.data(), c->verdict_host.p, nbytes);
     return MQ_OK;
   }
   if (nbytes) HIPCHK(hipMemcpyAsync(host.data(), c->verdict_buf.p, nbytes, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  T->in_flight = false;
   return MQ_OK;
 }
 
