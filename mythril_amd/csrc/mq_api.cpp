@@ -162,12 +162,14 @@ struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
   int dev = 0;
+  bool own = true;   // false: a view into another buffer (UploadPack), released with it
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
-  DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes), dev(o.dev) {
+  DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes), dev(o.dev), own(o.own) {
     o.p = nullptr;
     o.bytes = 0;
+    o.own = true;
   }
   DevBuf& operator=(DevBuf&& o) noexcept {
     if (this != &o) {
@@ -175,16 +177,25 @@ struct DevBuf {
       p = o.p;
       bytes = o.bytes;
       dev = o.dev;
+      own = o.own;
       o.p = nullptr;
       o.bytes = 0;
+      o.own = true;
     }
     return *this;
   }
   ~DevBuf() { release(); }
   void release() {
-    if (p) DevPool::get().put(dev, p, bytes);
+    if (p && own) DevPool::get().put(dev, p, bytes);
     p = nullptr;
     bytes = 0;
+    own = true;
+  }
+  void set_view(void* q, size_t n) {
+    release();
+    p = q;
+    bytes = n;
+    own = false;
   }
   hipError_t ensure(size_t n) {
     if (n <= bytes && p) return hipSuccess;
@@ -264,6 +275,32 @@ struct StageRing {
     std::memcpy(d, src, n);
     head += a;
     return d;
+  }
+};
+
+// Several small host arrays copied to the device as ONE block (one staged copy instead of one
+// copy each: the drop-in path's per-batch tables); the DevBufs become views into it.  The block
+// DevBuf must outlive its views (both live in the same mq_tapes).
+struct UploadPack {
+  std::vector<uint8_t> host;
+  struct V {
+    DevBuf* buf;
+    size_t off, bytes;
+  };
+  std::vector<V> views;
+  template <class T>
+  void add(DevBuf& v, const T* src, size_t count) {
+    const size_t off = (host.size() + 255) & ~size_t(255), n = sizeof(T) * count;
+    host.resize(off + std::max<size_t>(n, 1), 0);
+    if (n) std::memcpy(host.data() + off, src, n);
+    views.push_back(V{&v, off, std::max<size_t>(n, 1)});
+  }
+  hipError_t commit(DevBuf& block, hipStream_t st, StageRing& ring) {
+    for (const V& x : views) x.buf->release();   // (views of the previous block, if any)
+    const hipError_t e = block.upload_staged(host.data(), host.size(), st, ring);
+    if (e != hipSuccess) return e;
+    for (const V& x : views) x.buf->set_view((char*)block.p + x.off, x.bytes);
+    return hipSuccess;
   }
 };
 
@@ -539,6 +576,7 @@ struct mq_tapes {
   DevBuf cq_group_dev;
   // multi-device context: the same batch compiled on each peer device (ctx->peers order)
   std::vector<mq_tapes*> peers;
+  DevBuf pack0, pack1;   // UploadPack blocks: the upload's tables / qsa_prepare's (the views above point in)
   bool in_flight = false;   // copies or launches the host has not waited for (mq_tapes_free)
   ~mq_tapes() {
     for (mq_tapes* p : peers) delete p;
@@ -1990,14 +2028,18 @@ static int tapes_upload_one(mq_ctx* c, int32_t n_tapes, std::vector<CompiledTape
   consts.resize(consts.size() + 16, 0);
   prog.push_back(gword(G_END, 0, 0));
   if (descs.empty()) descs.push_back(GDesc{});
-  HIPCHK(T->descs.upload_staged(descs.data(), descs.size(), c->stream, c->stage));
   HIPCHK(T->qargs[0].ensure(sizeof(QArgs)));
   HIPCHK(T->qargs[1].ensure(sizeof(QArgs)));
-  HIPCHK(T->prog.upload_staged(prog.data(), prog.size(), c->stream, c->stage));
   // P's constant prefetch reads 8 words at a tape's constants + 0 even for a tape without any
   consts.insert(consts.end(), 8, 0u);
-  HIPCHK(T->consts.upload_staged(consts.data(), consts.size(), c->stream, c->stage));
-  HIPCHK(T->unsup_dev.upload_staged(T->unsupported.data(), T->unsupported.size(), c->stream, c->stage));
+  {
+    UploadPack pk;   // descriptors, programs, constants, unsupported flags: one copy
+    pk.add(T->descs, descs.data(), descs.size());
+    pk.add(T->prog, prog.data(), prog.size());
+    pk.add(T->consts, consts.data(), consts.size());
+    pk.add(T->unsup_dev, T->unsupported.data(), T->unsupported.size());
+    HIPCHK(pk.commit(T->pack0, c->stream, c->stage));
+  }
   T->in_flight = true;
   T->unsupported_base = T->unsupported;
   *out = T.release();
@@ -3611,8 +3653,9 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
     T->q_temps[k] = temps[k];
   }
   if (descs.empty()) descs.push_back(GDesc{});
-  HIPCHK(T->qdescs.upload_staged(descs.data(), descs.size(), c->stream, c->stage));
-  HIPCHK(T->qprog.upload_staged(prog.data(), prog.size(), c->stream, c->stage));
+  UploadPack pk;
+  pk.add(T->qdescs, descs.data(), descs.size());
+  pk.add(T->qprog, prog.data(), prog.size());
   if (T->fca) {
     T->fc_count = (int)fap.tape_out.size();
     T->fca_atoms = (int)fap.atoms.size();
@@ -3623,14 +3666,14 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
       if (fap.xfs.empty()) fap.xfs.push_back(FcXf{});
       if (fap.groups.empty()) fap.groups.push_back(FcaGroup{});
       if (fap.lists.empty()) fap.lists.push_back(0);
-      HIPCHK(T->fc_cmp_dev.upload_staged(fap.atoms.data(), fap.atoms.size(), c->stream, c->stage));
-      HIPCHK(T->fca_xf_dev.upload_staged(fap.xfs.data(), fap.xfs.size(), c->stream, c->stage));
-      HIPCHK(T->fca_group_dev.upload_staged(fap.groups.data(), fap.groups.size(), c->stream, c->stage));
-      HIPCHK(T->fc_mask_dev.upload_staged(fap.lists.data(), fap.lists.size(), c->stream, c->stage));
-      HIPCHK(T->fca_chunk_dev.upload_staged(fap.chunk_off.data(), fap.chunk_off.size(), c->stream, c->stage));
-      HIPCHK(T->fca_out_dev.upload_staged(fap.tape_out.data(), fap.tape_out.size(), c->stream, c->stage));
-      HIPCHK(T->fca_metric_dev.upload_staged(fap.metric.data(), fap.metric.size(), c->stream, c->stage));
-      HIPCHK(T->fc_smask_dev.upload_staged(fap.stage_masks.data(), fap.stage_masks.size(), c->stream, c->stage));
+      pk.add(T->fc_cmp_dev, fap.atoms.data(), fap.atoms.size());
+      pk.add(T->fca_xf_dev, fap.xfs.data(), fap.xfs.size());
+      pk.add(T->fca_group_dev, fap.groups.data(), fap.groups.size());
+      pk.add(T->fc_mask_dev, fap.lists.data(), fap.lists.size());
+      pk.add(T->fca_chunk_dev, fap.chunk_off.data(), fap.chunk_off.size());
+      pk.add(T->fca_out_dev, fap.tape_out.data(), fap.tape_out.size());
+      pk.add(T->fca_metric_dev, fap.metric.data(), fap.metric.size());
+      pk.add(T->fc_smask_dev, fap.stage_masks.data(), fap.stage_masks.size());
     }
   } else {
     T->fc_count = (int)fcp.tapes.size();
@@ -3642,15 +3685,20 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
     if (fcp.stage_masks.empty()) fcp.stage_masks.push_back(0);
     if (fcp.mask_lds.empty()) fcp.mask_lds.push_back(0);
     if (fcp.cmps.empty()) fcp.cmps.push_back(FcCmp{});
-    HIPCHK(T->fc_tapes_dev.upload_staged(fcp.tapes.data(), fcp.tapes.size(), c->stream, c->stage));
-    HIPCHK(T->fc_mask_dev.upload_staged(fcp.mask_lds.data(), fcp.mask_lds.size(), c->stream, c->stage));
-    HIPCHK(T->fc_cmp_dev.upload_staged(fcp.cmps.data(), fcp.cmps.size(), c->stream, c->stage));
-    HIPCHK(T->fc_stage_dev.upload_staged(fcp.stage_rows.data(), fcp.stage_rows.size(), c->stream, c->stage));
-    HIPCHK(T->fc_smask_dev.upload_staged(fcp.stage_masks.data(), fcp.stage_masks.size(), c->stream, c->stage));
-    HIPCHK(T->fc_prefix_dev.upload_staged(fcp.prefix.data(), fcp.prefix.size(), c->stream, c->stage));
+    pk.add(T->fc_tapes_dev, fcp.tapes.data(), fcp.tapes.size());
+    pk.add(T->fc_mask_dev, fcp.mask_lds.data(), fcp.mask_lds.size());
+    pk.add(T->fc_cmp_dev, fcp.cmps.data(), fcp.cmps.size());
+    pk.add(T->fc_stage_dev, fcp.stage_rows.data(), fcp.stage_rows.size());
+    pk.add(T->fc_smask_dev, fcp.stage_masks.data(), fcp.stage_masks.size());
+    pk.add(T->fc_prefix_dev, fcp.prefix.data(), fcp.prefix.size());
   }
-  if (T->stage_rows.empty()) HIPCHK(T->stage_dev.ensure(sizeof(uint32_t)));
-  else HIPCHK(T->stage_dev.upload_staged(T->stage_rows.data(), T->stage_rows.size(), c->stream, c->stage));
+  {
+    const uint32_t zero = 0;
+    if (T->stage_rows.empty()) pk.add(T->stage_dev, &zero, 1);
+    else pk.add(T->stage_dev, T->stage_rows.data(), T->stage_rows.size());
+  }
+  // (translated programs, descriptors, flat-kernel tables and staging rows: one copy)
+  HIPCHK(pk.commit(T->pack1, c->stream, c->stage));
   T->qargs_valid[0] = T->qargs_valid[1] = false;
   T->qsa_live = true;
   return MQ_OK;
