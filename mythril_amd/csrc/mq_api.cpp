@@ -1044,7 +1044,13 @@ static int upload_one(mq_ctx* c, const mq_model_batch* mb) {
   c->have_models = false;
   // variable rows followed by one all-zero row (the QSA preload points absent limbs at it)
   HIPCHK(c->vars.ensure(sizeof(uint32_t) * (size_t)(rows + 1) * M));
-  if (rows > 0) HIPCHK(hipMemcpyAsync(c->vars.p, mb->var_words, sizeof(uint32_t) * (size_t)rows * M, hipMemcpyHostToDevice, c->stream));
+  if (rows > 0) {
+    // (a drop-in batch's rows are a few KB: staged, no sync; a large batch: pageable + a sync)
+    const size_t n = sizeof(uint32_t) * (size_t)rows * M;
+    void* h = n <= StageRing::kMaxStaged ? c->stage.put(mb->var_words, n, c->stream) : nullptr;
+    HIPCHK(hipMemcpyAsync(c->vars.p, h ? h : mb->var_words, n, hipMemcpyHostToDevice, c->stream));
+    if (!h) HIPCHK(hipStreamSynchronize(c->stream));
+  }
   HIPCHK(hipMemsetAsync((uint32_t*)c->vars.p + (size_t)rows * M, 0, sizeof(uint32_t) * M, c->stream));
   {
     // canonical values: bits above a variable's width are cleared on the device (the kernels
@@ -1060,7 +1066,7 @@ static int upload_one(mq_ctx* c, const mq_model_batch* mb) {
       }
     }
     if (need) {
-      HIPCHK(c->rowmask.upload(rowmask.data(), rowmask.size(), c->stream));
+      HIPCHK(c->rowmask.upload_staged(rowmask.data(), rowmask.size(), c->stream, c->stage));
       HIPCHK(launch_mask_rows(c->vars.as<uint32_t>(), c->rowmask.as<uint32_t>(), rows, M, c->stream));
     }
   }
@@ -1088,7 +1094,7 @@ static int upload_one(mq_ctx* c, const mq_model_batch* mb) {
     const int64_t tiles = (M + 63) / 64;
     HIPCHK(c->bmasks.ensure(std::max<size_t>(8, sizeof(uint64_t) * (size_t)tiles * brows.size())));
     if (brows.empty()) brows.push_back(0);
-    HIPCHK(c->bmask_rows.upload(brows.data(), brows.size(), c->stream));
+    HIPCHK(c->bmask_rows.upload_staged(brows.data(), brows.size(), c->stream, c->stage));
     HIPCHK(launch_pack_bool(c->vars.as<uint32_t>(), c->bmasks.as<uint64_t>(), c->bmask_rows.as<uint32_t>(), nullptr,
                             c->n_bmask, c->n_bmask, M, c->stream));
   }
@@ -1116,25 +1122,24 @@ static int upload_one(mq_ctx* c, const mq_model_batch* mb) {
       c->layout_gen++;
     }
   }
-  HIPCHK(c->var_off.upload(voff.data(), voff.size(), c->stream));
-  HIPCHK(c->var_nl.upload(vnl.data(), vnl.size(), c->stream));
-  HIPCHK(c->funcs.upload(fd.data(), fd.size(), c->stream));
+  HIPCHK(c->var_off.upload_staged(voff.data(), voff.size(), c->stream, c->stage));
+  HIPCHK(c->var_nl.upload_staged(vnl.data(), vnl.size(), c->stream, c->stage));
+  HIPCHK(c->funcs.upload_staged(fd.data(), fd.size(), c->stream, c->stage));
   if (F > 0) {
-    HIPCHK(c->entry_ptr.upload(mb->entry_ptr, (size_t)F * (M + 1), c->stream));
+    HIPCHK(c->entry_ptr.upload_staged(mb->entry_ptr, (size_t)F * (M + 1), c->stream, c->stage));
     // (padded: G's table scan reads the first word of up to 7 entries past a model's last one,
     // gen_qsa.py sub_uf1)
     HIPCHK(c->entry_words.ensure(sizeof(uint32_t) * ((size_t)std::max<int64_t>(ew_total, 1) + kEntryPadWords)));
-    HIPCHK(c->entry_words.upload(mb->entry_words, (size_t)std::max<int64_t>(ew_total, 1), c->stream));
+    HIPCHK(c->entry_words.upload_staged(mb->entry_words, (size_t)std::max<int64_t>(ew_total, 1), c->stream, c->stage));
   } else {
     int64_t z = 0;
     uint32_t zw = 0;
-    HIPCHK(c->entry_ptr.upload(&z, 1, c->stream));
+    HIPCHK(c->entry_ptr.upload_staged(&z, 1, c->stream, c->stage));
     HIPCHK(c->entry_words.ensure(sizeof(uint32_t) * (1 + kEntryPadWords)));
-    HIPCHK(c->entry_words.upload(&zw, 1, c->stream));
+    HIPCHK(c->entry_words.upload_staged(&zw, 1, c->stream, c->stage));
   }
-  HIPCHK(c->else_words.upload(else_soa.data(), else_soa.size(), c->stream));
-  HIPCHK(c->dense_words.upload(dense.data(), dense.size(), c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(c->else_words.upload_staged(else_soa.data(), else_soa.size(), c->stream, c->stage));
+  HIPCHK(c->dense_words.upload_staged(dense.data(), dense.size(), c->stream, c->stage));
   c->M = M;
   c->index_base = mb->index_base;
   c->n_vars = mb->n_vars;
