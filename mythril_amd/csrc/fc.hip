@@ -398,8 +398,10 @@ __device__ __forceinline__ uint32_t fx_case(const uint32_t y[8], const FcCmpHead
 // (entries k-major per chunk: one coalesced load per entry) for the FC_TILES tiles.
 
 // (MODE: the launch's r.mode as a template parameter, so the first-hit kernel carries none of the
-// verdict / column store code and its loop-invariant addresses)
-template <int MODE>
+// verdict / column store code and its loop-invariant addresses; XF: the launch has unary atoms --
+// the transforms' registers made the kernel spill SGPRs and use scratch, so launches without one,
+// every launch by default, run the instantiation without them)
+template <int MODE, bool XF>
 __global__ __launch_bounds__(256) void fca_kernel(const FcaGroup* __restrict__ groups, const FcCmp* __restrict__ atoms,
                                                   const FcXf* __restrict__ xfs,
                                                   const uint32_t* __restrict__ lists,
@@ -463,8 +465,8 @@ __global__ __launch_bounds__(256) void fca_kernel(const FcaGroup* __restrict__ g
         const FcCmpHead h = atoms[a].h;
         const FcCmpTail t = atoms[a].t;
         uint64_t m[FC_TILES];
-        const uint32_t nx = xfs[a].n;
-        if (nx) {   // a unary atom: the transform of the variable, then the compare
+        const uint32_t nx = XF ? xfs[a].n : 0u;
+        if (XF && nx) {   // a unary atom: the transform of the variable, then the compare
           const FcXf X = xfs[a];
 #pragma unroll
           for (int j = 0; j < FC_TILES; j++) {
@@ -623,20 +625,27 @@ __global__ __launch_bounds__(256) void fca_kernel(const FcaGroup* __restrict__ g
   }
 }
 
+template <int MODE>
+static void launch_fca_mode(const FcaArgs& a, int64_t groups, size_t lds, hipStream_t st) {
+  if (a.xfs)
+    hipLaunchKernelGGL((fca_kernel<MODE, true>), dim3((unsigned)groups), dim3(256), lds, st, a.groups, a.atoms, a.xfs,
+                       a.lists, a.chunk_off, a.tape_out, a.tape_metric, a.vars, a.bool_masks, a.stage_masks, a);
+  else
+    hipLaunchKernelGGL((fca_kernel<MODE, false>), dim3((unsigned)groups), dim3(256), lds, st, a.groups, a.atoms, a.xfs,
+                       a.lists, a.chunk_off, a.tape_out, a.tape_metric, a.vars, a.bool_masks, a.stage_masks, a);
+}
+
 hipError_t launch_fca(const FcaArgs& a, hipStream_t st) {
   if (a.n <= 0 || a.M <= 0) return hipSuccess;
   const int64_t groups = (a.M + 64 * FC_TILES - 1) / (64 * FC_TILES);
   if (groups > 0x7FFFFFFF) return hipErrorInvalidValue;
   const size_t lds = (size_t)(1 + a.n_smask + a.n_atoms) * 8u * FC_TILES;
   if (a.mode == 0)
-    hipLaunchKernelGGL(fca_kernel<0>, dim3((unsigned)groups), dim3(256), lds, st, a.groups, a.atoms, a.xfs, a.lists,
-                       a.chunk_off, a.tape_out, a.tape_metric, a.vars, a.bool_masks, a.stage_masks, a);
+    launch_fca_mode<0>(a, groups, lds, st);
   else if (a.mode == 1)
-    hipLaunchKernelGGL(fca_kernel<1>, dim3((unsigned)groups), dim3(256), lds, st, a.groups, a.atoms, a.xfs, a.lists,
-                       a.chunk_off, a.tape_out, a.tape_metric, a.vars, a.bool_masks, a.stage_masks, a);
+    launch_fca_mode<1>(a, groups, lds, st);
   else if (a.mode == 3)
-    hipLaunchKernelGGL(fca_kernel<3>, dim3((unsigned)groups), dim3(256), lds, st, a.groups, a.atoms, a.xfs, a.lists,
-                       a.chunk_off, a.tape_out, a.tape_metric, a.vars, a.bool_masks, a.stage_masks, a);
+    launch_fca_mode<3>(a, groups, lds, st);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

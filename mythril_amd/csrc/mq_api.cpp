@@ -260,7 +260,8 @@ struct StageRing {
   PinnedBuf buf;
   size_t head = 0;
   std::vector<hipStream_t> used;
-  // pinned copy of src (n <= kMaxStaged) for an async copy on st; nullptr: stage failed
+  // pinned copy of src (n <= kMaxStaged; src nullptr: n bytes the caller fills) for an async copy
+  // on st; nullptr: stage failed
   void* put(const void* src, size_t n, hipStream_t st) {
     if (!buf.p && buf.ensure(kBytes) != hipSuccess) return nullptr;
     const size_t a = (n + 255) & ~size_t(255);
@@ -272,7 +273,7 @@ struct StageRing {
     }
     if (std::find(used.begin(), used.end(), st) == used.end()) used.push_back(st);
     void* d = (char*)buf.p + head;
-    std::memcpy(d, src, n);
+    if (src) std::memcpy(d, src, n);
     head += a;
     return d;
   }
@@ -288,12 +289,13 @@ struct UploadPack {
     size_t off, bytes;
   };
   std::vector<V> views;
+  // (pad: that many zero elements after the copied ones, inside the view)
   template <class T>
-  void add(DevBuf& v, const T* src, size_t count) {
-    const size_t off = (host.size() + 255) & ~size_t(255), n = sizeof(T) * count;
-    host.resize(off + std::max<size_t>(n, 1), 0);
+  void add(DevBuf& v, const T* src, size_t count, size_t pad = 0) {
+    const size_t off = (host.size() + 255) & ~size_t(255), n = sizeof(T) * count, b = std::max<size_t>(n + sizeof(T) * pad, 1);
+    host.resize(off + b, 0);
     if (n) std::memcpy(host.data() + off, src, n);
-    views.push_back(V{&v, off, std::max<size_t>(n, 1)});
+    views.push_back(V{&v, off, b});
   }
   hipError_t commit(DevBuf& block, hipStream_t st, StageRing& ring) {
     for (const V& x : views) x.buf->release();   // (views of the previous block, if any)
@@ -365,6 +367,7 @@ struct mq_ctx {
   DevBuf scratch;   // per-wave temp slots of the HIP C++ interpreter (persistent grid)
   DevBuf kec_data, kec_off, kec_out;   // mq_keccak256 buffers, grown and kept across calls
   DevBuf rowmask;   // per-row masks applied to uploaded variable words
+  DevBuf mpack;     // UploadPack block of the model batch's small tables (upload_one: the views above point in)
   // Bool variables as packed lane masks [tile][n_bmask] (G kernel PUSH_PKB): bmask_of_var[v] =
   // mask index of Bool variable v (-1: none); bmask_rows[j] = its variable row
   std::vector<int32_t> bmask_of_var;
@@ -559,6 +562,7 @@ struct mq_tapes {
   // the two-phase form (fca_kernel; MQ_FC_ONEPHASE=1: fc_kernel): atoms in fc_cmp_dev, lists in
   // fc_mask_dev
   bool fca = false;
+  bool fca_any_xf = false;   // the tape plan has unary atoms (FcaPlan::any_xf)
   int fca_atoms = 0;
   std::vector<FcaPlanSeg> fca_segs;
   DevBuf fca_chunk_dev, fca_out_dev, fca_metric_dev, fca_group_dev, fca_xf_dev;
@@ -566,6 +570,7 @@ struct mq_tapes {
   // before the level's G launch (cq_prepare); the level's G descriptors are the others
   struct FcLevel {   // fca_kernel mode 3 (fca_plan per level)
     int count = 0;
+    bool any_xf = false;   // (FcaPlan::any_xf)
     std::vector<FcaPlanSeg> segs;
     DevBuf atoms, xfs, groups, lists, chunk, out, metric, smask, colmask;
   };
@@ -1042,34 +1047,46 @@ static int upload_one(mq_ctx* c, const mq_model_batch* mb) {
   }
   if (dense.empty()) dense.push_back(0);
   c->have_models = false;
+  // the batch's small tables (row masks, Bool mask rows, variable offsets / limbs, functions,
+  // entries, else values, dense slots) go up as ONE staged block (UploadPack: c->mpack, the
+  // buffers below views into it); the variable rows, which can be large, stay a buffer of their own
+  UploadPack pk;
   // variable rows followed by one all-zero row (the QSA preload points absent limbs at it)
   HIPCHK(c->vars.ensure(sizeof(uint32_t) * (size_t)(rows + 1) * M));
-  if (rows > 0) {
-    // (a drop-in batch's rows are a few KB: staged, no sync; a large batch: pageable + a sync)
-    const size_t n = sizeof(uint32_t) * (size_t)rows * M;
-    void* h = n <= StageRing::kMaxStaged ? c->stage.put(mb->var_words, n, c->stream) : nullptr;
-    HIPCHK(hipMemcpyAsync(c->vars.p, h ? h : mb->var_words, n, hipMemcpyHostToDevice, c->stream));
-    if (!h) HIPCHK(hipStreamSynchronize(c->stream));
-  }
-  HIPCHK(hipMemsetAsync((uint32_t*)c->vars.p + (size_t)rows * M, 0, sizeof(uint32_t) * M, c->stream));
   {
-    // canonical values: bits above a variable's width are cleared on the device (the kernels
-    // and the asm interpreter read rows unmasked)
-    std::vector<uint32_t> rowmask((size_t)rows + 1, 0xFFFFFFFFu);
-    bool need = false;
-    for (int v = 0; v < mb->n_vars; v++) {
-      const int w = mb->var_width[v];
-      const uint32_t top = w == 0 ? 1u : ((w % 32) ? ((1u << (w % 32)) - 1u) : 0xFFFFFFFFu);
-      if (top != 0xFFFFFFFFu) {
-        rowmask[voff[v] + vnl[v] - 1] = top;
-        need = true;
+    const size_t n = sizeof(uint32_t) * (size_t)rows * M, nz = sizeof(uint32_t) * (size_t)M;
+    if (n + nz <= StageRing::kMaxStaged) {
+      // (a drop-in batch's rows are a few KB: the rows and the zero row in one staged copy, no sync)
+      void* h = c->stage.put(nullptr, n + nz, c->stream);
+      if (h) {
+        if (n) std::memcpy(h, mb->var_words, n);
+        std::memset((char*)h + n, 0, nz);
+        HIPCHK(hipMemcpyAsync(c->vars.p, h, n + nz, hipMemcpyHostToDevice, c->stream));
+      } else {
+        if (n) HIPCHK(hipMemcpyAsync(c->vars.p, mb->var_words, n, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemsetAsync((uint32_t*)c->vars.p + (size_t)rows * M, 0, nz, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
       }
-    }
-    if (need) {
-      HIPCHK(c->rowmask.upload_staged(rowmask.data(), rowmask.size(), c->stream, c->stage));
-      HIPCHK(launch_mask_rows(c->vars.as<uint32_t>(), c->rowmask.as<uint32_t>(), rows, M, c->stream));
+    } else {
+      // a large batch: pageable + a sync
+      if (n) HIPCHK(hipMemcpyAsync(c->vars.p, mb->var_words, n, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(hipMemsetAsync((uint32_t*)c->vars.p + (size_t)rows * M, 0, nz, c->stream));
+      if (n) HIPCHK(hipStreamSynchronize(c->stream));
     }
   }
+  // canonical values: bits above a variable's width are cleared on the device (the kernels
+  // and the asm interpreter read rows unmasked)
+  std::vector<uint32_t> rowmask((size_t)rows + 1, 0xFFFFFFFFu);
+  bool need_mask = false;
+  for (int v = 0; v < mb->n_vars; v++) {
+    const int w = mb->var_width[v];
+    const uint32_t top = w == 0 ? 1u : ((w % 32) ? ((1u << (w % 32)) - 1u) : 0xFFFFFFFFu);
+    if (top != 0xFFFFFFFFu) {
+      rowmask[voff[v] + vnl[v] - 1] = top;
+      need_mask = true;
+    }
+  }
+  if (need_mask) pk.add(c->rowmask, rowmask.data(), rowmask.size());
   // P kernel preload rows: var v < 8, limb l (the zero row where absent; a variable wider
   // than 256 bits is never preloaded: the translator sends its tapes to the G kernel)
   for (int v = 0; v < 8; v++)
@@ -1080,8 +1097,8 @@ static int upload_one(mq_ctx* c, const mq_model_batch* mb) {
     }
   // Bool variables as lane masks (at most 65535 of them; the others are read as rows;
   // MQ_BMASK_CAP lowers the cap so tests reach the row path)
+  std::vector<uint32_t> brows;
   {
-    std::vector<uint32_t> brows;
     c->bmask_of_var.assign(mb->n_vars, -1);
     size_t cap = 65535;
     if (const char* e = std::getenv("MQ_BMASK_CAP")) cap = std::min<size_t>(cap, (size_t)std::atol(e));
@@ -1094,9 +1111,7 @@ static int upload_one(mq_ctx* c, const mq_model_batch* mb) {
     const int64_t tiles = (M + 63) / 64;
     HIPCHK(c->bmasks.ensure(std::max<size_t>(8, sizeof(uint64_t) * (size_t)tiles * brows.size())));
     if (brows.empty()) brows.push_back(0);
-    HIPCHK(c->bmask_rows.upload_staged(brows.data(), brows.size(), c->stream, c->stage));
-    HIPCHK(launch_pack_bool(c->vars.as<uint32_t>(), c->bmasks.as<uint64_t>(), c->bmask_rows.as<uint32_t>(), nullptr,
-                            c->n_bmask, c->n_bmask, M, c->stream));
+    pk.add(c->bmask_rows, brows.data(), brows.size());
   }
   c->var_off_h.assign(voff.begin(), voff.begin() + mb->n_vars);
   c->var_nl_h.assign(vnl.begin(), vnl.begin() + mb->n_vars);
@@ -1122,24 +1137,26 @@ static int upload_one(mq_ctx* c, const mq_model_batch* mb) {
       c->layout_gen++;
     }
   }
-  HIPCHK(c->var_off.upload_staged(voff.data(), voff.size(), c->stream, c->stage));
-  HIPCHK(c->var_nl.upload_staged(vnl.data(), vnl.size(), c->stream, c->stage));
-  HIPCHK(c->funcs.upload_staged(fd.data(), fd.size(), c->stream, c->stage));
+  pk.add(c->var_off, voff.data(), voff.size());
+  pk.add(c->var_nl, vnl.data(), vnl.size());
+  pk.add(c->funcs, fd.data(), fd.size());
   if (F > 0) {
-    HIPCHK(c->entry_ptr.upload_staged(mb->entry_ptr, (size_t)F * (M + 1), c->stream, c->stage));
+    pk.add(c->entry_ptr, mb->entry_ptr, (size_t)F * (M + 1));
     // (padded: G's table scan reads the first word of up to 7 entries past a model's last one,
     // gen_qsa.py sub_uf1)
-    HIPCHK(c->entry_words.ensure(sizeof(uint32_t) * ((size_t)std::max<int64_t>(ew_total, 1) + kEntryPadWords)));
-    HIPCHK(c->entry_words.upload_staged(mb->entry_words, (size_t)std::max<int64_t>(ew_total, 1), c->stream, c->stage));
+    pk.add(c->entry_words, mb->entry_words, (size_t)std::max<int64_t>(ew_total, 1), kEntryPadWords);
   } else {
-    int64_t z = 0;
-    uint32_t zw = 0;
-    HIPCHK(c->entry_ptr.upload_staged(&z, 1, c->stream, c->stage));
-    HIPCHK(c->entry_words.ensure(sizeof(uint32_t) * (1 + kEntryPadWords)));
-    HIPCHK(c->entry_words.upload_staged(&zw, 1, c->stream, c->stage));
+    const int64_t z = 0;
+    const uint32_t zw = 0;
+    pk.add(c->entry_ptr, &z, 1);
+    pk.add(c->entry_words, &zw, 1, kEntryPadWords);
   }
-  HIPCHK(c->else_words.upload_staged(else_soa.data(), else_soa.size(), c->stream, c->stage));
-  HIPCHK(c->dense_words.upload_staged(dense.data(), dense.size(), c->stream, c->stage));
+  pk.add(c->else_words, else_soa.data(), else_soa.size());
+  pk.add(c->dense_words, dense.data(), dense.size());
+  HIPCHK(pk.commit(c->mpack, c->stream, c->stage));
+  if (need_mask) HIPCHK(launch_mask_rows(c->vars.as<uint32_t>(), c->rowmask.as<uint32_t>(), rows, M, c->stream));
+  HIPCHK(launch_pack_bool(c->vars.as<uint32_t>(), c->bmasks.as<uint64_t>(), c->bmask_rows.as<uint32_t>(), nullptr,
+                          c->n_bmask, c->n_bmask, M, c->stream));
   c->M = M;
   c->index_base = mb->index_base;
   c->n_vars = mb->n_vars;
@@ -3297,6 +3314,7 @@ static void fc_plan(const mq_ctx* c, const std::vector<std::vector<uint32_t>>& f
 struct FcaPlan {
   std::vector<FcCmp> atoms;
   std::vector<FcXf> xfs;   // parallel to atoms
+  bool any_xf = false;     // some atom has a unary transform (else the launches pass xfs = nullptr)
   std::vector<FcaGroup> groups;
   std::vector<uint32_t> lists, chunk_off, tape_out, metric, stage_masks;
   std::vector<int32_t> col_mask;   // (columns: per kept column its lane-mask index)
@@ -3398,6 +3416,7 @@ static void fca_plan(const mq_ctx* c, const std::vector<std::vector<uint32_t>>& 
         xf.op[k] = FcXop{key[o], key[o + 1], key[o + 2], key[o + 3]};
       }
       P.xfs.push_back(xf);
+      P.any_xf |= nx > 0;
       q.h.c01 = (uint64_t)cc[0] | ((uint64_t)cc[1] << 32);
       q.h.f01 = (uint64_t)ff[0] | ((uint64_t)ff[1] << 32);
       for (int l = 0; l < 6; l++) {
@@ -3665,6 +3684,7 @@ static int qsa_prepare(mq_ctx* c, mq_tapes* T, bool latency) {
     T->fc_count = (int)fap.tape_out.size();
     T->fca_atoms = (int)fap.atoms.size();
     T->fca_segs = fap.segs;
+    T->fca_any_xf = fap.any_xf;
     if (T->fc_count > 0) {
       if (fap.stage_masks.empty()) fap.stage_masks.push_back(0);
       if (fap.atoms.empty()) fap.atoms.push_back(FcCmp{});
@@ -3813,6 +3833,7 @@ static int cq_prepare(mq_ctx* c, mq_tapes* T) {
     mq_tapes::FcLevel& fl = *T->fc_lvl[li];
     fl.count = (int)fap.tape_out.size();
     fl.segs = fap.segs;
+    fl.any_xf = fap.any_xf;
     if (fl.count > 0) {
       if (fap.stage_masks.empty()) fap.stage_masks.push_back(0);
       if (fap.atoms.empty()) fap.atoms.push_back(FcCmp{});
@@ -4206,7 +4227,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
         f.n_groups = sg.n_groups;
         f.groups = fl.groups.as<FcaGroup>() + sg.group_off;
         f.atoms = fl.atoms.as<FcCmp>() + sg.atom_off;
-        f.xfs = fl.xfs.as<FcXf>() + sg.atom_off;
+        f.xfs = fl.any_xf ? fl.xfs.as<FcXf>() + sg.atom_off : nullptr;
         f.lists = fl.lists.as<uint32_t>();
         f.chunk_off = fl.chunk.as<uint32_t>() + sg.chunk_first;
         f.tape_out = fl.out.as<uint32_t>() + sg.tape_first;
@@ -4393,7 +4414,7 @@ static int launch_all(mq_ctx* c, mq_tapes* T, int32_t* best, uint8_t* verdicts, 
     f.n_groups = sg.n_groups;
     f.groups = T->fca_group_dev.as<FcaGroup>() + sg.group_off;
     f.atoms = T->fc_cmp_dev.as<FcCmp>() + sg.atom_off;
-    f.xfs = T->fca_xf_dev.as<FcXf>() + sg.atom_off;
+    f.xfs = T->fca_any_xf ? T->fca_xf_dev.as<FcXf>() + sg.atom_off : nullptr;
     f.lists = T->fc_mask_dev.as<uint32_t>();
     f.chunk_off = T->fca_chunk_dev.as<uint32_t>() + sg.chunk_first;
     f.tape_out = T->fca_out_dev.as<uint32_t>() + sg.tape_first;

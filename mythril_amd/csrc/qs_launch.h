@@ -294,7 +294,8 @@ struct FcaArgs {
   int n_groups;
   const FcaGroup* groups;
   const FcCmp* atoms;             // accept in {1, 2, 3} (x < c, x == c, x <= c); negations in the lists
-  const FcXf* xfs;                // per atom: its unary transform (n = 0: none); groups with one have nl = 8
+  const FcXf* xfs;                // per atom: its unary transform (n = 0: none); groups with one have nl = 8;
+                                  // nullptr: no unary atom (the kernel without the transforms)
   const uint32_t* lists;          // chunk c of 64 tapes: kmax(c) entries x 64 lanes, k-major, from chunk_off[c]
   const uint32_t* chunk_off;      // [n_chunks + 1]: kmax(c) = (chunk_off[c + 1] - chunk_off[c]) / 64
   const uint32_t* tape_out;       // per tape: its best / verdict row | negated result << 31

@@ -33,7 +33,7 @@ def section(path, name):
 
 def main():
     out = sys.argv[1] if len(sys.argv) > 1 else None
-    lib = os.path.join(ROOT, "mythril_amd", "libmq.so")
+    lib = os.environ.get("MQ_LIB") or os.path.join(ROOT, "mythril_amd", "libmq.so")
     fat = section(lib, ".hip_fatbin")
     res = {}
     magic = b"__CLANG_OFFLOAD_BUNDLE__"
