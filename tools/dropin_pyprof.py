@@ -38,8 +38,35 @@ class NullEv:
         return np.zeros((ct.n_tapes, self.M), bool), np.full(ct.n_tapes, -1, np.int32)
 
 
+def fresh(n, m):
+    """bench.py dropin_leg's cell: warm the engine with one batch, then time a batch of NEW paths
+    (another query seed) through a new ModelCache over the same models, per query seed."""
+    E.CompiledTapes = CT
+    ts, stages = [], []
+    for q in range(1, 21):
+        eng = sp.VerdictEngine(NullEv())
+        warm, recs, _ = dropin_workload(n, m, seed=7)
+        cache = sp.ModelCache(eng)
+        for r in reversed(recs):
+            cache.put(r, 1)
+        cache.check_quick_sat_batch(warm)
+        exprs, _, _ = dropin_workload(n, m, seed=7, query_seed=q)
+        cache = sp.ModelCache(eng)
+        for r in reversed(recs):
+            cache.put(r, 1)
+        before = dict(eng.timing)
+        t0 = time.perf_counter()
+        cache.check_quick_sat_batch(exprs)
+        ts.append(time.perf_counter() - t0)
+        stages.append({k: (eng.timing[k] - before[k]) * 1e3 for k in eng.timing})
+    st = {k: round(float(np.median([s[k] for s in stages])), 4) for k in stages[0]}
+    print(f"fresh: median {np.median(ts) * 1e3:.4f} ms per batch of {n} queries, M={m}; engine stages (median) {st}")
+
+
 def main():
     n, m = int(sys.argv[1]), int(sys.argv[2])
+    if "--fresh" in sys.argv:
+        return fresh(n, m)
     E.CompiledTapes = CT
     eng = sp.VerdictEngine(NullEv())
     warm, recs, _ = dropin_workload(n, m, seed=7)
