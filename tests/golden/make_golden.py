@@ -89,10 +89,12 @@ class Skip(Exception):
     pass
 
 
-def lower_program(code: bytes, t: Tape, calldata: bytes = b"", exp_conditions=None):
+def lower_program(code: bytes, t: Tape, calldata: bytes = b"", exp_conditions=None, pre_storage=None):
     """Symbolically run straight-line EVM code building tape terms with mythril's mapping.
     Returns {storage_key_int: node}.  Raises Skip for control flow / unsupported opcodes.
-    ``exp_conditions`` (a list) collects (base, exponent, result, condition term) per EXP."""
+    ``exp_conditions`` (a list) collects (base, exponent, result, condition term) per EXP.
+    ``pre_storage`` ({key: value}): the account's storage before the program (the test's "pre"),
+    what an SLOAD of a key the program has not stored reads."""
     stack = []
     store = {}
     mem = {}  # byte offset -> constant byte (sha3 tests only use constant memory)
@@ -241,7 +243,7 @@ def lower_program(code: bytes, t: Tape, calldata: bytes = b"", exp_conditions=No
             continue
         if op == 0x20:  # SHA3 over constant memory: emitted as an interpreted keccak node
             off, size = const_value(pop()), const_value(pop())
-            if size > 4096 or off > 1 << 20:
+            if size > 4096 or off > 1 << 32:   # (memory is sparse: only the size is read)
                 raise Skip("sha3 region too large")
             data = bytes(mem.get(off + k, 0) for k in range(size))
             stack.append(("sha3", data))
@@ -250,6 +252,13 @@ def lower_program(code: bytes, t: Tape, calldata: bytes = b"", exp_conditions=No
             k, v = pop(), pop()
             key = const_value(k)
             store[key] = v
+            continue
+        if op == 0x54:  # SLOAD with a concrete key: the word stored earlier, else the pre-state's
+            key = const_value(pop())
+            if key in store:
+                stack.append(store[key])
+            else:
+                stack.append(t.const(int((pre_storage or {}).get(key, 0)) & M256, 256))
             continue
         raise Skip(f"opcode 0x{op:02x}")
     return store
@@ -274,8 +283,9 @@ def vmtests():
                 calldata = bytes.fromhex(case["exec"].get("data", "0x")[2:])
                 t = Tape()
                 conds = []
+                pre = {int(k, 16): int(v, 16) for k, v in case.get("pre", {}).get(addr, {}).get("storage", {}).items()}
                 try:
-                    store = lower_program(code, t, calldata, conds)
+                    store = lower_program(code, t, calldata, conds, pre)
                 except Skip as e:
                     skipped[str(e)] = skipped.get(str(e), 0) + 1
                     continue

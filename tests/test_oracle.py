@@ -39,10 +39,13 @@ def test_vmtests_pyoracle(entry):
 
 
 def test_vmtests_cover_the_listed_kats():
-    """>= 400 of the 457 VMTests storage KATs of vmArithmeticTest / vmBitwiseLogicOperation are
-    pinned, the EXP programs (exp*.json, expPowerOf*) among them with their Power constraints."""
+    """All 445 value KATs of the VMTests storage entries of vmArithmeticTest /
+    vmBitwiseLogicOperation / vmSha3Test are pinned (the 12 sha3 digests are keccak_kats.json), the
+    EXP programs (exp*.json, expPowerOf*, expXY via SLOAD of stored calldata words) among them with
+    their Power constraints."""
     kats = load("vmtests_kats.json")
-    assert len(kats) >= 400
+    assert len(kats) == 445
+    assert sum("expXY" in e["name"] for e in kats) == 5
     exp = [e for e in kats if "constraint" in e]
     assert len(exp) >= 300 and all(e["power"] for e in exp)
     assert any("expPowerOf256Of256" in e["name"] for e in exp)
