@@ -441,6 +441,9 @@ _LEAVES = frozenset({S.SYM, S.VAL, S.TRUE, S.FALSE, S.ARRAY_SYM})
 _LOOKUP_WEIGHT = 8
 # nested hoisting threshold (nested_shared), in the same weighted nodes
 NESTED_MIN_NODES = 32
+# shared constant shifts whose column would store at least this many rows are inlined into their
+# readers (lower_batch; MQ_INLINE_SHIFTS overrides, 0 = never)
+INLINE_SHIFT_ROWS = 1
 NESTED_ROUNDS = 1     # rounds of nested_shared: later rounds chain C4's storage balances into ~10 levels
 
 
@@ -832,6 +835,22 @@ def lower_batch(roots: Sequence[S.Term], syms: Optional[SymbolTable] = None, hoi
         # every keccak application and Concat piece, also those already chosen as shared terms
         # (an address key x & (2^160 - 1) is both): never narrowed
         kpieces = {id(t) for t in keccak_subterms(list(roots), syms, [])}
+        inline_rows = int(os.environ.get("MQ_INLINE_SHIFTS", INLINE_SHIFT_ROWS))
+        if inline_rows > 0:
+            # a shared shift by a constant of a variable or of another column is recomputed by its
+            # readers when storing it would take >= inline_rows rows: its launch would read the
+            # operand's rows and write as many again, for two VALU ops a limb in each reader
+            ids = {id(t) for t in col_terms}
+            nots = os.environ.get("MQ_INLINE_NOTS") is not None
+            cheap = {id(t) for k, t in enumerate(col_terms)
+                     if k < n_shared and id(t) not in program and id(t) not in kpieces
+                     and ((t.kind in (S.LSHR, S.ASHR, S.SHL) and t.args[1].kind == S.VAL
+                           and (abs(_column_bits(t)) + 31) // 32 >= inline_rows)
+                          or (nots and t.kind == S.NOT))
+                     and (t.args[0].kind in _LEAVES or id(t.args[0]) in ids)}
+            if cheap:
+                n_shared -= sum(1 for k, t in enumerate(col_terms) if k < n_shared and id(t) in cheap)
+                col_terms = [t for t in col_terms if id(t) not in cheap]
         for k, t in enumerate(col_terms):
             # a column whose value has fewer significant bits stores only those (selectors
             # x >> 224, x urem 2^160, masks): fewer rows written and read; keccak columns and
