@@ -60,6 +60,35 @@ def test_calls_avoided_leg_counts_at_get_model(monkeypatch):
     assert on["solver_calls_avoided"] >= off["solver_calls_avoided"]
 
 
+class _NoTimers:
+    """The evaluator timing hooks the drop-in legs call (no device: nothing to time)."""
+
+    def time_kernels(self, on=True):
+        pass
+
+    def kernel_times(self, reset=True):
+        return []
+
+    def host_times(self, reset=False):
+        return {}
+
+
+def test_dropin_legs_time_several_new_batches_and_report_the_median(monkeypatch):
+    """bench.py's drop-in cells on the oracle engine (small): every timed batch is new paths (the
+    stream's rounds new parents), answers equal the reference loop replayed on the oracle, and the
+    cell is the median repetition with all samples beside it."""
+    import test_support as ts
+    from mythril_amd import support as sp
+    monkeypatch.setattr(sp, "VerdictEngine", lambda ev: ts.OracleEngine())
+    ev = _NoTimers()
+    for cell in bench.dropin_leg(ev, grid=((2, 4),), reps=3) + bench.dropin_stream_leg(ev, grid=((2, 4),), reps=3):
+        assert cell["timed_batches"] == 3 and len(cell["ms_samples"]) == 3
+        assert sorted(cell["ms_samples"])[1] == round(cell["ms_per_batch"], 4)
+        assert cell["answers_match_reference_loop"]
+    stream = bench.dropin_stream_leg(ev, grid=((2, 4),), reps=2)[0]
+    assert stream["n_queries"] == 4 and stream["conjuncts_cached"] > 0
+
+
 def test_two_rank_line_under_gloo_with_the_oracle_engine():
     """bench.py's N > 1 protocol end to end on CPU: torchrun world 2, gloo, the oracle answering
     for the GPU (--engine oracle).  The line keeps the driver's keys, the per-rank split of
