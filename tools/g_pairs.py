@@ -28,3 +28,6 @@ before = sorted(((v, a, b) for (a, b), v in pr.items() if match(b)), reverse=Tru
 after = sorted(((v, a, b) for (a, b), v in pr.items() if match(a)), reverse=True)
 print("before:", before[:15])
 print("after:", after[:15])
+# (with KIND = PUSH_MEM: a following stack reader without the _L form waits for the load)
+waits = sum(v for (a, b), v in pr.items() if a.startswith(kind) and not b.endswith("_L") and not b.startswith("PUSH"))
+print(f"pairs {kind} -> a waiting reader: {waits}; all pairs: {sum(pr.values())}")
